@@ -1,0 +1,15 @@
+"""pubsub_amd — MI355X batched gossip engine (host side).
+
+Mirrors the router-selection / parameter API of go-libp2p-pubsub over the
+C-ABI in include/gossip_engine.h; the compute runs in the HIP library
+build/libgossip_engine.so (gfx950).
+"""
+from ._abi import (GS_ROUTER_FLOODSUB, GS_ROUTER_GOSSIPSUB, GS_ROUTER_RANDOMSUB)  # noqa: F401
+from .params import (DefaultGossipSubParams, DefaultPeerGaterParams, GossipSubParams,  # noqa: F401
+                     Hour, Microsecond, Millisecond, Minute, NewPeerGaterParams, PeerGaterParams,
+                     PeerScoreParams, PeerScoreThresholds, ScoreParameterDecay,
+                     ScoreParameterDecayWithBase, Second, TopicScoreParams, eth2_peer_score_params,
+                     eth2_thresholds, eth2_topic_score_params)
+from .engine import (PRODUCT_LIB, Engine, GossipEngineError, NewFloodSub, NewGossipSub,  # noqa: F401
+                     NewRandomSub, WithDevice, WithDirectPeers, WithFloodPublish, WithGossipSubParams,
+                     WithHop, WithMessageWindow, WithPeerScore, WithRecordDeliveries, WithSeed, load)

@@ -1,0 +1,152 @@
+"""ctypes mirror of include/gossip_engine.h.
+
+Struct layouts and function signatures are declared once here and bound to
+whichever library exports the ABI: the product (libgossip_engine.so, HIP) or,
+in tests only, the CPU oracle (oracle/_build/libgossip_oracle.so).
+"""
+import ctypes as C
+import os
+
+GS_OK = 0
+GS_EINVAL = -1
+GS_ESTATE = -2
+GS_ENOMEM = -3
+GS_EDEVICE = -4
+GS_ECAPACITY = -5
+GS_EUNSUPPORTED = -6
+
+GS_ROUTER_FLOODSUB = 0
+GS_ROUTER_RANDOMSUB = 1
+GS_ROUTER_GOSSIPSUB = 2
+
+GS_FLAG_SCORING = 1 << 0
+GS_FLAG_FLOOD_PUBLISH = 1 << 1
+GS_FLAG_RECORD_DELIVERIES = 1 << 2
+
+i32, i64, u32, u64, f64, u8 = C.c_int32, C.c_int64, C.c_uint32, C.c_uint64, C.c_double, C.c_uint8
+
+
+class GossipSubParamsC(C.Structure):
+    _fields_ = [
+        ("D", i32), ("Dlo", i32), ("Dhi", i32), ("Dscore", i32), ("Dout", i32),
+        ("HistoryLength", i32), ("HistoryGossip", i32), ("Dlazy", i32),
+        ("GossipFactor", f64), ("GossipRetransmission", i32),
+        ("HeartbeatInitialDelay", i64), ("HeartbeatInterval", i64), ("FanoutTTL", i64),
+        ("PrunePeers", i32), ("PruneBackoff", i64), ("Connectors", i32),
+        ("MaxPendingConnections", i32), ("ConnectionTimeout", i64),
+        ("DirectConnectTicks", u64), ("DirectConnectInitialDelay", i64),
+        ("OpportunisticGraftTicks", u64), ("OpportunisticGraftPeers", i32),
+        ("GraftFloodThreshold", i64), ("MaxIHaveLength", i32), ("MaxIHaveMessages", i32),
+        ("IWantFollowupTime", i64),
+    ]
+
+
+class PeerScoreParamsC(C.Structure):
+    _fields_ = [
+        ("TopicScoreCap", f64), ("AppSpecificScorePresent", i32), ("AppSpecificWeight", f64),
+        ("IPColocationFactorWeight", f64), ("IPColocationFactorThreshold", i32),
+        ("BehaviourPenaltyWeight", f64), ("BehaviourPenaltyThreshold", f64),
+        ("BehaviourPenaltyDecay", f64), ("DecayInterval", i64), ("DecayToZero", f64),
+        ("RetainScore", i64),
+    ]
+
+
+class TopicScoreParamsC(C.Structure):
+    _fields_ = [
+        ("TopicWeight", f64), ("TimeInMeshWeight", f64), ("TimeInMeshQuantum", i64),
+        ("TimeInMeshCap", f64), ("FirstMessageDeliveriesWeight", f64),
+        ("FirstMessageDeliveriesDecay", f64), ("FirstMessageDeliveriesCap", f64),
+        ("MeshMessageDeliveriesWeight", f64), ("MeshMessageDeliveriesDecay", f64),
+        ("MeshMessageDeliveriesCap", f64), ("MeshMessageDeliveriesThreshold", f64),
+        ("MeshMessageDeliveriesWindow", i64), ("MeshMessageDeliveriesActivation", i64),
+        ("MeshFailurePenaltyWeight", f64), ("MeshFailurePenaltyDecay", f64),
+        ("InvalidMessageDeliveriesWeight", f64), ("InvalidMessageDeliveriesDecay", f64),
+    ]
+
+
+class PeerScoreThresholdsC(C.Structure):
+    _fields_ = [
+        ("GossipThreshold", f64), ("PublishThreshold", f64), ("GraylistThreshold", f64),
+        ("AcceptPXThreshold", f64), ("OpportunisticGraftThreshold", f64),
+    ]
+
+
+class PeerGaterParamsC(C.Structure):
+    _fields_ = [
+        ("Threshold", f64), ("GlobalDecay", f64), ("SourceDecay", f64), ("DecayInterval", i64),
+        ("DecayToZero", f64), ("RetainStats", i64), ("Quiet", i64), ("DuplicateWeight", f64),
+        ("IgnoreWeight", f64), ("RejectWeight", f64),
+    ]
+
+
+class ConfigC(C.Structure):
+    _fields_ = [
+        ("router", i32), ("randomsub_size", i32), ("num_nodes", i32), ("num_topics", i32),
+        ("slots_per_topic", i32), ("seed", u32), ("hop_ns", i64), ("flags", u32), ("device", i32),
+    ]
+
+
+class CountersC(C.Structure):
+    _fields_ = [
+        ("hops", i64), ("heartbeats", i64), ("published", i64), ("deliveries", i64),
+        ("duplicates", i64), ("transmissions", i64), ("grafts_sent", i64), ("prunes_sent", i64),
+        ("ihave_sent", i64), ("iwant_sent", i64), ("iwant_served", i64),
+        ("promises_broken", i64), ("graylisted", i64), ("reserved", i64 * 3),
+    ]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+
+
+P = C.c_void_p
+# (name, restype, argtypes) for every function declared in gossip_engine.h
+ABI_FUNCTIONS = [
+    ("gs_abi_version", C.c_int, []),
+    ("gs_last_error", C.c_char_p, []),
+    ("gs_default_gossipsub_params", None, [C.POINTER(GossipSubParamsC)]),
+    ("gs_default_peer_gater_params", None, [C.POINTER(PeerGaterParamsC)]),
+    ("gs_score_parameter_decay_with_base", f64, [i64, i64, f64]),
+    ("gs_score_parameter_decay", f64, [i64]),
+    ("gs_validate_thresholds", C.c_int, [C.POINTER(PeerScoreThresholdsC)]),
+    ("gs_validate_peer_score_params", C.c_int,
+     [C.POINTER(PeerScoreParamsC), C.POINTER(TopicScoreParamsC), C.POINTER(u8), i32]),
+    ("gs_validate_topic_score_params", C.c_int, [C.POINTER(TopicScoreParamsC)]),
+    ("gs_validate_peer_gater_params", C.c_int, [C.POINTER(PeerGaterParamsC)]),
+    ("gs_engine_create", C.c_int,
+     [C.POINTER(ConfigC), C.POINTER(GossipSubParamsC), C.POINTER(PeerScoreParamsC),
+      C.POINTER(TopicScoreParamsC), C.POINTER(u8), C.POINTER(PeerScoreThresholdsC),
+      C.POINTER(PeerGaterParamsC), C.POINTER(P)]),
+    ("gs_engine_destroy", C.c_int, [P]),
+    ("gs_set_graph", C.c_int, [P, C.POINTER(i64), C.POINTER(i32), C.POINTER(u8), C.POINTER(u8)]),
+    ("gs_set_subscriptions", C.c_int, [P, C.POINTER(u64)]),
+    ("gs_set_peer_attrs", C.c_int, [P, C.POINTER(f64), C.POINTER(u32)]),
+    ("gs_set_ip_whitelist", C.c_int, [P, i32, C.POINTER(u32), C.POINTER(u32)]),
+    ("gs_publish", C.c_int, [P, i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i64), C.POINTER(i64)]),
+    ("gs_step", C.c_int, [P, i64]),
+    ("gs_sync", C.c_int, [P]),
+    ("gs_set_topic_score_params", C.c_int, [P, i32, C.POINTER(TopicScoreParamsC)]),
+    ("gs_num_edges", i64, [P]),
+    ("gs_current_hop", i64, [P]),
+    ("gs_read_counters", C.c_int, [P, C.POINTER(CountersC)]),
+    ("gs_read_scores", C.c_int, [P, C.POINTER(f64)]),
+    ("gs_read_mesh", C.c_int, [P, C.POINTER(u64)]),
+    ("gs_read_fanout", C.c_int, [P, C.POINTER(u64)]),
+    ("gs_read_backoff", C.c_int, [P, C.POINTER(i64)]),
+    ("gs_read_topic_stats", C.c_int,
+     [P, C.POINTER(f64), C.POINTER(f64), C.POINTER(f64), C.POINTER(f64), C.POINTER(i64),
+      C.POINTER(i64), C.POINTER(u8)]),
+    ("gs_read_behaviour_penalty", C.c_int, [P, C.POINTER(f64)]),
+    ("gs_read_deliveries", C.c_int, [P, i64, C.POINTER(i32), C.POINTER(i32)]),
+]
+
+
+def bind(path):
+    """dlopen `path` and declare every gossip_engine.h function on it."""
+    if not os.path.exists(path):
+        raise OSError(f"gossip engine library not found: {path}")
+    lib = C.CDLL(path, mode=C.RTLD_LOCAL)
+    for name, res, args in ABI_FUNCTIONS:
+        fn = getattr(lib, name)  # AttributeError = missing export: fail loudly
+        fn.restype = res
+        fn.argtypes = args
+    return lib

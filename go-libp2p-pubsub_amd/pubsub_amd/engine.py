@@ -1,0 +1,247 @@
+"""Host-side mirror of the reference's router selection over the C-ABI.
+
+The reference builds one PubSub per host with NewFloodSub / NewRandomSub /
+NewGossipSub plus Options (pubsub.go:221, floodsub.go:25, randomsub.go:21,
+gossipsub.go:198-391).  This engine is one batched instance for N simulated
+hosts; the constructors below take the same parameter structs and options:
+
+    eng = NewGossipSub(n, topics, graph, WithGossipSubParams(p),
+                       WithPeerScore(score_params, thresholds), WithFloodPublish(True))
+
+The product path loads ONLY the HIP library (libgossip_engine.so, built for
+gfx950) and raises if it is missing: there is no CPU fallback.  Tests pass an
+explicit `lib=` to drive the CPU oracle through the identical ABI.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _abi
+from .params import GossipSubParams, Millisecond
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PRODUCT_LIB = os.path.join(os.path.dirname(_HERE), "build", "libgossip_engine.so")
+
+_lib_cache = {}
+
+
+def load(path=None):
+    """Bind the ABI on `path` (default: the HIP product library)."""
+    path = os.path.abspath(path or PRODUCT_LIB)
+    if path not in _lib_cache:
+        _lib_cache[path] = _abi.bind(path)
+    return _lib_cache[path]
+
+
+class GossipEngineError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"gossip engine error {code}: {msg}")
+        self.code = code
+
+
+def _check(lib, rc):
+    if rc != _abi.GS_OK:
+        raise GossipEngineError(rc, lib.gs_last_error().decode(errors="replace"))
+    return rc
+
+
+def _ptr(a, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype)) if a is not None else None
+
+
+# ---------------------------------------------------------------- options
+def WithGossipSubParams(cfg):
+    return ("gossipsub_params", cfg)
+
+
+def WithPeerScore(params, thresholds):
+    return ("peer_score", (params, thresholds))
+
+
+def WithFloodPublish(flood):
+    return ("flood_publish", bool(flood))
+
+
+def WithDirectPeers(direct_edges):
+    """direct_edges: uint8[E] flags in CSR order (WithDirectPeers, gossipsub.go:338)."""
+    return ("direct", direct_edges)
+
+
+def WithSeed(seed):
+    return ("seed", int(seed))
+
+
+def WithHop(hop_ns):
+    return ("hop_ns", int(hop_ns))
+
+
+def WithMessageWindow(slots_per_topic):
+    return ("slots_per_topic", int(slots_per_topic))
+
+
+def WithRecordDeliveries(on=True):
+    return ("record", bool(on))
+
+
+def WithDevice(dev):
+    return ("device", int(dev))
+
+
+class Engine:
+    """One batched simulation of N routers (see module docstring)."""
+
+    def __init__(self, router, num_nodes, num_topics, graph, subscriptions, *options,
+                 randomsub_size=0, app_score=None, ipv4=None, lib=None):
+        self.lib = load(lib)
+        opts = dict(options)
+        gsp = opts.get("gossipsub_params") or GossipSubParams()
+        score = opts.get("peer_score")
+        cfg = _abi.ConfigC()
+        cfg.router = router
+        cfg.randomsub_size = randomsub_size
+        cfg.num_nodes = num_nodes
+        cfg.num_topics = num_topics
+        cfg.slots_per_topic = opts.get("slots_per_topic", 1024)
+        cfg.seed = opts.get("seed", 1)
+        cfg.hop_ns = opts.get("hop_ns", 100 * Millisecond)
+        flags = 0
+        if score is not None:
+            flags |= _abi.GS_FLAG_SCORING
+        if opts.get("flood_publish"):
+            flags |= _abi.GS_FLAG_FLOOD_PUBLISH
+        if opts.get("record"):
+            flags |= _abi.GS_FLAG_RECORD_DELIVERIES
+        cfg.flags = flags
+        cfg.device = opts.get("device", 0)
+        self.N, self.T = num_nodes, num_topics
+        gsp_c = gsp.to_c()
+        psp_c = topics_c = scored_c = thr_c = None
+        if score is not None:
+            params, thresholds = score
+            psp_c = params.to_c()
+            topics_c, scored_c = params.topics_c(num_topics)
+            thr_c = thresholds.to_c()
+        h = C.c_void_p()
+        _check(self.lib, self.lib.gs_engine_create(
+            C.byref(cfg), C.byref(gsp_c),
+            C.byref(psp_c) if psp_c is not None else None,
+            topics_c, scored_c,
+            C.byref(thr_c) if thr_c is not None else None, None, C.byref(h)))
+        self.h = h
+        rowptr, col, outbound = graph
+        self.rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+        self.col = np.ascontiguousarray(col, dtype=np.int32)
+        self.E = int(self.rowptr[-1])
+        ob = np.ascontiguousarray(outbound, dtype=np.uint8) if outbound is not None else None
+        direct = opts.get("direct")
+        direct = np.ascontiguousarray(direct, dtype=np.uint8) if direct is not None else None
+        _check(self.lib, self.lib.gs_set_graph(h, _ptr(self.rowptr, C.c_int64), _ptr(self.col, C.c_int32),
+                                               _ptr(ob, C.c_uint8), _ptr(direct, C.c_uint8)))
+        subs = np.ascontiguousarray(subscriptions, dtype=np.uint64)
+        _check(self.lib, self.lib.gs_set_subscriptions(h, _ptr(subs, C.c_uint64)))
+        app = np.ascontiguousarray(app_score, dtype=np.float64) if app_score is not None else None
+        ips = np.ascontiguousarray(ipv4, dtype=np.uint32) if ipv4 is not None else None
+        if app is not None or ips is not None:
+            _check(self.lib, self.lib.gs_set_peer_attrs(h, _ptr(app, C.c_double), _ptr(ips, C.c_uint32)))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gs_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- driving
+    def publish(self, src, topic, hop):
+        src = np.ascontiguousarray(src, dtype=np.int32)
+        topic = np.ascontiguousarray(topic, dtype=np.int32)
+        hop = np.ascontiguousarray(hop, dtype=np.int64)
+        ids = np.empty(len(src), dtype=np.int64)
+        _check(self.lib, self.lib.gs_publish(self.h, len(src), _ptr(src, C.c_int32), _ptr(topic, C.c_int32),
+                                             _ptr(hop, C.c_int64), _ptr(ids, C.c_int64)))
+        return ids
+
+    def step(self, hops=1):
+        _check(self.lib, self.lib.gs_step(self.h, int(hops)))
+
+    def sync(self):
+        _check(self.lib, self.lib.gs_sync(self.h))
+
+    def set_topic_score_params(self, topic, p):
+        c = p.to_c()
+        _check(self.lib, self.lib.gs_set_topic_score_params(self.h, topic, C.byref(c)))
+
+    @property
+    def hop(self):
+        return int(self.lib.gs_current_hop(self.h))
+
+    # ---------------------------------------------------------------- readbacks
+    def counters(self):
+        c = _abi.CountersC()
+        _check(self.lib, self.lib.gs_read_counters(self.h, C.byref(c)))
+        return c.as_dict()
+
+    def scores(self):
+        a = np.empty(self.E, dtype=np.float64)
+        _check(self.lib, self.lib.gs_read_scores(self.h, _ptr(a, C.c_double)))
+        return a
+
+    def mesh(self):
+        a = np.empty(self.E, dtype=np.uint64)
+        _check(self.lib, self.lib.gs_read_mesh(self.h, _ptr(a, C.c_uint64)))
+        return a
+
+    def fanout(self):
+        a = np.empty(self.E, dtype=np.uint64)
+        _check(self.lib, self.lib.gs_read_fanout(self.h, _ptr(a, C.c_uint64)))
+        return a
+
+    def backoff(self):
+        a = np.empty(self.E * self.T, dtype=np.int64)
+        _check(self.lib, self.lib.gs_read_backoff(self.h, _ptr(a, C.c_int64)))
+        return a.reshape(self.T, self.E)
+
+    def topic_stats(self):
+        n = self.E * self.T
+        fmd, mmd, mfp, imd = (np.empty(n, dtype=np.float64) for _ in range(4))
+        mt, gt = np.empty(n, dtype=np.int64), np.empty(n, dtype=np.int64)
+        fl = np.empty(n, dtype=np.uint8)
+        _check(self.lib, self.lib.gs_read_topic_stats(
+            self.h, _ptr(fmd, C.c_double), _ptr(mmd, C.c_double), _ptr(mfp, C.c_double),
+            _ptr(imd, C.c_double), _ptr(mt, C.c_int64), _ptr(gt, C.c_int64), _ptr(fl, C.c_uint8)))
+        sh = (self.T, self.E)
+        return dict(fmd=fmd.reshape(sh), mmd=mmd.reshape(sh), mfp=mfp.reshape(sh), imd=imd.reshape(sh),
+                    mesh_time=mt.reshape(sh), graft_time=gt.reshape(sh), flags=fl.reshape(sh))
+
+    def behaviour_penalty(self):
+        a = np.empty(self.E, dtype=np.float64)
+        _check(self.lib, self.lib.gs_read_behaviour_penalty(self.h, _ptr(a, C.c_double)))
+        return a
+
+    def deliveries(self, msg_id):
+        hop = np.empty(self.N, dtype=np.int32)
+        frm = np.empty(self.N, dtype=np.int32)
+        _check(self.lib, self.lib.gs_read_deliveries(self.h, int(msg_id), _ptr(hop, C.c_int32),
+                                                     _ptr(frm, C.c_int32)))
+        return hop, frm
+
+
+def NewFloodSub(num_nodes, num_topics, graph, subscriptions, *options, **kw):
+    """floodsub.go:25-27 (batched)."""
+    return Engine(_abi.GS_ROUTER_FLOODSUB, num_nodes, num_topics, graph, subscriptions, *options, **kw)
+
+
+def NewRandomSub(num_nodes, num_topics, graph, subscriptions, size, *options, **kw):
+    """randomsub.go:21-27 (batched)."""
+    return Engine(_abi.GS_ROUTER_RANDOMSUB, num_nodes, num_topics, graph, subscriptions, *options,
+                  randomsub_size=size, **kw)
+
+
+def NewGossipSub(num_nodes, num_topics, graph, subscriptions, *options, **kw):
+    """gossipsub.go:198-222 (batched)."""
+    return Engine(_abi.GS_ROUTER_GOSSIPSUB, num_nodes, num_topics, graph, subscriptions, *options, **kw)

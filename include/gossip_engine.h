@@ -1,0 +1,266 @@
+/*
+ * gossip_engine.h — C-ABI of the MI355X batched gossip engine.
+ *
+ * One engine handle simulates N go-libp2p-pubsub routers in lock step over a
+ * static peer graph.  It is the drop-in boundary for the router hot path of
+ * the reference (seveirbian/go-libp2p-pubsub, mounted at /root/reference):
+ *
+ *   PubSubRouter interface           pubsub.go:158-187
+ *   FloodSubRouter.Publish           floodsub.go:76-100
+ *   RandomSubRouter.Publish          randomsub.go:99-160
+ *   GossipSubRouter (Publish, HandleRPC, heartbeat, emitGossip, Join)
+ *                                    gossipsub.go:591-1078, 1299-1712
+ *   MessageCache                     mcache.go:23-104
+ *   peerScore (score, refreshScores, delivery hooks)
+ *                                    score.go:256-964
+ *   gossipTracer promises            gossip_tracer.go:48-126
+ *
+ * Every entry point takes plain host pointers and sizes (the caller owns all
+ * host arrays; they are copied in and out).  The engine owns device memory.
+ * Return value: GS_OK (0) or a negative GS_E* code; gs_last_error() returns a
+ * thread-local message for the most recent failure.  A handle must not be
+ * used concurrently (mirrors the single processLoop goroutine, pubsub.go:471).
+ *
+ * Durations are int64 nanoseconds (Go time.Duration).  Peers are int32 node
+ * indices, topics are int32 indices in [0, num_topics), messages are int64
+ * ids assigned by gs_publish in publish order.
+ *
+ * Two libraries export this ABI:
+ *   libgossip_engine.so  — the product: HIP kernels for gfx950 (MI355X).
+ *   oracle/_build/libgossip_oracle.so — the CPU restatement used ONLY by
+ *                          tests/bench as the parity checker.
+ */
+#ifndef GOSSIP_ENGINE_H
+#define GOSSIP_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GS_ABI_VERSION 1
+
+/* ---- error codes ------------------------------------------------------- */
+#define GS_OK 0
+#define GS_EINVAL (-1)       /* invalid argument / parameter validation failed */
+#define GS_ESTATE (-2)       /* call not valid in the engine's current state */
+#define GS_ENOMEM (-3)       /* host or device allocation failed */
+#define GS_EDEVICE (-4)      /* HIP runtime error / no device */
+#define GS_ECAPACITY (-5)    /* a bounded table or the message window overflowed */
+#define GS_EUNSUPPORTED (-6) /* configuration outside what this build supports */
+
+/* ---- router selection (NewFloodSub / NewRandomSub / NewGossipSub) ------ */
+#define GS_ROUTER_FLOODSUB 0  /* floodsub.go:25  */
+#define GS_ROUTER_RANDOMSUB 1 /* randomsub.go:21 */
+#define GS_ROUTER_GOSSIPSUB 2 /* gossipsub.go:198 */
+
+/* ---- engine flags ------------------------------------------------------ */
+#define GS_FLAG_SCORING (1u << 0)       /* WithPeerScore (gossipsub.go:258)    */
+#define GS_FLAG_FLOOD_PUBLISH (1u << 1) /* WithFloodPublish (gossipsub.go:304) */
+#define GS_FLAG_RECORD_DELIVERIES (1u << 2) /* keep per-(node,message) first
+                                               delivery hop/sender for readback */
+
+/* GossipSubParams — gossipsub.go:62-195, defaults gossipsub.go:226-255. */
+typedef struct gs_gossipsub_params {
+  int32_t D, Dlo, Dhi, Dscore, Dout;
+  int32_t HistoryLength, HistoryGossip;
+  int32_t Dlazy;
+  double GossipFactor;
+  int32_t GossipRetransmission;
+  int64_t HeartbeatInitialDelay;
+  int64_t HeartbeatInterval;
+  int64_t FanoutTTL;
+  int32_t PrunePeers;
+  int64_t PruneBackoff;
+  int32_t Connectors;
+  int32_t MaxPendingConnections;
+  int64_t ConnectionTimeout;
+  uint64_t DirectConnectTicks;
+  int64_t DirectConnectInitialDelay;
+  uint64_t OpportunisticGraftTicks;
+  int32_t OpportunisticGraftPeers;
+  int64_t GraftFloodThreshold;
+  int32_t MaxIHaveLength;
+  int32_t MaxIHaveMessages;
+  int64_t IWantFollowupTime;
+} gs_gossipsub_params;
+
+/* PeerScoreParams — score_params.go:53-96.  AppSpecificScore (a Go func) is
+ * replaced by a per-node array given to gs_set_peer_attrs; the flag below
+ * says whether that function "is set" for validation (score_params.go:165). */
+typedef struct gs_peer_score_params {
+  double TopicScoreCap;
+  int32_t AppSpecificScorePresent;
+  double AppSpecificWeight;
+  double IPColocationFactorWeight;
+  int32_t IPColocationFactorThreshold;
+  double BehaviourPenaltyWeight;
+  double BehaviourPenaltyThreshold;
+  double BehaviourPenaltyDecay;
+  int64_t DecayInterval;
+  double DecayToZero;
+  int64_t RetainScore;
+} gs_peer_score_params;
+
+/* TopicScoreParams — score_params.go:98-148. */
+typedef struct gs_topic_score_params {
+  double TopicWeight;
+  double TimeInMeshWeight;
+  int64_t TimeInMeshQuantum;
+  double TimeInMeshCap;
+  double FirstMessageDeliveriesWeight;
+  double FirstMessageDeliveriesDecay;
+  double FirstMessageDeliveriesCap;
+  double MeshMessageDeliveriesWeight;
+  double MeshMessageDeliveriesDecay;
+  double MeshMessageDeliveriesCap;
+  double MeshMessageDeliveriesThreshold;
+  int64_t MeshMessageDeliveriesWindow;
+  int64_t MeshMessageDeliveriesActivation;
+  double MeshFailurePenaltyWeight;
+  double MeshFailurePenaltyDecay;
+  double InvalidMessageDeliveriesWeight;
+  double InvalidMessageDeliveriesDecay;
+} gs_topic_score_params;
+
+/* PeerScoreThresholds — score_params.go:12-32. */
+typedef struct gs_peer_score_thresholds {
+  double GossipThreshold;
+  double PublishThreshold;
+  double GraylistThreshold;
+  double AcceptPXThreshold;
+  double OpportunisticGraftThreshold;
+} gs_peer_score_thresholds;
+
+/* PeerGaterParams — peer_gater.go:31-55 (TopicDeliveryWeights omitted). */
+typedef struct gs_peer_gater_params {
+  double Threshold;
+  double GlobalDecay;
+  double SourceDecay;
+  int64_t DecayInterval;
+  double DecayToZero;
+  int64_t RetainStats;
+  int64_t Quiet;
+  double DuplicateWeight;
+  double IgnoreWeight;
+  double RejectWeight;
+} gs_peer_gater_params;
+
+/* Engine configuration (not a reference struct: the simulator's own knobs). */
+typedef struct gs_config {
+  int32_t router;          /* GS_ROUTER_* */
+  int32_t randomsub_size;  /* NewRandomSub(size) */
+  int32_t num_nodes;       /* N */
+  int32_t num_topics;      /* T, 1..64 */
+  int32_t slots_per_topic; /* message window per topic, multiple of 64 */
+  uint32_t seed;           /* counter-based RNG seed (replaces math/rand) */
+  int64_t hop_ns;          /* virtual time per propagation hop */
+  uint32_t flags;          /* GS_FLAG_* */
+  int32_t device;          /* HIP device ordinal (product library only) */
+} gs_config;
+
+/* Aggregate counters since create (read with gs_read_counters). */
+typedef struct gs_counters {
+  int64_t hops;
+  int64_t heartbeats;
+  int64_t published;       /* local publishes (PublishMessage)               */
+  int64_t deliveries;      /* first deliveries (DeliverMessage)              */
+  int64_t duplicates;      /* duplicate receptions (DuplicateMessage)        */
+  int64_t transmissions;   /* message copies sent over edges, dups included */
+  int64_t grafts_sent;     /* GRAFT control entries sent                     */
+  int64_t prunes_sent;     /* PRUNE control entries sent                     */
+  int64_t ihave_sent;      /* IHAVE control entries sent (one per topic)     */
+  int64_t iwant_sent;      /* message ids requested through IWANT            */
+  int64_t iwant_served;    /* messages served in response to IWANT           */
+  int64_t promises_broken; /* broken IWANT promises turned into P7 penalties */
+  int64_t graylisted;      /* RPCs dropped by AcceptFrom == AcceptNone       */
+  int64_t reserved[3];
+} gs_counters;
+
+/* ---- defaults / helpers ------------------------------------------------ */
+int gs_abi_version(void);
+const char* gs_last_error(void);
+void gs_default_gossipsub_params(gs_gossipsub_params* out); /* gossipsub.go:226 */
+void gs_default_peer_gater_params(gs_peer_gater_params* out); /* peer_gater.go:114 */
+/* ScoreParameterDecayWithBase — score_params.go:282-287. */
+double gs_score_parameter_decay_with_base(int64_t decay, int64_t base, double decay_to_zero);
+double gs_score_parameter_decay(int64_t decay); /* score_params.go:277 */
+/* validate() — score_params.go:34-51, 151-198, 200-268; peer_gater.go:57-88. */
+int gs_validate_thresholds(const gs_peer_score_thresholds* p);
+int gs_validate_peer_score_params(const gs_peer_score_params* p,
+                                  const gs_topic_score_params* topics,
+                                  const uint8_t* topic_scored, int32_t num_topics);
+int gs_validate_topic_score_params(const gs_topic_score_params* p);
+int gs_validate_peer_gater_params(const gs_peer_gater_params* p);
+
+/* ---- engine lifecycle -------------------------------------------------- */
+typedef struct gs_engine gs_engine;
+
+/* Creates the engine.  gossipsub/score/threshold/gater params may be NULL
+ * when unused by the router.  topics[T] and topic_scored[T] give the
+ * PeerScoreParams.Topics map (topic_scored[t] != 0 <=> key present). */
+int gs_engine_create(const gs_config* cfg, const gs_gossipsub_params* gsp,
+                     const gs_peer_score_params* psp,
+                     const gs_topic_score_params* topics,
+                     const uint8_t* topic_scored,
+                     const gs_peer_score_thresholds* thr,
+                     const gs_peer_gater_params* gater, gs_engine** out);
+int gs_engine_destroy(gs_engine* eng);
+
+/* Static symmetric graph in CSR: neighbours of node u are col[rowptr[u] ..
+ * rowptr[u+1]), strictly ascending, each edge present in both directions.
+ * outbound[e] != 0: u dialed col[e] (AddPeer direction, gossipsub.go:505-532).
+ * direct[e]   != 0: col[e] is a direct peer of u (WithDirectPeers).  NULL = 0. */
+int gs_set_graph(gs_engine* eng, const int64_t* rowptr, const int32_t* col,
+                 const uint8_t* outbound, const uint8_t* direct);
+/* Topic subscriptions (bit t of sub_mask[u]): Join(t) at hop 0. */
+int gs_set_subscriptions(gs_engine* eng, const uint64_t* sub_mask);
+/* Per-node attributes: app_score[N] (P5, AppSpecificScore), ipv4[N] (P6),
+ * either may be NULL (zeros). */
+int gs_set_peer_attrs(gs_engine* eng, const double* app_score, const uint32_t* ipv4);
+/* IPColocationFactorWhitelist as IPv4 (net, mask) pairs. */
+int gs_set_ip_whitelist(gs_engine* eng, int32_t n, const uint32_t* net, const uint32_t* mask);
+
+/* Schedules n local publishes (Topic.Publish at node src[i] at hop hop[i]).
+ * hop[] must be non-decreasing and >= the engine's current hop.  Message ids
+ * are assigned in call order and written to ids_out (may be NULL). */
+int gs_publish(gs_engine* eng, int32_t n, const int32_t* src, const int32_t* topic,
+               const int64_t* hop, int64_t* ids_out);
+
+/* Advances the simulation by `hops` lock-step hops. */
+int gs_step(gs_engine* eng, int64_t hops);
+/* Waits for all queued device work (no-op on the oracle). */
+int gs_sync(gs_engine* eng);
+
+/* Replaces topic score params at the current time (Topic.SetScoreParams ->
+ * peerScore.SetTopicScoreParams, score.go:192-232, including the recap). */
+int gs_set_topic_score_params(gs_engine* eng, int32_t topic, const gs_topic_score_params* p);
+
+/* ---- readbacks (host arrays sized by the caller) ----------------------- */
+int64_t gs_num_edges(const gs_engine* eng);
+int64_t gs_current_hop(const gs_engine* eng);
+int gs_read_counters(gs_engine* eng, gs_counters* out);
+/* Score(p) for every edge (observer u, neighbour col[e]) at the current state. */
+int gs_read_scores(gs_engine* eng, double* score /*[E]*/);
+/* mesh / fanout topic masks per edge (bit t: col[e] in mesh[t] of u). */
+int gs_read_mesh(gs_engine* eng, uint64_t* mesh /*[E]*/);
+int gs_read_fanout(gs_engine* eng, uint64_t* fanout /*[E]*/);
+/* backoff expiry (ns) per [t*E + e]; 0 = no backoff entry. */
+int gs_read_backoff(gs_engine* eng, int64_t* expire /*[T*E]*/);
+/* peerStats topic counters per [t*E + e]; flags bit0 inMesh, bit1 P3 active. */
+int gs_read_topic_stats(gs_engine* eng, double* fmd, double* mmd, double* mfp,
+                        double* imd, int64_t* mesh_time, int64_t* graft_time,
+                        uint8_t* flags);
+int gs_read_behaviour_penalty(gs_engine* eng, double* bp /*[E]*/);
+/* Per node: hop of first delivery of message `id` (-1: never) and the node it
+ * was first received from (-1: origin or never).  Valid while the message's
+ * slot has not been recycled. */
+int gs_read_deliveries(gs_engine* eng, int64_t id, int32_t* hop /*[N]*/,
+                       int32_t* from /*[N]*/);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GOSSIP_ENGINE_H */

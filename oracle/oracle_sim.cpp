@@ -1,0 +1,1032 @@
+// oracle_sim.cpp — TEST INFRASTRUCTURE ONLY (parity checker, never shipped).
+//
+// Lock-step CPU restatement of N go-libp2p-pubsub routers exchanging RPCs
+// over a static graph; exports include/gossip_engine.h so tests drive the
+// oracle and the HIP engine through identical calls.  Per-node code follows
+// the reference line by line (citations inline).  The round schedule
+// (DESIGN.md "Canonical round") is:
+//   hop h, now = h*hop_ns:
+//     [h==0] Join(t) for every subscribed topic (gossipsub.go:1011-1060)
+//     score memo S0 of every neighbour (used by AcceptFrom and Publish filters)
+//     local publishes of hop h (topic.go:207 -> publishMessage, pubsub.go:1056)
+//     phase A: every node handles the payload messages of the RPCs sent to it
+//              in hop h-1, senders ascending, RPCs in send order
+//              (handleIncomingRPC pubsub.go:902-967, pushMsg :978-1022)
+//     phase B: every node handles the control of those RPCs, per RPC, senders
+//              ascending (HandleRPC gossipsub.go:591-608)
+//     refreshScores if a DecayInterval tick falls on `now` (score.go:495)
+//     heartbeat if a heartbeat tick falls on `now` (gossipsub.go:1299-1552)
+//   RPCs produced during hop h are delivered in hop h+1.
+#include <algorithm>
+#include <cstdio>
+#include <memory>
+#include <unordered_map>
+
+#include "oracle_core.hpp"
+
+namespace oracle {
+
+static thread_local std::string g_err;
+void set_error(const std::string& s) { g_err = s; }
+
+struct IHaveEntry { int topic; std::vector<int64_t> mids; };
+struct PruneEntry { int topic; uint64_t backoff; bool hasBackoff; };
+struct Control {
+  std::vector<IHaveEntry> ihave;
+  std::vector<int64_t> iwant;
+  std::vector<int> graft;
+  std::vector<PruneEntry> prune;
+};
+struct RPC {
+  std::vector<int64_t> publish;
+  bool hasCtl = false;
+  Control ctl;
+};
+
+struct Sim;
+
+struct Node {
+  Sim* sim = nullptr;
+  int id = 0;
+  std::vector<int> nbrs;                 // ascending
+  std::map<int, bool> outbound;          // gs.outbound
+  std::set<int> direct;                  // gs.direct
+  std::map<int, std::set<int>> topics;   // p.topics (static subscriptions of peers)
+  uint64_t mySubs = 0;                   // p.mySubs
+  std::set<int64_t> seen;                // p.seenMessages (timecache, no expiry in-window)
+  // gossipsub router state — gossipsub.go:400-457
+  std::map<int, std::set<int>> mesh, fanout;
+  std::map<int, int64_t> lastpub;
+  std::map<int, std::vector<IHaveEntry>> gossip;  // pending gossip (gs.gossip)
+  std::map<int, int> peerhave, iasked;
+  std::map<int, std::map<int, int64_t>> backoff;
+  MessageCache mcache;
+  PeerScore score;
+  GossipTracer gtracer;
+  uint64_t heartbeatTicks = 0;
+  std::map<int, double> memo;            // S0: hop-start score snapshot
+  std::map<int, std::vector<RPC>> out;   // RPCs sent during this hop, per destination
+  std::map<int, int> acceptStatus;       // AcceptFrom result per sender this hop
+
+  double Score(int p);                   // gs.score.Score (0 when scoring is off)
+  void sendRPC(int p, RPC rpc);
+  void localPublish(const Msg& m);
+  void handleMessage(int from, const Msg& m);
+  void routerPublish(const Msg& m, int from);
+  void gsPublish(const Msg& m, int from);
+  std::vector<int> getPeers(int topic, int count, int site, const std::function<bool(int)>& filter);
+  void join(int topic);
+  void handleRPC(int from, const Control& ctl);
+  std::vector<int64_t> handleIHave(int p, const Control& ctl);
+  std::vector<int64_t> handleIWant(int p, const Control& ctl);
+  std::vector<PruneEntry> handleGraft(int p, const Control& ctl);
+  void handlePrune(int p, const Control& ctl);
+  void addBackoff(int p, int topic);
+  void doAddBackoff(int p, int topic, int64_t interval);
+  PruneEntry makePrune(int p, int topic);
+  void heartbeat();
+  void emitGossip(int topic, const std::set<int>& exclude);
+  void applyIwantPenalties();
+  void clearBackoff();
+};
+
+struct Sim {
+  gs_config cfg{};
+  gs_gossipsub_params gp{};
+  gs_peer_score_params sp{};
+  std::vector<gs_topic_score_params> tparams;
+  std::vector<uint8_t> tscored;
+  gs_peer_score_thresholds thr{};
+  bool scoring = false, floodPublish = false, record = false;
+  int N = 0, T = 0;
+  int64_t E = 0;
+  std::vector<int64_t> rowptr;
+  std::vector<int32_t> col;
+  std::vector<uint8_t> outboundE, directE;
+  std::vector<uint64_t> subs;
+  std::vector<double> appScore;
+  std::vector<uint32_t> ipv4;
+  std::vector<std::pair<uint32_t, uint32_t>> whitelist;
+  std::vector<Node> nodes;
+  bool graphSet = false, started = false;
+  int64_t hop = 0;
+  // messages
+  std::vector<Msg> msgs;           // by id
+  std::vector<int64_t> msgHop;     // scheduled publish hop
+  size_t nextPub = 0;
+  std::vector<std::unordered_map<int64_t, std::pair<int32_t, int32_t>>> deliv;  // per node
+  gs_counters ctr{};
+  int64_t now() const { return hop * cfg.hop_ns; }
+
+  int edgeIndex(int u, int v) const {
+    auto b = col.begin() + rowptr[u], e = col.begin() + rowptr[u + 1];
+    auto it = std::lower_bound(b, e, v);
+    if (it == e || *it != v) return -1;
+    return (int)(it - col.begin());
+  }
+  bool heartbeatDue(int64_t t) const {
+    if (cfg.router != GS_ROUTER_GOSSIPSUB) return false;
+    if (t < gp.HeartbeatInitialDelay) return false;
+    return (t - gp.HeartbeatInitialDelay) % gp.HeartbeatInterval == 0;
+  }
+  bool refreshDue(int64_t t) const { return scoring && t > 0 && t % sp.DecayInterval == 0; }
+  void start();
+  void step();
+};
+
+double Node::Score(int p) { return sim->scoring ? score.score(p) : 0.0; }
+
+// sendRPC / doSendRPC — gossipsub.go:1092-1156 (queues never drop in the
+// simulator; pending gossip is piggybacked exactly as sendRPC does).
+void Node::sendRPC(int p, RPC rpc) {
+  auto g = gossip.find(p);
+  if (g != gossip.end()) {  // piggybackGossip gossipsub.go:1736-1744
+    rpc.hasCtl = true;
+    rpc.ctl.ihave = g->second;
+    gossip.erase(g);
+  }
+  sim->ctr.transmissions += (int64_t)rpc.publish.size();
+  sim->ctr.grafts_sent += (int64_t)rpc.ctl.graft.size();
+  sim->ctr.prunes_sent += (int64_t)rpc.ctl.prune.size();
+  sim->ctr.ihave_sent += (int64_t)rpc.ctl.ihave.size();
+  sim->ctr.iwant_sent += (int64_t)rpc.ctl.iwant.size();
+  out[p].push_back(std::move(rpc));
+}
+
+// getPeers — gossipsub.go:1841-1861 with the keyed shuffle (gs_rng.h).
+std::vector<int> Node::getPeers(int topic, int count, int site, const std::function<bool(int)>& filter) {
+  auto tm = topics.find(topic);
+  if (tm == topics.end()) return {};
+  std::vector<std::pair<uint64_t, int>> peers;
+  for (int p : tm->second)  // all peers speak gossipsub (GossipSubFeatureMesh)
+    if (filter(p))
+      peers.push_back({gs_key64(sim->cfg.seed, site, id, (uint32_t)sim->hop, p, topic), p});
+  std::sort(peers.begin(), peers.end());
+  std::vector<int> res;
+  for (auto& kp : peers) res.push_back(kp.second);
+  if (count > 0 && (int)res.size() > count) res.resize(count);
+  return res;
+}
+
+// Join — gossipsub.go:1011-1060 (router); floodsub/randomsub Join only trace.
+void Node::join(int topic) {
+  if (sim->cfg.router != GS_ROUTER_GOSSIPSUB) return;
+  if (mesh.count(topic)) return;
+  std::set<int> gmap;
+  auto fo = fanout.find(topic);
+  if (fo != fanout.end()) {
+    gmap = fo->second;
+    for (auto it = gmap.begin(); it != gmap.end();) {
+      if (Score(*it) < 0) it = gmap.erase(it); else ++it;
+    }
+    if ((int)gmap.size() < sim->gp.D) {
+      auto more = getPeers(topic, sim->gp.D - (int)gmap.size(), GS_SITE_GP_JOIN, [&](int p) {
+        return !gmap.count(p) && !direct.count(p) && Score(p) >= 0;
+      });
+      for (int p : more) gmap.insert(p);
+    }
+    fanout.erase(topic);
+    lastpub.erase(topic);
+  } else {
+    auto peers = getPeers(topic, sim->gp.D, GS_SITE_GP_JOIN, [&](int p) {
+      return !direct.count(p) && Score(p) >= 0;
+    });
+    gmap.insert(peers.begin(), peers.end());
+  }
+  mesh[topic] = gmap;
+  for (int p : gmap) {
+    if (sim->scoring) score.Graft(p, topic, sim->now());  // tracer.Graft
+    RPC r; r.hasCtl = true; r.ctl.graft.push_back(topic);  // sendGraft gossipsub.go:1080
+    sendRPC(p, std::move(r));
+  }
+}
+
+// Topic.Publish -> PushLocal -> validate(sync) -> markSeen -> publishMessage
+// (topic.go:207-245, validation.go:216-226, pubsub.go:1056-1060).  Raw tracers
+// skip self-originated messages (trace.go:89,101,132,162).
+void Node::localPublish(const Msg& m) {
+  seen.insert(m.id);
+  sim->ctr.published++;
+  if (sim->record) sim->deliv[id][m.id] = {(int32_t)sim->hop, -1};
+  routerPublish(m, id);
+}
+
+// pushMsg — pubsub.go:978-1022 with instantaneous accept (no validators, no
+// signature: validation.go:230-243 returns true), then publishMessage.
+void Node::handleMessage(int from, const Msg& m) {
+  if (!((mySubs >> m.topic) & 1)) return;  // subscribedToMsg / canRelayMsg (pubsub.go:959)
+  if (m.from == id && from != id) {         // self-origin rejection (pubsub.go:1001-1006)
+    if (sim->scoring) score.RejectMessage(m, from, RejectSelfOrigin, sim->now());
+    return;
+  }
+  if (seen.count(m.id)) {                   // duplicate (pubsub.go:1010-1013)
+    sim->ctr.duplicates++;
+    if (sim->scoring) score.DuplicateMessage(m, from, sim->now());
+    return;
+  }
+  seen.insert(m.id);                        // markSeen
+  sim->ctr.deliveries++;
+  if (sim->record) sim->deliv[id][m.id] = {(int32_t)sim->hop, from};
+  if (sim->scoring) {                       // tracer.DeliverMessage -> raw tracers
+    score.DeliverMessage(m, from, sim->now());
+    gtracer.DeliverMessage(m.id);
+  }
+  routerPublish(m, from);
+}
+
+void Node::routerPublish(const Msg& m, int from) {
+  const int router = sim->cfg.router;
+  if (router == GS_ROUTER_FLOODSUB) {  // FloodSubRouter.Publish floodsub.go:76-100
+    auto tm = topics.find(m.topic);
+    if (tm == topics.end()) return;
+    for (int pid : tm->second) {
+      if (pid == from || pid == m.from) continue;
+      RPC r; r.publish.push_back(m.id);
+      sendRPC(pid, std::move(r));
+    }
+    return;
+  }
+  if (router == GS_ROUTER_RANDOMSUB) {  // RandomSubRouter.Publish randomsub.go:99-160
+    auto tm = topics.find(m.topic);
+    if (tm == topics.end()) return;
+    std::set<int> tosend;
+    std::vector<int> rspeers;  // every peer speaks randomsub in this engine
+    for (int p : tm->second) {
+      if (p == from || p == m.from) continue;
+      rspeers.push_back(p);
+    }
+    const int RandomSubD = 6;  // randomsub.go:17
+    if ((int)rspeers.size() > RandomSubD) {
+      int target = RandomSubD;
+      int sq = (int)std::ceil(std::sqrt((double)sim->cfg.randomsub_size));
+      if (sq > target) target = sq;
+      if (target > (int)rspeers.size()) target = (int)rspeers.size();
+      std::vector<std::pair<uint64_t, int>> keyed;
+      for (int p : rspeers)
+        keyed.push_back({gs_key64(sim->cfg.seed, GS_SITE_RANDOMSUB, id, (uint32_t)m.id, p, 0), p});
+      std::sort(keyed.begin(), keyed.end());
+      for (int i = 0; i < target; ++i) tosend.insert(keyed[i].second);
+    } else {
+      tosend.insert(rspeers.begin(), rspeers.end());
+    }
+    for (int p : tosend) {
+      RPC r; r.publish.push_back(m.id);
+      sendRPC(p, std::move(r));
+    }
+    return;
+  }
+  gsPublish(m, from);
+}
+
+// GossipSubRouter.Publish — gossipsub.go:939-1009.  Score filters read the
+// hop-start memo S0 (forwarding decisions inside a hop).
+void Node::gsPublish(const Msg& m, int from) {
+  mcache.Put(m);
+  int topic = m.topic;
+  std::set<int> tosend;
+  auto tm = topics.find(topic);
+  if (tm == topics.end()) return;
+  auto s0 = [&](int p) { return sim->scoring ? memo[p] : 0.0; };
+  if (sim->floodPublish && from == id) {
+    for (int p : tm->second)
+      if (direct.count(p) || s0(p) >= sim->thr.PublishThreshold) tosend.insert(p);
+  } else {
+    for (int p : direct)
+      if (tm->second.count(p)) tosend.insert(p);
+    // floodsub peers: none (every peer speaks gossipsub in this engine)
+    auto gm = mesh.find(topic);
+    std::set<int> gmap;
+    if (gm == mesh.end()) {
+      auto fo = fanout.find(topic);
+      if (fo == fanout.end() || fo->second.empty()) {
+        auto peers = getPeers(topic, sim->gp.D, GS_SITE_GP_FANOUT_PUB, [&](int p) {
+          return !direct.count(p) && s0(p) >= sim->thr.PublishThreshold;
+        });
+        if (!peers.empty()) fanout[topic] = std::set<int>(peers.begin(), peers.end());
+      }
+      fo = fanout.find(topic);
+      if (fo != fanout.end()) gmap = fo->second;
+      lastpub[topic] = sim->now();
+    } else {
+      gmap = gm->second;
+    }
+    tosend.insert(gmap.begin(), gmap.end());
+  }
+  for (int pid : tosend) {
+    if (pid == from || pid == m.from) continue;
+    RPC r; r.publish.push_back(m.id);
+    sendRPC(pid, std::move(r));
+  }
+}
+
+// HandleRPC — gossipsub.go:591-608 (one call per control-carrying RPC).
+void Node::handleRPC(int from, const Control& ctl) {
+  auto iwant = handleIHave(from, ctl);
+  auto ihave = handleIWant(from, ctl);
+  auto prune = handleGraft(from, ctl);
+  handlePrune(from, ctl);
+  if (iwant.empty() && ihave.empty() && prune.empty()) return;
+  RPC r;
+  r.hasCtl = true;
+  r.publish = ihave;
+  if (!iwant.empty()) r.ctl.iwant = iwant;
+  r.ctl.prune = prune;
+  sim->ctr.iwant_served += (int64_t)ihave.size();
+  sendRPC(from, std::move(r));
+}
+
+// handleIHave — gossipsub.go:610-672.  The iwant set is shuffled by key
+// (GS_SITE_IWANT) and the promise taken on the first element (the uniform
+// rand.Intn(len) pick of gossip_tracer.go:53 on a uniformly shuffled list).
+std::vector<int64_t> Node::handleIHave(int p, const Control& ctl) {
+  double sc = Score(p);
+  if (sc < sim->thr.GossipThreshold) return {};
+  peerhave[p]++;
+  if (peerhave[p] > sim->gp.MaxIHaveMessages) return {};
+  if (iasked[p] >= sim->gp.MaxIHaveLength) return {};
+  std::set<int64_t> iwant;
+  for (const IHaveEntry& ih : ctl.ihave) {
+    if (!mesh.count(ih.topic)) continue;
+    for (int64_t mid : ih.mids) {
+      if (seen.count(mid)) continue;
+      iwant.insert(mid);
+    }
+  }
+  if (iwant.empty()) return {};
+  int iask = (int)iwant.size();
+  if (iask + iasked[p] > sim->gp.MaxIHaveLength) iask = sim->gp.MaxIHaveLength - iasked[p];
+  std::vector<std::pair<uint64_t, int64_t>> keyed;
+  for (int64_t mid : iwant)
+    keyed.push_back({gs_key64(sim->cfg.seed, GS_SITE_IWANT, id, p, (uint32_t)mid, (uint32_t)sim->hop), mid});
+  std::sort(keyed.begin(), keyed.end());
+  std::vector<int64_t> lst;
+  for (int i = 0; i < iask; ++i) lst.push_back(keyed[i].second);
+  iasked[p] += iask;
+  if (sim->scoring) gtracer.AddPromise(p, lst, 0, sim->now());
+  return lst;
+}
+
+// handleIWant — gossipsub.go:674-711 (served in ascending message id).
+std::vector<int64_t> Node::handleIWant(int p, const Control& ctl) {
+  double sc = Score(p);
+  if (sc < sim->thr.GossipThreshold) return {};
+  std::set<int64_t> ihave;
+  for (int64_t mid : ctl.iwant) {
+    int count = 0;
+    if (!mcache.GetForPeer(mid, p, nullptr, &count)) continue;
+    if (count > sim->gp.GossipRetransmission) continue;
+    ihave.insert(mid);
+  }
+  return std::vector<int64_t>(ihave.begin(), ihave.end());
+}
+
+// handleGraft — gossipsub.go:713-804 (no PX records are produced: doPX off).
+std::vector<PruneEntry> Node::handleGraft(int p, const Control& ctl) {
+  std::vector<int> prune;
+  double sc = Score(p);
+  int64_t now = sim->now();
+  for (int topic : ctl.graft) {
+    auto pm = mesh.find(topic);
+    if (pm == mesh.end()) continue;
+    std::set<int>& peers = pm->second;
+    if (peers.count(p)) continue;
+    if (direct.count(p)) { prune.push_back(topic); continue; }
+    auto bt = backoff.find(topic);
+    if (bt != backoff.end()) {
+      auto be = bt->second.find(p);
+      if (be != bt->second.end() && now < be->second) {
+        if (sim->scoring) score.AddPenalty(p, 1);
+        int64_t floodCutoff = be->second + (sim->gp.GraftFloodThreshold - sim->gp.PruneBackoff);
+        if (now < floodCutoff && sim->scoring) score.AddPenalty(p, 1);
+        addBackoff(p, topic);
+        prune.push_back(topic);
+        continue;
+      }
+    }
+    if (sc < 0) { prune.push_back(topic); addBackoff(p, topic); continue; }
+    if ((int)peers.size() >= sim->gp.Dhi && !outbound[p]) {
+      prune.push_back(topic);
+      addBackoff(p, topic);
+      continue;
+    }
+    if (sim->scoring) score.Graft(p, topic, now);
+    peers.insert(p);
+  }
+  std::vector<PruneEntry> res;
+  for (int t : prune) res.push_back(makePrune(p, t));
+  return res;
+}
+
+// handlePrune — gossipsub.go:806-838 (PX ignored: no peer records).
+void Node::handlePrune(int p, const Control& ctl) {
+  for (const PruneEntry& pr : ctl.prune) {
+    auto pm = mesh.find(pr.topic);
+    if (pm == mesh.end()) continue;
+    if (sim->scoring) score.Prune(p, pr.topic);
+    pm->second.erase(p);
+    if (pr.hasBackoff && pr.backoff > 0)
+      doAddBackoff(p, pr.topic, (int64_t)pr.backoff * kSecond);
+    else
+      addBackoff(p, pr.topic);
+  }
+}
+
+void Node::addBackoff(int p, int topic) { doAddBackoff(p, topic, sim->gp.PruneBackoff); }  // :840
+void Node::doAddBackoff(int p, int topic, int64_t interval) {  // :844-854
+  auto& b = backoff[topic];
+  int64_t expire = sim->now() + interval;
+  auto it = b.find(p);
+  int64_t cur = it == b.end() ? kTimeZero : it->second;
+  if (cur < expire) b[p] = expire;
+}
+// makePrune — gossipsub.go:1803-1839 (v1.1 peers: backoff in whole seconds)
+PruneEntry Node::makePrune(int p, int topic) {
+  (void)p;
+  PruneEntry e;
+  e.topic = topic;
+  e.hasBackoff = true;
+  e.backoff = (uint64_t)(sim->gp.PruneBackoff / kSecond);
+  return e;
+}
+
+// clearBackoff — gossipsub.go:1573-1592 (slack uses the package var, 1s)
+void Node::clearBackoff() {
+  if (heartbeatTicks % 15 != 0) return;
+  int64_t now = sim->now();
+  for (auto it = backoff.begin(); it != backoff.end();) {
+    for (auto jt = it->second.begin(); jt != it->second.end();) {
+      if (jt->second + 2 * kSecond < now) jt = it->second.erase(jt); else ++jt;
+    }
+    if (it->second.empty()) it = backoff.erase(it); else ++it;
+  }
+}
+
+void Node::applyIwantPenalties() {  // gossipsub.go:1566-1571
+  if (!sim->scoring) return;
+  auto broken = gtracer.GetBrokenPromises(sim->now());
+  for (auto& kv : broken) {
+    score.AddPenalty(kv.first, kv.second);
+    sim->ctr.promises_broken += kv.second;
+  }
+}
+
+// emitGossip — gossipsub.go:1658-1712
+void Node::emitGossip(int topic, const std::set<int>& exclude) {
+  std::vector<int64_t> mids = mcache.GetGossipIDs(topic);
+  if (mids.empty()) return;
+  std::vector<int> peers;
+  auto tm = topics.find(topic);
+  if (tm != topics.end())
+    for (int p : tm->second)
+      if (!exclude.count(p) && !direct.count(p) && Score(p) >= sim->thr.GossipThreshold) peers.push_back(p);
+  int target = sim->gp.Dlazy;
+  int factor = (int)(sim->gp.GossipFactor * (double)peers.size());
+  if (factor > target) target = factor;
+  if (target > (int)peers.size()) {
+    target = (int)peers.size();
+  } else {
+    std::vector<std::pair<uint64_t, int>> keyed;
+    for (int p : peers)
+      keyed.push_back({gs_key64(sim->cfg.seed, GS_SITE_EMIT_PEERS, id, (uint32_t)sim->hop, p, topic), p});
+    std::sort(keyed.begin(), keyed.end());
+    peers.clear();
+    for (auto& kp : keyed) peers.push_back(kp.second);
+  }
+  peers.resize(target);
+  std::sort(mids.begin(), mids.end());  // the IHAVE payload is a set of ids
+  for (int p : peers) {
+    IHaveEntry e;
+    e.topic = topic;
+    if ((int)mids.size() > sim->gp.MaxIHaveLength) {
+      std::vector<std::pair<uint64_t, int64_t>> keyed;
+      for (int64_t mid : mids)
+        keyed.push_back({gs_key64(sim->cfg.seed, GS_SITE_EMIT_MIDS, id, p, (uint32_t)mid, (uint32_t)sim->hop), mid});
+      std::sort(keyed.begin(), keyed.end());
+      for (int i = 0; i < sim->gp.MaxIHaveLength; ++i) e.mids.push_back(keyed[i].second);
+    } else {
+      e.mids = mids;
+    }
+    gossip[p].push_back(std::move(e));  // enqueueGossip
+  }
+}
+
+// heartbeat — gossipsub.go:1299-1552
+void Node::heartbeat() {
+  const gs_gossipsub_params& gp = sim->gp;
+  const int64_t now = sim->now();
+  const uint32_t hopw = (uint32_t)sim->hop;
+  heartbeatTicks++;
+  std::map<int, std::vector<int>> tograft, toprune;
+  std::map<int, bool> noPX;
+  clearBackoff();
+  peerhave.clear();  // clearIHaveCounters
+  iasked.clear();
+  applyIwantPenalties();
+  std::map<int, double> scores;  // score memo
+  auto score = [&](int p) {
+    auto it = scores.find(p);
+    if (it != scores.end()) return it->second;
+    double s = Score(p);
+    scores[p] = s;
+    return s;
+  };
+  for (auto& mt : mesh) {
+    const int topic = mt.first;
+    std::set<int>& peers = mt.second;
+    auto prunePeer = [&](int p) {
+      if (sim->scoring) this->score.Prune(p, topic);
+      peers.erase(p);
+      addBackoff(p, topic);
+      toprune[p].push_back(topic);
+    };
+    auto graftPeer = [&](int p) {
+      if (sim->scoring) this->score.Graft(p, topic, now);
+      peers.insert(p);
+      tograft[p].push_back(topic);
+    };
+    // drop all peers with negative score, without PX
+    std::vector<int> cur(peers.begin(), peers.end());
+    for (int p : cur)
+      if (score(p) < 0) { prunePeer(p); noPX[p] = true; }
+    // do we have enough peers?
+    if ((int)peers.size() < gp.Dlo) {
+      auto& bo = backoff[topic];
+      int ineed = gp.D - (int)peers.size();
+      auto plst = getPeers(topic, ineed, GS_SITE_GP_DLO, [&](int p) {
+        return !peers.count(p) && !bo.count(p) && !direct.count(p) && score(p) >= 0;
+      });
+      for (int p : plst) graftPeer(p);
+      if (bo.empty()) backoff.erase(topic);
+    }
+    // do we have too many peers?
+    if ((int)peers.size() > gp.Dhi) {
+      // shuffle then sort by score desc == sort by (score desc, key asc)
+      std::vector<std::pair<double, std::pair<uint64_t, int>>> ks;
+      for (int p : peers)
+        ks.push_back({score(p), {gs_key64(sim->cfg.seed, GS_SITE_DHI_SHUFFLE, id, hopw, p, topic), p}});
+      std::sort(ks.begin(), ks.end(), [](const auto& a, const auto& b) {
+        if (a.first != b.first) return a.first > b.first;
+        return a.second < b.second;
+      });
+      std::vector<int> plst;
+      for (auto& k : ks) plst.push_back(k.second.second);
+      // shuffle the tail [Dscore:]
+      {
+        std::vector<std::pair<uint64_t, int>> tail;
+        for (size_t i = gp.Dscore; i < plst.size(); ++i)
+          tail.push_back({gs_key64(sim->cfg.seed, GS_SITE_DHI_TAIL, id, hopw, plst[i], topic), plst[i]});
+        std::sort(tail.begin(), tail.end());
+        for (size_t i = 0; i < tail.size(); ++i) plst[gp.Dscore + i] = tail[i].second;
+      }
+      int outb = 0;
+      for (int i = 0; i < gp.D; ++i) if (outbound[plst[i]]) outb++;
+      if (outb < gp.Dout) {
+        auto rotate = [&](int i) {
+          int p = plst[i];
+          for (int j = i; j > 0; --j) plst[j] = plst[j - 1];
+          plst[0] = p;
+        };
+        if (outb > 0) {
+          int ih = outb;
+          for (int i = 1; i < gp.D && ih > 0; ++i)
+            if (outbound[plst[i]]) { rotate(i); ih--; }
+        }
+        int ineed = gp.Dout - outb;
+        for (int i = gp.D; i < (int)plst.size() && ineed > 0; ++i)
+          if (outbound[plst[i]]) { rotate(i); ineed--; }
+      }
+      for (size_t i = gp.D; i < plst.size(); ++i) prunePeer(plst[i]);
+    }
+    // do we have enough outbound peers?
+    if ((int)peers.size() >= gp.Dlo) {
+      int outb = 0;
+      for (int p : peers) if (outbound[p]) outb++;
+      if (outb < gp.Dout) {
+        int ineed = gp.Dout - outb;
+        auto& bo = backoff[topic];
+        auto plst = getPeers(topic, ineed, GS_SITE_GP_DOUT, [&](int p) {
+          return !peers.count(p) && !bo.count(p) && !direct.count(p) && outbound[p] && score(p) >= 0;
+        });
+        for (int p : plst) graftPeer(p);
+        if (bo.empty()) backoff.erase(topic);
+      }
+    }
+    // opportunistic grafting
+    if (heartbeatTicks % gp.OpportunisticGraftTicks == 0 && peers.size() > 1) {
+      std::vector<double> sc;
+      for (int p : peers) sc.push_back(score(p));
+      std::sort(sc.begin(), sc.end());
+      double medianScore = sc[peers.size() / 2];
+      if (medianScore < sim->thr.OpportunisticGraftThreshold) {
+        auto& bo = backoff[topic];
+        auto plst = getPeers(topic, gp.OpportunisticGraftPeers, GS_SITE_GP_OPPORTUNISTIC, [&](int p) {
+          return !peers.count(p) && !bo.count(p) && !direct.count(p) && score(p) > medianScore;
+        });
+        for (int p : plst) graftPeer(p);
+        if (bo.empty()) backoff.erase(topic);
+      }
+    }
+    emitGossip(topic, peers);
+  }
+  // expire fanout for topics we haven't published to in a while
+  for (auto it = lastpub.begin(); it != lastpub.end();) {
+    if (it->second + gp.FanoutTTL < now) {
+      fanout.erase(it->first);
+      it = lastpub.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  // maintain our fanout for topics we are publishing but we have not joined
+  for (auto& ft : fanout) {
+    const int topic = ft.first;
+    std::set<int>& peers = ft.second;
+    for (auto it = peers.begin(); it != peers.end();) {
+      bool inTopic = topics.count(topic) && topics[topic].count(*it);
+      if (!inTopic || score(*it) < sim->thr.PublishThreshold) it = peers.erase(it); else ++it;
+    }
+    if ((int)peers.size() < gp.D) {
+      int ineed = gp.D - (int)peers.size();
+      auto plst = getPeers(topic, ineed, GS_SITE_GP_FANOUT_HB, [&](int p) {
+        return !peers.count(p) && !direct.count(p) && score(p) >= sim->thr.PublishThreshold;
+      });
+      for (int p : plst) peers.insert(p);
+    }
+    emitGossip(topic, peers);
+  }
+  // sendGraftPrune — gossipsub.go:1618-1654
+  for (auto& kv : tograft) {
+    int p = kv.first;
+    RPC r;
+    r.hasCtl = true;
+    r.ctl.graft = kv.second;
+    auto pr = toprune.find(p);
+    if (pr != toprune.end()) {
+      for (int topic : pr->second) r.ctl.prune.push_back(makePrune(p, topic));
+      toprune.erase(pr);
+    }
+    sendRPC(p, std::move(r));
+  }
+  for (auto& kv : toprune) {
+    RPC r;
+    r.hasCtl = true;
+    for (int topic : kv.second) r.ctl.prune.push_back(makePrune(kv.first, topic));
+    sendRPC(kv.first, std::move(r));
+  }
+  // flush — gossipsub.go:1714-1728
+  std::vector<int> gpeers;
+  for (auto& kv : gossip) gpeers.push_back(kv.first);
+  for (int p : gpeers) {
+    RPC r;
+    r.hasCtl = true;
+    sendRPC(p, std::move(r));  // sendRPC piggybacks the pending IHAVE
+  }
+  mcache.Shift();
+}
+
+void Sim::start() {
+  nodes.assign(N, Node());
+  if (record) deliv.assign(N, {});
+  for (int u = 0; u < N; ++u) {
+    Node& nd = nodes[u];
+    nd.sim = this;
+    nd.id = u;
+    nd.mySubs = subs.empty() ? 0 : subs[u];
+    nd.mcache.init(gp.HistoryGossip, gp.HistoryLength);
+    nd.score.params = sp;
+    for (int t = 0; t < T; ++t)
+      if (tscored[t]) nd.score.topics[t] = tparams[t];
+    nd.score.appSpecificScore = [this](int p) { return appScore.empty() ? 0.0 : appScore[p]; };
+    nd.score.whitelist = whitelist;
+    nd.gtracer.followUpTime = gp.IWantFollowupTime;
+    for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) {
+      int v = col[e];
+      nd.nbrs.push_back(v);
+      nd.outbound[v] = outboundE.empty() ? false : outboundE[e] != 0;  // AddPeer gossipsub.go:505-532
+      if (!directE.empty() && directE[e]) nd.direct.insert(v);
+      std::vector<uint32_t> ips;
+      if (!ipv4.empty() && ipv4[v] != 0) ips.push_back(ipv4[v]);
+      if (scoring) nd.score.AddPeer(v, ips);
+      for (int t = 0; t < T; ++t)
+        if (!subs.empty() && ((subs[v] >> t) & 1)) nd.topics[t].insert(v);
+    }
+  }
+  started = true;
+}
+
+void Sim::step() {
+  const int64_t t = now();
+  if (hop == 0) {
+    for (int u = 0; u < N; ++u)
+      for (int tp = 0; tp < T; ++tp)
+        if ((nodes[u].mySubs >> tp) & 1) nodes[u].join(tp);
+  }
+  // S0 memo
+  if (scoring)
+    for (Node& nd : nodes) {
+      nd.memo.clear();
+      for (int v : nd.nbrs) nd.memo[v] = nd.score.score(v);
+    }
+  // the RPCs sent during hop h-1 are this hop's inbox
+  std::vector<std::map<int, std::vector<RPC>>> inbox(N);
+  for (Node& nd : nodes) {
+    for (auto& kv : nd.out) inbox[kv.first][nd.id] = std::move(kv.second);
+    nd.out.clear();
+  }
+  // local publishes of this hop
+  while (nextPub < msgs.size() && msgHop[nextPub] == hop) {
+    const Msg& m = msgs[nextPub];
+    nodes[m.from].localPublish(m);
+    nextPub++;
+  }
+  // phase A: payload messages, senders ascending
+  for (Node& nd : nodes) {
+    nd.acceptStatus.clear();
+    for (auto& kv : inbox[nd.id]) {
+      int s = kv.first;
+      int st = PeerGater::AcceptAll;
+      if (cfg.router == GS_ROUTER_GOSSIPSUB) {  // AcceptFrom gossipsub.go:578-589
+        if (nd.direct.count(s)) st = PeerGater::AcceptAll;
+        else if (scoring && nd.memo[s] < thr.GraylistThreshold) st = PeerGater::AcceptNone;
+      }
+      nd.acceptStatus[s] = st;
+      if (st == PeerGater::AcceptNone) { ctr.graylisted += (int64_t)kv.second.size(); continue; }
+      for (const RPC& r : kv.second)
+        for (int64_t mid : r.publish) nd.handleMessage(s, msgs[mid]);
+    }
+  }
+  // phase B: control, per RPC, senders ascending
+  if (cfg.router == GS_ROUTER_GOSSIPSUB) {
+    for (Node& nd : nodes) {
+      for (auto& kv : inbox[nd.id]) {
+        int s = kv.first;
+        if (nd.acceptStatus[s] == PeerGater::AcceptNone) continue;
+        for (const RPC& r : kv.second)
+          if (r.hasCtl) nd.handleRPC(s, r.ctl);
+      }
+    }
+  }
+  if (refreshDue(t))
+    for (Node& nd : nodes) nd.score.refreshScores(t);
+  if (scoring && t > 0 && t % (60 * kSecond) == 0)
+    for (Node& nd : nodes) nd.score.gc(t);
+  if (heartbeatDue(t)) {
+    for (Node& nd : nodes) nd.heartbeat();
+    ctr.heartbeats++;
+  }
+  ctr.hops++;
+  hop++;
+}
+
+}  // namespace oracle
+
+using namespace oracle;
+
+struct gs_engine {
+  Sim sim;
+};
+
+extern "C" {
+
+int gs_abi_version(void) { return GS_ABI_VERSION; }
+const char* gs_last_error(void) { return g_err.c_str(); }
+void gs_default_gossipsub_params(gs_gossipsub_params* out) { defaultGossipSubParams(out); }
+void gs_default_peer_gater_params(gs_peer_gater_params* out) { defaultPeerGaterParams(out); }
+double gs_score_parameter_decay_with_base(int64_t decay, int64_t base, double dtz) {
+  return scoreParameterDecayWithBase(decay, base, dtz);
+}
+double gs_score_parameter_decay(int64_t decay) { return scoreParameterDecayWithBase(decay, kSecond, 0.01); }
+int gs_validate_thresholds(const gs_peer_score_thresholds* p) { return validateThresholds(p); }
+int gs_validate_peer_score_params(const gs_peer_score_params* p, const gs_topic_score_params* topics,
+                                  const uint8_t* scored, int32_t T) {
+  return validatePeerScoreParams(p, topics, scored, T);
+}
+int gs_validate_topic_score_params(const gs_topic_score_params* p) { return validateTopicParams(p); }
+int gs_validate_peer_gater_params(const gs_peer_gater_params* p) { return validateGaterParams(p); }
+
+int gs_engine_create(const gs_config* cfg, const gs_gossipsub_params* gsp, const gs_peer_score_params* psp,
+                     const gs_topic_score_params* topics, const uint8_t* topic_scored,
+                     const gs_peer_score_thresholds* thr, const gs_peer_gater_params* gater, gs_engine** out) {
+  (void)gater;
+  if (!cfg || !out) { set_error("null argument"); return GS_EINVAL; }
+  if (cfg->num_nodes <= 0 || cfg->num_topics <= 0 || cfg->num_topics > 64 || cfg->hop_ns <= 0) {
+    set_error("invalid config: num_nodes > 0, 1 <= num_topics <= 64, hop_ns > 0 required");
+    return GS_EINVAL;
+  }
+  if (cfg->router < 0 || cfg->router > 2) { set_error("unknown router"); return GS_EINVAL; }
+  std::unique_ptr<gs_engine> eng(new gs_engine());
+  Sim& s = eng->sim;
+  s.cfg = *cfg;
+  s.N = cfg->num_nodes;
+  s.T = cfg->num_topics;
+  if (gsp) s.gp = *gsp; else defaultGossipSubParams(&s.gp);
+  s.scoring = (cfg->flags & GS_FLAG_SCORING) != 0 && cfg->router == GS_ROUTER_GOSSIPSUB;
+  s.floodPublish = (cfg->flags & GS_FLAG_FLOOD_PUBLISH) != 0;
+  s.record = (cfg->flags & GS_FLAG_RECORD_DELIVERIES) != 0;
+  s.tparams.assign(s.T, gs_topic_score_params{});
+  s.tscored.assign(s.T, 0);
+  if (cfg->router == GS_ROUTER_GOSSIPSUB) {
+    if (s.gp.HistoryGossip > s.gp.HistoryLength) {
+      set_error("invalid parameters for message cache; gossip slots cannot be larger than history slots");
+      return GS_EINVAL;
+    }
+    if (s.gp.HeartbeatInterval <= 0 || s.gp.HeartbeatInterval % cfg->hop_ns != 0 ||
+        s.gp.HeartbeatInitialDelay < 0 || s.gp.HeartbeatInitialDelay % cfg->hop_ns != 0) {
+      set_error("HeartbeatInterval and HeartbeatInitialDelay must be multiples of hop_ns");
+      return GS_EUNSUPPORTED;
+    }
+  }
+  if (s.scoring) {
+    if (!psp || !topics || !topic_scored || !thr) { set_error("scoring needs score params and thresholds"); return GS_EINVAL; }
+    int rc = validatePeerScoreParams(psp, topics, topic_scored, s.T);
+    if (rc) return rc;
+    rc = validateThresholds(thr);
+    if (rc) return rc;
+    if (psp->DecayInterval % cfg->hop_ns != 0) { set_error("DecayInterval must be a multiple of hop_ns"); return GS_EUNSUPPORTED; }
+    s.sp = *psp;
+    s.thr = *thr;
+    for (int t = 0; t < s.T; ++t) { s.tparams[t] = topics[t]; s.tscored[t] = topic_scored[t]; }
+  }
+  *out = eng.release();
+  return GS_OK;
+}
+
+int gs_engine_destroy(gs_engine* eng) { delete eng; return GS_OK; }
+
+int gs_set_graph(gs_engine* eng, const int64_t* rowptr, const int32_t* col, const uint8_t* outbound,
+                 const uint8_t* direct) {
+  Sim& s = eng->sim;
+  if (s.started) { set_error("graph must be set before the first step"); return GS_ESTATE; }
+  s.rowptr.assign(rowptr, rowptr + s.N + 1);
+  s.E = s.rowptr[s.N];
+  s.col.assign(col, col + s.E);
+  for (int u = 0; u < s.N; ++u)
+    for (int64_t e = s.rowptr[u]; e < s.rowptr[u + 1]; ++e) {
+      int v = s.col[e];
+      if (v < 0 || v >= s.N || v == u || (e > s.rowptr[u] && s.col[e - 1] >= v)) {
+        set_error("graph rows must hold strictly ascending neighbour ids != self"); return GS_EINVAL; }
+    }
+  for (int u = 0; u < s.N; ++u)
+    for (int64_t e = s.rowptr[u]; e < s.rowptr[u + 1]; ++e)
+      if (s.edgeIndex(s.col[e], u) < 0) { set_error("graph must be symmetric"); return GS_EINVAL; }
+  s.outboundE.assign(s.E, 0);
+  s.directE.assign(s.E, 0);
+  if (outbound) s.outboundE.assign(outbound, outbound + s.E);
+  if (direct) s.directE.assign(direct, direct + s.E);
+  s.graphSet = true;
+  return GS_OK;
+}
+
+int gs_set_subscriptions(gs_engine* eng, const uint64_t* sub_mask) {
+  Sim& s = eng->sim;
+  if (s.started) { set_error("subscriptions must be set before the first step"); return GS_ESTATE; }
+  s.subs.assign(sub_mask, sub_mask + s.N);
+  return GS_OK;
+}
+
+int gs_set_peer_attrs(gs_engine* eng, const double* app_score, const uint32_t* ipv4) {
+  Sim& s = eng->sim;
+  if (s.started) { set_error("peer attributes must be set before the first step"); return GS_ESTATE; }
+  if (app_score) s.appScore.assign(app_score, app_score + s.N);
+  if (ipv4) s.ipv4.assign(ipv4, ipv4 + s.N);
+  return GS_OK;
+}
+
+int gs_set_ip_whitelist(gs_engine* eng, int32_t n, const uint32_t* net, const uint32_t* mask) {
+  Sim& s = eng->sim;
+  if (s.started) { set_error("whitelist must be set before the first step"); return GS_ESTATE; }
+  s.whitelist.clear();
+  for (int i = 0; i < n; ++i) s.whitelist.push_back({net[i], mask[i]});
+  return GS_OK;
+}
+
+int gs_publish(gs_engine* eng, int32_t n, const int32_t* src, const int32_t* topic, const int64_t* hop,
+               int64_t* ids_out) {
+  Sim& s = eng->sim;
+  int64_t last = s.msgHop.empty() ? s.hop : std::max(s.hop, s.msgHop.back());
+  for (int i = 0; i < n; ++i) {
+    if (src[i] < 0 || src[i] >= s.N || topic[i] < 0 || topic[i] >= s.T || hop[i] < last) {
+      set_error("publish: bad src/topic or hop not non-decreasing from the current hop"); return GS_EINVAL; }
+    last = hop[i];
+  }
+  for (int i = 0; i < n; ++i) {
+    int64_t id = (int64_t)s.msgs.size();
+    s.msgs.push_back(Msg{id, topic[i], src[i]});
+    s.msgHop.push_back(hop[i]);
+    if (ids_out) ids_out[i] = id;
+  }
+  return GS_OK;
+}
+
+int gs_step(gs_engine* eng, int64_t hops) {
+  Sim& s = eng->sim;
+  if (!s.graphSet) { set_error("graph not set"); return GS_ESTATE; }
+  if (!s.started) s.start();
+  for (int64_t i = 0; i < hops; ++i) s.step();
+  return GS_OK;
+}
+int gs_sync(gs_engine*) { return GS_OK; }
+
+int gs_set_topic_score_params(gs_engine* eng, int32_t topic, const gs_topic_score_params* p) {
+  Sim& s = eng->sim;
+  if (topic < 0 || topic >= s.T) { set_error("bad topic"); return GS_EINVAL; }
+  int rc = validateTopicParams(p);
+  if (rc) return rc;
+  s.tparams[topic] = *p;
+  s.tscored[topic] = 1;
+  for (Node& nd : s.nodes) nd.score.SetTopicScoreParams(topic, *p);
+  return GS_OK;
+}
+
+int64_t gs_num_edges(const gs_engine* eng) { return eng->sim.E; }
+int64_t gs_current_hop(const gs_engine* eng) { return eng->sim.hop; }
+int gs_read_counters(gs_engine* eng, gs_counters* out) { *out = eng->sim.ctr; return GS_OK; }
+
+int gs_read_scores(gs_engine* eng, double* score) {
+  Sim& s = eng->sim;
+  if (!s.started) s.start();
+  for (int u = 0; u < s.N; ++u)
+    for (int64_t e = s.rowptr[u]; e < s.rowptr[u + 1]; ++e)
+      score[e] = s.nodes[u].Score(s.col[e]);
+  return GS_OK;
+}
+
+int gs_read_mesh(gs_engine* eng, uint64_t* mesh) {
+  Sim& s = eng->sim;
+  std::fill(mesh, mesh + s.E, 0);
+  if (!s.started) return GS_OK;
+  for (int u = 0; u < s.N; ++u)
+    for (auto& kv : s.nodes[u].mesh)
+      for (int p : kv.second) mesh[s.edgeIndex(u, p)] |= 1ull << kv.first;
+  return GS_OK;
+}
+
+int gs_read_fanout(gs_engine* eng, uint64_t* fanout) {
+  Sim& s = eng->sim;
+  std::fill(fanout, fanout + s.E, 0);
+  if (!s.started) return GS_OK;
+  for (int u = 0; u < s.N; ++u)
+    for (auto& kv : s.nodes[u].fanout)
+      for (int p : kv.second) fanout[s.edgeIndex(u, p)] |= 1ull << kv.first;
+  return GS_OK;
+}
+
+int gs_read_backoff(gs_engine* eng, int64_t* expire) {
+  Sim& s = eng->sim;
+  std::fill(expire, expire + s.E * s.T, 0);
+  if (!s.started) return GS_OK;
+  for (int u = 0; u < s.N; ++u)
+    for (auto& kv : s.nodes[u].backoff)
+      for (auto& pe : kv.second) expire[(int64_t)kv.first * s.E + s.edgeIndex(u, pe.first)] = pe.second;
+  return GS_OK;
+}
+
+int gs_read_topic_stats(gs_engine* eng, double* fmd, double* mmd, double* mfp, double* imd, int64_t* mesh_time,
+                        int64_t* graft_time, uint8_t* flags) {
+  Sim& s = eng->sim;
+  const int64_t n = s.E * s.T;
+  std::fill(fmd, fmd + n, 0.0); std::fill(mmd, mmd + n, 0.0);
+  std::fill(mfp, mfp + n, 0.0); std::fill(imd, imd + n, 0.0);
+  std::fill(mesh_time, mesh_time + n, 0); std::fill(graft_time, graft_time + n, 0);
+  std::fill(flags, flags + n, 0);
+  if (!s.started) return GS_OK;
+  for (int u = 0; u < s.N; ++u)
+    for (auto& ps : s.nodes[u].score.peerStats) {
+      int64_t e = s.edgeIndex(u, ps.first);
+      for (auto& ts : ps.second.topics) {
+        int64_t i = (int64_t)ts.first * s.E + e;
+        fmd[i] = ts.second.firstMessageDeliveries;
+        mmd[i] = ts.second.meshMessageDeliveries;
+        mfp[i] = ts.second.meshFailurePenalty;
+        imd[i] = ts.second.invalidMessageDeliveries;
+        mesh_time[i] = ts.second.meshTime;
+        graft_time[i] = ts.second.graftTime;
+        flags[i] = (ts.second.inMesh ? 1 : 0) | (ts.second.meshMessageDeliveriesActive ? 2 : 0);
+      }
+    }
+  return GS_OK;
+}
+
+int gs_read_behaviour_penalty(gs_engine* eng, double* bp) {
+  Sim& s = eng->sim;
+  std::fill(bp, bp + s.E, 0.0);
+  if (!s.started) return GS_OK;
+  for (int u = 0; u < s.N; ++u)
+    for (auto& ps : s.nodes[u].score.peerStats) bp[s.edgeIndex(u, ps.first)] = ps.second.behaviourPenalty;
+  return GS_OK;
+}
+
+int gs_read_deliveries(gs_engine* eng, int64_t id, int32_t* hop, int32_t* from) {
+  Sim& s = eng->sim;
+  if (!s.record) { set_error("GS_FLAG_RECORD_DELIVERIES not set"); return GS_ESTATE; }
+  if (id < 0 || id >= (int64_t)s.msgs.size()) { set_error("unknown message id"); return GS_EINVAL; }
+  for (int u = 0; u < s.N; ++u) {
+    hop[u] = -1; from[u] = -1;
+    if (!s.started) continue;
+    auto it = s.deliv[u].find(id);
+    if (it != s.deliv[u].end()) { hop[u] = it->second.first; from[u] = it->second.second; }
+  }
+  return GS_OK;
+}
+
+}  // extern "C"
