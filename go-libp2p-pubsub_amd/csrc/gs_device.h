@@ -1,0 +1,237 @@
+// gs_device.h — device-side state and helpers of the MI355X gossip engine.
+//
+// Layout: message slots are topic-segmented, slot s belongs to
+// topic s / St; a node bitset is W = T*Wt 64-bit words.  Per-node arrays are
+// row-major [node][word]; per-edge arrays are indexed by the CSR edge id e
+// (observer u = edge_src[e], neighbour col[e]); per-(edge,topic) score state
+// is topic-major [t*E + e] so a thread-per-edge pass is coalesced.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gs_rng.h"
+
+#define GS_WAVE 64
+#define GS_MAX_WPL 4   // words per lane in the node-wave kernels: W <= 256
+#define GS_TABLE 64    // promise / IWANT-retransmission table entries per node (one per lane)
+
+// device counter slots (same order as gs_counters)
+enum {
+  C_HOPS = 0, C_HEARTBEATS, C_PUBLISHED, C_DELIVERIES, C_DUPLICATES, C_TRANSMISSIONS, C_GRAFTS,
+  C_PRUNES, C_IHAVE, C_IWANT_SENT, C_IWANT_SERVED, C_PROMISES_BROKEN, C_GRAYLISTED, C_NCOUNTERS = 16
+};
+// device error codes (first one wins)
+enum {
+  E_NONE = 0, E_POOL = 1, E_PROMISES = 2, E_PEERTX = 3, E_LATE = 4, E_TRUNCATE = 5, E_DOUBLE = 6
+};
+
+struct TopicP {  // TopicScoreParams (score_params.go:98-148) + scored flag
+  double TopicWeight, TimeInMeshWeight;
+  int64_t TimeInMeshQuantum;
+  double TimeInMeshCap;
+  double FmdWeight, FmdDecay, FmdCap;
+  double MmdWeight, MmdDecay, MmdCap, MmdThreshold;
+  int64_t MmdWindow, MmdActivation;
+  double MfpWeight, MfpDecay, ImdWeight, ImdDecay;
+  int32_t scored;
+  int32_t pad;
+};
+
+struct Dev {
+  // sizes
+  int32_t N, T, Wt, W, St, S, R, HL, HG;
+  int64_t E;
+  int32_t router, scoring, floodPublish, rsTarget, maxAge;
+  uint32_t seed;
+  int64_t hop_ns;
+  // graph (static)
+  const int64_t* rowptr;
+  const int32_t* col;
+  const int32_t* esrc;
+  const int32_t* rev;
+  const uint8_t* outbound;
+  const uint8_t* direct;
+  const uint64_t* sub;
+  // score params
+  const TopicP* tp;
+  const double* app;
+  const double* p6;
+  double TopicScoreCap, AppW, IPW, BPW, BPThr, BPDecay, DecayToZero;
+  double gossipThr, publishThr, graylistThr, oppThr;
+  // gossipsub params (gossipsub.go:62-195)
+  int32_t D, Dlo, Dhi, Dscore, Dout, Dlazy, GR, OGP, MaxIHaveLength, MaxIHaveMessages;
+  double GossipFactor;
+  int64_t PruneBackoff, GraftFloodThreshold, IWantFollowupTime, FanoutTTL, PruneRecv;
+  uint64_t OGT;
+  // per-node state
+  uint64_t* seen;
+  uint64_t* newb[2];
+  uint64_t* hist;  // [R][N][W]
+  int16_t* age;    // [N][S] first-delivery hop - publish hop
+  uint8_t* ffrom;  // [N][S] first-deliverer neighbour slot (255 = self)
+  uint64_t* sel;   // [N][S] randomsub target mask (randomsub only)
+  int64_t* lastpub;        // [N][T], INT64_MIN = none
+  uint64_t* fanoutPresent; // [N]
+  int64_t* promMid;  // [N][64]
+  int64_t* promExp;
+  int32_t* promSlot;
+  uint8_t* promEdge;
+  int32_t* promN;
+  int64_t* ptxMid;   // [N][64]
+  int32_t* ptxSlot;
+  int32_t* ptxCnt;
+  uint8_t* ptxEdge;
+  int32_t* ptxN;
+  // per-edge state
+  uint64_t* mesh;
+  uint64_t* fanout;
+  uint64_t* fwdRelay[2];
+  uint64_t* fwdPub[2];
+  double* score0;  // hop-start score memo (S0)
+  double* score1;  // after the message phase (S1) / heartbeat memo
+  int64_t* backoff;  // [T][E], 0 = none
+  double *fmd, *mmd, *mfp, *imd;  // [T][E]
+  int64_t *graftTime, *meshTime;  // [T][E]
+  uint8_t* flags;                 // [T][E] bit0 inMesh, bit1 P3 active
+  double* bp;                     // [E] behaviourPenalty
+  int32_t *peerhave, *iasked;     // [E]
+  // control outbox, double-buffered by hop parity; written by the sender on
+  // its own edge, read by the receiver through rev[]
+  uint8_t* cPre[2];   // number of control RPCs before the heartbeat RPC (join + reply RPCs)
+  uint8_t* cHb[2];    // heartbeat RPC present
+  uint64_t* cGraftJoin[2];
+  uint64_t* cGraftHb[2];
+  uint64_t* cPruneReply[2];
+  uint64_t* cPruneHb[2];
+  uint64_t* cIhave[2];
+  int32_t* cIwant[2];
+  int32_t* cIresp[2];
+  uint64_t* pool[2];  // [POOLCAP][W] IWANT request / response bitsets
+  int32_t* poolCnt;   // [2]
+  int32_t poolCap;
+  // message slots
+  int32_t* slotSrc;
+  int64_t* slotPubHop;
+  int64_t* slotMid;
+  uint64_t* pubmask[2];  // slots published in hop h (also the retire mask of hop h)
+  const int32_t* mSrc;
+  const int32_t* mTopic;
+  const int32_t* mSlot;
+  const int64_t* mId;
+  // counters / error
+  unsigned long long* ctr;
+  int32_t* err;
+};
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ void set_err(const Dev& d, int code) { atomicCAS(d.err, 0, code); }
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+  return (uint64_t)__shfl((unsigned long long)v, src);
+}
+
+__device__ __forceinline__ int wave_sum_int(int v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// k smallest (key, lane) among candidate lanes: the keyed "shuffle then take
+// k" of gs_rng.h.  k <= 0 selects every candidate (getPeers count semantics).
+__device__ __forceinline__ bool select_k(bool cand, uint64_t key, int k) {
+  const int lane = lane_id();
+  unsigned long long m = __ballot(cand);
+  if (k <= 0 || __popcll(m) <= k) return cand;
+  int rank = 0;
+  while (m) {
+    int j = __ffsll((long long)m) - 1;
+    m &= m - 1;
+    uint64_t kj = shfl_u64(key, j);
+    if (kj < key || (kj == key && j < lane)) rank++;
+  }
+  return cand && rank < k;
+}
+
+// "+1, cap" applied n times — markFirstMessageDelivery / markDuplicate-
+// MessageDelivery (score.go:915-928, 960-963) one message at a time, since
+// (x+1)+1 != x+2 for fractional decayed counters.
+__device__ __forceinline__ double add_ones_capped(double x, int n, double cap) {
+  for (int i = 0; i < n; ++i) {
+    x += 1.0;
+    if (x > cap) { x = cap; break; }
+  }
+  return x;
+}
+
+// peerScore.score — score.go:256-333, topics summed in ascending order.
+// Compiled with -ffp-contract=off: every product/sum rounds as in Go.
+__device__ __noinline__ double edge_score(const Dev& d, int64_t e) {
+  if (!d.scoring) return 0.0;
+  double score = 0.0;
+  for (int t = 0; t < d.T; ++t) {
+    const TopicP& tp = d.tp[t];
+    if (!tp.scored) continue;
+    const int64_t i = (int64_t)t * d.E + e;
+    const uint8_t fl = d.flags[i];
+    double topicScore = 0.0;
+    if (fl & 1) {
+      double p1 = (double)(d.meshTime[i] / tp.TimeInMeshQuantum);
+      if (p1 > tp.TimeInMeshCap) p1 = tp.TimeInMeshCap;
+      topicScore += p1 * tp.TimeInMeshWeight;
+    }
+    topicScore += d.fmd[i] * tp.FmdWeight;
+    if (fl & 2) {
+      const double mm = d.mmd[i];
+      if (mm < tp.MmdThreshold) {
+        const double deficit = tp.MmdThreshold - mm;
+        const double p3 = deficit * deficit;
+        topicScore += p3 * tp.MmdWeight;
+      }
+    }
+    topicScore += d.mfp[i] * tp.MfpWeight;
+    const double im = d.imd[i];
+    const double p4 = im * im;
+    topicScore += p4 * tp.ImdWeight;
+    score += topicScore * tp.TopicWeight;
+  }
+  if (d.TopicScoreCap > 0 && score > d.TopicScoreCap) score = d.TopicScoreCap;
+  score += d.app[d.col[e]] * d.AppW;
+  score += d.p6[e] * d.IPW;
+  const double b = d.bp[e];
+  if (b > d.BPThr) {
+    const double excess = b - d.BPThr;
+    const double p7 = excess * excess;
+    score += p7 * d.BPW;
+  }
+  return score;
+}
+
+// peerScore.Graft — score.go:640-658 (scored topics only)
+__device__ __forceinline__ void stats_graft(const Dev& d, int64_t e, int t, int64_t now) {
+  if (!d.scoring || !d.tp[t].scored) return;
+  const int64_t i = (int64_t)t * d.E + e;
+  d.flags[i] = 1;  // inMesh, P3 inactive
+  d.graftTime[i] = now;
+  d.meshTime[i] = 0;
+}
+
+// peerScore.Prune — score.go:660-682
+__device__ __forceinline__ void stats_prune(const Dev& d, int64_t e, int t) {
+  if (!d.scoring || !d.tp[t].scored) return;
+  const int64_t i = (int64_t)t * d.E + e;
+  const uint8_t fl = d.flags[i];
+  const double thr = d.tp[t].MmdThreshold;
+  if ((fl & 2) && d.mmd[i] < thr) {
+    const double deficit = thr - d.mmd[i];
+    d.mfp[i] += deficit * deficit;
+  }
+  d.flags[i] = fl & ~1;
+}
+
+// doAddBackoff — gossipsub.go:844-854 (0 = no entry)
+__device__ __forceinline__ void add_backoff(const Dev& d, int64_t e, int t, int64_t now, int64_t interval) {
+  const int64_t i = (int64_t)t * d.E + e;
+  const int64_t expire = now + interval;
+  const int64_t cur = d.backoff[i];
+  if (cur == 0 || cur < expire) d.backoff[i] = expire;
+}

@@ -1,0 +1,735 @@
+// gs_engine.hip — product C-ABI (include/gossip_engine.h) over HIP kernels
+// for gfx950.  Host side: validation, graph preprocessing (reverse edges,
+// P6 colocation factors), message-slot assignment, device allocation and the
+// per-hop launch schedule (DESIGN.md §4 "Canonical round").  Every kernel runs
+// on one HIP stream per engine; gs_step enqueues many hops and synchronises
+// once at the end to check the device error word.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/gossip_engine.h"
+#include "gs_host.h"
+#include "gs_kernels.h"
+#include "gs_kernels_ctl.h"
+
+static thread_local std::string g_err;
+void gs_set_error(const std::string& msg) { g_err = msg; }
+
+#define HIPCHECK(expr)                                                        \
+  do {                                                                        \
+    hipError_t _e = (expr);                                                   \
+    if (_e != hipSuccess) {                                                   \
+      gs_set_error(std::string("HIP error: ") + hipGetErrorString(_e) + " at " #expr); \
+      return GS_EDEVICE;                                                      \
+    }                                                                         \
+  } while (0)
+
+static const int64_t kSec = 1000000000LL;
+
+struct gs_engine {
+  gs_config cfg{};
+  gs_gossipsub_params gp{};
+  gs_peer_score_params sp{};
+  gs_peer_score_thresholds thr{};
+  std::vector<gs_topic_score_params> tps;
+  std::vector<uint8_t> tscored;
+  bool scoring = false, floodPublish = false;
+  int N = 0, T = 0, St = 0, Wt = 0, W = 0, S = 0, R = 0;
+  int64_t E = 0;
+  int H = 16;  // hops per heartbeat (or a nominal 16 for floodsub/randomsub)
+  int64_t retireHops = 0;
+  int maxAge = 0;
+  // host graph / attributes
+  std::vector<int64_t> rowptr;
+  std::vector<int32_t> col, rev, esrc;
+  std::vector<uint8_t> outbound, direct;
+  std::vector<uint64_t> sub;
+  std::vector<double> app;
+  std::vector<uint32_t> ipv4;
+  std::vector<std::pair<uint32_t, uint32_t>> whitelist;
+  bool graphSet = false, started = false;
+  // schedule
+  int64_t hop = 0;
+  uint64_t ticks = 0;
+  int head = 0;
+  int64_t heartbeats = 0;
+  std::vector<int32_t> mSrc, mTopic, mSlot;
+  std::vector<int64_t> mId, mHop;
+  size_t uploaded = 0, msgCap = 0, nextMsg = 0;
+  std::vector<int64_t> topicCounter, slotOwnerHop, slotOwnerId;
+  // device
+  Dev d{};
+  std::vector<void*> allocs;
+  hipStream_t stream = nullptr;
+  TopicP* dTp = nullptr;
+  int32_t* dPairs = nullptr;
+  int pairCap = 0;
+  double* dScoreTmp = nullptr;
+  int32_t *dHopOut = nullptr, *dFromOut = nullptr;
+
+  ~gs_engine() {
+    for (void* p : allocs) (void)hipFree(p);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+  template <class X>
+  X* dalloc(size_t n, int fill = 0) {
+    void* p = nullptr;
+    size_t bytes = std::max<size_t>(n * sizeof(X), 16);
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    allocs.push_back(p);
+    (void)hipMemsetAsync(p, fill, bytes, stream);
+    return (X*)p;
+  }
+  bool heartbeatDue(int64_t t) const {
+    if (cfg.router != GS_ROUTER_GOSSIPSUB) return false;
+    if (t < gp.HeartbeatInitialDelay) return false;
+    return (t - gp.HeartbeatInitialDelay) % gp.HeartbeatInterval == 0;
+  }
+  bool refreshDue(int64_t t) const { return scoring && t > 0 && t % sp.DecayInterval == 0; }
+  int start();
+  int stepOne();
+  int uploadMessages();
+  int checkDeviceError();
+};
+
+static TopicP to_dev(const gs_topic_score_params& p, bool scored) {
+  TopicP t{};
+  t.TopicWeight = p.TopicWeight;
+  t.TimeInMeshWeight = p.TimeInMeshWeight;
+  t.TimeInMeshQuantum = p.TimeInMeshQuantum ? p.TimeInMeshQuantum : 1;
+  t.TimeInMeshCap = p.TimeInMeshCap;
+  t.FmdWeight = p.FirstMessageDeliveriesWeight;
+  t.FmdDecay = p.FirstMessageDeliveriesDecay;
+  t.FmdCap = p.FirstMessageDeliveriesCap;
+  t.MmdWeight = p.MeshMessageDeliveriesWeight;
+  t.MmdDecay = p.MeshMessageDeliveriesDecay;
+  t.MmdCap = p.MeshMessageDeliveriesCap;
+  t.MmdThreshold = p.MeshMessageDeliveriesThreshold;
+  t.MmdWindow = p.MeshMessageDeliveriesWindow;
+  t.MmdActivation = p.MeshMessageDeliveriesActivation;
+  t.MfpWeight = p.MeshFailurePenaltyWeight;
+  t.MfpDecay = p.MeshFailurePenaltyDecay;
+  t.ImdWeight = p.InvalidMessageDeliveriesWeight;
+  t.ImdDecay = p.InvalidMessageDeliveriesDecay;
+  t.scored = scored ? 1 : 0;
+  return t;
+}
+
+static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+int gs_engine::start() {
+  HIPCHECK(hipSetDevice(cfg.device));
+  HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  // reverse edges, edge sources, P6
+  rev.assign(E, -1);
+  esrc.assign(E, 0);
+  int maxdeg = 0;
+  for (int u = 0; u < N; ++u) {
+    maxdeg = std::max<int>(maxdeg, (int)(rowptr[u + 1] - rowptr[u]));
+    for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) {
+      esrc[e] = u;
+      const int v = col[e];
+      auto b = col.begin() + rowptr[v], en = col.begin() + rowptr[v + 1];
+      auto it = std::lower_bound(b, en, u);
+      if (it == en || *it != u) {
+        gs_set_error("graph must be symmetric");
+        return GS_EINVAL;
+      }
+      rev[e] = (int32_t)(it - col.begin());
+    }
+  }
+  if (maxdeg > 64) {
+    gs_set_error("this build supports node degree <= 64 (one wave per node)");
+    return GS_EUNSUPPORTED;
+  }
+  if (E > INT32_MAX) {
+    gs_set_error("this build supports < 2^31 edges per engine");
+    return GS_EUNSUPPORTED;
+  }
+  std::vector<double> p6(E, 0.0);
+  if (scoring && sp.IPColocationFactorWeight != 0 && !ipv4.empty()) {
+    // ipColocationFactor (score.go:335-379): peers per IP among the observer's peers
+    std::unordered_map<uint32_t, int> cnt;
+    for (int u = 0; u < N; ++u) {
+      cnt.clear();
+      for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e)
+        if (ipv4[col[e]] != 0) cnt[ipv4[col[e]]]++;
+      for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) {
+        const uint32_t ip = ipv4[col[e]];
+        if (ip == 0) continue;
+        bool wl = false;
+        for (auto& nm : whitelist)
+          if ((ip & nm.second) == (nm.first & nm.second)) { wl = true; break; }
+        if (wl) continue;
+        const int c = cnt[ip];
+        if (c > sp.IPColocationFactorThreshold) {
+          const double s = (double)(c - sp.IPColocationFactorThreshold);
+          p6[e] = s * s;
+        }
+      }
+    }
+  }
+  if (app.empty()) app.assign(N, 0.0);
+  if (sub.empty()) sub.assign(N, 0);
+  if (outbound.empty()) outbound.assign(E, 0);
+  if (direct.empty()) direct.assign(E, 0);
+
+  Dev& x = d;
+  x.N = N; x.T = T; x.Wt = Wt; x.W = W; x.St = St; x.S = S; x.R = R;
+  x.HL = gp.HistoryLength; x.HG = gp.HistoryGossip; x.E = E;
+  x.router = cfg.router; x.scoring = scoring; x.floodPublish = floodPublish;
+  x.rsTarget = 6;
+  if (cfg.router == GS_ROUTER_RANDOMSUB) {
+    const int sq = (int)std::ceil(std::sqrt((double)cfg.randomsub_size));
+    x.rsTarget = std::max(6, sq);
+  }
+  x.maxAge = maxAge; x.seed = cfg.seed; x.hop_ns = cfg.hop_ns;
+  x.TopicScoreCap = sp.TopicScoreCap; x.AppW = sp.AppSpecificWeight; x.IPW = sp.IPColocationFactorWeight;
+  x.BPW = sp.BehaviourPenaltyWeight; x.BPThr = sp.BehaviourPenaltyThreshold; x.BPDecay = sp.BehaviourPenaltyDecay;
+  x.DecayToZero = sp.DecayToZero;
+  x.gossipThr = thr.GossipThreshold; x.publishThr = thr.PublishThreshold; x.graylistThr = thr.GraylistThreshold;
+  x.oppThr = thr.OpportunisticGraftThreshold;
+  x.D = gp.D; x.Dlo = gp.Dlo; x.Dhi = gp.Dhi; x.Dscore = gp.Dscore; x.Dout = gp.Dout; x.Dlazy = gp.Dlazy;
+  x.GR = gp.GossipRetransmission; x.OGP = gp.OpportunisticGraftPeers; x.MaxIHaveLength = gp.MaxIHaveLength;
+  x.MaxIHaveMessages = gp.MaxIHaveMessages; x.GossipFactor = gp.GossipFactor;
+  x.PruneBackoff = gp.PruneBackoff; x.GraftFloodThreshold = gp.GraftFloodThreshold;
+  x.IWantFollowupTime = gp.IWantFollowupTime; x.FanoutTTL = gp.FanoutTTL;
+  // the PRUNE we receive carries the sender's PruneBackoff in whole seconds
+  // (makePrune gossipsub.go:1809, handlePrune :819-825)
+  x.PruneRecv = (gp.PruneBackoff / kSec) > 0 ? (gp.PruneBackoff / kSec) * kSec : gp.PruneBackoff;
+  x.OGT = gp.OpportunisticGraftTicks ? gp.OpportunisticGraftTicks : 1;
+
+  const size_t NW = (size_t)N * W, NS = (size_t)N * S, TE = (size_t)T * E;
+  bool ok = true;
+  auto chk = [&](const void* p) { if (!p) ok = false; };
+  int64_t* dRowptr = dalloc<int64_t>(N + 1); chk(dRowptr);
+  int32_t* dCol = dalloc<int32_t>(E); chk(dCol);
+  int32_t* dEsrc = dalloc<int32_t>(E); chk(dEsrc);
+  int32_t* dRev = dalloc<int32_t>(E); chk(dRev);
+  uint8_t* dOut = dalloc<uint8_t>(E); chk(dOut);
+  uint8_t* dDir = dalloc<uint8_t>(E); chk(dDir);
+  uint64_t* dSub = dalloc<uint64_t>(N); chk(dSub);
+  double* dApp = dalloc<double>(N); chk(dApp);
+  double* dP6 = dalloc<double>(E); chk(dP6);
+  dTp = dalloc<TopicP>(T); chk(dTp);
+  if (!ok) { gs_set_error("device allocation failed (graph)"); return GS_ENOMEM; }
+  HIPCHECK(hipMemcpyAsync(dRowptr, rowptr.data(), (N + 1) * 8, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipMemcpyAsync(dCol, col.data(), E * 4, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipMemcpyAsync(dEsrc, esrc.data(), E * 4, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipMemcpyAsync(dRev, rev.data(), E * 4, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipMemcpyAsync(dOut, outbound.data(), E, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipMemcpyAsync(dDir, direct.data(), E, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipMemcpyAsync(dSub, sub.data(), N * 8, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipMemcpyAsync(dApp, app.data(), N * 8, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipMemcpyAsync(dP6, p6.data(), E * 8, hipMemcpyHostToDevice, stream));
+  std::vector<TopicP> htp(T);
+  for (int t = 0; t < T; ++t) htp[t] = to_dev(tps[t], scoring && tscored[t]);
+  HIPCHECK(hipMemcpyAsync(dTp, htp.data(), T * sizeof(TopicP), hipMemcpyHostToDevice, stream));
+  x.rowptr = dRowptr; x.col = dCol; x.esrc = dEsrc; x.rev = dRev; x.outbound = dOut; x.direct = dDir;
+  x.sub = dSub; x.app = dApp; x.p6 = dP6; x.tp = dTp;
+
+  x.seen = dalloc<uint64_t>(NW); chk(x.seen);
+  for (int k = 0; k < 2; ++k) { x.newb[k] = dalloc<uint64_t>(NW); chk(x.newb[k]); }
+  x.hist = dalloc<uint64_t>((size_t)R * NW); chk(x.hist);
+  x.age = dalloc<int16_t>(NS); chk(x.age);
+  x.ffrom = dalloc<uint8_t>(NS); chk(x.ffrom);
+  x.sel = cfg.router == GS_ROUTER_RANDOMSUB ? dalloc<uint64_t>(NS) : nullptr;
+  if (cfg.router == GS_ROUTER_RANDOMSUB) chk(x.sel);
+  x.lastpub = dalloc<int64_t>((size_t)N * T); chk(x.lastpub);
+  x.fanoutPresent = dalloc<uint64_t>(N); chk(x.fanoutPresent);
+  const size_t NQ = (size_t)N * GS_TABLE;
+  x.promMid = dalloc<int64_t>(NQ); x.promExp = dalloc<int64_t>(NQ); x.promSlot = dalloc<int32_t>(NQ);
+  x.promEdge = dalloc<uint8_t>(NQ); x.promN = dalloc<int32_t>(N);
+  x.ptxMid = dalloc<int64_t>(NQ); x.ptxSlot = dalloc<int32_t>(NQ); x.ptxCnt = dalloc<int32_t>(NQ);
+  x.ptxEdge = dalloc<uint8_t>(NQ); x.ptxN = dalloc<int32_t>(N);
+  chk(x.promMid); chk(x.promExp); chk(x.promSlot); chk(x.promEdge); chk(x.promN);
+  chk(x.ptxMid); chk(x.ptxSlot); chk(x.ptxCnt); chk(x.ptxEdge); chk(x.ptxN);
+  x.mesh = dalloc<uint64_t>(E); x.fanout = dalloc<uint64_t>(E);
+  chk(x.mesh); chk(x.fanout);
+  for (int k = 0; k < 2; ++k) {
+    x.fwdRelay[k] = dalloc<uint64_t>(E); x.fwdPub[k] = dalloc<uint64_t>(E);
+    chk(x.fwdRelay[k]); chk(x.fwdPub[k]);
+    x.cPre[k] = dalloc<uint8_t>(E); x.cHb[k] = dalloc<uint8_t>(E);
+    x.cGraftJoin[k] = dalloc<uint64_t>(E); x.cGraftHb[k] = dalloc<uint64_t>(E);
+    x.cPruneReply[k] = dalloc<uint64_t>(E); x.cPruneHb[k] = dalloc<uint64_t>(E);
+    x.cIhave[k] = dalloc<uint64_t>(E);
+    x.cIwant[k] = dalloc<int32_t>(E, 0xFF); x.cIresp[k] = dalloc<int32_t>(E, 0xFF);
+    chk(x.cPre[k]); chk(x.cHb[k]); chk(x.cGraftJoin[k]); chk(x.cGraftHb[k]); chk(x.cPruneReply[k]);
+    chk(x.cPruneHb[k]); chk(x.cIhave[k]); chk(x.cIwant[k]); chk(x.cIresp[k]);
+    x.pubmask[k] = dalloc<uint64_t>(W); chk(x.pubmask[k]);
+  }
+  x.score0 = dalloc<double>(E); x.score1 = dalloc<double>(E);
+  x.backoff = dalloc<int64_t>(TE);
+  x.fmd = dalloc<double>(TE); x.mmd = dalloc<double>(TE); x.mfp = dalloc<double>(TE); x.imd = dalloc<double>(TE);
+  x.graftTime = dalloc<int64_t>(TE); x.meshTime = dalloc<int64_t>(TE); x.flags = dalloc<uint8_t>(TE);
+  x.bp = dalloc<double>(E); x.peerhave = dalloc<int32_t>(E); x.iasked = dalloc<int32_t>(E);
+  chk(x.score0); chk(x.score1); chk(x.backoff); chk(x.fmd); chk(x.mmd); chk(x.mfp); chk(x.imd);
+  chk(x.graftTime); chk(x.meshTime); chk(x.flags); chk(x.bp); chk(x.peerhave); chk(x.iasked);
+  x.poolCap = cfg.router == GS_ROUTER_GOSSIPSUB ? 2 * N + 1024 : 1;
+  for (int k = 0; k < 2; ++k) { x.pool[k] = dalloc<uint64_t>((size_t)x.poolCap * W); chk(x.pool[k]); }
+  x.poolCnt = dalloc<int32_t>(2); chk(x.poolCnt);
+  x.slotSrc = dalloc<int32_t>(S, 0xFF); x.slotPubHop = dalloc<int64_t>(S); x.slotMid = dalloc<int64_t>(S, 0xFF);
+  chk(x.slotSrc); chk(x.slotPubHop); chk(x.slotMid);
+  x.ctr = dalloc<unsigned long long>(C_NCOUNTERS); x.err = dalloc<int32_t>(1);
+  chk(x.ctr); chk(x.err);
+  dScoreTmp = dalloc<double>(E); chk(dScoreTmp);
+  dHopOut = dalloc<int32_t>(N); dFromOut = dalloc<int32_t>(N); chk(dHopOut); chk(dFromOut);
+  if (!ok) {
+    gs_set_error("device allocation failed (state); reduce num_nodes or slots_per_topic");
+    return GS_ENOMEM;
+  }
+  {
+    std::vector<int64_t> lp((size_t)N * T, INT64_MIN);
+    HIPCHECK(hipMemcpyAsync(x.lastpub, lp.data(), lp.size() * 8, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
+  }
+  started = true;
+  return uploadMessages();
+}
+
+int gs_engine::uploadMessages() {
+  if (!started) return GS_OK;
+  const size_t n = mSrc.size();
+  if (n == uploaded) return GS_OK;
+  if (n > msgCap) {
+    size_t cap = std::max<size_t>(1024, n * 2);
+    int32_t *s = nullptr, *t = nullptr, *sl = nullptr;
+    int64_t* id = nullptr;
+    HIPCHECK(hipMalloc(&s, cap * 4));
+    HIPCHECK(hipMalloc(&t, cap * 4));
+    HIPCHECK(hipMalloc(&sl, cap * 4));
+    HIPCHECK(hipMalloc(&id, cap * 8));
+    allocs.push_back(s); allocs.push_back(t); allocs.push_back(sl); allocs.push_back(id);
+    d.mSrc = s; d.mTopic = t; d.mSlot = sl; d.mId = id;
+    msgCap = cap;
+    uploaded = 0;
+  }
+  const size_t k = n - uploaded;
+  HIPCHECK(hipMemcpyAsync((void*)(d.mSrc + uploaded), mSrc.data() + uploaded, k * 4, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipMemcpyAsync((void*)(d.mTopic + uploaded), mTopic.data() + uploaded, k * 4, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipMemcpyAsync((void*)(d.mSlot + uploaded), mSlot.data() + uploaded, k * 4, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipMemcpyAsync((void*)(d.mId + uploaded), mId.data() + uploaded, k * 8, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipStreamSynchronize(stream));
+  uploaded = n;
+  return GS_OK;
+}
+
+template <class F>
+static void launch_wpl(int W, F f) {
+  const int wpl = (W + 63) / 64;
+  switch (wpl) {
+    case 1: f(std::integral_constant<int, 1>()); break;
+    case 2: f(std::integral_constant<int, 2>()); break;
+    case 3: f(std::integral_constant<int, 3>()); break;
+    default: f(std::integral_constant<int, 4>()); break;
+  }
+}
+
+int gs_engine::stepOne() {
+  const int64_t h = hop;
+  const int64_t now = h * cfg.hop_ns;
+  const int cur = (int)(h & 1);
+  const bool gossip = cfg.router == GS_ROUTER_GOSSIPSUB;
+  // this hop's local publishes [b, e)
+  size_t b = nextMsg, e = b;
+  while (e < mHop.size() && mHop[e] == h) e++;
+  nextMsg = e;
+  const int n = (int)(e - b);
+  HIPCHECK(hipMemsetAsync(d.pubmask[cur], 0, (size_t)W * 8, stream));
+  HIPCHECK(hipMemsetAsync(d.poolCnt + cur, 0, 4, stream));
+  const unsigned eb = nblk(E, 256);
+  if (scoring) k_score<<<eb, 256, 0, stream>>>(d, d.score0);
+  if (h == 0 && gossip) k_join<<<N, 64, 0, stream>>>(d, h, now, cur);
+  if (gossip && !floodPublish && n > 0) {
+    // Publish to a topic we have not joined: fanout (gossipsub.go:977-994)
+    std::vector<int32_t> pairs;
+    std::vector<uint64_t> seenPair;
+    for (size_t i = b; i < e; ++i) {
+      const int src = mSrc[i], t = mTopic[i];
+      if ((sub[src] >> t) & 1) continue;
+      const uint64_t key = ((uint64_t)src << 6) | (uint64_t)t;
+      if (std::find(seenPair.begin(), seenPair.end(), key) != seenPair.end()) continue;
+      seenPair.push_back(key);
+      pairs.push_back(src);
+      pairs.push_back(t);
+    }
+    if (!pairs.empty()) {
+      const int np = (int)pairs.size() / 2;
+      if (np > pairCap) {
+        int32_t* p = nullptr;
+        HIPCHECK(hipMalloc(&p, (size_t)np * 2 * 4 * 2));
+        allocs.push_back(p);
+        dPairs = p;
+        pairCap = np * 2;
+      }
+      HIPCHECK(hipMemcpyAsync(dPairs, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, stream));
+      k_fanout_pub<<<np, 64, 0, stream>>>(d, dPairs, np, h, now);
+      HIPCHECK(hipStreamSynchronize(stream));  // `pairs` is pageable host memory
+    }
+  }
+  k_fwd<<<eb, 256, 0, stream>>>(d, cur);
+  if (n > 0) k_pubmask<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, cur);
+  launch_wpl(W, [&](auto wpl) { k_phase_a<decltype(wpl)::value><<<N, 64, 0, stream>>>(d, h, cur, head); });
+  if (n > 0) {
+    k_publish<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, h, cur, head);
+    if (cfg.router == GS_ROUTER_RANDOMSUB) k_publish_rs<<<n, 64, 0, stream>>>(d, (int)b);
+  }
+  if (gossip) {
+    if (scoring) k_score<<<eb, 256, 0, stream>>>(d, d.score1);
+    launch_wpl(W, [&](auto wpl) { k_phase_b<decltype(wpl)::value><<<N, 64, 0, stream>>>(d, h, now, cur, head); });
+  }
+  if (refreshDue(now)) k_refresh<<<eb, 256, 0, stream>>>(d, now);
+  if (heartbeatDue(now)) {
+    ticks++;
+    k_hb_pre<<<N, 64, 0, stream>>>(d, now, ticks);
+    if (scoring) k_score<<<eb, 256, 0, stream>>>(d, d.score1);
+    const int newhead = (head + R - 1) % R;
+    k_heartbeat<<<N, 64, 0, stream>>>(d, h, now, ticks, cur, head, newhead);
+    head = newhead;
+    heartbeats++;
+  }
+  HIPCHECK(hipGetLastError());
+  hop++;
+  return GS_OK;
+}
+
+int gs_engine::checkDeviceError() {
+  HIPCHECK(hipStreamSynchronize(stream));
+  int32_t err = 0;
+  HIPCHECK(hipMemcpy(&err, d.err, 4, hipMemcpyDeviceToHost));
+  switch (err) {
+    case E_NONE: return GS_OK;
+    case E_POOL: gs_set_error("IWANT record pool overflow"); return GS_ECAPACITY;
+    case E_PROMISES: gs_set_error("per-node promise table overflow (64 entries)"); return GS_ECAPACITY;
+    case E_PEERTX: gs_set_error("per-node IWANT retransmission table overflow (64 entries)"); return GS_ECAPACITY;
+    case E_LATE:
+      gs_set_error("a message was first delivered later than the message window allows; raise slots_per_topic");
+      return GS_ECAPACITY;
+    case E_TRUNCATE:
+      gs_set_error("IHAVE/IWANT truncation at MaxIHaveLength is not built in this version");
+      return GS_EUNSUPPORTED;
+    case E_DOUBLE:
+      gs_set_error("a peer sent the same message twice in one hop (outside the canonical model)");
+      return GS_EUNSUPPORTED;
+    default: gs_set_error("unknown device error"); return GS_EDEVICE;
+  }
+}
+
+extern "C" {
+
+const char* gs_last_error(void) { return g_err.c_str(); }
+
+int gs_engine_create(const gs_config* cfg, const gs_gossipsub_params* gsp, const gs_peer_score_params* psp,
+                     const gs_topic_score_params* topics, const uint8_t* topic_scored,
+                     const gs_peer_score_thresholds* thr, const gs_peer_gater_params* gater, gs_engine** out) {
+  (void)gater;
+  if (!cfg || !out) { gs_set_error("null argument"); return GS_EINVAL; }
+  if (cfg->num_nodes <= 0 || cfg->num_topics <= 0 || cfg->num_topics > 64 || cfg->hop_ns <= 0) {
+    gs_set_error("invalid config: num_nodes > 0, 1 <= num_topics <= 64, hop_ns > 0 required");
+    return GS_EINVAL;
+  }
+  if (cfg->router < 0 || cfg->router > 2) { gs_set_error("unknown router"); return GS_EINVAL; }
+  if (cfg->slots_per_topic <= 0 || cfg->slots_per_topic % 64 != 0) {
+    gs_set_error("slots_per_topic must be a positive multiple of 64");
+    return GS_EINVAL;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    gs_set_error("no HIP device available: the gossip engine needs an MI355X (gfx950)");
+    return GS_EDEVICE;
+  }
+  if (cfg->device < 0 || cfg->device >= ndev) { gs_set_error("bad device ordinal"); return GS_EINVAL; }
+  std::unique_ptr<gs_engine> g(new gs_engine());
+  g->cfg = *cfg;
+  g->N = cfg->num_nodes;
+  g->T = cfg->num_topics;
+  g->St = cfg->slots_per_topic;
+  g->Wt = g->St / 64;
+  g->W = g->T * g->Wt;
+  g->S = g->T * g->St;
+  if (g->W > 64 * GS_MAX_WPL) {
+    gs_set_error("num_topics * slots_per_topic must be <= 16384 in this build");
+    return GS_EUNSUPPORTED;
+  }
+  if (gsp) g->gp = *gsp; else gs_default_gossipsub_params(&g->gp);
+  g->scoring = (cfg->flags & GS_FLAG_SCORING) != 0 && cfg->router == GS_ROUTER_GOSSIPSUB;
+  g->floodPublish = (cfg->flags & GS_FLAG_FLOOD_PUBLISH) != 0;
+  g->tps.assign(g->T, gs_topic_score_params{});
+  g->tscored.assign(g->T, 0);
+  if (cfg->router == GS_ROUTER_GOSSIPSUB) {
+    const gs_gossipsub_params& p = g->gp;
+    if (p.HistoryGossip > p.HistoryLength || p.HistoryLength < 1) {
+      gs_set_error("invalid parameters for message cache; gossip slots cannot be larger than history slots");
+      return GS_EINVAL;
+    }
+    if (p.HeartbeatInterval % cfg->hop_ns != 0 || p.HeartbeatInterval < 2 * cfg->hop_ns ||
+        p.HeartbeatInitialDelay % cfg->hop_ns != 0 || p.HeartbeatInitialDelay < cfg->hop_ns) {
+      gs_set_error("HeartbeatInterval must be a multiple of hop_ns and >= 2 hops; "
+                   "HeartbeatInitialDelay a multiple of hop_ns and >= 1 hop");
+      return GS_EUNSUPPORTED;
+    }
+    if (p.GossipRetransmission < 0 || p.MaxIHaveMessages < 0 || p.D < 0 || p.Dhi < 0 || p.Dscore < 0 ||
+        p.Dscore > p.D || p.D > p.Dhi) {
+      gs_set_error("invalid gossipsub degree parameters");
+      return GS_EINVAL;
+    }
+    g->H = (int)(p.HeartbeatInterval / cfg->hop_ns);
+    g->R = p.HistoryLength + 1;  // + the ghost slot holding the just-shifted window
+  } else {
+    g->R = 1;
+  }
+  // message-window policy: a message must be first delivered within maxAge
+  // hops of its publish, and its slot is recycled only after retireHops
+  g->maxAge = 3 * g->H;
+  g->retireHops = g->maxAge + (int64_t)(g->gp.HistoryLength + 2) * g->H;
+  if (cfg->router != GS_ROUTER_GOSSIPSUB) g->retireHops = g->maxAge + 2;
+  if (g->maxAge > 30000) { gs_set_error("heartbeat interval too long in hops"); return GS_EUNSUPPORTED; }
+  if (g->scoring) {
+    if (!psp || !topics || !topic_scored || !thr) {
+      gs_set_error("scoring needs score params and thresholds");
+      return GS_EINVAL;
+    }
+    int rc = gs_validate_peer_score_params(psp, topics, topic_scored, g->T);
+    if (rc) return rc;
+    rc = gs_validate_thresholds(thr);
+    if (rc) return rc;
+    if (psp->DecayInterval % cfg->hop_ns != 0) {
+      gs_set_error("DecayInterval must be a multiple of hop_ns");
+      return GS_EUNSUPPORTED;
+    }
+    g->sp = *psp;
+    g->thr = *thr;
+    for (int t = 0; t < g->T; ++t) { g->tps[t] = topics[t]; g->tscored[t] = topic_scored[t]; }
+  }
+  g->topicCounter.assign(g->T, 0);
+  g->slotOwnerHop.assign(g->S, INT64_MIN);
+  g->slotOwnerId.assign(g->S, -1);
+  *out = g.release();
+  return GS_OK;
+}
+
+int gs_engine_destroy(gs_engine* eng) {
+  delete eng;
+  return GS_OK;
+}
+
+int gs_set_graph(gs_engine* g, const int64_t* rowptr, const int32_t* col, const uint8_t* outbound,
+                 const uint8_t* direct) {
+  if (g->started) { gs_set_error("graph must be set before the first step"); return GS_ESTATE; }
+  g->rowptr.assign(rowptr, rowptr + g->N + 1);
+  g->E = g->rowptr[g->N];
+  g->col.assign(col, col + g->E);
+  for (int u = 0; u < g->N; ++u)
+    for (int64_t e = g->rowptr[u]; e < g->rowptr[u + 1]; ++e) {
+      const int v = g->col[e];
+      if (v < 0 || v >= g->N || v == u || (e > g->rowptr[u] && g->col[e - 1] >= v)) {
+        gs_set_error("graph rows must hold strictly ascending neighbour ids != self");
+        return GS_EINVAL;
+      }
+    }
+  g->outbound.assign(g->E, 0);
+  g->direct.assign(g->E, 0);
+  if (outbound) g->outbound.assign(outbound, outbound + g->E);
+  if (direct) g->direct.assign(direct, direct + g->E);
+  g->graphSet = true;
+  return GS_OK;
+}
+
+int gs_set_subscriptions(gs_engine* g, const uint64_t* sub_mask) {
+  if (g->started) { gs_set_error("subscriptions must be set before the first step"); return GS_ESTATE; }
+  g->sub.assign(sub_mask, sub_mask + g->N);
+  return GS_OK;
+}
+
+int gs_set_peer_attrs(gs_engine* g, const double* app_score, const uint32_t* ipv4) {
+  if (g->started) { gs_set_error("peer attributes must be set before the first step"); return GS_ESTATE; }
+  if (app_score) g->app.assign(app_score, app_score + g->N);
+  if (ipv4) g->ipv4.assign(ipv4, ipv4 + g->N);
+  return GS_OK;
+}
+
+int gs_set_ip_whitelist(gs_engine* g, int32_t n, const uint32_t* net, const uint32_t* mask) {
+  if (g->started) { gs_set_error("whitelist must be set before the first step"); return GS_ESTATE; }
+  g->whitelist.clear();
+  for (int i = 0; i < n; ++i) g->whitelist.push_back({net[i], mask[i]});
+  return GS_OK;
+}
+
+int gs_publish(gs_engine* g, int32_t n, const int32_t* src, const int32_t* topic, const int64_t* hop,
+               int64_t* ids_out) {
+  int64_t last = g->mHop.empty() ? g->hop : std::max(g->hop, g->mHop.back());
+  for (int i = 0; i < n; ++i) {
+    if (src[i] < 0 || src[i] >= g->N || topic[i] < 0 || topic[i] >= g->T || hop[i] < last) {
+      gs_set_error("publish: bad src/topic or hop not non-decreasing from the current hop");
+      return GS_EINVAL;
+    }
+    last = hop[i];
+  }
+  // assign message-window slots; a slot is recycled only after retireHops
+  std::vector<int64_t> cnt = g->topicCounter, owner = g->slotOwnerHop;
+  std::vector<int32_t> slots(n);
+  for (int i = 0; i < n; ++i) {
+    const int t = topic[i];
+    const int slot = t * g->St + (int)(cnt[t] % g->St);
+    cnt[t]++;
+    if (owner[slot] != INT64_MIN && hop[i] - owner[slot] < g->retireHops) {
+      gs_set_error("message window too small: more than slots_per_topic messages of one topic within " +
+                   std::to_string(g->retireHops) + " hops");
+      return GS_ECAPACITY;
+    }
+    owner[slot] = hop[i];
+    slots[i] = slot;
+  }
+  g->topicCounter = cnt;
+  g->slotOwnerHop = owner;
+  for (int i = 0; i < n; ++i) {
+    const int64_t id = (int64_t)g->mSrc.size();
+    g->mSrc.push_back(src[i]);
+    g->mTopic.push_back(topic[i]);
+    g->mSlot.push_back(slots[i]);
+    g->mId.push_back(id);
+    g->mHop.push_back(hop[i]);
+    g->slotOwnerId[slots[i]] = id;
+    if (ids_out) ids_out[i] = id;
+  }
+  return g->uploadMessages();
+}
+
+int gs_step(gs_engine* g, int64_t hops) {
+  if (!g->graphSet) { gs_set_error("graph not set"); return GS_ESTATE; }
+  if (!g->started) {
+    int rc = g->start();
+    if (rc) return rc;
+  }
+  for (int64_t i = 0; i < hops; ++i) {
+    int rc = g->stepOne();
+    if (rc) return rc;
+  }
+  return g->checkDeviceError();
+}
+
+int gs_sync(gs_engine* g) {
+  if (!g->started) return GS_OK;
+  HIPCHECK(hipStreamSynchronize(g->stream));
+  return GS_OK;
+}
+
+int gs_set_topic_score_params(gs_engine* g, int32_t topic, const gs_topic_score_params* p) {
+  if (topic < 0 || topic >= g->T) { gs_set_error("bad topic"); return GS_EINVAL; }
+  int rc = gs_validate_topic_score_params(p);
+  if (rc) return rc;
+  const bool existed = g->tscored[topic] != 0;
+  const gs_topic_score_params old = g->tps[topic];
+  g->tps[topic] = *p;
+  g->tscored[topic] = 1;
+  if (!g->started) return GS_OK;
+  TopicP tp = to_dev(*p, g->scoring);
+  HIPCHECK(hipMemcpyAsync(g->dTp + topic, &tp, sizeof(TopicP), hipMemcpyHostToDevice, g->stream));
+  if (existed && g->scoring &&
+      (p->FirstMessageDeliveriesCap < old.FirstMessageDeliveriesCap ||
+       p->MeshMessageDeliveriesCap < old.MeshMessageDeliveriesCap))
+    k_recap<<<nblk(g->E, 256), 256, 0, g->stream>>>(g->d, topic, p->FirstMessageDeliveriesCap,
+                                                    p->MeshMessageDeliveriesCap);
+  HIPCHECK(hipStreamSynchronize(g->stream));
+  return GS_OK;
+}
+
+int64_t gs_num_edges(const gs_engine* g) { return g->E; }
+int64_t gs_current_hop(const gs_engine* g) { return g->hop; }
+
+int gs_read_counters(gs_engine* g, gs_counters* out) {
+  std::memset(out, 0, sizeof(*out));
+  if (g->started) {
+    unsigned long long c[C_NCOUNTERS];
+    HIPCHECK(hipStreamSynchronize(g->stream));
+    HIPCHECK(hipMemcpy(c, g->d.ctr, sizeof(c), hipMemcpyDeviceToHost));
+    out->published = (int64_t)c[C_PUBLISHED];
+    out->deliveries = (int64_t)c[C_DELIVERIES];
+    out->duplicates = (int64_t)c[C_DUPLICATES];
+    out->transmissions = (int64_t)c[C_TRANSMISSIONS];
+    out->grafts_sent = (int64_t)c[C_GRAFTS];
+    out->prunes_sent = (int64_t)c[C_PRUNES];
+    out->ihave_sent = (int64_t)c[C_IHAVE];
+    out->iwant_sent = (int64_t)c[C_IWANT_SENT];
+    out->iwant_served = (int64_t)c[C_IWANT_SERVED];
+    out->promises_broken = (int64_t)c[C_PROMISES_BROKEN];
+    out->graylisted = (int64_t)c[C_GRAYLISTED];
+  }
+  out->hops = g->hop;
+  out->heartbeats = g->heartbeats;
+  return GS_OK;
+}
+
+#define NEED_STARTED(g)                        \
+  do {                                         \
+    if (!(g)->started) {                       \
+      int _rc = (g)->start();                  \
+      if (_rc) return _rc;                     \
+    }                                          \
+  } while (0)
+
+int gs_read_scores(gs_engine* g, double* score) {
+  if (!g->graphSet) { gs_set_error("graph not set"); return GS_ESTATE; }
+  NEED_STARTED(g);
+  k_score<<<nblk(g->E, 256), 256, 0, g->stream>>>(g->d, g->dScoreTmp);
+  HIPCHECK(hipMemcpyAsync(score, g->dScoreTmp, g->E * 8, hipMemcpyDeviceToHost, g->stream));
+  HIPCHECK(hipStreamSynchronize(g->stream));
+  return GS_OK;
+}
+
+static int copy_back(gs_engine* g, void* dst, const void* src, size_t bytes) {
+  if (!g->started) {
+    std::memset(dst, 0, bytes);
+    return GS_OK;
+  }
+  HIPCHECK(hipStreamSynchronize(g->stream));
+  HIPCHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return GS_OK;
+}
+
+int gs_read_mesh(gs_engine* g, uint64_t* mesh) { return copy_back(g, mesh, g->d.mesh, g->E * 8); }
+int gs_read_fanout(gs_engine* g, uint64_t* fanout) { return copy_back(g, fanout, g->d.fanout, g->E * 8); }
+int gs_read_backoff(gs_engine* g, int64_t* expire) {
+  return copy_back(g, expire, g->d.backoff, (size_t)g->T * g->E * 8);
+}
+int gs_read_topic_stats(gs_engine* g, double* fmd, double* mmd, double* mfp, double* imd, int64_t* mesh_time,
+                        int64_t* graft_time, uint8_t* flags) {
+  const size_t n = (size_t)g->T * g->E;
+  int rc;
+  if ((rc = copy_back(g, fmd, g->d.fmd, n * 8))) return rc;
+  if ((rc = copy_back(g, mmd, g->d.mmd, n * 8))) return rc;
+  if ((rc = copy_back(g, mfp, g->d.mfp, n * 8))) return rc;
+  if ((rc = copy_back(g, imd, g->d.imd, n * 8))) return rc;
+  if ((rc = copy_back(g, mesh_time, g->d.meshTime, n * 8))) return rc;
+  if ((rc = copy_back(g, graft_time, g->d.graftTime, n * 8))) return rc;
+  return copy_back(g, flags, g->d.flags, n);
+}
+int gs_read_behaviour_penalty(gs_engine* g, double* bp) { return copy_back(g, bp, g->d.bp, g->E * 8); }
+
+int gs_read_deliveries(gs_engine* g, int64_t id, int32_t* hop, int32_t* from) {
+  if (id < 0 || id >= (int64_t)g->mId.size()) { gs_set_error("unknown message id"); return GS_EINVAL; }
+  const int slot = g->mSlot[id];
+  if (g->slotOwnerId[slot] != id) {
+    gs_set_error("message slot already recycled (window moved on)");
+    return GS_ESTATE;
+  }
+  if (!g->started || g->mHop[id] >= g->hop) {
+    for (int v = 0; v < g->N; ++v) { hop[v] = -1; from[v] = -1; }
+    return GS_OK;
+  }
+  k_read_deliv<<<nblk(g->N, 256), 256, 0, g->stream>>>(g->d, slot, g->mHop[id], g->dHopOut, g->dFromOut);
+  HIPCHECK(hipMemcpyAsync(hop, g->dHopOut, (size_t)g->N * 4, hipMemcpyDeviceToHost, g->stream));
+  HIPCHECK(hipMemcpyAsync(from, g->dFromOut, (size_t)g->N * 4, hipMemcpyDeviceToHost, g->stream));
+  HIPCHECK(hipStreamSynchronize(g->stream));
+  return GS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,141 @@
+"""Seeded simulation scenarios shared by the oracle tests (CPU) and the GPU
+parity tests.  Each builder takes the ABI library path so the same calls
+drive the oracle and the HIP engine; `compare()` checks every readback
+bit-exactly (float64 compared on their bit patterns)."""
+import numpy as np
+
+from pubsub_amd import (NewFloodSub, NewGossipSub, NewRandomSub, PeerScoreParams, Second,
+                        TopicScoreParams, WithFloodPublish, WithGossipSubParams, WithHop,
+                        WithMessageWindow, WithPeerScore, WithRecordDeliveries, WithSeed,
+                        eth2_peer_score_params, eth2_thresholds, eth2_topic_score_params)
+from pubsub_amd import graphs
+from pubsub_amd.params import GossipSubParams, Millisecond, PeerScoreThresholds
+
+HOP = 100 * Millisecond
+
+
+def _publish_schedule(n, topics, count, start, every, seed, srcs=None):
+    rng = np.random.default_rng(seed)
+    src = rng.integers(0, n, count) if srcs is None else rng.choice(srcs, count)
+    top = rng.integers(0, topics, count)
+    hops = start + np.arange(count) * every if every else np.full(count, start)
+    return src.astype(np.int32), top.astype(np.int32), np.asarray(hops, dtype=np.int64)
+
+
+def floodsub_dense(lib, seed=1):
+    """TestFloodsubDense-like: 20 hosts, denseConnect, 100 messages."""
+    n = 20
+    g = graphs.dense_connect(n, seed)
+    e = NewFloodSub(n, 1, g, graphs.all_subscribed(n, 1), WithRecordDeliveries(), WithSeed(seed),
+                    WithMessageWindow(128), lib=lib)
+    src, top, hops = _publish_schedule(n, 1, 100, 1, 2, seed)
+    e.publish(src, top, hops)
+    return e, int(hops[-1]) + 20
+
+
+def randomsub(lib, size, n=200, k=16, seed=2, msgs=60):
+    g = graphs.random_regular(n, k, seed)
+    e = NewRandomSub(n, 1, g, graphs.all_subscribed(n, 1), size, WithRecordDeliveries(), WithSeed(seed),
+                     WithMessageWindow(128), lib=lib)
+    src, top, hops = _publish_schedule(n, 1, msgs, 0, 1, seed)
+    e.publish(src, top, hops)
+    return e, int(hops[-1]) + 20
+
+
+def gossipsub_dense(lib, seed=1, msgs=100):
+    """TestDenseGossipsub (gossipsub_test.go:84-123): 20 hosts, denseConnect,
+    2 s of heartbeats, then 100 messages from random owners."""
+    n = 20
+    g = graphs.dense_connect(n, seed)
+    e = NewGossipSub(n, 1, g, graphs.all_subscribed(n, 1), WithRecordDeliveries(), WithSeed(seed),
+                     WithHop(HOP), WithMessageWindow(256), lib=lib)
+    src, top, hops = _publish_schedule(n, 1, msgs, 20, 1, seed)
+    e.publish(src, top, hops)
+    return e, int(hops[-1]) + 40
+
+
+def gossipsub_scored(lib, n=300, k=20, topics=1, seed=3, msgs=300, hb=12, flood=False, sub_frac=1.0,
+                     app_neg_frac=0.0, ip_groups=0, params=None, window=256):
+    """gossipsub v1.1 with Eth2-derived scoring over a random regular graph."""
+    rng = np.random.default_rng(seed)
+    g = graphs.random_regular(n, k, seed)
+    if sub_frac >= 1.0:
+        subs = graphs.all_subscribed(n, topics)
+    else:
+        subs = np.zeros(n, dtype=np.uint64)
+        for t in range(topics):
+            subs |= (rng.random(n) < sub_frac).astype(np.uint64) << np.uint64(t)
+    sp = eth2_peer_score_params(topics)
+    thr = eth2_thresholds()
+    app = np.zeros(n)
+    if app_neg_frac:
+        app[rng.random(n) < app_neg_frac] = -150.0
+    ipv4 = None
+    if ip_groups:
+        ipv4 = (rng.integers(0, ip_groups, n) + (10 << 24)).astype(np.uint32)
+    opts = [WithPeerScore(sp, thr), WithRecordDeliveries(), WithSeed(seed), WithHop(HOP),
+            WithMessageWindow(window)]
+    if params is not None:
+        opts.append(WithGossipSubParams(params))
+    if flood:
+        opts.append(WithFloodPublish(True))
+    e = NewGossipSub(n, topics, g, subs, *opts, app_score=app, ipv4=ipv4, lib=lib)
+    rng2 = np.random.default_rng(seed + 100)
+    src = rng2.integers(0, n, msgs).astype(np.int32)
+    top = rng2.integers(0, topics, msgs).astype(np.int32)
+    hops = (5 + (np.arange(msgs) * (hb * 10 - 20)) // msgs).astype(np.int64)
+    e.publish(src, top, hops)
+    return e, hb * 10 + 5
+
+
+SCENARIOS = {
+    "floodsub_dense": lambda lib: floodsub_dense(lib),
+    "randomsub_100": lambda lib: randomsub(lib, 100),
+    "randomsub_N": lambda lib: randomsub(lib, 200),
+    "gossipsub_dense": lambda lib: gossipsub_dense(lib),
+    "gossipsub_scored": lambda lib: gossipsub_scored(lib),
+    "gossipsub_flood_publish": lambda lib: gossipsub_scored(lib, n=200, flood=True, seed=5),
+    "gossipsub_multitopic": lambda lib: gossipsub_scored(lib, n=200, topics=3, sub_frac=0.7, seed=7, msgs=240),
+    "gossipsub_negative_app": lambda lib: gossipsub_scored(lib, n=200, app_neg_frac=0.2, ip_groups=40, seed=9),
+    "gossipsub_dense_dhi": lambda lib: gossipsub_scored(lib, n=120, k=40, seed=11, hb=20, msgs=200),
+}
+
+
+def snapshot(e, msg_ids):
+    out = dict(counters=e.counters(), mesh=e.mesh(), fanout=e.fanout(), backoff=e.backoff(),
+               scores=e.scores(), bp=e.behaviour_penalty())
+    out.update({"ts_" + k: v for k, v in e.topic_stats().items()})
+    out["deliv"] = [e.deliveries(i) for i in msg_ids]
+    return out
+
+
+def run(lib, name, extra_hops=0):
+    e, hops = SCENARIOS[name](lib)
+    e.step(hops + extra_hops)
+    ids = range(int(e.counters()["published"]))
+    return snapshot(e, ids)
+
+
+def _bits(a):
+    a = np.asarray(a)
+    return a.view(np.uint64) if a.dtype == np.float64 else a
+
+
+def compare(a, b):
+    """Returns a list of human-readable mismatches (empty = bit-exact)."""
+    bad = []
+    for k in a:
+        if k == "counters":
+            if a[k] != b[k]:
+                bad.append(f"counters: {a[k]} != {b[k]}")
+        elif k == "deliv":
+            for i, ((h1, f1), (h2, f2)) in enumerate(zip(a[k], b[k])):
+                if not (np.array_equal(h1, h2) and np.array_equal(f1, f2)):
+                    bad.append(f"deliveries of message {i} differ")
+                    break
+        else:
+            x, y = _bits(a[k]), _bits(b[k])
+            if not np.array_equal(x, y):
+                idx = np.argwhere(x != y)[:5]
+                bad.append(f"{k}: {int((x != y).sum())} mismatches, first at {idx.tolist()}")
+    return bad
