@@ -168,7 +168,7 @@ typedef struct gs_counters {
   int64_t published;       /* local publishes (PublishMessage)               */
   int64_t deliveries;      /* first deliveries (DeliverMessage)              */
   int64_t duplicates;      /* duplicate receptions (DuplicateMessage)        */
-  int64_t transmissions;   /* message copies sent over edges, dups included */
+  int64_t transmissions;   /* message copies delivered over edges (counted on arrival), dups included */
   int64_t grafts_sent;     /* GRAFT control entries sent                     */
   int64_t prunes_sent;     /* PRUNE control entries sent                     */
   int64_t ihave_sent;      /* IHAVE control entries sent (one per topic)     */

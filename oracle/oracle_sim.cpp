@@ -145,7 +145,6 @@ void Node::sendRPC(int p, RPC rpc) {
     rpc.ctl.ihave = g->second;
     gossip.erase(g);
   }
-  sim->ctr.transmissions += (int64_t)rpc.publish.size();
   sim->ctr.grafts_sent += (int64_t)rpc.ctl.graft.size();
   sim->ctr.prunes_sent += (int64_t)rpc.ctl.prune.size();
   sim->ctr.ihave_sent += (int64_t)rpc.ctl.ihave.size();
@@ -716,7 +715,13 @@ void Sim::start() {
 
 void Sim::step() {
   const int64_t t = now();
-  if (hop == 0) {
+  // the RPCs sent during hop h-1 are this hop's inbox
+  std::vector<std::map<int, std::vector<RPC>>> inbox(N);
+  for (Node& nd : nodes) {
+    for (auto& kv : nd.out) inbox[kv.first][nd.id] = std::move(kv.second);
+    nd.out.clear();
+  }
+  if (hop == 0) {  // Join: the GRAFTs it sends arrive in hop 1
     for (int u = 0; u < N; ++u)
       for (int tp = 0; tp < T; ++tp)
         if ((nodes[u].mySubs >> tp) & 1) nodes[u].join(tp);
@@ -727,12 +732,6 @@ void Sim::step() {
       nd.memo.clear();
       for (int v : nd.nbrs) nd.memo[v] = nd.score.score(v);
     }
-  // the RPCs sent during hop h-1 are this hop's inbox
-  std::vector<std::map<int, std::vector<RPC>>> inbox(N);
-  for (Node& nd : nodes) {
-    for (auto& kv : nd.out) inbox[kv.first][nd.id] = std::move(kv.second);
-    nd.out.clear();
-  }
   // local publishes of this hop
   while (nextPub < msgs.size() && msgHop[nextPub] == hop) {
     const Msg& m = msgs[nextPub];
@@ -750,6 +749,7 @@ void Sim::step() {
         else if (scoring && nd.memo[s] < thr.GraylistThreshold) st = PeerGater::AcceptNone;
       }
       nd.acceptStatus[s] = st;
+      for (const RPC& r : kv.second) ctr.transmissions += (int64_t)r.publish.size();  // copies on the wire
       if (st == PeerGater::AcceptNone) { ctr.graylisted += (int64_t)kv.second.size(); continue; }
       for (const RPC& r : kv.second)
         for (int64_t mid : r.publish) nd.handleMessage(s, msgs[mid]);

@@ -55,7 +55,7 @@ def gossipsub_dense(lib, seed=1, msgs=100):
 
 
 def gossipsub_scored(lib, n=300, k=20, topics=1, seed=3, msgs=300, hb=12, flood=False, sub_frac=1.0,
-                     app_neg_frac=0.0, ip_groups=0, params=None, window=256):
+                     app_neg_frac=0.0, ip_groups=0, params=None, window=1024):
     """gossipsub v1.1 with Eth2-derived scoring over a random regular graph."""
     rng = np.random.default_rng(seed)
     g = graphs.random_regular(n, k, seed)
