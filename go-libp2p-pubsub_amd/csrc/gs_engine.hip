@@ -74,8 +74,33 @@ struct gs_engine {
   int pairCap = 0;
   double* dScoreTmp = nullptr;
   int32_t *dHopOut = nullptr, *dFromOut = nullptr;
+  // kernel timing: (kernel id, start event, end event) pending until a sync
+  bool profiling = false;
+  std::vector<hipEvent_t> evPool;
+  size_t evUsed = 0;
+  std::vector<int> pendKid;
+  double kMs[GS_NUM_KERNELS] = {0};
+  int64_t kLaunches[GS_NUM_KERNELS] = {0};
+  hipEvent_t nextEvent() {
+    if (evUsed == evPool.size()) {
+      hipEvent_t ev;
+      (void)hipEventCreate(&ev);
+      evPool.push_back(ev);
+    }
+    return evPool[evUsed++];
+  }
+  void resolveTimings() {  // call after a stream sync
+    for (size_t i = 0; i < pendKid.size(); ++i) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, evPool[2 * i], evPool[2 * i + 1]) == hipSuccess) kMs[pendKid[i]] += ms;
+      kLaunches[pendKid[i]]++;
+    }
+    pendKid.clear();
+    evUsed = 0;
+  }
 
   ~gs_engine() {
+    for (hipEvent_t ev : evPool) (void)hipEventDestroy(ev);
     for (void* p : allocs) (void)hipFree(p);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -124,6 +149,21 @@ static TopicP to_dev(const gs_topic_score_params& p, bool scored) {
 }
 
 static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+// Launch `stmt` on g's stream; with profiling on, bracket it with HIP events
+// recorded on that same stream (so the measured interval is the kernel's).
+#define TIMED(g, kid, stmt)                                   \
+  do {                                                        \
+    if ((g)->profiling) {                                     \
+      hipEvent_t _a = (g)->nextEvent(), _b = (g)->nextEvent(); \
+      (void)hipEventRecord(_a, (g)->stream);                  \
+      stmt;                                                   \
+      (void)hipEventRecord(_b, (g)->stream);                  \
+      (g)->pendKid.push_back(kid);                            \
+    } else {                                                  \
+      stmt;                                                   \
+    }                                                         \
+  } while (0)
 
 int gs_engine::start() {
   HIPCHECK(hipSetDevice(cfg.device));
@@ -346,8 +386,8 @@ int gs_engine::stepOne() {
   HIPCHECK(hipMemsetAsync(d.pubmask[cur], 0, (size_t)W * 8, stream));
   HIPCHECK(hipMemsetAsync(d.poolCnt + cur, 0, 4, stream));
   const unsigned eb = nblk(E, 256);
-  if (scoring) k_score<<<eb, 256, 0, stream>>>(d, d.score0);
-  if (h == 0 && gossip) k_join<<<N, 64, 0, stream>>>(d, h, now, cur);
+  if (scoring) TIMED(this, GS_K_SCORE, (k_score<<<eb, 256, 0, stream>>>(d, d.score0)));
+  if (h == 0 && gossip) TIMED(this, GS_K_JOIN, (k_join<<<N, 64, 0, stream>>>(d, h, now, cur)));
   if (gossip && !floodPublish && n > 0) {
     // Publish to a topic we have not joined: fanout (gossipsub.go:977-994)
     std::vector<int32_t> pairs;
@@ -371,28 +411,30 @@ int gs_engine::stepOne() {
         pairCap = np * 2;
       }
       HIPCHECK(hipMemcpyAsync(dPairs, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, stream));
-      k_fanout_pub<<<np, 64, 0, stream>>>(d, dPairs, np, h, now);
+      TIMED(this, GS_K_FANOUT, (k_fanout_pub<<<np, 64, 0, stream>>>(d, dPairs, np, h, now)));
       HIPCHECK(hipStreamSynchronize(stream));  // `pairs` is pageable host memory
     }
   }
-  k_fwd<<<eb, 256, 0, stream>>>(d, cur);
+  TIMED(this, GS_K_FWD, (k_fwd<<<eb, 256, 0, stream>>>(d, cur)));
   if (n > 0) k_pubmask<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, cur);
-  launch_wpl(W, [&](auto wpl) { k_phase_a<decltype(wpl)::value><<<N, 64, 0, stream>>>(d, h, cur, head); });
+  TIMED(this, GS_K_PHASE_A,
+        launch_wpl(W, [&](auto wpl) { k_phase_a<decltype(wpl)::value><<<N, 64, 0, stream>>>(d, h, cur, head); }));
   if (n > 0) {
-    k_publish<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, h, cur, head);
+    TIMED(this, GS_K_PUBLISH, (k_publish<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, h, cur, head)));
     if (cfg.router == GS_ROUTER_RANDOMSUB) k_publish_rs<<<n, 64, 0, stream>>>(d, (int)b);
   }
   if (gossip) {
-    if (scoring) k_score<<<eb, 256, 0, stream>>>(d, d.score1);
-    launch_wpl(W, [&](auto wpl) { k_phase_b<decltype(wpl)::value><<<N, 64, 0, stream>>>(d, h, now, cur, head); });
+    if (scoring) TIMED(this, GS_K_SCORE, (k_score<<<eb, 256, 0, stream>>>(d, d.score1)));
+    TIMED(this, GS_K_PHASE_B,
+          launch_wpl(W, [&](auto wpl) { k_phase_b<decltype(wpl)::value><<<N, 64, 0, stream>>>(d, h, now, cur, head); }));
   }
-  if (refreshDue(now)) k_refresh<<<eb, 256, 0, stream>>>(d, now);
+  if (refreshDue(now)) TIMED(this, GS_K_REFRESH, (k_refresh<<<eb, 256, 0, stream>>>(d, now)));
   if (heartbeatDue(now)) {
     ticks++;
-    k_hb_pre<<<N, 64, 0, stream>>>(d, now, ticks);
-    if (scoring) k_score<<<eb, 256, 0, stream>>>(d, d.score1);
+    TIMED(this, GS_K_HB_PRE, (k_hb_pre<<<N, 64, 0, stream>>>(d, now, ticks)));
+    if (scoring) TIMED(this, GS_K_SCORE, (k_score<<<eb, 256, 0, stream>>>(d, d.score1)));
     const int newhead = (head + R - 1) % R;
-    k_heartbeat<<<N, 64, 0, stream>>>(d, h, now, ticks, cur, head, newhead);
+    TIMED(this, GS_K_HEARTBEAT, (k_heartbeat<<<N, 64, 0, stream>>>(d, h, now, ticks, cur, head, newhead)));
     head = newhead;
     heartbeats++;
   }
@@ -403,6 +445,7 @@ int gs_engine::stepOne() {
 
 int gs_engine::checkDeviceError() {
   HIPCHECK(hipStreamSynchronize(stream));
+  resolveTimings();
   int32_t err = 0;
   HIPCHECK(hipMemcpy(&err, d.err, 4, hipMemcpyDeviceToHost));
   switch (err) {
@@ -612,6 +655,10 @@ int gs_step(gs_engine* g, int64_t hops) {
   for (int64_t i = 0; i < hops; ++i) {
     int rc = g->stepOne();
     if (rc) return rc;
+    if (g->pendKid.size() > 4096) {
+      HIPCHECK(hipStreamSynchronize(g->stream));
+      g->resolveTimings();
+    }
   }
   return g->checkDeviceError();
 }
@@ -729,6 +776,25 @@ int gs_read_deliveries(gs_engine* g, int64_t id, int32_t* hop, int32_t* from) {
   HIPCHECK(hipMemcpyAsync(hop, g->dHopOut, (size_t)g->N * 4, hipMemcpyDeviceToHost, g->stream));
   HIPCHECK(hipMemcpyAsync(from, g->dFromOut, (size_t)g->N * 4, hipMemcpyDeviceToHost, g->stream));
   HIPCHECK(hipStreamSynchronize(g->stream));
+  return GS_OK;
+}
+
+int gs_set_profiling(gs_engine* g, int on) {
+  if (g->started) {
+    HIPCHECK(hipStreamSynchronize(g->stream));
+    g->resolveTimings();
+  }
+  g->profiling = on != 0;
+  for (int i = 0; i < GS_NUM_KERNELS; ++i) { g->kMs[i] = 0; g->kLaunches[i] = 0; }
+  return GS_OK;
+}
+
+int gs_read_kernel_stats(gs_engine* g, double* total_ms, int64_t* launches) {
+  if (g->started) {
+    HIPCHECK(hipStreamSynchronize(g->stream));
+    g->resolveTimings();
+  }
+  for (int i = 0; i < GS_NUM_KERNELS; ++i) { total_ms[i] = g->kMs[i]; launches[i] = g->kLaunches[i]; }
   return GS_OK;
 }
 

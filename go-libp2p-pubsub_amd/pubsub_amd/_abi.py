@@ -137,7 +137,12 @@ ABI_FUNCTIONS = [
       C.POINTER(i64), C.POINTER(u8)]),
     ("gs_read_behaviour_penalty", C.c_int, [P, C.POINTER(f64)]),
     ("gs_read_deliveries", C.c_int, [P, i64, C.POINTER(i32), C.POINTER(i32)]),
+    ("gs_set_profiling", C.c_int, [P, C.c_int]),
+    ("gs_read_kernel_stats", C.c_int, [P, C.POINTER(f64), C.POINTER(i64)]),
 ]
+
+KERNEL_NAMES = ["score", "refresh", "join", "fanout", "fwd", "phase_a", "publish", "phase_b",
+                "hb_pre", "heartbeat"]
 
 
 def bind(path):

@@ -223,6 +223,17 @@ class Engine:
         _check(self.lib, self.lib.gs_read_behaviour_penalty(self.h, _ptr(a, C.c_double)))
         return a
 
+    def set_profiling(self, on=True):
+        _check(self.lib, self.lib.gs_set_profiling(self.h, 1 if on else 0))
+
+    def kernel_stats(self):
+        """{kernel: (total_ms, launches)} accumulated since set_profiling(True)."""
+        n = len(_abi.KERNEL_NAMES)
+        ms = np.zeros(n, dtype=np.float64)
+        cnt = np.zeros(n, dtype=np.int64)
+        _check(self.lib, self.lib.gs_read_kernel_stats(self.h, _ptr(ms, C.c_double), _ptr(cnt, C.c_int64)))
+        return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(_abi.KERNEL_NAMES)}
+
     def deliveries(self, msg_id):
         hop = np.empty(self.N, dtype=np.int32)
         frm = np.empty(self.N, dtype=np.int32)

@@ -260,6 +260,25 @@ int gs_read_behaviour_penalty(gs_engine* eng, double* bp /*[E]*/);
 int gs_read_deliveries(gs_engine* eng, int64_t id, int32_t* hop /*[N]*/,
                        int32_t* from /*[N]*/);
 
+/* ---- kernel timing (HIP events on the engine's stream) ----------------- */
+/* Kernel classes timed when profiling is on (gs_set_profiling(eng, 1)). */
+#define GS_K_SCORE 0     /* peerScore.score over all edges              */
+#define GS_K_REFRESH 1   /* refreshScores decay                          */
+#define GS_K_JOIN 2      /* Join at hop 0                                */
+#define GS_K_FANOUT 3    /* publish-time fanout creation                 */
+#define GS_K_FWD 4       /* forwarding-target snapshot                   */
+#define GS_K_PHASE_A 5   /* payload messages (propagation hop)           */
+#define GS_K_PUBLISH 6   /* local publish bookkeeping                    */
+#define GS_K_PHASE_B 7   /* HandleRPC control processing                 */
+#define GS_K_HB_PRE 8    /* heartbeat prelude (backoff, penalties)       */
+#define GS_K_HEARTBEAT 9 /* mesh maintenance + emitGossip + mcache shift */
+#define GS_NUM_KERNELS 10
+/* Starts/stops per-kernel timing and clears the accumulators.  The oracle
+ * accepts the call and reports zeros. */
+int gs_set_profiling(gs_engine* eng, int on);
+/* total_ms[GS_NUM_KERNELS], launches[GS_NUM_KERNELS] since gs_set_profiling(1). */
+int gs_read_kernel_stats(gs_engine* eng, double* total_ms, int64_t* launches);
+
 #ifdef __cplusplus
 }
 #endif
