@@ -13,7 +13,8 @@
 
 #define GS_WAVE 64
 #define GS_MAX_WPL 4   // words per lane in the node-wave kernels: W <= 256
-#define GS_TABLE 64    // promise / IWANT-retransmission table entries per node (one per lane)
+#define GS_TABLE 64    // promise table entries per node (one per lane)
+#define GS_PTX 512     // IWANT-retransmission (mcache peertx) entries per node
 
 // device counter slots (same order as gs_counters)
 enum {
@@ -77,10 +78,7 @@ struct Dev {
   int32_t* promSlot;
   uint8_t* promEdge;
   int32_t* promN;
-  int64_t* ptxMid;   // [N][64]
-  int32_t* ptxSlot;
-  int32_t* ptxCnt;
-  uint8_t* ptxEdge;
+  uint64_t* ptx;     // [N][GS_PTX] packed (slot << 32 | edge << 8 | count)
   int32_t* ptxN;
   // per-edge state
   uint64_t* mesh;
@@ -104,11 +102,11 @@ struct Dev {
   uint64_t* cPruneReply[2];
   uint64_t* cPruneHb[2];
   uint64_t* cIhave[2];
-  int32_t* cIwant[2];
-  int32_t* cIresp[2];
-  uint64_t* pool[2];  // [POOLCAP][W] IWANT request / response bitsets
-  int32_t* poolCnt;   // [2]
-  int32_t poolCap;
+  int64_t* cIwant[2];  // IWANT request list: arena record (off << 24 | count), -1 = none
+  int64_t* cIresp[2];  // messages served for an IWANT: arena record, -1 = none
+  int32_t* pool[2];    // slot-id arena for IWANT lists / responses
+  unsigned long long* poolCnt;  // [2] bump pointers
+  int64_t poolCap;     // ids per arena
   // message slots
   int32_t* slotSrc;
   int64_t* slotPubHop;
@@ -234,4 +232,54 @@ __device__ __forceinline__ void add_backoff(const Dev& d, int64_t e, int t, int6
   const int64_t expire = now + interval;
   const int64_t cur = d.backoff[i];
   if (cur == 0 || cur < expire) d.backoff[i] = expire;
+}
+
+// ---- slot-id arena: compact IWANT request / response payloads ----------
+// Writes the set bits of a wave-distributed bitset (word w = lane + 64*j) as
+// slot ids; returns the packed record (off << 24 | count) or -1 when empty.
+template <int WPL>
+__device__ __forceinline__ int64_t arena_write(const Dev& d, int buf, const uint64_t (&bits)[WPL]) {
+  const int lane = lane_id();
+  int mine = 0;
+#pragma unroll
+  for (int j = 0; j < WPL; ++j) mine += __popcll(bits[j]);
+  int incl = mine;  // inclusive prefix over lanes
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  const int total = __shfl(incl, 63);
+  if (total == 0) return -1;
+  unsigned long long off = 0;
+  if (lane == 0) off = atomicAdd(&d.poolCnt[buf], (unsigned long long)total);
+  off = __shfl(off, 0);
+  if ((int64_t)(off + total) > d.poolCap) {
+    if (lane == 0) set_err(d, E_POOL);
+    return -1;
+  }
+  int pos = (int)off + incl - mine;
+#pragma unroll
+  for (int j = 0; j < WPL; ++j) {
+    uint64_t y = bits[j];
+    while (y) {
+      const int b = __ffsll((long long)y) - 1;
+      y &= y - 1;
+      d.pool[buf][pos++] = (lane + 64 * j) * 64 + b;
+    }
+  }
+  return ((int64_t)off << 24) | (int64_t)total;
+}
+
+// Expands an arena record into the wave's LDS bitset lds[0..W).
+__device__ __forceinline__ void arena_read(const Dev& d, int buf, int64_t rec, unsigned long long* lds) {
+  const int lane = lane_id();
+  for (int w = lane; w < d.W; w += 64) lds[w] = 0;
+  __syncthreads();
+  const int64_t off = rec >> 24;
+  const int n = (int)(rec & 0xFFFFFF);
+  for (int k = lane; k < n; k += 64) {
+    const int slot = d.pool[buf][off + k];
+    atomicOr(&lds[slot >> 6], 1ull << (slot & 63));
+  }
+  __syncthreads();
 }

@@ -288,10 +288,9 @@ int gs_engine::start() {
   const size_t NQ = (size_t)N * GS_TABLE;
   x.promMid = dalloc<int64_t>(NQ); x.promExp = dalloc<int64_t>(NQ); x.promSlot = dalloc<int32_t>(NQ);
   x.promEdge = dalloc<uint8_t>(NQ); x.promN = dalloc<int32_t>(N);
-  x.ptxMid = dalloc<int64_t>(NQ); x.ptxSlot = dalloc<int32_t>(NQ); x.ptxCnt = dalloc<int32_t>(NQ);
-  x.ptxEdge = dalloc<uint8_t>(NQ); x.ptxN = dalloc<int32_t>(N);
+  x.ptx = dalloc<uint64_t>((size_t)N * GS_PTX); x.ptxN = dalloc<int32_t>(N);
   chk(x.promMid); chk(x.promExp); chk(x.promSlot); chk(x.promEdge); chk(x.promN);
-  chk(x.ptxMid); chk(x.ptxSlot); chk(x.ptxCnt); chk(x.ptxEdge); chk(x.ptxN);
+  chk(x.ptx); chk(x.ptxN);
   x.mesh = dalloc<uint64_t>(E); x.fanout = dalloc<uint64_t>(E);
   chk(x.mesh); chk(x.fanout);
   for (int k = 0; k < 2; ++k) {
@@ -301,7 +300,7 @@ int gs_engine::start() {
     x.cGraftJoin[k] = dalloc<uint64_t>(E); x.cGraftHb[k] = dalloc<uint64_t>(E);
     x.cPruneReply[k] = dalloc<uint64_t>(E); x.cPruneHb[k] = dalloc<uint64_t>(E);
     x.cIhave[k] = dalloc<uint64_t>(E);
-    x.cIwant[k] = dalloc<int32_t>(E, 0xFF); x.cIresp[k] = dalloc<int32_t>(E, 0xFF);
+    x.cIwant[k] = dalloc<int64_t>(E, 0xFF); x.cIresp[k] = dalloc<int64_t>(E, 0xFF);
     chk(x.cPre[k]); chk(x.cHb[k]); chk(x.cGraftJoin[k]); chk(x.cGraftHb[k]); chk(x.cPruneReply[k]);
     chk(x.cPruneHb[k]); chk(x.cIhave[k]); chk(x.cIwant[k]); chk(x.cIresp[k]);
     x.pubmask[k] = dalloc<uint64_t>(W); chk(x.pubmask[k]);
@@ -313,9 +312,10 @@ int gs_engine::start() {
   x.bp = dalloc<double>(E); x.peerhave = dalloc<int32_t>(E); x.iasked = dalloc<int32_t>(E);
   chk(x.score0); chk(x.score1); chk(x.backoff); chk(x.fmd); chk(x.mmd); chk(x.mfp); chk(x.imd);
   chk(x.graftTime); chk(x.meshTime); chk(x.flags); chk(x.bp); chk(x.peerhave); chk(x.iasked);
-  x.poolCap = cfg.router == GS_ROUTER_GOSSIPSUB ? 2 * N + 1024 : 1;
-  for (int k = 0; k < 2; ++k) { x.pool[k] = dalloc<uint64_t>((size_t)x.poolCap * W); chk(x.pool[k]); }
-  x.poolCnt = dalloc<int32_t>(2); chk(x.poolCnt);
+  // IWANT payload arena (slot ids): 4 ids per edge per hop, >= 16M
+  x.poolCap = cfg.router == GS_ROUTER_GOSSIPSUB ? std::max<int64_t>(1 << 24, 4 * E) : 16;
+  for (int k = 0; k < 2; ++k) { x.pool[k] = dalloc<int32_t>((size_t)x.poolCap); chk(x.pool[k]); }
+  x.poolCnt = dalloc<unsigned long long>(2); chk(x.poolCnt);
   x.slotSrc = dalloc<int32_t>(S, 0xFF); x.slotPubHop = dalloc<int64_t>(S); x.slotMid = dalloc<int64_t>(S, 0xFF);
   chk(x.slotSrc); chk(x.slotPubHop); chk(x.slotMid);
   x.ctr = dalloc<unsigned long long>(C_NCOUNTERS); x.err = dalloc<int32_t>(1);
@@ -384,7 +384,7 @@ int gs_engine::stepOne() {
   nextMsg = e;
   const int n = (int)(e - b);
   HIPCHECK(hipMemsetAsync(d.pubmask[cur], 0, (size_t)W * 8, stream));
-  HIPCHECK(hipMemsetAsync(d.poolCnt + cur, 0, 4, stream));
+  HIPCHECK(hipMemsetAsync(d.poolCnt + cur, 0, 8, stream));
   const unsigned eb = nblk(E, 256);
   if (scoring) TIMED(this, GS_K_SCORE, (k_score<<<eb, 256, 0, stream>>>(d, d.score0)));
   if (h == 0 && gossip) TIMED(this, GS_K_JOIN, (k_join<<<N, 64, 0, stream>>>(d, h, now, cur)));
@@ -450,9 +450,9 @@ int gs_engine::checkDeviceError() {
   HIPCHECK(hipMemcpy(&err, d.err, 4, hipMemcpyDeviceToHost));
   switch (err) {
     case E_NONE: return GS_OK;
-    case E_POOL: gs_set_error("IWANT record pool overflow"); return GS_ECAPACITY;
+    case E_POOL: gs_set_error("IWANT payload arena overflow (4 ids per edge per hop)"); return GS_ECAPACITY;
     case E_PROMISES: gs_set_error("per-node promise table overflow (64 entries)"); return GS_ECAPACITY;
-    case E_PEERTX: gs_set_error("per-node IWANT retransmission table overflow (64 entries)"); return GS_ECAPACITY;
+    case E_PEERTX: gs_set_error("per-node IWANT retransmission table overflow (512 entries)"); return GS_ECAPACITY;
     case E_LATE:
       gs_set_error("a message was first delivered later than the message window allows; raise slots_per_topic");
       return GS_ECAPACITY;

@@ -200,6 +200,7 @@ template <int WPL>
 __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int head) {
   __shared__ int cntF[64];
   __shared__ int cntD[64];
+  __shared__ unsigned long long xrb[64 * GS_MAX_WPL];
   const int v = blockIdx.x;
   const int lane = lane_id();
   const int prv = cur ^ 1;
@@ -235,8 +236,9 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     const int jr = (int)(r - d.rowptr[u]);
     const uint64_t relay = d.fwdRelay[prv][r];
     const uint64_t pub = d.fwdPub[prv][r];
-    const int iresp = d.cIresp[prv][r];
+    const int64_t iresp = d.cIresp[prv][r];
     if ((relay | pub) == 0 && iresp < 0) continue;
+    if (iresp >= 0) arena_read(d, prv, iresp, xrb);
     const bool gray = (glmask >> i) & 1;
     int myF = 0, myDup = 0;
     long long sent = 0, rpcs = 0;
@@ -261,7 +263,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
         }
         x = keep;
       }
-      const uint64_t xr = iresp >= 0 ? d.pool[prv][(int64_t)iresp * W + w] : 0;
+      const uint64_t xr = iresp >= 0 ? xrb[w] : 0;
       if (x & xr) set_err(d, E_DOUBLE);
       const uint64_t tmask = ((sv >> tw) & 1) ? ~0ull : 0ull;
       const uint64_t xa = (x | xr) & tmask;

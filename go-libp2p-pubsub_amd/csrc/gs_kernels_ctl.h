@@ -5,17 +5,6 @@
 #pragma once
 #include "gs_device.h"
 
-__device__ __forceinline__ int64_t pool_alloc(const Dev& d, int buf) {
-  int r = 0;
-  if (lane_id() == 0) r = atomicAdd(&d.poolCnt[buf], 1);
-  r = __shfl(r, 0);
-  if (r >= d.poolCap) {
-    if (lane_id() == 0) set_err(d, E_POOL);
-    return -1;
-  }
-  return r;
-}
-
 // handleGraft for one topic from sender edge e (gossipsub.go:713-792).
 // Scalar (wave-uniform) code; meshcnt is held by lane t.  Returns true when a
 // PRUNE for t must be sent back.
@@ -72,6 +61,8 @@ __device__ __forceinline__ void prune_topics(const Dev& d, int64_t e, int v, uin
 
 template <int WPL>
 __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, int cur, int head) {
+  __shared__ unsigned long long reqb[64 * GS_MAX_WPL];
+  __shared__ unsigned long long ptx[GS_PTX];
   const int v = blockIdx.x;
   const int lane = lane_id();
   const int prv = cur ^ 1;
@@ -97,11 +88,10 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
   int32_t pSlot = lane < promN ? d.promSlot[(int64_t)v * GS_TABLE + lane] : 0;
   int pEdge = lane < promN ? d.promEdge[(int64_t)v * GS_TABLE + lane] : 0;
   bool promDirty = false;
+  // mcache.peertx for this node: (slot, requester edge) -> count, staged in LDS
   int ptxN = d.ptxN[v];
-  int64_t xMid = lane < ptxN ? d.ptxMid[(int64_t)v * GS_TABLE + lane] : -1;
-  int xCnt = lane < ptxN ? d.ptxCnt[(int64_t)v * GS_TABLE + lane] : 0;
-  int xSlot = lane < ptxN ? d.ptxSlot[(int64_t)v * GS_TABLE + lane] : 0;
-  int xEdge = lane < ptxN ? d.ptxEdge[(int64_t)v * GS_TABLE + lane] : 0;
+  for (int q = lane; q < ptxN; q += 64) ptx[q] = d.ptx[(int64_t)v * GS_PTX + q];
+  __syncthreads();
   bool ptxDirty = false;
   long long cPrunes = 0, cIwantSent = 0, cServed = 0, cGray = 0;
   for (int i = 0; i < deg; ++i) {
@@ -116,7 +106,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     const uint64_t pRep = d.cPruneReply[prv][r];
     const uint64_t pHb = d.cPruneHb[prv][r];
     const uint64_t ihaveT = d.cIhave[prv][r];
-    const int iwRec = d.cIwant[prv][r];
+    const int64_t iwRec = d.cIwant[prv][r];
     // consume the outbox entry (the sender re-writes it two hops later)
     if (lane == 0) {
       d.cPre[prv][r] = 0;
@@ -140,7 +130,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     int ia = d.iasked[e];
     uint64_t pruneOut = 0;
     int nReplies = 0;
-    int respRec = -1, iwantRec = -1;
+    int64_t respRec = -1, iwantRec = -1;
     // (1) Join RPCs: one GRAFT each (gossipsub.go:1080-1084)
     const int nJoin = __popcll(gJoin);
     {
@@ -167,12 +157,13 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
         // per-peer retransmissions (mcache.GetForPeer)
         uint64_t served[WPL];
         int nServed = 0;
+        arena_read(d, prv, iwRec, reqb);
 #pragma unroll
         for (int j = 0; j < WPL; ++j) {
           const int w = lane + 64 * j;
           uint64_t req = 0, cache = 0;
           if (w < W) {
-            req = d.pool[prv][(int64_t)iwRec * W + w];
+            req = reqb[w];
             for (int k = 0; k < d.HL; ++k) cache |= d.hist[((int64_t)((head + k) % d.R) * d.N + v) * W + w];
           }
           uint64_t cand = req & cache;
@@ -187,22 +178,31 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
               const int b = __ffsll((long long)cw) - 1;
               cw &= cw - 1;
               const int slot = (src + 64 * j) * 64 + b;
-              const int64_t mid = d.slotMid[slot];
-              const unsigned long long hit = __ballot(lane < ptxN && xMid == mid && xEdge == i);
+              // GetForPeer (mcache.go:66-80): ++peertx[mid][p]
+              const uint64_t key = ((uint64_t)(uint32_t)slot << 32) | ((uint64_t)i << 8);
+              int found = -1;
+              for (int q = lane; q < ptxN; q += 64)
+                if ((ptx[q] & ~0xFFull) == key) found = q;
+              const unsigned long long hit = __ballot(found >= 0);
               int count;
               if (hit) {
-                const int q = __ffsll((long long)hit) - 1;
-                if (lane == q) xCnt++;
-                count = __shfl(xCnt, q);
-              } else {
-                if (ptxN >= GS_TABLE) {
-                  if (lane == 0) set_err(d, E_PEERTX);
-                  count = 1;
-                } else {
-                  if (lane == ptxN) { xMid = mid; xEdge = i; xCnt = 1; xSlot = slot; }
-                  ptxN++;
-                  count = 1;
+                const int fl = __ffsll((long long)hit) - 1;
+                const int q = __shfl(found, fl);
+                if (lane == 0) {
+                  const uint64_t c = ptx[q] & 0xFF;
+                  ptx[q] = key | (c < 255 ? c + 1 : 255);
                 }
+                __syncthreads();
+                count = (int)(ptx[q] & 0xFF);
+              } else {
+                if (ptxN >= GS_PTX) {
+                  if (lane == 0) set_err(d, E_PEERTX);
+                } else {
+                  if (lane == 0) ptx[ptxN] = key | 1;
+                  ptxN++;
+                  __syncthreads();
+                }
+                count = 1;
               }
               ptxDirty = true;
               if (count <= d.GR && lane == src) served[j] |= 1ull << b;
@@ -212,15 +212,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
         }
         nServed = wave_sum_int(nServed);
         if (nServed > 0) {
-          const int64_t rec = pool_alloc(d, cur);
-          if (rec >= 0) {
-#pragma unroll
-            for (int j = 0; j < WPL; ++j) {
-              const int w = lane + 64 * j;
-              if (w < W) d.pool[cur][rec * W + w] = served[j];
-            }
-            respRec = (int)rec;
-          }
+          respRec = arena_write<WPL>(d, cur, served);
           nReplies++;
           cServed += nServed;
         }
@@ -281,15 +273,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
               const int os = __shfl(bestSlot, lane ^ o);
               if (ok < bestKey || (ok == bestKey && om < bestMid)) { bestKey = ok; bestMid = om; bestSlot = os; }
             }
-            const int64_t rec = pool_alloc(d, cur);
-            if (rec >= 0) {
-#pragma unroll
-              for (int j = 0; j < WPL; ++j) {
-                const int w = lane + 64 * j;
-                if (w < W) d.pool[cur][rec * W + w] = want[j];
-              }
-              iwantRec = (int)rec;
-            }
+            iwantRec = arena_write<WPL>(d, cur, want);
             ia += iask;
             cIwantSent += iask;
             iwantAny = true;
@@ -351,13 +335,10 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     if (lane == 0) d.promN[v] = promN < GS_TABLE ? promN : GS_TABLE;
   }
   if (ptxDirty) {
-    if (lane < ptxN && lane < GS_TABLE) {
-      d.ptxMid[(int64_t)v * GS_TABLE + lane] = xMid;
-      d.ptxCnt[(int64_t)v * GS_TABLE + lane] = xCnt;
-      d.ptxSlot[(int64_t)v * GS_TABLE + lane] = xSlot;
-      d.ptxEdge[(int64_t)v * GS_TABLE + lane] = (uint8_t)xEdge;
-    }
-    if (lane == 0) d.ptxN[v] = ptxN < GS_TABLE ? ptxN : GS_TABLE;
+    __syncthreads();
+    const int n = ptxN < GS_PTX ? ptxN : GS_PTX;
+    for (int q = lane; q < n; q += 64) d.ptx[(int64_t)v * GS_PTX + q] = ptx[q];
+    if (lane == 0) d.ptxN[v] = n;
   }
   if (lane == 0) {
     if (cPrunes) atomicAdd(&d.ctr[C_PRUNES], (unsigned long long)cPrunes);
@@ -688,28 +669,24 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
   // "ghost" slot until the next shift (IHAVE payload of this heartbeat).
   const int n = d.ptxN[v];
   if (n > 0) {
-    const int64_t ti = (int64_t)v * GS_TABLE + lane;
-    int64_t mid = -1;
-    int cnt = 0, slot = 0, edge = 0;
-    bool live = lane < n;
-    if (live) {
-      mid = d.ptxMid[ti];
-      cnt = d.ptxCnt[ti];
-      slot = d.ptxSlot[ti];
-      edge = d.ptxEdge[ti];
-      const int last = (head + d.HL - 1) % d.R;
-      if ((d.hist[((int64_t)last * d.N + v) * d.W + (slot >> 6)] >> (slot & 63)) & 1) live = false;
+    const int last = (head + d.HL - 1) % d.R;
+    const uint64_t* lastw = d.hist + ((int64_t)last * d.N + v) * d.W;
+    int kept = 0;
+    for (int base = 0; base < n; base += 64) {
+      const int q = base + lane;
+      uint64_t ent = 0;
+      bool live = q < n;
+      if (live) {
+        ent = d.ptx[(int64_t)v * GS_PTX + q];
+        const int slot = (int)(ent >> 32);
+        if ((lastw[slot >> 6] >> (slot & 63)) & 1) live = false;
+      }
+      const unsigned long long lm = __ballot(live);
+      const int pos = kept + __popcll(lm & ((1ull << lane) - 1));
+      if (live) d.ptx[(int64_t)v * GS_PTX + pos] = ent;  // pos <= q: in-place compaction is safe
+      kept += __popcll(lm);
     }
-    const unsigned long long lm = __ballot(live);
-    const int pos = __popcll(lm & ((1ull << lane) - 1));
-    if (live) {
-      const int64_t to = (int64_t)v * GS_TABLE + pos;
-      d.ptxMid[to] = mid;
-      d.ptxCnt[to] = cnt;
-      d.ptxSlot[to] = slot;
-      d.ptxEdge[to] = (uint8_t)edge;
-    }
-    if (lane == 0) d.ptxN[v] = __popcll(lm);
+    if (lane == 0) d.ptxN[v] = kept;
   }
   for (int w = lane; w < d.W; w += 64) d.hist[((int64_t)newhead * d.N + v) * d.W + w] = 0;
 }
