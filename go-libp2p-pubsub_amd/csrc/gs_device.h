@@ -68,8 +68,13 @@ struct Dev {
   uint64_t* seen;
   uint64_t* newb[2];
   uint64_t* hist;  // [R][N][W]
-  int16_t* age;    // [N][S] first-delivery hop - publish hop
-  uint8_t* ffrom;  // [N][S] first-deliverer neighbour slot (255 = self)
+  int16_t* age;    // [N][S] first-delivery hop - publish hop   (record / short-window mode)
+  uint8_t* ffrom;  // [N][S] first-deliverer neighbour slot, 255 = self (record mode)
+  uint8_t* ffc[2]; // [N][FCAP] first-deliverer of each message first delivered in hop h,
+                   // in ascending slot order (rank among the node's fresh bits)
+  int32_t* fpre[2]; // [N][T] fresh-rank prefix per topic (T > 1)
+  int32_t fcap;
+  int32_t needAge, record;
   uint64_t* sel;   // [N][S] randomsub target mask (randomsub only)
   int64_t* lastpub;        // [N][T], INT64_MIN = none
   uint64_t* fanoutPresent; // [N]
@@ -124,6 +129,12 @@ struct Dev {
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 __device__ __forceinline__ void set_err(const Dev& d, int code) { atomicCAS(d.err, 0, code); }
+// Event counters are spread over GS_CTR_SPREAD copies (by workgroup) so a
+// million waves do not serialise on one L2 line; the host sums the copies.
+#define GS_CTR_SPREAD 256
+__device__ __forceinline__ void ctr_add(const Dev& d, int k, unsigned long long v) {
+  atomicAdd(&d.ctr[(blockIdx.x & (GS_CTR_SPREAD - 1)) * C_NCOUNTERS + k], v);
+}
 
 __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
   return (uint64_t)__shfl((unsigned long long)v, src);
@@ -163,7 +174,7 @@ __device__ __forceinline__ double add_ones_capped(double x, int n, double cap) {
 
 // peerScore.score — score.go:256-333, topics summed in ascending order.
 // Compiled with -ffp-contract=off: every product/sum rounds as in Go.
-__device__ __noinline__ double edge_score(const Dev& d, int64_t e) {
+__device__ __forceinline__ double edge_score(const Dev& d, int64_t e) {
   if (!d.scoring) return 0.0;
   double score = 0.0;
   for (int t = 0; t < d.T; ++t) {

@@ -41,7 +41,7 @@ struct gs_engine {
   gs_peer_score_thresholds thr{};
   std::vector<gs_topic_score_params> tps;
   std::vector<uint8_t> tscored;
-  bool scoring = false, floodPublish = false;
+  bool scoring = false, floodPublish = false, record = false;
   int N = 0, T = 0, St = 0, Wt = 0, W = 0, S = 0, R = 0;
   int64_t E = 0;
   int H = 16;  // hops per heartbeat (or a nominal 16 for floodsub/randomsub)
@@ -72,6 +72,8 @@ struct gs_engine {
   TopicP* dTp = nullptr;
   int32_t* dPairs = nullptr;
   int pairCap = 0;
+  int32_t* dRetire = nullptr;
+  int retireCap = 0;
   double* dScoreTmp = nullptr;
   int32_t *dHopOut = nullptr, *dFromOut = nullptr;
   // kernel timing: (kernel id, start event, end event) pending until a sync
@@ -279,8 +281,22 @@ int gs_engine::start() {
   x.seen = dalloc<uint64_t>(NW); chk(x.seen);
   for (int k = 0; k < 2; ++k) { x.newb[k] = dalloc<uint64_t>(NW); chk(x.newb[k]); }
   x.hist = dalloc<uint64_t>((size_t)R * NW); chk(x.hist);
-  x.age = dalloc<int16_t>(NS); chk(x.age);
-  x.ffrom = dalloc<uint8_t>(NS); chk(x.ffrom);
+  // per-slot first-delivery hops only when read back or when the P3 window
+  // check can consult them (topic params may change after start, so any
+  // scored engine keeps them)
+  x.record = record ? 1 : 0;
+  x.needAge = (x.record || scoring) ? 1 : 0;
+  x.age = x.needAge ? dalloc<int16_t>(NS) : nullptr;
+  x.ffrom = x.record ? dalloc<uint8_t>(NS) : nullptr;
+  if (x.needAge) chk(x.age);
+  if (x.record) chk(x.ffrom);
+  // compact first-deliverer arrays: one byte per message first delivered in a hop
+  x.fcap = ((size_t)N * S * 2 <= (16ull << 30)) ? S : std::min(S, 4096);
+  for (int k = 0; k < 2; ++k) {
+    x.ffc[k] = dalloc<uint8_t>((size_t)N * x.fcap); chk(x.ffc[k]);
+    x.fpre[k] = T > 1 ? dalloc<int32_t>((size_t)N * T) : nullptr;
+    if (T > 1) chk(x.fpre[k]);
+  }
   x.sel = cfg.router == GS_ROUTER_RANDOMSUB ? dalloc<uint64_t>(NS) : nullptr;
   if (cfg.router == GS_ROUTER_RANDOMSUB) chk(x.sel);
   x.lastpub = dalloc<int64_t>((size_t)N * T); chk(x.lastpub);
@@ -318,7 +334,7 @@ int gs_engine::start() {
   x.poolCnt = dalloc<unsigned long long>(2); chk(x.poolCnt);
   x.slotSrc = dalloc<int32_t>(S, 0xFF); x.slotPubHop = dalloc<int64_t>(S); x.slotMid = dalloc<int64_t>(S, 0xFF);
   chk(x.slotSrc); chk(x.slotPubHop); chk(x.slotMid);
-  x.ctr = dalloc<unsigned long long>(C_NCOUNTERS); x.err = dalloc<int32_t>(1);
+  x.ctr = dalloc<unsigned long long>((size_t)C_NCOUNTERS * GS_CTR_SPREAD); x.err = dalloc<int32_t>(1);
   chk(x.ctr); chk(x.err);
   dScoreTmp = dalloc<double>(E); chk(dScoreTmp);
   dHopOut = dalloc<int32_t>(N); dFromOut = dalloc<int32_t>(N); chk(dHopOut); chk(dFromOut);
@@ -383,6 +399,26 @@ int gs_engine::stepOne() {
   while (e < mHop.size() && mHop[e] == h) e++;
   nextMsg = e;
   const int n = (int)(e - b);
+  // active word windows: amW = words of messages published in [h - maxAge, h]
+  // (what this hop's frontier may hold), amR = the previous hop's (what the
+  // senders' frontiers hold)
+  WMask amR{}, amW{};
+  {
+    auto build = [&](int64_t lo, int64_t hi, WMask& m) {
+      auto it = std::lower_bound(mHop.begin(), mHop.end(), lo);
+      for (size_t k = (size_t)(it - mHop.begin()); k < mHop.size() && mHop[k] <= hi; ++k) {
+        const int w = mSlot[k] >> 6;
+        m.m[w >> 6] |= 1ull << (w & 63);
+      }
+    };
+    build(h - 1 - maxAge, h - 1, amR);
+    build(h - maxAge, h, amW);
+  }
+  std::vector<int32_t> retireWords;
+  for (size_t k = b; k < e; ++k) {
+    const int w = mSlot[k] >> 6;
+    if (std::find(retireWords.begin(), retireWords.end(), w) == retireWords.end()) retireWords.push_back(w);
+  }
   HIPCHECK(hipMemsetAsync(d.pubmask[cur], 0, (size_t)W * 8, stream));
   HIPCHECK(hipMemsetAsync(d.poolCnt + cur, 0, 8, stream));
   const unsigned eb = nblk(E, 256);
@@ -417,8 +453,28 @@ int gs_engine::stepOne() {
   }
   TIMED(this, GS_K_FWD, (k_fwd<<<eb, 256, 0, stream>>>(d, cur)));
   if (n > 0) k_pubmask<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, cur);
-  TIMED(this, GS_K_PHASE_A,
-        launch_wpl(W, [&](auto wpl) { k_phase_a<decltype(wpl)::value><<<N, 64, 0, stream>>>(d, h, cur, head); }));
+  {
+    const int wpl = (W + 63) / 64;
+    const int nR = __builtin_popcountll(amR.m[0]) + __builtin_popcountll(amR.m[1]) +
+                   __builtin_popcountll(amR.m[2]) + __builtin_popcountll(amR.m[3]);
+    const size_t lds = (size_t)64 * wpl * 8 + 512 + (size_t)64 * wpl * 4 + (size_t)nR * 64;
+    TIMED(this, GS_K_PHASE_A, launch_wpl(W, [&](auto w) {
+            k_phase_a<decltype(w)::value><<<N, 64, lds, stream>>>(d, h, cur, head, amR, amW);
+          }));
+  }
+  if (!retireWords.empty()) {
+    if ((int)retireWords.size() > retireCap) {
+      int32_t* p = nullptr;
+      HIPCHECK(hipMalloc(&p, retireWords.size() * 2 * 4));
+      allocs.push_back(p);
+      dRetire = p;
+      retireCap = (int)retireWords.size() * 2;
+    }
+    HIPCHECK(hipMemcpyAsync(dRetire, retireWords.data(), retireWords.size() * 4, hipMemcpyHostToDevice, stream));
+    const int nw = (int)retireWords.size();
+    k_retire<<<nblk((int64_t)N * nw, 256), 256, 0, stream>>>(d, cur, dRetire, nw);
+    HIPCHECK(hipStreamSynchronize(stream));  // retireWords is pageable host memory
+  }
   if (n > 0) {
     TIMED(this, GS_K_PUBLISH, (k_publish<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, h, cur, head)));
     if (cfg.router == GS_ROUTER_RANDOMSUB) k_publish_rs<<<n, 64, 0, stream>>>(d, (int)b);
@@ -505,6 +561,7 @@ int gs_engine_create(const gs_config* cfg, const gs_gossipsub_params* gsp, const
   if (gsp) g->gp = *gsp; else gs_default_gossipsub_params(&g->gp);
   g->scoring = (cfg->flags & GS_FLAG_SCORING) != 0 && cfg->router == GS_ROUTER_GOSSIPSUB;
   g->floodPublish = (cfg->flags & GS_FLAG_FLOOD_PUBLISH) != 0;
+  g->record = (cfg->flags & GS_FLAG_RECORD_DELIVERIES) != 0;
   g->tps.assign(g->T, gs_topic_score_params{});
   g->tscored.assign(g->T, 0);
   if (cfg->router == GS_ROUTER_GOSSIPSUB) {
@@ -695,9 +752,12 @@ int64_t gs_current_hop(const gs_engine* g) { return g->hop; }
 int gs_read_counters(gs_engine* g, gs_counters* out) {
   std::memset(out, 0, sizeof(*out));
   if (g->started) {
-    unsigned long long c[C_NCOUNTERS];
+    std::vector<unsigned long long> all((size_t)C_NCOUNTERS * GS_CTR_SPREAD);
     HIPCHECK(hipStreamSynchronize(g->stream));
-    HIPCHECK(hipMemcpy(c, g->d.ctr, sizeof(c), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(all.data(), g->d.ctr, all.size() * 8, hipMemcpyDeviceToHost));
+    unsigned long long c[C_NCOUNTERS] = {};
+    for (int s = 0; s < GS_CTR_SPREAD; ++s)
+      for (int k = 0; k < C_NCOUNTERS; ++k) c[k] += all[(size_t)s * C_NCOUNTERS + k];
     out->published = (int64_t)c[C_PUBLISHED];
     out->deliveries = (int64_t)c[C_DELIVERIES];
     out->duplicates = (int64_t)c[C_DUPLICATES];
@@ -762,6 +822,7 @@ int gs_read_topic_stats(gs_engine* g, double* fmd, double* mmd, double* mfp, dou
 int gs_read_behaviour_penalty(gs_engine* g, double* bp) { return copy_back(g, bp, g->d.bp, g->E * 8); }
 
 int gs_read_deliveries(gs_engine* g, int64_t id, int32_t* hop, int32_t* from) {
+  if (!g->record) { gs_set_error("GS_FLAG_RECORD_DELIVERIES not set"); return GS_ESTATE; }
   if (id < 0 || id >= (int64_t)g->mId.size()) { gs_set_error("unknown message id"); return GS_EINVAL; }
   const int slot = g->mSlot[id];
   if (g->slotOwnerId[slot] != id) {

@@ -94,13 +94,23 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
   __syncthreads();
   bool ptxDirty = false;
   long long cPrunes = 0, cIwantSent = 0, cServed = 0, cGray = 0;
-  for (int i = 0; i < deg; ++i) {
+  // senders with control RPCs this hop (lane i = in-edge i), then visit only those
+  int64_t rL = 0;
+  int npreL = 0, hbL = 0;
+  if (lane < deg) {
+    rL = d.rev[base + lane];
+    npreL = d.cPre[prv][rL];
+    hbL = d.cHb[prv][rL];
+  }
+  unsigned long long cmask = __ballot(npreL != 0 || hbL != 0);
+  while (cmask) {
+    const int i = __ffsll((long long)cmask) - 1;
+    cmask &= cmask - 1;
     const int64_t e = base + i;
     const int u = d.col[e];
-    const int64_t r = d.rev[e];
-    const int npre = d.cPre[prv][r];
-    const int hb = d.cHb[prv][r];
-    if (npre == 0 && hb == 0) continue;
+    const int64_t r = (int64_t)shfl_u64((uint64_t)rL, i);
+    const int npre = __shfl(npreL, i);
+    const int hb = __shfl(hbL, i);
     const uint64_t gJoin = d.cGraftJoin[prv][r];
     const uint64_t gHb = d.cGraftHb[prv][r];
     const uint64_t pRep = d.cPruneReply[prv][r];
@@ -341,10 +351,10 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     if (lane == 0) d.ptxN[v] = n;
   }
   if (lane == 0) {
-    if (cPrunes) atomicAdd(&d.ctr[C_PRUNES], (unsigned long long)cPrunes);
-    if (cIwantSent) atomicAdd(&d.ctr[C_IWANT_SENT], (unsigned long long)cIwantSent);
-    if (cServed) atomicAdd(&d.ctr[C_IWANT_SERVED], (unsigned long long)cServed);
-    if (cGray) atomicAdd(&d.ctr[C_GRAYLISTED], (unsigned long long)cGray);
+    if (cPrunes) ctr_add(d, C_PRUNES, (unsigned long long)cPrunes);
+    if (cIwantSent) ctr_add(d, C_IWANT_SENT, (unsigned long long)cIwantSent);
+    if (cServed) ctr_add(d, C_IWANT_SERVED, (unsigned long long)cServed);
+    if (cGray) ctr_add(d, C_GRAYLISTED, (unsigned long long)cGray);
   }
 }
 
@@ -412,7 +422,7 @@ __global__ __launch_bounds__(64) void k_hb_pre(Dev d, int64_t now, uint64_t tick
   }
   if (lane == 0) {
     d.promN[v] = __popcll(lm);
-    if (total) atomicAdd(&d.ctr[C_PROMISES_BROKEN], (unsigned long long)total);
+    if (total) ctr_add(d, C_PROMISES_BROKEN, (unsigned long long)total);
   }
 }
 
@@ -659,9 +669,9 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
   const int ih = wave_sum_int(__popcll(ihave));
   if (lane == 0) {
     d.fanoutPresent[v] = fpres;
-    if (g) atomicAdd(&d.ctr[C_GRAFTS], (unsigned long long)g);
-    if (p) atomicAdd(&d.ctr[C_PRUNES], (unsigned long long)p);
-    if (ih) atomicAdd(&d.ctr[C_IHAVE], (unsigned long long)ih);
+    if (g) ctr_add(d, C_GRAFTS, (unsigned long long)g);
+    if (p) ctr_add(d, C_PRUNES, (unsigned long long)p);
+    if (ih) ctr_add(d, C_IHAVE, (unsigned long long)ih);
   }
   // mcache.Shift (mcache.go:94-104): drop the IWANT retransmission counters of
   // messages leaving the cache (pre-shift window HL-1), then clear the ring
@@ -693,6 +703,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
 
 // gs_read_deliveries gather
 __global__ void k_read_deliv(Dev d, int slot, int64_t pubhop, int32_t* hop, int32_t* from) {
+  // needs GS_FLAG_RECORD_DELIVERIES (age / ffrom kept per slot)
   const int v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= d.N) return;
   const bool s = (d.seen[(int64_t)v * d.W + (slot >> 6)] >> (slot & 63)) & 1;
