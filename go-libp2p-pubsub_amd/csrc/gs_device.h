@@ -23,7 +23,8 @@ enum {
 };
 // device error codes (first one wins)
 enum {
-  E_NONE = 0, E_POOL = 1, E_PROMISES = 2, E_PEERTX = 3, E_LATE = 4, E_TRUNCATE = 5, E_DOUBLE = 6
+  E_NONE = 0, E_POOL = 1, E_PROMISES = 2, E_PEERTX = 3, E_LATE = 4, E_TRUNCATE = 5, E_DOUBLE = 6,
+  E_FCAP = 7
 };
 
 struct TopicP {  // TopicScoreParams (score_params.go:98-148) + scored flag
@@ -70,10 +71,12 @@ struct Dev {
   uint64_t* hist;  // [R][N][W]
   int16_t* age;    // [N][S] first-delivery hop - publish hop   (record / short-window mode)
   uint8_t* ffrom;  // [N][S] first-deliverer neighbour slot, 255 = self (record mode)
-  uint8_t* ffc[2]; // [N][FCAP] first-deliverer of each message first delivered in hop h,
-                   // in ascending slot order (rank among the node's fresh bits)
-  int32_t* fpre[2]; // [N][T] fresh-rank prefix per topic (T > 1)
-  int32_t fcap;
+  uint8_t* ffc[2]; // [N][T][Kt] first deliverer (in-edge index) of each message first
+                   // delivered in hop h, per topic in ascending slot order (rank among
+                   // the node's fresh bits of that topic)
+  int32_t Kt;      // per-topic capacity of ffc rows
+  uint64_t* oldm;  // [W] slots whose message is too old to be first-delivered this hop
+  int32_t* nAuth;  // [N] live message slots authored by the node
   int32_t needAge, record;
   uint64_t* sel;   // [N][S] randomsub target mask (randomsub only)
   int64_t* lastpub;        // [N][T], INT64_MIN = none
@@ -172,37 +175,36 @@ __device__ __forceinline__ double add_ones_capped(double x, int n, double cap) {
   return x;
 }
 
-// peerScore.score — score.go:256-333, topics summed in ascending order.
-// Compiled with -ffp-contract=off: every product/sum rounds as in Go.
-__device__ __forceinline__ double edge_score(const Dev& d, int64_t e) {
-  if (!d.scoring) return 0.0;
-  double score = 0.0;
-  for (int t = 0; t < d.T; ++t) {
-    const TopicP& tp = d.tp[t];
-    if (!tp.scored) continue;
-    const int64_t i = (int64_t)t * d.E + e;
-    const uint8_t fl = d.flags[i];
-    double topicScore = 0.0;
-    if (fl & 1) {
-      double p1 = (double)(d.meshTime[i] / tp.TimeInMeshQuantum);
-      if (p1 > tp.TimeInMeshCap) p1 = tp.TimeInMeshCap;
-      topicScore += p1 * tp.TimeInMeshWeight;
-    }
-    topicScore += d.fmd[i] * tp.FmdWeight;
-    if (fl & 2) {
-      const double mm = d.mmd[i];
-      if (mm < tp.MmdThreshold) {
-        const double deficit = tp.MmdThreshold - mm;
-        const double p3 = deficit * deficit;
-        topicScore += p3 * tp.MmdWeight;
-      }
-    }
-    topicScore += d.mfp[i] * tp.MfpWeight;
-    const double im = d.imd[i];
-    const double p4 = im * im;
-    topicScore += p4 * tp.ImdWeight;
-    score += topicScore * tp.TopicWeight;
+// One topic's contribution topicScore * TopicWeight (score.go:265-311) for
+// state index i = t*E + e.  kEager: every load is issued up front (latency-
+// bound callers); otherwise meshTime / mmd are read only when P1 / P3 apply
+// (the bandwidth-bound streaming pass).
+template <bool kEager>
+__device__ __forceinline__ double topic_term(const Dev& d, const TopicP& tp, int64_t i) {
+  const uint8_t fl = d.flags[i];
+  const int64_t mt = (kEager || (fl & 1)) ? d.meshTime[i] : 0;
+  const double mm = (kEager || (fl & 2)) ? d.mmd[i] : 0.0;
+  const double fmd = d.fmd[i], mfp = d.mfp[i], im = d.imd[i];
+  double topicScore = 0.0;
+  if (fl & 1) {
+    double p1 = (double)(mt / tp.TimeInMeshQuantum);
+    if (p1 > tp.TimeInMeshCap) p1 = tp.TimeInMeshCap;
+    topicScore += p1 * tp.TimeInMeshWeight;
   }
+  topicScore += fmd * tp.FmdWeight;
+  if ((fl & 2) && mm < tp.MmdThreshold) {
+    const double deficit = tp.MmdThreshold - mm;
+    const double p3 = deficit * deficit;
+    topicScore += p3 * tp.MmdWeight;
+  }
+  topicScore += mfp * tp.MfpWeight;
+  const double p4 = im * im;
+  topicScore += p4 * tp.ImdWeight;
+  return topicScore * tp.TopicWeight;
+}
+
+// The topic-independent tail of score(): cap, P5, P6, P7 (score.go:313-332).
+__device__ __forceinline__ double score_tail(const Dev& d, int64_t e, double score) {
   if (d.TopicScoreCap > 0 && score > d.TopicScoreCap) score = d.TopicScoreCap;
   score += d.app[d.col[e]] * d.AppW;
   score += d.p6[e] * d.IPW;
@@ -213,6 +215,37 @@ __device__ __forceinline__ double edge_score(const Dev& d, int64_t e) {
     score += p7 * d.BPW;
   }
   return score;
+}
+
+// peerScore.score — score.go:256-333, topics summed in ascending order.
+// Compiled with -ffp-contract=off: every product/sum rounds as in Go.
+__device__ __forceinline__ double edge_score(const Dev& d, int64_t e) {
+  if (!d.scoring) return 0.0;
+  double score = 0.0;
+#pragma unroll 4
+  for (int t = 0; t < d.T; ++t) {
+    const TopicP& tp = d.tp[t];
+    if (!tp.scored) continue;
+    score += topic_term<false>(d, tp, (int64_t)t * d.E + e);
+  }
+  return score_tail(d, e, score);
+}
+
+// Score of ONE edge computed by the whole wave (e wave-uniform): lane t loads
+// topic t's state, so every load is in flight at once; the terms are then
+// added in ascending topic order exactly as edge_score does.  lds: 64 doubles.
+__device__ __forceinline__ double edge_score_wave(const Dev& d, int64_t e, double* lds) {
+  if (!d.scoring) return 0.0;
+  const int lane = lane_id();
+  double term = 0.0;
+  if (lane < d.T && d.tp[lane].scored) term = topic_term<true>(d, d.tp[lane], (int64_t)lane * d.E + e);
+  __syncthreads();
+  lds[lane] = term;
+  __syncthreads();
+  double score = 0.0;
+  for (int t = 0; t < d.T; ++t)
+    if (d.tp[t].scored) score += lds[t];
+  return score_tail(d, e, score);
 }
 
 // peerScore.Graft — score.go:640-658 (scored topics only)
@@ -247,19 +280,25 @@ __device__ __forceinline__ void add_backoff(const Dev& d, int64_t e, int t, int6
 
 // ---- slot-id arena: compact IWANT request / response payloads ----------
 // Writes the set bits of a wave-distributed bitset (word w = lane + 64*j) as
-// slot ids; returns the packed record (off << 24 | count) or -1 when empty.
+// slot ids in ascending slot order (phase A walks them with a cursor);
+// returns the packed record (off << 24 | count) or -1 when empty.
 template <int WPL>
 __device__ __forceinline__ int64_t arena_write(const Dev& d, int buf, const uint64_t (&bits)[WPL]) {
   const int lane = lane_id();
-  int mine = 0;
+  int incl[WPL], tot[WPL];
+  int total = 0;
 #pragma unroll
-  for (int j = 0; j < WPL; ++j) mine += __popcll(bits[j]);
-  int incl = mine;  // inclusive prefix over lanes
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(incl, o);
-    if (lane >= o) incl += y;
+  for (int j = 0; j < WPL; ++j) {
+    const int c = __popcll(bits[j]);
+    int s = c;  // inclusive prefix over lanes of word row j
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(s, o);
+      if (lane >= o) s += y;
+    }
+    incl[j] = s - c;
+    tot[j] = __shfl(s, 63);
+    total += tot[j];
   }
-  const int total = __shfl(incl, 63);
   if (total == 0) return -1;
   unsigned long long off = 0;
   if (lane == 0) off = atomicAdd(&d.poolCnt[buf], (unsigned long long)total);
@@ -268,15 +307,17 @@ __device__ __forceinline__ int64_t arena_write(const Dev& d, int buf, const uint
     if (lane == 0) set_err(d, E_POOL);
     return -1;
   }
-  int pos = (int)off + incl - mine;
+  int rowBase = (int)off;
 #pragma unroll
   for (int j = 0; j < WPL; ++j) {
+    int pos = rowBase + incl[j];
     uint64_t y = bits[j];
     while (y) {
       const int b = __ffsll((long long)y) - 1;
       y &= y - 1;
       d.pool[buf][pos++] = (lane + 64 * j) * 64 + b;
     }
+    rowBase += tot[j];
   }
   return ((int64_t)off << 24) | (int64_t)total;
 }

@@ -115,6 +115,11 @@ struct gs_engine {
     (void)hipMemsetAsync(p, fill, bytes, stream);
     return (X*)p;
   }
+  bool ageWindowNeeded() const {
+    for (int t = 0; t < T; ++t)
+      if (tscored[t] && tps[t].MeshMessageDeliveriesWindow < retireHops * cfg.hop_ns) return true;
+    return false;
+  }
   bool heartbeatDue(int64_t t) const {
     if (cfg.router != GS_ROUTER_GOSSIPSUB) return false;
     if (t < gp.HeartbeatInitialDelay) return false;
@@ -282,21 +287,26 @@ int gs_engine::start() {
   for (int k = 0; k < 2; ++k) { x.newb[k] = dalloc<uint64_t>(NW); chk(x.newb[k]); }
   x.hist = dalloc<uint64_t>((size_t)R * NW); chk(x.hist);
   // per-slot first-delivery hops only when read back or when the P3 window
-  // check can consult them (topic params may change after start, so any
-  // scored engine keeps them)
+  // check can fail: a duplicate always arrives less than retireHops after the
+  // message's first delivery, so a MeshMessageDeliveriesWindow of at least
+  // that long always credits it (score.go:955)
   x.record = record ? 1 : 0;
-  x.needAge = (x.record || scoring) ? 1 : 0;
+  x.needAge = (x.record || (scoring && ageWindowNeeded())) ? 1 : 0;
   x.age = x.needAge ? dalloc<int16_t>(NS) : nullptr;
   x.ffrom = x.record ? dalloc<uint8_t>(NS) : nullptr;
   if (x.needAge) chk(x.age);
   if (x.record) chk(x.ffrom);
-  // compact first-deliverer arrays: one byte per message first delivered in a hop
-  x.fcap = ((size_t)N * S * 2 <= (16ull << 30)) ? S : std::min(S, 4096);
-  for (int k = 0; k < 2; ++k) {
-    x.ffc[k] = dalloc<uint8_t>((size_t)N * x.fcap); chk(x.ffc[k]);
-    x.fpre[k] = T > 1 ? dalloc<int32_t>((size_t)N * T) : nullptr;
-    if (T > 1) chk(x.fpre[k]);
+  // first-deliverer tables: per (node, topic) Kt bytes, one per message first
+  // delivered in a hop (ranked in slot order); Kt is a multiple of 16
+  {
+    const int64_t budget = 8ll << 30;  // bytes per parity
+    int64_t kt = std::min<int64_t>(St, budget / ((int64_t)N * T));
+    kt = std::max<int64_t>(16, kt & ~15ll);
+    x.Kt = (int32_t)std::min<int64_t>(kt, ((int64_t)St + 15) & ~15ll);
   }
+  for (int k = 0; k < 2; ++k) { x.ffc[k] = dalloc<uint8_t>((size_t)N * T * x.Kt); chk(x.ffc[k]); }
+  x.oldm = dalloc<uint64_t>(W); chk(x.oldm);
+  x.nAuth = dalloc<int32_t>(N); chk(x.nAuth);
   x.sel = cfg.router == GS_ROUTER_RANDOMSUB ? dalloc<uint64_t>(NS) : nullptr;
   if (cfg.router == GS_ROUTER_RANDOMSUB) chk(x.sel);
   x.lastpub = dalloc<int64_t>((size_t)N * T); chk(x.lastpub);
@@ -453,15 +463,10 @@ int gs_engine::stepOne() {
   }
   TIMED(this, GS_K_FWD, (k_fwd<<<eb, 256, 0, stream>>>(d, cur)));
   if (n > 0) k_pubmask<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, cur);
-  {
-    const int wpl = (W + 63) / 64;
-    const int nR = __builtin_popcountll(amR.m[0]) + __builtin_popcountll(amR.m[1]) +
-                   __builtin_popcountll(amR.m[2]) + __builtin_popcountll(amR.m[3]);
-    const size_t lds = (size_t)64 * wpl * 8 + 512 + (size_t)64 * wpl * 4 + (size_t)nR * 64;
-    TIMED(this, GS_K_PHASE_A, launch_wpl(W, [&](auto w) {
-            k_phase_a<decltype(w)::value><<<N, 64, lds, stream>>>(d, h, cur, head, amR, amW);
-          }));
-  }
+  k_oldmask<<<nblk(S, 256), 256, 0, stream>>>(d, h);
+  TIMED(this, GS_K_PHASE_A, launch_wpl(W, [&](auto w) {
+          k_phase_a<decltype(w)::value><<<N, 64, 0, stream>>>(d, h, cur, head, amR, amW);
+        }));
   if (!retireWords.empty()) {
     if ((int)retireWords.size() > retireCap) {
       int32_t* p = nullptr;
@@ -515,6 +520,10 @@ int gs_engine::checkDeviceError() {
     case E_TRUNCATE:
       gs_set_error("IHAVE/IWANT truncation at MaxIHaveLength is not built in this version");
       return GS_EUNSUPPORTED;
+    case E_FCAP:
+      gs_set_error("more first deliveries of one topic at one node in one hop than the per-topic "
+                   "first-deliverer table holds (min(slots_per_topic, 8 GiB / (num_nodes * num_topics)))");
+      return GS_ECAPACITY;
     case E_DOUBLE:
       gs_set_error("a peer sent the same message twice in one hop (outside the canonical model)");
       return GS_EUNSUPPORTED;
@@ -730,6 +739,12 @@ int gs_set_topic_score_params(gs_engine* g, int32_t topic, const gs_topic_score_
   if (topic < 0 || topic >= g->T) { gs_set_error("bad topic"); return GS_EINVAL; }
   int rc = gs_validate_topic_score_params(p);
   if (rc) return rc;
+  if (g->started && g->scoring && !g->d.needAge &&
+      p->MeshMessageDeliveriesWindow < g->retireHops * g->cfg.hop_ns) {
+    gs_set_error("MeshMessageDeliveriesWindow shorter than the message lifetime can only be set "
+                 "before the first step (per-message first-delivery hops are not kept)");
+    return GS_EUNSUPPORTED;
+  }
   const bool existed = g->tscored[topic] != 0;
   const gs_topic_score_params old = g->tps[topic];
   g->tps[topic] = *p;

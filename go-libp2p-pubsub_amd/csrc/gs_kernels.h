@@ -205,294 +205,341 @@ __device__ __forceinline__ int wm_rank(const WMask& a, int w) {
   return r + __popcll(a.m[w >> 6] & ((1ull << (w & 63)) - 1));
 }
 
-// Phase A — one wave per receiving node v; lane j*64+l holds word w = l + 64 j
-// of v's bitsets.  The frontier of a node (what it forwards this hop) is a
-// bitset restricted to the active words amR (messages young enough to be in
-// flight) plus a compact array ffc of its first deliverers in slot order, so
-// a receiver can skip what a sender got from it (ReceivedFrom exclusion,
-// gossipsub.go:1003) by reading ~one cache line instead of per-slot bytes.
-// Senders are scanned in ascending node id — the canonical arrival order.
+// Exclusive prefix-OR of a 64-bit value over ascending lanes (lane 0 gets 0).
+__device__ __forceinline__ uint64_t wave_prefix_or_excl(uint64_t x) {
+  const int lane = lane_id();
+  uint64_t incl = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = shfl_u64(incl, (lane - o) & 63);
+    if (lane >= o) incl |= y;
+  }
+  const uint64_t prev = shfl_u64(incl, (lane - 1) & 63);
+  return lane == 0 ? 0ull : prev;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum_ll(long long v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return (unsigned long long)v;
+}
+
+// Phase A — handleIncomingRPC / pushMsg for the payload of every RPC sent to
+// node v in the previous hop (pubsub.go:946-1022, score.go:693-964).  One
+// wave per receiving node; lane i = in-edge i, i.e. sender u_i = col[base+i],
+// so the lanes are in the canonical arrival order (senders ascending).
+// Topics are walked ascending and the words of a topic ascending; per word,
+//   A_i      = what sender i hands over (relay/publish frontier + IWANT response),
+//   P_i      = OR of A_j over non-graylisted senders j < i  (exclusive prefix-OR),
+//   fresh_i  = A_i & ~seen & ~P_i            (DeliverMessage from sender i),
+//   dup_i    = A_i & (seen | P_i) minus the copies the sender never sent
+//              (ReceivedFrom / author exclusion, gossipsub.go:1003),
+// which is exactly the sender-by-sender scan of the reference with each
+// sender's messages in ascending slot order.  The per-(edge, topic) score
+// counters of a topic are then updated for all senders at once, one
+// coalesced access per array (state is topic-major [t][E]).
+// Exclusion: a sender never returns a message to the neighbour it first got
+// it from.  The receiver checks its duplicate candidates against the sender's
+// first-deliverer table ffc[u][t][rank] (written by u one hop earlier, ranks
+// are u's fresh bits of topic t in slot order).
 template <int WPL>
 __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int head, WMask amR, WMask amW) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned long long* xrb = (unsigned long long*)smem;  // [64*WPL] IWANT-response bits of one sender
-  int* cntF = (int*)(smem + 64 * WPL * 8);               // [64] per-topic fresh counts
-  int* cntD = cntF + 64;                                  // [64] per-topic creditable duplicates
-  int* wscan = cntD + 64;                                 // [64*WPL] exclusive fresh-rank scan per word
-  uint8_t* ffTmp = (uint8_t*)(wscan + 64 * WPL);          // [popc(amR)*64] first deliverer per active slot
+  __shared__ uint64_t sseen[64 * WPL];  // v's seen words (amR + lazily loaded)
+  __shared__ uint64_t sU[64 * WPL];     // v's fresh union per word (its next frontier)
+  __shared__ uint64_t spm[64 * WPL];    // slots published in the previous hop
+  __shared__ uint64_t sold[64 * WPL];   // slots too old for a first delivery
   const int v = blockIdx.x;
   const int lane = lane_id();
   const int prv = cur ^ 1;
   const int W = d.W;
   const int Wt = d.Wt;
+  const int T = d.T;
+  const int Kt = d.Kt;
   const int64_t base = d.rowptr[v];
   const int deg = (int)(d.rowptr[v + 1] - base);
   const uint64_t sv = d.sub[v];
-  const int64_t S = d.S;
-  cntF[lane] = 0;
-  cntD[lane] = 0;
-  // in-edge metadata, lane i = in-edge i (one coalesced/gathered load each)
-  int uL = 0, jrL = 0;
-  uint64_t relayL = 0, pubL = 0;
-  int64_t irL = -1;
-  bool gl = false;
-  if (lane < deg) {
+  const bool valid = lane < deg;
+  // in-edge metadata (lane = in-edge)
+  int u = 0, jr = 0;
+  uint64_t relay = 0, pub = 0;
+  bool gray = false;
+  int irOff = 0, irN = 0;
+  if (valid) {
     const int64_t e = base + lane;
-    uL = d.col[e];
+    u = d.col[e];
     const int64_t r = d.rev[e];
-    jrL = (int)(r - d.rowptr[uL]);
-    relayL = d.fwdRelay[prv][r] & sv;
-    pubL = d.fwdPub[prv][r] & sv;
-    irL = d.cIresp[prv][r];
-    gl = d.router == 2 && d.scoring && !d.direct[e] && d.score0[e] < d.graylistThr;
+    jr = (int)(r - d.rowptr[u]);
+    relay = d.fwdRelay[prv][r] & sv;
+    pub = d.fwdPub[prv][r] & sv;
+    const int64_t ir = d.cIresp[prv][r];
+    if (ir >= 0) {
+      irOff = (int)(ir >> 24);
+      irN = (int)(ir & 0xFFFFFF);
+    }
+    gray = d.router == 2 && d.scoring && !d.direct[e] && d.score0[e] < d.graylistThr;
   }
-  unsigned long long amask = __ballot(lane < deg && ((relayL | pubL) != 0 || irL >= 0));
-  const unsigned long long glmask = __ballot(gl);
-  const int myPeer = (d.router == 1 && lane < deg) ? uL : -1;
-  const uint64_t myPeerSub = myPeer >= 0 ? d.sub[myPeer] : 0;
-  uint64_t seen[WPL], facc[WPL];
-  unsigned loaded = 0;
+  int irPos = 0;
+  int nextSlot = irN > 0 ? d.pool[prv][irOff] : 0x7FFFFFFF;
+  const bool authV = d.nAuth[v] > 0;  // v authored a live message: author exclusion possible
+  WMask loaded = amR;
 #pragma unroll
   for (int j = 0; j < WPL; ++j) {
     const int w = lane + 64 * j;
-    seen[j] = 0;
-    facc[j] = 0;
-    if (w < W && wm_has(amR, w)) {
-      seen[j] = d.seen[(int64_t)v * W + w];
-      loaded |= 1u << j;
+    if (w < W) {
+      sseen[w] = wm_has(amR, w) ? d.seen[(int64_t)v * W + w] : 0ull;
+      sU[w] = 0ull;
+      spm[w] = d.pubmask[prv][w];
+      sold[w] = d.oldm[w];
     }
   }
   long long nDeliv = 0, nDup = 0, nSent = 0, nGray = 0;
-  while (amask) {
-    const int i = __ffsll((long long)amask) - 1;
-    amask &= amask - 1;
-    const int u = __shfl(uL, i);
-    const int jr = __shfl(jrL, i);
-    const uint64_t relay = shfl_u64(relayL, i);
-    const uint64_t pub = shfl_u64(pubL, i);
-    const int64_t iresp = (int64_t)shfl_u64((uint64_t)irL, i);
-    const bool gray = (glmask >> i) & 1;
-    const int64_t e = base + i;
-    if (iresp >= 0) arena_read(d, prv, iresp, xrb);
-    // the sender's frontier words of the topics it forwards to us
-    uint64_t nwv[WPL], pmv[WPL];
-    int fc[WPL];
+  const uint8_t* ffcU = d.ffc[prv] + (int64_t)u * T * Kt;
+  uint8_t* ffcV = d.ffc[cur] + (int64_t)v * T * Kt;
+  const bool scoring = d.scoring != 0;
+  const int64_t eIdx = base + lane;
+
+  // ---- software pipeline over chunks (topic t, words w0..w0+3): the loads of
+  // the next chunk (sender frontier words; at a topic start also the sender's
+  // first-deliverer window and the edge's score counters) are issued before
+  // the current chunk is processed, so their latency overlaps its work.
+  auto nextTopic = [&](int t0) {
+    const uint64_t rest = t0 < 64 ? (sv >> t0) : 0ull;
+    return rest ? t0 + __ffsll((long long)rest) - 1 : T;
+  };
+  uint64_t pnw[4];
+  uint64_t pLo = 0, pHi = 0;
+  double pF = 0.0, pM = 0.0;
+  uint8_t pFl = 0;
+  auto issue = [&](int tt, int ww0, bool start) {
+    const uint64_t tb = 1ull << tt;
+    const bool fw = ((relay | pub) & tb) != 0;
 #pragma unroll
-    for (int j = 0; j < WPL; ++j) {
-      const int w = lane + 64 * j;
-      nwv[j] = 0;
-      pmv[j] = 0;
-      if (w < W && wm_has(amR, w) && (((relay | pub) >> (w / Wt)) & 1)) {
-        nwv[j] = d.newb[prv][(int64_t)u * W + w];
-        pmv[j] = d.pubmask[prv][w];
-      }
-      fc[j] = __popcll(nwv[j] & ~pmv[j]);
+    for (int k = 0; k < 4; ++k) {
+      const int w = ww0 + k;
+      pnw[k] = 0;
+      if (fw && w < (tt + 1) * Wt && wm_has(amR, w)) pnw[k] = d.newb[prv][(int64_t)u * W + w];
     }
-    // exclusive scan of the sender's relayed-bit counts over ascending words
-    // (only needed when a duplicate candidate must be checked against ffc)
-    int running = 0;
-#pragma unroll
-    for (int j = 0; j < WPL; ++j) {
-      int incl = fc[j];
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
+    if (start) {
+      pLo = pHi = 0;
+      if (relay & tb) {
+        const uint64_t* p = (const uint64_t*)(ffcU + (int64_t)tt * Kt);
+        pLo = p[0];
+        pHi = p[1];
       }
-      wscan[lane + 64 * j] = running + incl - fc[j];
-      running += __shfl(incl, 63);
+      pF = pM = 0.0;
+      pFl = 0;
+      if (scoring && valid && (fw || nextSlot < (tt + 1) * d.St)) {
+        const int64_t ti = (int64_t)tt * d.E + eIdx;
+        pFl = d.flags[ti];
+        pF = d.fmd[ti];
+        pM = d.mmd[ti];
+      }
     }
-    __syncthreads();
-    // step 1 (lane = word): what the sender hands us, split fresh / already seen
-    uint64_t X[WPL], FR[WPL], DU[WPL];
+  };
+  __syncthreads();
+  int t = nextTopic(0);
+  int w0 = t * Wt;
+  if (t < T) issue(t, w0, true);
+  int nf = 0, ndc = 0;  // this lane's fresh / creditable-duplicate counts in topic t
+  int rankT = 0;        // v's fresh count in topic t so far (wave-uniform)
+  int uRank = 0;        // sender's relayed-fresh count in topic t before the current word
+  int cBase = 0;        // cached 16-byte window of the sender's ffc row for topic t
+  uint64_t cLo = 0, cHi = 0;
+  double curF = 0.0, curM = 0.0;
+  uint8_t curFl = 0;
+  bool start = true;
+  while (t < T) {
+    uint64_t nwv[4];
 #pragma unroll
-    for (int j = 0; j < WPL; ++j) {
-      const int w = lane + 64 * j;
-      X[j] = FR[j] = DU[j] = 0;
-      if (w >= W) continue;
-      const int tw = w / Wt;
-      const uint64_t nw = nwv[j], pm = pmv[j];
-      uint64_t x = (nw & ~pm & (((relay >> tw) & 1) ? ~0ull : 0ull)) |
-                   (nw & pm & (((pub >> tw) & 1) ? ~0ull : 0ull));
-      if (d.router == 1 && x) {  // randomsub: per-message target sets
-        uint64_t y = x, keep = 0;
-        while (y) {
-          const int b = __ffsll((long long)y) - 1;
-          y &= y - 1;
-          if ((d.sel[(int64_t)u * S + (int64_t)w * 64 + b] >> jr) & 1) keep |= 1ull << b;
+    for (int k = 0; k < 4; ++k) nwv[k] = pnw[k];
+    if (start) {
+      cLo = pLo;
+      cHi = pHi;
+      cBase = 0;
+      curF = pF;
+      curM = pM;
+      curFl = pFl;
+      nf = ndc = rankT = uRank = 0;
+    }
+    const int tEnd = (t + 1) * Wt;
+    int nt = t, nw0 = w0 + 4;
+    bool nStart = false;
+    if (nw0 >= tEnd) {
+      nt = nextTopic(t + 1);
+      nw0 = nt * Wt;
+      nStart = true;
+    }
+    if (nt < T) issue(nt, nw0, nStart);
+    const uint64_t tb = 1ull << t;
+    const bool fwdRelay = (relay & tb) != 0, fwdPub = (pub & tb) != 0;
+    if (__ballot(fwdRelay || fwdPub || nextSlot < tEnd * 64)) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int w = w0 + k;
+        if (w >= tEnd) break;
+        const uint64_t nw = nwv[k];
+        const uint64_t pm = spm[w];
+        uint64_t x = (fwdRelay ? (nw & ~pm) : 0ull) | (fwdPub ? (nw & pm) : 0ull);
+        if (d.router == 1 && x) {  // randomsub: per-message target sets of the sender
+          uint64_t y = x, keep = 0;
+          while (y) {
+            const int b = __ffsll((long long)y) - 1;
+            y &= y - 1;
+            if ((d.sel[(int64_t)u * d.S + (int64_t)w * 64 + b] >> jr) & 1) keep |= 1ull << b;
+          }
+          x = keep;
         }
-        x = keep;
-      }
-      const uint64_t xr = iresp >= 0 ? (uint64_t)xrb[w] : 0ull;
-      const uint64_t xa = x | xr;
-      if (!xa) continue;
-      if (!((loaded >> j) & 1)) {  // an IWANT response outside the active window
-        seen[j] = d.seen[(int64_t)v * W + w];
-        loaded |= 1u << j;
-      }
-      X[j] = x;
-      FR[j] = xa & ~seen[j];
-      DU[j] = xa & seen[j];
-      if (!gray) {
-        seen[j] |= FR[j];
-        facc[j] |= FR[j];
-      }
-    }
-    // step 2 (lane = bit of one active word): exclusion, P3 window, records.
-    // Every per-message load is one coalesced vector access per word.
-    int nF = 0, nDupK = 0, nCred = 0;
-    long long sent = 0, rpcs = 0;
-#pragma unroll
-    for (int j = 0; j < WPL; ++j) {
-      unsigned long long act = __ballot((FR[j] | DU[j]) != 0);
-      while (act) {
-        const int o = __ffsll((long long)act) - 1;
-        act &= act - 1;
-        const int w = o + 64 * j;
-        const int tw = w / Wt;
-        const uint64_t fresh = shfl_u64(FR[j], o), dup = shfl_u64(DU[j], o), x = shfl_u64(X[j], o);
-        const uint64_t nw = shfl_u64(nwv[j], o), pm = shfl_u64(pmv[j], o);
-        const uint64_t bit = 1ull << lane;
-        const int64_t slot = (int64_t)w * 64 + lane;
-        const bool isF = fresh & bit, isD = dup & bit;
-        const bool cand = isD && (x & bit);  // ReceivedFrom / author exclusion (gossipsub.go:1003)
-        const bool needPh = isF || (isD && !gray && d.needAge);
-        const int64_t ph = needPh ? d.slotPubHop[slot] : 0;
-        int sSrc = -1, ffb = -1;
-        if (cand) {
-          sSrc = d.slotSrc[slot];
-          if (!(pm & bit)) {
-            const int rank = (d.T > 1 ? d.fpre[prv][(int64_t)u * d.T + tw] : 0) + (wscan[w] - wscan[tw * Wt]) +
-                             __popcll(nw & ~pm & (bit - 1));
-            if (rank < d.fcap) ffb = d.ffc[prv][(int64_t)u * d.fcap + rank];
+        uint64_t xr = 0;  // IWANT response (slot ids ascending)
+        while (nextSlot < (w + 1) * 64) {
+          if (nextSlot >= w * 64) xr |= 1ull << (nextSlot & 63);
+          ++irPos;
+          nextSlot = irPos < irN ? d.pool[prv][irOff + irPos] : 0x7FFFFFFF;
+        }
+        const uint64_t A = x | xr;
+        const uint64_t relF = nw & ~pm;  // the sender's relayed-fresh bits of this word
+        if (!__ballot(A != 0)) {
+          uRank += __popcll(relF);
+          continue;
+        }
+        if (!wm_has(loaded, w)) {  // IWANT response outside the active window
+          if (lane == 0) sseen[w] = d.seen[(int64_t)v * W + w];
+          loaded.m[w >> 6] |= 1ull << (w & 63);
+          __syncthreads();
+        }
+        const uint64_t S = sseen[w];
+        // ---- copies the sender never sent (it got them from us / we are the author)
+        uint64_t excl = 0;
+        uint64_t cand = x & ~pm & S;
+        while (cand) {
+          const int b = __ffsll((long long)cand) - 1;
+          cand &= cand - 1;
+          const int rank = uRank + __popcll(relF & ((1ull << b) - 1));
+          int ffb = -1;  // rank >= Kt: the sender raised E_FCAP when it stored this rank
+          if (rank < Kt) {
+            const int cb = rank & ~15;
+            if (cb != cBase) {
+              const uint64_t* p = (const uint64_t*)(ffcU + (int64_t)t * Kt + cb);
+              cLo = p[0];
+              cHi = p[1];
+              cBase = cb;
+            }
+            const int o = rank - cb;
+            ffb = (int)(((o < 8 ? cLo >> (8 * o) : cHi >> (8 * (o - 8)))) & 0xFF);
+          }
+          if (ffb == jr) excl |= 1ull << b;
+        }
+        if (authV) {
+          uint64_t c2 = x & S & ~excl;
+          while (c2) {
+            const int b = __ffsll((long long)c2) - 1;
+            c2 &= c2 - 1;
+            if (d.slotSrc[w * 64 + b] == v) excl |= 1ull << b;
           }
         }
-        const int ag = (isD && !gray && d.needAge) ? d.age[(int64_t)v * S + slot] : 0;
-        const bool excl = cand && (sSrc == v || ffb == jr);
-        const bool dupK = isD && !excl;
-        const int64_t window = d.tp[tw].MmdWindow;
-        const bool cred = dupK && (!d.needAge || !((h - (ph + ag)) * d.hop_ns > window));
-        const int kD = __popcll(__ballot(dupK));
-        const int kF = __popcll(fresh);
-        sent += kF + kD;
-        rpcs += __popcll(__ballot((isF || dupK) && (x & bit)));
-        if (gray) continue;
-        const int kC = __popcll(__ballot(cred));
-        if (isF) {
-          const int64_t a = h - ph;
-          const bool inWin = wm_has(amR, w);
-          if (a > d.maxAge || !inWin) set_err(d, E_LATE);
-          if (inWin) ffTmp[wm_rank(amR, w) * 64 + lane] = (uint8_t)i;
-          if (d.needAge) d.age[(int64_t)v * S + slot] = (int16_t)a;
-          if (d.record) d.ffrom[(int64_t)v * S + slot] = (uint8_t)i;
+        uRank += __popcll(relF);
+        // ---- dedup in sender order
+        const uint64_t Ag = gray ? 0ull : A;
+        const uint64_t P = wave_prefix_or_excl(Ag);
+        const uint64_t fresh = Ag & ~S & ~P;
+        const uint64_t U = shfl_u64(P | Ag, 63) & ~S;
+        const uint64_t sentBits = A & ~excl;
+        nSent += __popcll(sentBits);
+        if (gray) nGray += __popcll(x & ~excl);  // one RPC per relayed message, all dropped
+        const uint64_t dupK = gray ? 0ull : (sentBits & ~fresh);
+        uint64_t cred = dupK;
+        if (d.needAge && dupK) {
+          // markDuplicateMessageDelivery window (score.go:955): first delivered at
+          // pubHop + age; copies of messages first delivered earlier in this hop
+          // (bits in P) are within any window
+          const int64_t window = d.tp[t].MmdWindow;
+          uint64_t y = dupK & S;
+          while (y) {
+            const int b = __ffsll((long long)y) - 1;
+            y &= y - 1;
+            const int64_t slot = (int64_t)w * 64 + b;
+            const int64_t firstHop = d.slotPubHop[slot] + d.age[(int64_t)v * d.S + slot];
+            if ((h - firstHop) * d.hop_ns > window) cred &= ~(1ull << b);
+          }
         }
-        nF += kF;
-        nDupK += kD;
-        nCred += kC;
-        if (d.scoring && d.T > 1 && lane == 0) {
-          cntF[tw] += kF;
-          cntD[tw] += kC;
+        nf += __popcll(fresh);
+        ndc += __popcll(cred);
+        nDeliv += __popcll(fresh);
+        nDup += __popcll(dupK);
+        // ---- v's first deliverers (ffc), ranks in slot order within topic t
+        uint64_t f = fresh;
+        while (f) {
+          const int b = __ffsll((long long)f) - 1;
+          f &= f - 1;
+          const int rank = rankT + __popcll(U & ((1ull << b) - 1));
+          if (rank < Kt) ffcV[(int64_t)t * Kt + rank] = (uint8_t)lane;
+          else set_err(d, E_FCAP);
+          if (d.needAge || d.record) {
+            const int64_t slot = (int64_t)w * 64 + b;
+            const int64_t a = h - d.slotPubHop[slot];
+            if (d.needAge) d.age[(int64_t)v * d.S + slot] = (int16_t)a;
+            if (d.record) d.ffrom[(int64_t)v * d.S + slot] = (uint8_t)lane;
+          }
+        }
+        if (U) {
+          if (lane == 0) {
+            if ((U & sold[w]) || !wm_has(amW, w)) set_err(d, E_LATE);
+            sseen[w] = S | U;
+            sU[w] = U;
+          }
+          rankT += __popcll(U);
+          if (d.router == 1) {  // randomsub: targets of every message first delivered here
+            uint64_t y = U;
+            while (y) {
+              const int b = __ffsll((long long)y) - 1;
+              y &= y - 1;
+              const int ff = __ffsll((long long)__ballot((fresh >> b) & 1)) - 1;
+              rs_select(d, v, deg, valid ? u : -1, valid ? d.sub[u] : 0, w * 64 + b, ff);
+            }
+          }
         }
       }
     }
-    const int myF = nF, myNd = nCred, myDup = nDupK;
-    nSent += sent;
-    if (gray) {
-      nGray += rpcs;  // the IWANT-response RPC is counted with the control RPCs in phase B
-      continue;
-    }
-    nDeliv += myF;
-    nDup += myDup;
-    // score counters of edge (v <- u): fmd += fresh, mmd += fresh + creditable dups
-    if (d.scoring && (myF > 0 || myNd > 0)) {
-      const int nfT1 = myF;
-      const int ndT1 = myNd;
-      __syncthreads();
-      if (lane < d.T) {
-        const int nf = d.T == 1 ? nfT1 : cntF[lane];
-        const int nd = d.T == 1 ? ndT1 : cntD[lane];
-        const TopicP& tp = d.tp[lane];
-        if ((nf || nd) && tp.scored) {
-          const int64_t ti = (int64_t)lane * d.E + e;
-          if (nf) d.fmd[ti] = add_ones_capped(d.fmd[ti], nf, tp.FmdCap);
-          if (d.flags[ti] & 1) d.mmd[ti] = add_ones_capped(d.mmd[ti], nf + nd, tp.MmdCap);
-        }
-        cntF[lane] = 0;
-        cntD[lane] = 0;
+    if (nStart || nt >= T) {
+      // score counters of the in-edges for topic t: fmd += fresh, mmd += fresh +
+      // creditable duplicates while in the mesh (score.go:915-928, 945-963)
+      if (scoring && valid && (nf | ndc) && d.tp[t].scored) {
+        const TopicP& tp = d.tp[t];
+        const int64_t ti = (int64_t)t * d.E + eIdx;
+        if (nf) d.fmd[ti] = add_ones_capped(curF, nf, tp.FmdCap);
+        if (curFl & 1) d.mmd[ti] = add_ones_capped(curM, nf + ndc, tp.MmdCap);
       }
-      __syncthreads();
     }
+    t = nt;
+    w0 = nw0;
+    start = nStart;
   }
+  __syncthreads();
   // ---- write back: seen, frontier (active words of this hop), mcache Put
 #pragma unroll
   for (int j = 0; j < WPL; ++j) {
     const int w = lane + 64 * j;
     if (w >= W) continue;
-    if ((loaded >> j) & 1) d.seen[(int64_t)v * W + w] = seen[j];
-    if (wm_has(amW, w)) d.newb[cur][(int64_t)v * W + w] = facc[j];
-    else if (facc[j]) set_err(d, E_LATE);
-    if (d.router == 2 && facc[j]) d.hist[((int64_t)head * d.N + v) * W + w] |= facc[j];
+    const uint64_t U = sU[w];
+    if (wm_has(loaded, w)) d.seen[(int64_t)v * W + w] = sseen[w];
+    if (wm_has(amW, w)) d.newb[cur][(int64_t)v * W + w] = U;
+    if (d.router == 2 && U) d.hist[((int64_t)head * d.N + v) * W + w] |= U;
   }
-  // ---- first deliverers in slot order (ffc) and per-topic rank prefixes (fpre);
-  // written bit-parallel, one coalesced byte store per active word
-  {
-    int running = 0;
-#pragma unroll
-    for (int j = 0; j < WPL; ++j) {
-      const int w = lane + 64 * j;
-      const int c = __popcll(facc[j]);
-      int incl = c;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-      }
-      const int rankW = running + incl - c;
-      if (d.T > 1 && w < W && (w % Wt) == 0) d.fpre[cur][(int64_t)v * d.T + w / Wt] = rankW;
-      unsigned long long act = __ballot(facc[j] != 0);
-      while (act) {
-        const int o = __ffsll((long long)act) - 1;
-        act &= act - 1;
-        const int wo = o + 64 * j;
-        const uint64_t f = shfl_u64(facc[j], o);
-        const int r0 = __shfl(rankW, o);
-        const uint64_t bit = 1ull << lane;
-        if (f & bit) {
-          const int rank = r0 + __popcll(f & (bit - 1));
-          if (rank < d.fcap && wm_has(amR, wo))
-            d.ffc[cur][(int64_t)v * d.fcap + rank] = ffTmp[wm_rank(amR, wo) * 64 + lane];
-          else
-            set_err(d, E_LATE);
-        }
-      }
-      running += __shfl(incl, 63);
-    }
-  }
-  // ---- randomsub: choose the targets of every message first delivered here
-  if (d.router == 1) {
-#pragma unroll
-    for (int j = 0; j < WPL; ++j) {
-      unsigned long long lanesWith = __ballot(facc[j] != 0);
-      while (lanesWith) {
-        const int src = __ffsll((long long)lanesWith) - 1;
-        lanesWith &= lanesWith - 1;
-        uint64_t fw = shfl_u64(facc[j], src);
-        const int w = src + 64 * j;
-        if (!wm_has(amR, w)) continue;  // E_LATE already raised
-        const int cw = wm_rank(amR, w);
-        while (fw) {
-          const int b = __ffsll((long long)fw) - 1;
-          fw &= fw - 1;
-          rs_select(d, v, deg, myPeer, myPeerSub, w * 64 + b, ffTmp[cw * 64 + b]);
-        }
-      }
-    }
-  }
-  const long long sums[4] = {nDeliv, nDup, nSent, nGray};  // wave-uniform
+  const unsigned long long s0 = wave_sum_ll(nDeliv), s1 = wave_sum_ll(nDup), s2 = wave_sum_ll(nSent),
+                           s3 = wave_sum_ll(nGray);
   if (lane == 0) {
-    if (sums[0]) ctr_add(d, C_DELIVERIES, (unsigned long long)sums[0]);
-    if (sums[1]) ctr_add(d, C_DUPLICATES, (unsigned long long)sums[1]);
-    if (sums[2]) ctr_add(d, C_TRANSMISSIONS, (unsigned long long)sums[2]);
-    if (sums[3]) ctr_add(d, C_GRAYLISTED, (unsigned long long)sums[3]);
+    if (s0) ctr_add(d, C_DELIVERIES, s0);
+    if (s1) ctr_add(d, C_DUPLICATES, s1);
+    if (s2) ctr_add(d, C_TRANSMISSIONS, s2);
+    if (s3) ctr_add(d, C_GRAYLISTED, s3);
   }
+}
+
+// Slots whose message was published more than maxAge hops ago: a first
+// delivery of one of them in hop h is outside the engine's window (E_LATE).
+__global__ void k_oldmask(Dev d, int64_t h) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool old = s < d.S && d.slotSrc[s] >= 0 && d.slotPubHop[s] < h - d.maxAge;
+  const unsigned long long m = __ballot(old);
+  if (s < d.S && (s & 63) == 0) d.oldm[s >> 6] = m;
 }
 
 // Clears the seen bits of recycled message slots (the slots published in
@@ -514,6 +561,9 @@ __global__ void k_publish(Dev d, int b, int n, int64_t h, int cur, int head) {
   if (i >= n) return;
   const int slot = d.mSlot[b + i];
   const int src = d.mSrc[b + i];
+  const int prevAuthor = d.slotSrc[slot];  // the retired message of this slot
+  if (prevAuthor >= 0) atomicSub(&d.nAuth[prevAuthor], 1);
+  atomicAdd(&d.nAuth[src], 1);
   d.slotSrc[slot] = src;
   d.slotPubHop[slot] = h;
   d.slotMid[slot] = d.mId[b + i];

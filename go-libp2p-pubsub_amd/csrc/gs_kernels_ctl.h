@@ -63,6 +63,7 @@ template <int WPL>
 __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, int cur, int head) {
   __shared__ unsigned long long reqb[64 * GS_MAX_WPL];
   __shared__ unsigned long long ptx[GS_PTX];
+  __shared__ double sterm[64];
   const int v = blockIdx.x;
   const int lane = lane_id();
   const int prv = cur ^ 1;
@@ -148,7 +149,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
       while (gj) {
         const int t = __ffsll((long long)gj) - 1;
         gj &= gj - 1;
-        if (dirty) { sc = edge_score(d, e); dirty = false; }
+        if (dirty) { sc = edge_score_wave(d, e, sterm); dirty = false; }
         if (sc >= d.gossipThr) ph++;  // handleIHave's counter (no IHAVE entries)
         if (graft_one(d, e, v, t, sc, now, meshcnt, meshE, dirty)) {
           pruneOut |= 1ull << t;
@@ -159,7 +160,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     // (2) reply RPCs: IWANT requests and PRUNEs answering our own control
     const int nRep = npre - nJoin;
     if (nRep > 0) {
-      if (dirty) { sc = edge_score(d, e); dirty = false; }
+      if (dirty) { sc = edge_score_wave(d, e, sterm); dirty = false; }
       const bool gossipOK = sc >= d.gossipThr;
       if (gossipOK) ph += nRep;
       if (gossipOK && iwRec >= 0) {
@@ -231,7 +232,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     }
     // (3) heartbeat RPC: IHAVE, GRAFT, PRUNE (gossipsub.go:1618-1654 sends it last)
     if (hb) {
-      if (dirty) { sc = edge_score(d, e); dirty = false; }
+      if (dirty) { sc = edge_score_wave(d, e, sterm); dirty = false; }
       bool iwantAny = false;
       if (sc >= d.gossipThr) {
         ph++;
@@ -427,9 +428,12 @@ __global__ __launch_bounds__(64) void k_hb_pre(Dev d, int64_t now, uint64_t tick
 }
 
 // emitGossip (gossipsub.go:1658-1712) for topic t of node v; lanes = edges.
+// The peer filter uses the live Score(p) (:1681): Slive caches it per lane and
+// is recomputed (one wave-parallel score per lane) only after the peer's stats
+// changed earlier in this heartbeat.
 __device__ __forceinline__ uint64_t emit_gossip(const Dev& d, int v, int t, int64_t hop, int head, bool valid,
-                                                int vcol, bool inTopic, bool excl, bool dir, double S, bool dirty,
-                                                int64_t e) {
+                                                int vcol, bool inTopic, bool excl, bool dir, double& Slive,
+                                                bool& dirty, int64_t rowBase, double* lds) {
   const int lane = lane_id();
   int nm = 0;
   for (int w = t * d.Wt + lane; w < (t + 1) * d.Wt; w += 64) {
@@ -440,9 +444,18 @@ __device__ __forceinline__ uint64_t emit_gossip(const Dev& d, int v, int t, int6
   nm = wave_sum_int(nm);
   if (nm == 0) return 0;
   if (nm > d.MaxIHaveLength && lane == 0) set_err(d, E_TRUNCATE);
-  double live = S;
-  if (dirty && valid) live = edge_score(d, e);
-  const bool cand = valid && inTopic && !excl && !dir && live >= d.gossipThr;
+  const bool base = valid && inTopic && !excl && !dir;
+  unsigned long long dm = __ballot(base && dirty);
+  while (dm) {
+    const int j = __ffsll((long long)dm) - 1;
+    dm &= dm - 1;
+    const double s = edge_score_wave(d, rowBase + j, lds);
+    if (lane == j) {
+      Slive = s;
+      dirty = false;
+    }
+  }
+  const bool cand = base && Slive >= d.gossipThr;
   const int n = __popcll(__ballot(cand));
   int target = d.Dlazy;
   const int factor = (int)(d.GossipFactor * (double)n);
@@ -466,6 +479,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
   __shared__ int plst[64];
   __shared__ int obs[64];
   __shared__ int posOf[64];
+  __shared__ double sterm[64];
   const int v = blockIdx.x;
   const int lane = lane_id();
   const int64_t base = d.rowptr[v];
@@ -477,6 +491,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
   uint64_t meshl = valid ? d.mesh[e] : 0;
   uint64_t fanl = valid ? d.fanout[e] : 0;
   const double S = valid ? d.score1[e] : 0.0;
+  double Slive = S;  // live Score(p) for emitGossip
   const bool dir = valid && d.direct[e];
   const bool ob = valid && d.outbound[e];
   bool dirty = false;
@@ -620,7 +635,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
         }
       }
     }
-    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, m, dir, S, dirty, e);
+    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, m, dir, Slive, dirty, base, sterm);
   }
   // expire fanout for topics we haven't published to in a while
   uint64_t fpres = d.fanoutPresent[v];
@@ -651,7 +666,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
         f = true;
       }
     }
-    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, f, dir, S, dirty, e);
+    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, f, dir, Slive, dirty, base, sterm);
   }
   // sendGraftPrune + flush: one heartbeat RPC per peer with any control
   if (valid) {
