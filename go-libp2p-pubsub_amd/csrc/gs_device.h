@@ -67,14 +67,15 @@ struct Dev {
   uint64_t OGT;
   // per-node state
   uint64_t* seen;
-  uint64_t* newb[2];
   uint64_t* hist;  // [R][N][W]
+  uint64_t* gw;    // [N][W] IHAVE payload of the node's last heartbeat (gossip windows)
   int16_t* age;    // [N][S] first-delivery hop - publish hop   (record / short-window mode)
   uint8_t* ffrom;  // [N][S] first-deliverer neighbour slot, 255 = self (record mode)
-  uint8_t* ffc[2]; // [N][T][Kt] first deliverer (in-edge index) of each message first
-                   // delivered in hop h, per topic in ascending slot order (rank among
-                   // the node's fresh bits of that topic)
-  int32_t Kt;      // per-topic capacity of ffc rows
+  uint32_t* fl[2]; // [N][FC] frontier list of hop h: slots first delivered in hop h
+                   // (| in-edge index << 16) and own publishes (| 255 << 16), ascending
+  int32_t* fln[2]; // [N] list lengths
+  int32_t FC;      // list capacity per node (multiple of 4)
+  int32_t maxDeg;  // largest node degree (<= 64)
   uint64_t* oldm;  // [W] slots whose message is too old to be first-delivered this hop
   int32_t* nAuth;  // [N] live message slots authored by the node
   int32_t needAge, record;

@@ -284,8 +284,9 @@ int gs_engine::start() {
   x.sub = dSub; x.app = dApp; x.p6 = dP6; x.tp = dTp;
 
   x.seen = dalloc<uint64_t>(NW); chk(x.seen);
-  for (int k = 0; k < 2; ++k) { x.newb[k] = dalloc<uint64_t>(NW); chk(x.newb[k]); }
   x.hist = dalloc<uint64_t>((size_t)R * NW); chk(x.hist);
+  x.gw = cfg.router == GS_ROUTER_GOSSIPSUB ? dalloc<uint64_t>(NW) : nullptr;
+  if (cfg.router == GS_ROUTER_GOSSIPSUB) chk(x.gw);
   // per-slot first-delivery hops only when read back or when the P3 window
   // check can fail: a duplicate always arrives less than retireHops after the
   // message's first delivery, so a MeshMessageDeliveriesWindow of at least
@@ -296,15 +297,18 @@ int gs_engine::start() {
   x.ffrom = x.record ? dalloc<uint8_t>(NS) : nullptr;
   if (x.needAge) chk(x.age);
   if (x.record) chk(x.ffrom);
-  // first-deliverer tables: per (node, topic) Kt bytes, one per message first
-  // delivered in a hop (ranked in slot order); Kt is a multiple of 16
+  // frontier lists: per node FC entries of 4 bytes (a node's first deliveries
+  // of one hop plus its own publishes), at most 8 GiB per parity
   {
-    const int64_t budget = 8ll << 30;  // bytes per parity
-    int64_t kt = std::min<int64_t>(St, budget / ((int64_t)N * T));
-    kt = std::max<int64_t>(16, kt & ~15ll);
-    x.Kt = (int32_t)std::min<int64_t>(kt, ((int64_t)St + 15) & ~15ll);
+    const int64_t budget = 8ll << 30;
+    int64_t fc = std::min<int64_t>(S + 64, budget / (4 * (int64_t)N));
+    x.FC = (int32_t)std::max<int64_t>(64, fc & ~3ll);
   }
-  for (int k = 0; k < 2; ++k) { x.ffc[k] = dalloc<uint8_t>((size_t)N * T * x.Kt); chk(x.ffc[k]); }
+  for (int k = 0; k < 2; ++k) {
+    x.fl[k] = dalloc<uint32_t>((size_t)N * x.FC); chk(x.fl[k]);
+    x.fln[k] = dalloc<int32_t>(N); chk(x.fln[k]);
+  }
+  x.maxDeg = std::max(1, maxdeg);
   x.oldm = dalloc<uint64_t>(W); chk(x.oldm);
   x.nAuth = dalloc<int32_t>(N); chk(x.nAuth);
   x.sel = cfg.router == GS_ROUTER_RANDOMSUB ? dalloc<uint64_t>(NS) : nullptr;
@@ -464,9 +468,15 @@ int gs_engine::stepOne() {
   TIMED(this, GS_K_FWD, (k_fwd<<<eb, 256, 0, stream>>>(d, cur)));
   if (n > 0) k_pubmask<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, cur);
   k_oldmask<<<nblk(S, 256), 256, 0, stream>>>(d, h);
-  TIMED(this, GS_K_PHASE_A, launch_wpl(W, [&](auto w) {
-          k_phase_a<decltype(w)::value><<<N, 64, 0, stream>>>(d, h, cur, head, amR, amW);
-        }));
+  {
+    const int nR = __builtin_popcountll(amR.m[0]) + __builtin_popcountll(amR.m[1]) +
+                   __builtin_popcountll(amR.m[2]) + __builtin_popcountll(amR.m[3]);
+    const size_t nCnt = ((size_t)T * d.maxDeg + 3) & ~(size_t)3;
+    const size_t lds = 4 * nCnt + 8 * (size_t)nR + 64 * (size_t)nR + (d.needAge ? 4 * nCnt : 0);
+    TIMED(this, GS_K_PHASE_A, launch_wpl(W, [&](auto w) {
+            k_phase_a<decltype(w)::value><<<N, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR);
+          }));
+  }
   if (!retireWords.empty()) {
     if ((int)retireWords.size() > retireCap) {
       int32_t* p = nullptr;
@@ -482,6 +492,7 @@ int gs_engine::stepOne() {
   }
   if (n > 0) {
     TIMED(this, GS_K_PUBLISH, (k_publish<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, h, cur, head)));
+    k_publist<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, cur);
     if (cfg.router == GS_ROUTER_RANDOMSUB) k_publish_rs<<<n, 64, 0, stream>>>(d, (int)b);
   }
   if (gossip) {
@@ -521,8 +532,8 @@ int gs_engine::checkDeviceError() {
       gs_set_error("IHAVE/IWANT truncation at MaxIHaveLength is not built in this version");
       return GS_EUNSUPPORTED;
     case E_FCAP:
-      gs_set_error("more first deliveries of one topic at one node in one hop than the per-topic "
-                   "first-deliverer table holds (min(slots_per_topic, 8 GiB / (num_nodes * num_topics)))");
+      gs_set_error("more first deliveries (plus own publishes) at one node in one hop than its "
+                   "frontier list holds (min(slots + 64, 2^31 / num_nodes) entries)");
       return GS_ECAPACITY;
     case E_DOUBLE:
       gs_set_error("a peer sent the same message twice in one hop (outside the canonical model)");

@@ -223,43 +223,61 @@ __device__ __forceinline__ unsigned long long wave_sum_ll(long long v) {
   return (unsigned long long)v;
 }
 
+__device__ __forceinline__ int wave_min_int(int x) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const int y = __shfl_xor(x, o);
+    x = y < x ? y : x;
+  }
+  return x;
+}
+
+#define GS_NO_SLOT 0x7FFFFFFF
+
 // Phase A — handleIncomingRPC / pushMsg for the payload of every RPC sent to
 // node v in the previous hop (pubsub.go:946-1022, score.go:693-964).  One
 // wave per receiving node; lane i = in-edge i, i.e. sender u_i = col[base+i],
-// so the lanes are in the canonical arrival order (senders ascending).
-// Topics are walked ascending and the words of a topic ascending; per word,
-//   A_i      = what sender i hands over (relay/publish frontier + IWANT response),
-//   P_i      = OR of A_j over non-graylisted senders j < i  (exclusive prefix-OR),
-//   fresh_i  = A_i & ~seen & ~P_i            (DeliverMessage from sender i),
-//   dup_i    = A_i & (seen | P_i) minus the copies the sender never sent
-//              (ReceivedFrom / author exclusion, gossipsub.go:1003),
-// which is exactly the sender-by-sender scan of the reference with each
-// sender's messages in ascending slot order.  The per-(edge, topic) score
-// counters of a topic are then updated for all senders at once, one
-// coalesced access per array (state is topic-major [t][E]).
-// Exclusion: a sender never returns a message to the neighbour it first got
-// it from.  The receiver checks its duplicate candidates against the sender's
-// first-deliverer table ffc[u][t][rank] (written by u one hop earlier, ranks
-// are u's fresh bits of topic t in slot order).
+// in the canonical arrival order (senders ascending).
+//
+// What a sender forwarded is its frontier list fl[u]: the slots it first
+// received in the previous hop, tagged with the in-edge they came from, and
+// its own publishes (tag 255), ascending by slot, filtered here by the
+// sender's per-edge forwarding topics.  A copy the sender never sent — back to
+// the neighbour it got the message from, or to the author (gossipsub.go:1003)
+// — is dropped by its tag.
+//   pass 1 (lane = sender): every delivered copy records the lowest
+//          non-graylisted sender per slot (LDS byte min) and its count per
+//          (topic, sender);
+//   pass 2 (lane = word):   fresh = delivered & ~seen; the first deliverer of a
+//          fresh slot is its lowest sender, exactly the reference's sender-by-
+//          sender scan (DeliverMessage from that sender, DuplicateMessage from
+//          every other copy); seen, mcache and v's own frontier list are written;
+//   pass 3 (lane = edge):   fmd / mmd of every (topic, in-edge) updated once.
+// LDS slot tables cover the words of the active window amR (messages young
+// enough to be in flight), indexed by the word's rank in amR.
 template <int WPL>
-__global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int head, WMask amR, WMask amW) {
-  __shared__ uint64_t sseen[64 * WPL];  // v's seen words (amR + lazily loaded)
-  __shared__ uint64_t sU[64 * WPL];     // v's fresh union per word (its next frontier)
-  __shared__ uint64_t spm[64 * WPL];    // slots published in the previous hop
-  __shared__ uint64_t sold[64 * WPL];   // slots too old for a first delivery
+__global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int head, WMask amR, WMask amW,
+                                                int nR) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
+  const int nCnt = (d.T * d.maxDeg + 3) & ~3;
+  uint32_t* scnt = smem32;                                // [T][MD] copies | fresh << 16
+  uint64_t* sD = (uint64_t*)(smem32 + nCnt);              // [nR] delivered slots (non-graylisted)
+  uint8_t* sFirst = (uint8_t*)(sD + nR);                  // [nR * 64] lowest deliverer
+  uint32_t* sUnc = (uint32_t*)(sFirst + nR * 64);         // [T][MD] uncredited duplicates (needAge)
   const int v = blockIdx.x;
   const int lane = lane_id();
   const int prv = cur ^ 1;
   const int W = d.W;
-  const int Wt = d.Wt;
   const int T = d.T;
-  const int Kt = d.Kt;
+  const int St = d.St;
+  const int MD = d.maxDeg;
+  const int FC = d.FC;
   const int64_t base = d.rowptr[v];
   const int deg = (int)(d.rowptr[v + 1] - base);
   const uint64_t sv = d.sub[v];
   const bool valid = lane < deg;
+  const bool scoring = d.scoring != 0;
   // in-edge metadata (lane = in-edge)
-  int u = 0, jr = 0;
+  int u = 0, jr = -1, Ln = 0;
   uint64_t relay = 0, pub = 0;
   bool gray = false;
   int irOff = 0, irN = 0;
@@ -275,259 +293,215 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
       irOff = (int)(ir >> 24);
       irN = (int)(ir & 0xFFFFFF);
     }
-    gray = d.router == 2 && d.scoring && !d.direct[e] && d.score0[e] < d.graylistThr;
+    gray = d.router == 2 && scoring && !d.direct[e] && d.score0[e] < d.graylistThr;
+    if (relay | pub) Ln = d.fln[prv][u];
   }
-  int irPos = 0;
-  int nextSlot = irN > 0 ? d.pool[prv][irOff] : 0x7FFFFFFF;
   const bool authV = d.nAuth[v] > 0;  // v authored a live message: author exclusion possible
-  WMask loaded = amR;
-#pragma unroll
-  for (int j = 0; j < WPL; ++j) {
-    const int w = lane + 64 * j;
-    if (w < W) {
-      sseen[w] = wm_has(amR, w) ? d.seen[(int64_t)v * W + w] : 0ull;
-      sU[w] = 0ull;
-      spm[w] = d.pubmask[prv][w];
-      sold[w] = d.oldm[w];
-    }
-  }
-  long long nDeliv = 0, nDup = 0, nSent = 0, nGray = 0;
-  const uint8_t* ffcU = d.ffc[prv] + (int64_t)u * T * Kt;
-  uint8_t* ffcV = d.ffc[cur] + (int64_t)v * T * Kt;
-  const bool scoring = d.scoring != 0;
-  const int64_t eIdx = base + lane;
-
-  // ---- software pipeline over chunks (topic t, words w0..w0+3): the loads of
-  // the next chunk (sender frontier words; at a topic start also the sender's
-  // first-deliverer window and the edge's score counters) are issued before
-  // the current chunk is processed, so their latency overlaps its work.
-  auto nextTopic = [&](int t0) {
-    const uint64_t rest = t0 < 64 ? (sv >> t0) : 0ull;
-    return rest ? t0 + __ffsll((long long)rest) - 1 : T;
-  };
-  uint64_t pnw[4];
-  uint64_t pLo = 0, pHi = 0;
-  double pF = 0.0, pM = 0.0;
-  uint8_t pFl = 0;
-  auto issue = [&](int tt, int ww0, bool start) {
-    const uint64_t tb = 1ull << tt;
-    const bool fw = ((relay | pub) & tb) != 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int w = ww0 + k;
-      pnw[k] = 0;
-      if (fw && w < (tt + 1) * Wt && wm_has(amR, w)) pnw[k] = d.newb[prv][(int64_t)u * W + w];
-    }
-    if (start) {
-      pLo = pHi = 0;
-      if (relay & tb) {
-        const uint64_t* p = (const uint64_t*)(ffcU + (int64_t)tt * Kt);
-        pLo = p[0];
-        pHi = p[1];
-      }
-      pF = pM = 0.0;
-      pFl = 0;
-      if (scoring && valid && (fw || nextSlot < (tt + 1) * d.St)) {
-        const int64_t ti = (int64_t)tt * d.E + eIdx;
-        pFl = d.flags[ti];
-        pF = d.fmd[ti];
-        pM = d.mmd[ti];
-      }
-    }
-  };
+  for (int k = lane; k < T * MD; k += 64) scnt[k] = 0;
+  if (d.needAge)
+    for (int k = lane; k < T * MD; k += 64) sUnc[k] = 0;
+  for (int k = lane; k < nR; k += 64) sD[k] = 0;
+  for (int k = lane; k < nR * 16; k += 64) ((uint32_t*)sFirst)[k] = 0xFFFFFFFFu;
   __syncthreads();
-  int t = nextTopic(0);
-  int w0 = t * Wt;
-  if (t < T) issue(t, w0, true);
-  int nf = 0, ndc = 0;  // this lane's fresh / creditable-duplicate counts in topic t
-  int rankT = 0;        // v's fresh count in topic t so far (wave-uniform)
-  int uRank = 0;        // sender's relayed-fresh count in topic t before the current word
-  int cBase = 0;        // cached 16-byte window of the sender's ffc row for topic t
-  uint64_t cLo = 0, cHi = 0;
-  double curF = 0.0, curM = 0.0;
-  uint8_t curFl = 0;
-  bool start = true;
-  while (t < T) {
-    uint64_t nwv[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) nwv[k] = pnw[k];
-    if (start) {
-      cLo = pLo;
-      cHi = pHi;
-      cBase = 0;
-      curF = pF;
-      curM = pM;
-      curFl = pFl;
-      nf = ndc = rankT = uRank = 0;
-    }
-    const int tEnd = (t + 1) * Wt;
-    int nt = t, nw0 = w0 + 4;
-    bool nStart = false;
-    if (nw0 >= tEnd) {
-      nt = nextTopic(t + 1);
-      nw0 = nt * Wt;
-      nStart = true;
-    }
-    if (nt < T) issue(nt, nw0, nStart);
-    const uint64_t tb = 1ull << t;
-    const bool fwdRelay = (relay & tb) != 0, fwdPub = (pub & tb) != 0;
-    if (__ballot(fwdRelay || fwdPub || nextSlot < tEnd * 64)) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int w = w0 + k;
-        if (w >= tEnd) break;
-        const uint64_t nw = nwv[k];
-        const uint64_t pm = spm[w];
-        uint64_t x = (fwdRelay ? (nw & ~pm) : 0ull) | (fwdPub ? (nw & pm) : 0ull);
-        if (d.router == 1 && x) {  // randomsub: per-message target sets of the sender
-          uint64_t y = x, keep = 0;
-          while (y) {
-            const int b = __ffsll((long long)y) - 1;
-            y &= y - 1;
-            if ((d.sel[(int64_t)u * d.S + (int64_t)w * 64 + b] >> jr) & 1) keep |= 1ull << b;
-          }
-          x = keep;
+
+  // ---- pass 1: walk the sender's list (4 entries per 16-byte load, one block
+  // ahead) and its IWANT response
+  long long nSent = 0, nGray = 0;
+  {
+    const uint32_t* L = d.fl[prv] + (int64_t)u * FC;
+    uint4 q = make_uint4(0, 0, 0, 0), qn = make_uint4(0, 0, 0, 0);
+    if (Ln > 0) q = *(const uint4*)L;
+    if (Ln > 4) qn = *(const uint4*)(L + 4);
+    int irPos = 0;
+    int nextIr = irN > 0 ? d.pool[prv][irOff] : GS_NO_SLOT;
+    int lp = 0;
+    int tCur = -1, cnt = 0;  // running copies count of (tCur, lane)
+    while (true) {
+      // next entry: the smaller of the list head and the IWANT-response head
+      int slot = GS_NO_SLOT;
+      bool fromList = false;
+      uint32_t ent = 0;
+      if (lp < Ln) {
+        const int o = lp & 3;
+        ent = o == 0 ? q.x : (o == 1 ? q.y : (o == 2 ? q.z : q.w));
+        slot = (int)(ent & 0xFFFF);
+        fromList = true;
+      }
+      if (nextIr < slot) {
+        slot = nextIr;
+        fromList = false;
+      }
+      if (slot == GS_NO_SLOT) break;
+      bool sent;
+      if (fromList) {
+        ++lp;
+        if ((lp & 3) == 0) {
+          q = qn;
+          if (lp + 4 < Ln) qn = *(const uint4*)(L + lp + 4);
         }
-        uint64_t xr = 0;  // IWANT response (slot ids ascending)
-        while (nextSlot < (w + 1) * 64) {
-          if (nextSlot >= w * 64) xr |= 1ull << (nextSlot & 63);
-          ++irPos;
-          nextSlot = irPos < irN ? d.pool[prv][irOff + irPos] : 0x7FFFFFFF;
+        const int t = slot / St;
+        const int tag = (int)(ent >> 16);
+        sent = tag == 255 ? ((pub >> t) & 1) : ((relay >> t) & 1);
+        sent = sent && tag != jr;  // ReceivedFrom exclusion
+        if (sent && d.router == 1) sent = (d.sel[(int64_t)u * d.S + slot] >> jr) & 1;
+        if (sent && authV && d.slotSrc[slot] == v) sent = false;  // never to the author
+        if (sent && gray) ++nGray;  // one RPC per relayed message, all dropped
+      } else {
+        ++irPos;
+        nextIr = irPos < irN ? d.pool[prv][irOff + irPos] : GS_NO_SLOT;
+        sent = true;
+      }
+      if (!sent) continue;
+      ++nSent;
+      if (gray) continue;
+      const int w = slot >> 6;
+      const int t = slot / St;
+      if (t != tCur) {
+        if (tCur >= 0 && cnt) scnt[tCur * MD + lane] += (uint32_t)cnt;
+        tCur = t;
+        cnt = 0;
+      }
+      ++cnt;
+      if (d.needAge || !wm_has(amR, w)) {
+        const bool had = (d.seen[(int64_t)v * W + w] >> (slot & 63)) & 1;
+        // markDuplicateMessageDelivery window (score.go:955): a copy of a message
+        // first delivered before this hop is credited only within the window
+        if (had && d.needAge) {
+          const int64_t firstHop = d.slotPubHop[slot] + d.age[(int64_t)v * d.S + slot];
+          if ((h - firstHop) * d.hop_ns > d.tp[t].MmdWindow) atomicAdd(&sUnc[t * MD + lane], 1u);
         }
-        const uint64_t A = x | xr;
-        const uint64_t relF = nw & ~pm;  // the sender's relayed-fresh bits of this word
-        if (!__ballot(A != 0)) {
-          uRank += __popcll(relF);
+        if (!wm_has(amR, w)) {
+          // outside the window only an old duplicate is possible; a first
+          // delivery there is later than the engine's window allows
+          if (!had) set_err(d, E_LATE);
           continue;
         }
-        if (!wm_has(loaded, w)) {  // IWANT response outside the active window
-          if (lane == 0) sseen[w] = d.seen[(int64_t)v * W + w];
-          loaded.m[w >> 6] |= 1ull << (w & 63);
-          __syncthreads();
-        }
-        const uint64_t S = sseen[w];
-        // ---- copies the sender never sent (it got them from us / we are the author)
-        uint64_t excl = 0;
-        uint64_t cand = x & ~pm & S;
-        while (cand) {
-          const int b = __ffsll((long long)cand) - 1;
-          cand &= cand - 1;
-          const int rank = uRank + __popcll(relF & ((1ull << b) - 1));
-          int ffb = -1;  // rank >= Kt: the sender raised E_FCAP when it stored this rank
-          if (rank < Kt) {
-            const int cb = rank & ~15;
-            if (cb != cBase) {
-              const uint64_t* p = (const uint64_t*)(ffcU + (int64_t)t * Kt + cb);
-              cLo = p[0];
-              cHi = p[1];
-              cBase = cb;
-            }
-            const int o = rank - cb;
-            ffb = (int)(((o < 8 ? cLo >> (8 * o) : cHi >> (8 * (o - 8)))) & 0xFF);
-          }
-          if (ffb == jr) excl |= 1ull << b;
-        }
-        if (authV) {
-          uint64_t c2 = x & S & ~excl;
-          while (c2) {
-            const int b = __ffsll((long long)c2) - 1;
-            c2 &= c2 - 1;
-            if (d.slotSrc[w * 64 + b] == v) excl |= 1ull << b;
-          }
-        }
-        uRank += __popcll(relF);
-        // ---- dedup in sender order
-        const uint64_t Ag = gray ? 0ull : A;
-        const uint64_t P = wave_prefix_or_excl(Ag);
-        const uint64_t fresh = Ag & ~S & ~P;
-        const uint64_t U = shfl_u64(P | Ag, 63) & ~S;
-        const uint64_t sentBits = A & ~excl;
-        nSent += __popcll(sentBits);
-        if (gray) nGray += __popcll(x & ~excl);  // one RPC per relayed message, all dropped
-        const uint64_t dupK = gray ? 0ull : (sentBits & ~fresh);
-        uint64_t cred = dupK;
-        if (d.needAge && dupK) {
-          // markDuplicateMessageDelivery window (score.go:955): first delivered at
-          // pubHop + age; copies of messages first delivered earlier in this hop
-          // (bits in P) are within any window
-          const int64_t window = d.tp[t].MmdWindow;
-          uint64_t y = dupK & S;
-          while (y) {
-            const int b = __ffsll((long long)y) - 1;
-            y &= y - 1;
-            const int64_t slot = (int64_t)w * 64 + b;
-            const int64_t firstHop = d.slotPubHop[slot] + d.age[(int64_t)v * d.S + slot];
-            if ((h - firstHop) * d.hop_ns > window) cred &= ~(1ull << b);
-          }
-        }
-        nf += __popcll(fresh);
-        ndc += __popcll(cred);
-        nDeliv += __popcll(fresh);
-        nDup += __popcll(dupK);
-        // ---- v's first deliverers (ffc), ranks in slot order within topic t
-        uint64_t f = fresh;
-        while (f) {
-          const int b = __ffsll((long long)f) - 1;
-          f &= f - 1;
-          const int rank = rankT + __popcll(U & ((1ull << b) - 1));
-          if (rank < Kt) ffcV[(int64_t)t * Kt + rank] = (uint8_t)lane;
-          else set_err(d, E_FCAP);
-          if (d.needAge || d.record) {
-            const int64_t slot = (int64_t)w * 64 + b;
-            const int64_t a = h - d.slotPubHop[slot];
-            if (d.needAge) d.age[(int64_t)v * d.S + slot] = (int16_t)a;
-            if (d.record) d.ffrom[(int64_t)v * d.S + slot] = (uint8_t)lane;
-          }
-        }
-        if (U) {
-          if (lane == 0) {
-            if ((U & sold[w]) || !wm_has(amW, w)) set_err(d, E_LATE);
-            sseen[w] = S | U;
-            sU[w] = U;
-          }
-          rankT += __popcll(U);
-          if (d.router == 1) {  // randomsub: targets of every message first delivered here
-            uint64_t y = U;
-            while (y) {
-              const int b = __ffsll((long long)y) - 1;
-              y &= y - 1;
-              const int ff = __ffsll((long long)__ballot((fresh >> b) & 1)) - 1;
-              rs_select(d, v, deg, valid ? u : -1, valid ? d.sub[u] : 0, w * 64 + b, ff);
-            }
-          }
-        }
+      }
+      const int ix = wm_rank(amR, w) * 64 + (slot & 63);
+      atomicOr((unsigned long long*)&sD[ix >> 6], 1ull << (slot & 63));
+      // byte-wise min of the lowest deliverer (lanes ascending = senders ascending)
+      uint32_t* wp = (uint32_t*)(sFirst + (ix & ~3));
+      const int sh = 8 * (ix & 3);
+      uint32_t old = *wp;
+      while ((int)((old >> sh) & 0xFF) > lane) {
+        const uint32_t nw = (old & ~(0xFFu << sh)) | ((uint32_t)lane << sh);
+        const uint32_t prev = atomicCAS(wp, old, nw);
+        if (prev == old) break;
+        old = prev;
       }
     }
-    if (nStart || nt >= T) {
-      // score counters of the in-edges for topic t: fmd += fresh, mmd += fresh +
-      // creditable duplicates while in the mesh (score.go:915-928, 945-963)
-      if (scoring && valid && (nf | ndc) && d.tp[t].scored) {
-        const TopicP& tp = d.tp[t];
-        const int64_t ti = (int64_t)t * d.E + eIdx;
-        if (nf) d.fmd[ti] = add_ones_capped(curF, nf, tp.FmdCap);
-        if (curFl & 1) d.mmd[ti] = add_ones_capped(curM, nf + ndc, tp.MmdCap);
-      }
-    }
-    t = nt;
-    w0 = nw0;
-    start = nStart;
+    if (tCur >= 0 && cnt) scnt[tCur * MD + lane] += (uint32_t)cnt;
   }
   __syncthreads();
-  // ---- write back: seen, frontier (active words of this hop), mcache Put
-#pragma unroll
-  for (int j = 0; j < WPL; ++j) {
-    const int w = lane + 64 * j;
-    if (w >= W) continue;
-    const uint64_t U = sU[w];
-    if (wm_has(loaded, w)) d.seen[(int64_t)v * W + w] = sseen[w];
-    if (wm_has(amW, w)) d.newb[cur][(int64_t)v * W + w] = U;
-    if (d.router == 2 && U) d.hist[((int64_t)head * d.N + v) * W + w] |= U;
+
+  // ---- pass 2 (lane = word of the active window): first deliveries
+  uint32_t* Lv = d.fl[cur] + (int64_t)v * FC;
+  long long nDeliv = 0;
+  int running = 0;  // rank of the next entry of v's own frontier list
+  for (int c0 = 0; c0 < W; c0 += 64) {
+    const int w = c0 + lane;
+    const bool act = w < W && wm_has(amR, w);
+    uint64_t U = 0, S = 0;
+    int ix0 = 0;
+    if (act) {
+      ix0 = wm_rank(amR, w) * 64;
+      const uint64_t D = sD[ix0 >> 6];
+      if (D) {
+        S = d.seen[(int64_t)v * W + w];
+        U = D & ~S;
+      }
+    }
+    const int k = __popcll(U);
+    int incl = k;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    int rank = running + incl - k;
+    running += __shfl(incl, 63);
+    if (U) {
+      if ((U & d.oldm[w]) || !wm_has(amW, w)) set_err(d, E_LATE);
+      d.seen[(int64_t)v * W + w] = S | U;
+      if (d.router == 2) d.hist[((int64_t)head * d.N + v) * W + w] |= U;
+      nDeliv += k;
+      const int t = w / d.Wt;
+      uint64_t y = U;
+      while (y) {
+        const int b = __ffsll((long long)y) - 1;
+        y &= y - 1;
+        const int slot = w * 64 + b;
+        const int ff = sFirst[ix0 + b];
+        if (rank < FC) Lv[rank] = (uint32_t)slot | ((uint32_t)ff << 16);
+        else set_err(d, E_FCAP);
+        ++rank;
+        if (scoring) atomicAdd(&scnt[t * MD + ff], 1u << 16);
+        if (d.needAge || d.record) {
+          const int64_t a = h - d.slotPubHop[slot];
+          if (d.needAge) d.age[(int64_t)v * d.S + slot] = (int16_t)a;
+          if (d.record) d.ffrom[(int64_t)v * d.S + slot] = (uint8_t)ff;
+        }
+      }
+    }
+    if (d.router == 1) {  // randomsub: targets of every message first delivered here
+      unsigned long long lanesWith = __ballot(U != 0);
+      while (lanesWith) {
+        const int src = __ffsll((long long)lanesWith) - 1;
+        lanesWith &= lanesWith - 1;
+        uint64_t y = shfl_u64(U, src);
+        const int wsrc = c0 + src;
+        const int ixs = __shfl(ix0, src);
+        while (y) {
+          const int b = __ffsll((long long)y) - 1;
+          y &= y - 1;
+          rs_select(d, v, deg, valid ? u : -1, valid ? d.sub[u] : 0, wsrc * 64 + b, sFirst[ixs + b]);
+        }
+      }
+    }
   }
-  const unsigned long long s0 = wave_sum_ll(nDeliv), s1 = wave_sum_ll(nDup), s2 = wave_sum_ll(nSent),
-                           s3 = wave_sum_ll(nGray);
+  __syncthreads();
+
+  // ---- pass 3 (lane = in-edge): fmd += fresh, mmd += fresh + creditable
+  // duplicates while in the mesh (score.go:915-928, 945-963)
+  long long nCopies = 0;
+  for (int t = 0; t < T; ++t) nCopies += valid ? (scnt[t * MD + lane] & 0xFFFF) : 0;
+  if (scoring && valid) {
+    for (int t0 = 0; t0 < T; t0 += 8) {
+      uint32_t c[8];
+      uint8_t fl[8];
+      double fm[8], mm[8];
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        const int t = t0 + kk;
+        c[kk] = (t < T && d.tp[t].scored) ? scnt[t * MD + lane] : 0u;
+        fl[kk] = 0;
+        fm[kk] = mm[kk] = 0.0;
+        if (c[kk]) {
+          const int64_t ti = (int64_t)t * d.E + base + lane;
+          fl[kk] = d.flags[ti];
+          fm[kk] = d.fmd[ti];
+          mm[kk] = d.mmd[ti];
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        if (!c[kk]) continue;
+        const int t = t0 + kk;
+        const TopicP& tp = d.tp[t];
+        const int copies = (int)(c[kk] & 0xFFFF), nf = (int)(c[kk] >> 16);
+        int credited = copies - nf;
+        const int64_t ti = (int64_t)t * d.E + base + lane;
+        if (d.needAge) credited -= (int)sUnc[t * MD + lane];
+        if (nf) d.fmd[ti] = add_ones_capped(fm[kk], nf, tp.FmdCap);
+        if (fl[kk] & 1) d.mmd[ti] = add_ones_capped(mm[kk], nf + credited, tp.MmdCap);
+      }
+    }
+  }
+  if (lane == 0) d.fln[cur][v] = running < FC ? running : FC;
+  const long long deliv = (long long)wave_sum_ll(nDeliv);
+  const unsigned long long copies = wave_sum_ll(nCopies), s2 = wave_sum_ll(nSent), s3 = wave_sum_ll(nGray);
   if (lane == 0) {
-    if (s0) ctr_add(d, C_DELIVERIES, s0);
-    if (s1) ctr_add(d, C_DUPLICATES, s1);
+    if (deliv) ctr_add(d, C_DELIVERIES, (unsigned long long)deliv);
+    if (copies - deliv) ctr_add(d, C_DUPLICATES, copies - deliv);
     if (s2) ctr_add(d, C_TRANSMISSIONS, s2);
     if (s3) ctr_add(d, C_GRAYLISTED, s3);
   }
@@ -570,11 +544,40 @@ __global__ void k_publish(Dev d, int b, int n, int64_t h, int cur, int head) {
   const int w = slot >> 6;
   const unsigned long long bit = 1ull << (slot & 63);
   atomicOr((unsigned long long*)&d.seen[(int64_t)src * d.W + w], bit);
-  atomicOr((unsigned long long*)&d.newb[cur][(int64_t)src * d.W + w], bit);
   if (d.router == 2) atomicOr((unsigned long long*)&d.hist[((int64_t)head * d.N + src) * d.W + w], bit);
   if (d.needAge) d.age[(int64_t)src * d.S + slot] = 0;
   if (d.record) d.ffrom[(int64_t)src * d.S + slot] = 255;
   ctr_add(d, C_PUBLISHED, 1ull);
+}
+
+// Adds this hop's local publishes to the publisher's frontier list (tag 255 =
+// own publish, forwarded on the edges of fwdPub), keeping the list sorted by
+// slot.  One thread per message; the thread of a node's first message of the
+// hop inserts all of that node's messages.
+__global__ void k_publist(Dev d, int b, int n, int cur) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int src = d.mSrc[b + i];
+  for (int j = 0; j < i; ++j)
+    if (d.mSrc[b + j] == src) return;
+  uint32_t* L = d.fl[cur] + (int64_t)src * d.FC;
+  int len = d.fln[cur][src];
+  for (int j = i; j < n; ++j) {
+    if (d.mSrc[b + j] != src) continue;
+    const uint32_t slot = (uint32_t)d.mSlot[b + j];
+    if (len >= d.FC) {
+      set_err(d, E_FCAP);
+      break;
+    }
+    int pos = len;
+    while (pos > 0 && (L[pos - 1] & 0xFFFFu) > slot) {
+      L[pos] = L[pos - 1];
+      --pos;
+    }
+    L[pos] = slot | (255u << 16);
+    ++len;
+  }
+  d.fln[cur][src] = len;
 }
 
 // Randomsub targets of the messages published this hop (one wave per message).

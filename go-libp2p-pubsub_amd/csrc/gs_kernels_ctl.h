@@ -175,7 +175,8 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
           uint64_t req = 0, cache = 0;
           if (w < W) {
             req = reqb[w];
-            for (int k = 0; k < d.HL; ++k) cache |= d.hist[((int64_t)((head + k) % d.R) * d.N + v) * W + w];
+            if (req)
+              for (int k = 0; k < d.HL; ++k) cache |= d.hist[((int64_t)((head + k) % d.R) * d.N + v) * W + w];
           }
           uint64_t cand = req & cache;
           served[j] = 0;
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
             const int tw = w / d.Wt;
             if (!((ihaveT >> tw) & 1)) continue;
             uint64_t mids = 0;
-            for (int k = 1; k <= d.HG; ++k) mids |= d.hist[((int64_t)((head + k) % d.R) * d.N + u) * W + w];
+            mids = d.gw[(int64_t)u * W + w];
             nMids += __popcll(mids);
             if (!((sv >> tw) & 1)) continue;  // topic not in our mesh map
             want[j] = mids & ~d.seen[(int64_t)v * W + w];
@@ -433,14 +434,11 @@ __global__ __launch_bounds__(64) void k_hb_pre(Dev d, int64_t now, uint64_t tick
 // changed earlier in this heartbeat.
 __device__ __forceinline__ uint64_t emit_gossip(const Dev& d, int v, int t, int64_t hop, int head, bool valid,
                                                 int vcol, bool inTopic, bool excl, bool dir, double& Slive,
-                                                bool& dirty, int64_t rowBase, double* lds) {
+                                                bool& dirty, int64_t rowBase, double* lds,
+                                                const uint64_t* sgw) {
   const int lane = lane_id();
   int nm = 0;
-  for (int w = t * d.Wt + lane; w < (t + 1) * d.Wt; w += 64) {
-    uint64_t x = 0;
-    for (int k = 0; k < d.HG; ++k) x |= d.hist[((int64_t)((head + k) % d.R) * d.N + v) * d.W + w];
-    nm += __popcll(x);
-  }
+  for (int w = t * d.Wt + lane; w < (t + 1) * d.Wt; w += 64) nm += __popcll(sgw[w]);
   nm = wave_sum_int(nm);
   if (nm == 0) return 0;
   if (nm > d.MaxIHaveLength && lane == 0) set_err(d, E_TRUNCATE);
@@ -480,6 +478,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
   __shared__ int obs[64];
   __shared__ int posOf[64];
   __shared__ double sterm[64];
+  __shared__ uint64_t sgw[64 * GS_MAX_WPL];
   const int v = blockIdx.x;
   const int lane = lane_id();
   const int64_t base = d.rowptr[v];
@@ -487,6 +486,15 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
   const bool valid = lane < deg;
   const int64_t e = base + lane;
   const int vcol = valid ? d.col[e] : -1;
+  // mcache.GetGossipIDs windows 0..HG-1 (mcache.go:82-92): this heartbeat's
+  // IHAVE payload, kept as the node's gw row for the receivers' handleIHave
+  for (int w = lane; w < d.W; w += 64) {
+    uint64_t x = 0;
+    for (int k = 0; k < d.HG; ++k) x |= d.hist[((int64_t)((head + k) % d.R) * d.N + v) * d.W + w];
+    sgw[w] = x;
+    d.gw[(int64_t)v * d.W + w] = x;
+  }
+  __syncthreads();
   const uint64_t subv = valid ? d.sub[vcol] : 0;
   uint64_t meshl = valid ? d.mesh[e] : 0;
   uint64_t fanl = valid ? d.fanout[e] : 0;
@@ -635,7 +643,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
         }
       }
     }
-    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, m, dir, Slive, dirty, base, sterm);
+    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, m, dir, Slive, dirty, base, sterm, sgw);
   }
   // expire fanout for topics we haven't published to in a while
   uint64_t fpres = d.fanoutPresent[v];
@@ -666,7 +674,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
         f = true;
       }
     }
-    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, f, dir, Slive, dirty, base, sterm);
+    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, f, dir, Slive, dirty, base, sterm, sgw);
   }
   // sendGraftPrune + flush: one heartbeat RPC per peer with any control
   if (valid) {
