@@ -75,6 +75,7 @@ struct Dev {
                    // (| in-edge index << 16) and own publishes (| 255 << 16), ascending
   int32_t* fln[2]; // [N] list lengths
   int32_t FC;      // list capacity per node (multiple of 4)
+  uint32_t stMagic; // ceil(2^32 / St): topic of slot s = umulhi(s, stMagic) (s < 2^16)
   int32_t maxDeg;  // largest node degree (<= 64)
   uint64_t* oldm;  // [W] slots whose message is too old to be first-delivered this hop
   int32_t* nAuth;  // [N] live message slots authored by the node
@@ -96,6 +97,7 @@ struct Dev {
   uint64_t* fwdPub[2];
   double* score0;  // hop-start score memo (S0)
   double* score1;  // after the message phase (S1) / heartbeat memo
+  uint8_t* sdirty; // [E] a score-lowering change (graft/prune/penalty/refresh) since score0
   int64_t* backoff;  // [T][E], 0 = none
   double *fmd, *mmd, *mfp, *imd;  // [T][E]
   int64_t *graftTime, *meshTime;  // [T][E]
@@ -253,6 +255,7 @@ __device__ __forceinline__ double edge_score_wave(const Dev& d, int64_t e, doubl
 __device__ __forceinline__ void stats_graft(const Dev& d, int64_t e, int t, int64_t now) {
   if (!d.scoring || !d.tp[t].scored) return;
   const int64_t i = (int64_t)t * d.E + e;
+  d.sdirty[e] = 1;
   d.flags[i] = 1;  // inMesh, P3 inactive
   d.graftTime[i] = now;
   d.meshTime[i] = 0;
@@ -262,6 +265,7 @@ __device__ __forceinline__ void stats_graft(const Dev& d, int64_t e, int t, int6
 __device__ __forceinline__ void stats_prune(const Dev& d, int64_t e, int t) {
   if (!d.scoring || !d.tp[t].scored) return;
   const int64_t i = (int64_t)t * d.E + e;
+  d.sdirty[e] = 1;
   const uint8_t fl = d.flags[i];
   const double thr = d.tp[t].MmdThreshold;
   if ((fl & 2) && d.mmd[i] < thr) {

@@ -309,6 +309,7 @@ int gs_engine::start() {
     x.fln[k] = dalloc<int32_t>(N); chk(x.fln[k]);
   }
   x.maxDeg = std::max(1, maxdeg);
+  x.stMagic = (uint32_t)(((1ull << 32) + (uint64_t)St - 1) / (uint64_t)St);
   x.oldm = dalloc<uint64_t>(W); chk(x.oldm);
   x.nAuth = dalloc<int32_t>(N); chk(x.nAuth);
   x.sel = cfg.router == GS_ROUTER_RANDOMSUB ? dalloc<uint64_t>(NS) : nullptr;
@@ -336,6 +337,7 @@ int gs_engine::start() {
     x.pubmask[k] = dalloc<uint64_t>(W); chk(x.pubmask[k]);
   }
   x.score0 = dalloc<double>(E); x.score1 = dalloc<double>(E);
+  x.sdirty = dalloc<uint8_t>(E, 1); chk(x.sdirty);
   x.backoff = dalloc<int64_t>(TE);
   x.fmd = dalloc<double>(TE); x.mmd = dalloc<double>(TE); x.mfp = dalloc<double>(TE); x.imd = dalloc<double>(TE);
   x.graftTime = dalloc<int64_t>(TE); x.meshTime = dalloc<int64_t>(TE); x.flags = dalloc<uint8_t>(TE);
@@ -436,7 +438,7 @@ int gs_engine::stepOne() {
   HIPCHECK(hipMemsetAsync(d.pubmask[cur], 0, (size_t)W * 8, stream));
   HIPCHECK(hipMemsetAsync(d.poolCnt + cur, 0, 8, stream));
   const unsigned eb = nblk(E, 256);
-  if (scoring) TIMED(this, GS_K_SCORE, (k_score<<<eb, 256, 0, stream>>>(d, d.score0)));
+  if (scoring) TIMED(this, GS_K_SCORE, (k_score0<<<eb, 256, 0, stream>>>(d)));
   if (h == 0 && gossip) TIMED(this, GS_K_JOIN, (k_join<<<N, 64, 0, stream>>>(d, h, now, cur)));
   if (gossip && !floodPublish && n > 0) {
     // Publish to a topic we have not joined: fanout (gossipsub.go:977-994)
@@ -496,7 +498,7 @@ int gs_engine::stepOne() {
     if (cfg.router == GS_ROUTER_RANDOMSUB) k_publish_rs<<<n, 64, 0, stream>>>(d, (int)b);
   }
   if (gossip) {
-    if (scoring) TIMED(this, GS_K_SCORE, (k_score<<<eb, 256, 0, stream>>>(d, d.score1)));
+    if (scoring) TIMED(this, GS_K_SCORE, (k_score1<<<eb, 256, 0, stream>>>(d)));
     TIMED(this, GS_K_PHASE_B,
           launch_wpl(W, [&](auto wpl) { k_phase_b<decltype(wpl)::value><<<N, 64, 0, stream>>>(d, h, now, cur, head); }));
   }
@@ -763,6 +765,7 @@ int gs_set_topic_score_params(gs_engine* g, int32_t topic, const gs_topic_score_
   if (!g->started) return GS_OK;
   TopicP tp = to_dev(*p, g->scoring);
   HIPCHECK(hipMemcpyAsync(g->dTp + topic, &tp, sizeof(TopicP), hipMemcpyHostToDevice, g->stream));
+  HIPCHECK(hipMemsetAsync(g->d.sdirty, 1, (size_t)g->E, g->stream));  // every score may have changed
   if (existed && g->scoring &&
       (p->FirstMessageDeliveriesCap < old.FirstMessageDeliveriesCap ||
        p->MeshMessageDeliveriesCap < old.MeshMessageDeliveriesCap))

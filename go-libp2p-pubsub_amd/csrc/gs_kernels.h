@@ -26,6 +26,35 @@ __global__ void k_score(Dev d, double* __restrict__ out) {
   out[e] = edge_score(d, e);
 }
 
+// Hop-start memo S0.  Every consumer of S0 only asks "score >= threshold" for
+// thresholds <= PublishThreshold (AcceptFrom graylist, publish / fanout
+// filters; thresholds are <= 0 by validation, score_params.go:34-51), and
+// between two recomputations the score can only rise unless a graft, prune,
+// penalty or refresh touched the edge (message deliveries raise P2 and lower
+// the P3 deficit; FirstMessageDeliveriesWeight >= 0 and MeshMessageDeliveries-
+// Weight <= 0 by validation).  So a memo that is >= PublishThreshold and not
+// dirty gives the same decisions as the exact score; everything else is
+// recomputed exactly.
+__global__ void k_score0(Dev d) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.E) return;
+  const double s = d.score0[e];
+  if (d.sdirty[e] || !(s >= d.publishThr)) {
+    d.score0[e] = edge_score(d, e);
+    d.sdirty[e] = 0;
+  }
+}
+
+// Memo S1 for HandleRPC (after the message phase): its decisions compare with
+// 0 and GossipThreshold (<= 0), and only deliveries happened since S0, so a
+// non-negative S0 decides exactly like the exact score.
+__global__ void k_score1(Dev d) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.E) return;
+  const double s = d.score0[e];
+  d.score1[e] = s >= 0.0 ? s : edge_score(d, e);
+}
+
 // refreshScores — score.go:495-556 (every peer is connected: no retention path)
 __global__ void k_refresh(Dev d, int64_t now) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -56,6 +85,7 @@ __global__ void k_refresh(Dev d, int64_t now) {
   double b = d.bp[e] * d.BPDecay;
   if (b < d.DecayToZero) b = 0;
   d.bp[e] = b;
+  d.sdirty[e] = 1;
 }
 
 // SetTopicScoreParams recap — score.go:215-229
@@ -244,8 +274,9 @@ __device__ __forceinline__ int wave_min_int(int x) {
 // sender's per-edge forwarding topics.  A copy the sender never sent — back to
 // the neighbour it got the message from, or to the author (gossipsub.go:1003)
 // — is dropped by its tag.
-//   pass 1 (lane = sender): every delivered copy records the lowest
-//          non-graylisted sender per slot (LDS byte min) and its count per
+//   pass 1 (every 16-byte block of every sender's list is a work item, spread
+//          over the lanes): each delivered copy records the lowest non-
+//          graylisted sender per slot (LDS byte min) and its count per
 //          (topic, sender);
 //   pass 2 (lane = word):   fresh = delivered & ~seen; the first deliverer of a
 //          fresh slot is its lowest sender, exactly the reference's sender-by-
@@ -263,6 +294,10 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   uint64_t* sD = (uint64_t*)(smem32 + nCnt);              // [nR] delivered slots (non-graylisted)
   uint8_t* sFirst = (uint8_t*)(sD + nR);                  // [nR * 64] lowest deliverer
   uint32_t* sUnc = (uint32_t*)(sFirst + nR * 64);         // [T][MD] uncredited duplicates (needAge)
+  __shared__ int sBlk[64];        // first list block of each sender
+  __shared__ uint64_t sRelay[64], sPub[64];
+  __shared__ int sSnd[64];        // sender node | jr << 24 | graylisted << 31
+  __shared__ int sLn[64];
   const int v = blockIdx.x;
   const int lane = lane_id();
   const int prv = cur ^ 1;
@@ -302,95 +337,112 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     for (int k = lane; k < T * MD; k += 64) sUnc[k] = 0;
   for (int k = lane; k < nR; k += 64) sD[k] = 0;
   for (int k = lane; k < nR * 16; k += 64) ((uint32_t*)sFirst)[k] = 0xFFFFFFFFu;
+  // per-sender view for the block-parallel walk
+  const int nb = (Ln + 3) >> 2;  // 16-byte blocks of the sender's list
+  int bincl = nb;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(bincl, o);
+    if (lane >= o) bincl += y;
+  }
+  const int totalBlk = __shfl(bincl, 63);
+  sBlk[lane] = bincl - nb;
+  sRelay[lane] = relay;
+  sPub[lane] = pub;
+  sSnd[lane] = valid ? (u | (jr << 24) | (gray ? (1 << 31) : 0)) : 0;
+  sLn[lane] = Ln;
   __syncthreads();
 
-  // ---- pass 1: walk the sender's list (4 entries per 16-byte load, one block
-  // ahead) and its IWANT response
   long long nSent = 0, nGray = 0;
-  {
-    const uint32_t* L = d.fl[prv] + (int64_t)u * FC;
-    uint4 q = make_uint4(0, 0, 0, 0), qn = make_uint4(0, 0, 0, 0);
-    if (Ln > 0) q = *(const uint4*)L;
-    if (Ln > 4) qn = *(const uint4*)(L + 4);
-    int irPos = 0;
-    int nextIr = irN > 0 ? d.pool[prv][irOff] : GS_NO_SLOT;
-    int lp = 0;
-    int tCur = -1, cnt = 0;  // running copies count of (tCur, lane)
-    while (true) {
-      // next entry: the smaller of the list head and the IWANT-response head
-      int slot = GS_NO_SLOT;
-      bool fromList = false;
-      uint32_t ent = 0;
-      if (lp < Ln) {
-        const int o = lp & 3;
-        ent = o == 0 ? q.x : (o == 1 ? q.y : (o == 2 ? q.z : q.w));
-        slot = (int)(ent & 0xFFFF);
-        fromList = true;
+  // One delivered copy of `slot` from sender i (already known to be sent).
+  auto deliver = [&](int i, int slot, bool isGray) {
+    if (isGray) return;
+    const int w = slot >> 6;
+    const int t = (int)__umulhi((unsigned)slot, d.stMagic);
+    atomicAdd(&scnt[t * MD + i], 1u);
+    if (d.needAge || !wm_has(amR, w)) {
+      const bool had = (d.seen[(int64_t)v * W + w] >> (slot & 63)) & 1;
+      // markDuplicateMessageDelivery window (score.go:955): a copy of a message
+      // first delivered before this hop is credited only within the window
+      if (had && d.needAge) {
+        const int64_t firstHop = d.slotPubHop[slot] + d.age[(int64_t)v * d.S + slot];
+        if ((h - firstHop) * d.hop_ns > d.tp[t].MmdWindow) atomicAdd(&sUnc[t * MD + i], 1u);
       }
-      if (nextIr < slot) {
-        slot = nextIr;
-        fromList = false;
-      }
-      if (slot == GS_NO_SLOT) break;
-      bool sent;
-      if (fromList) {
-        ++lp;
-        if ((lp & 3) == 0) {
-          q = qn;
-          if (lp + 4 < Ln) qn = *(const uint4*)(L + lp + 4);
-        }
-        const int t = slot / St;
-        const int tag = (int)(ent >> 16);
-        sent = tag == 255 ? ((pub >> t) & 1) : ((relay >> t) & 1);
-        sent = sent && tag != jr;  // ReceivedFrom exclusion
-        if (sent && d.router == 1) sent = (d.sel[(int64_t)u * d.S + slot] >> jr) & 1;
-        if (sent && authV && d.slotSrc[slot] == v) sent = false;  // never to the author
-        if (sent && gray) ++nGray;  // one RPC per relayed message, all dropped
-      } else {
-        ++irPos;
-        nextIr = irPos < irN ? d.pool[prv][irOff + irPos] : GS_NO_SLOT;
-        sent = true;
-      }
-      if (!sent) continue;
-      ++nSent;
-      if (gray) continue;
-      const int w = slot >> 6;
-      const int t = slot / St;
-      if (t != tCur) {
-        if (tCur >= 0 && cnt) scnt[tCur * MD + lane] += (uint32_t)cnt;
-        tCur = t;
-        cnt = 0;
-      }
-      ++cnt;
-      if (d.needAge || !wm_has(amR, w)) {
-        const bool had = (d.seen[(int64_t)v * W + w] >> (slot & 63)) & 1;
-        // markDuplicateMessageDelivery window (score.go:955): a copy of a message
-        // first delivered before this hop is credited only within the window
-        if (had && d.needAge) {
-          const int64_t firstHop = d.slotPubHop[slot] + d.age[(int64_t)v * d.S + slot];
-          if ((h - firstHop) * d.hop_ns > d.tp[t].MmdWindow) atomicAdd(&sUnc[t * MD + lane], 1u);
-        }
-        if (!wm_has(amR, w)) {
-          // outside the window only an old duplicate is possible; a first
-          // delivery there is later than the engine's window allows
-          if (!had) set_err(d, E_LATE);
-          continue;
-        }
-      }
-      const int ix = wm_rank(amR, w) * 64 + (slot & 63);
-      atomicOr((unsigned long long*)&sD[ix >> 6], 1ull << (slot & 63));
-      // byte-wise min of the lowest deliverer (lanes ascending = senders ascending)
-      uint32_t* wp = (uint32_t*)(sFirst + (ix & ~3));
-      const int sh = 8 * (ix & 3);
-      uint32_t old = *wp;
-      while ((int)((old >> sh) & 0xFF) > lane) {
-        const uint32_t nw = (old & ~(0xFFu << sh)) | ((uint32_t)lane << sh);
-        const uint32_t prev = atomicCAS(wp, old, nw);
-        if (prev == old) break;
-        old = prev;
+      if (!wm_has(amR, w)) {
+        // outside the window only an old duplicate is possible; a first
+        // delivery there is later than the engine's window allows
+        if (!had) set_err(d, E_LATE);
+        return;
       }
     }
-    if (tCur >= 0 && cnt) scnt[tCur * MD + lane] += (uint32_t)cnt;
+    const int ix = wm_rank(amR, w) * 64 + (slot & 63);
+    atomicOr((unsigned long long*)&sD[ix >> 6], 1ull << (slot & 63));
+    // byte-wise min of the lowest deliverer (senders ascending)
+    uint32_t* wp = (uint32_t*)(sFirst + (ix & ~3));
+    const int sh = 8 * (ix & 3);
+    uint32_t old = *wp;
+    while ((int)((old >> sh) & 0xFF) > i) {
+      const uint32_t nw = (old & ~(0xFFu << sh)) | ((uint32_t)i << sh);
+      const uint32_t prev = atomicCAS(wp, old, nw);
+      if (prev == old) break;
+      old = prev;
+    }
+  };
+  // ---- pass 1a: every 16-byte block of every sender's list is one work item;
+  // lane l takes items l, l+64, ...  (four loads in flight per lane)
+  for (int b0 = 0; b0 < totalBlk; b0 += 256) {
+    int si[4], kb[4];
+    uint4 q[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int bidx = b0 + r * 64 + lane;
+      si[r] = -1;
+      kb[r] = 0;
+      q[r] = make_uint4(0, 0, 0, 0);
+      if (bidx < totalBlk) {
+        int lo = 0, hi = 63;  // last sender whose first block is <= bidx
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (sBlk[mid] <= bidx) lo = mid; else hi = mid - 1;
+        }
+        si[r] = lo;
+        kb[r] = bidx - sBlk[lo];
+        const int uu = sSnd[lo] & 0xFFFFFF;
+        q[r] = *(const uint4*)(d.fl[prv] + (int64_t)uu * FC + 4 * kb[r]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (si[r] < 0) continue;
+      const int i = si[r];
+      const int snd = sSnd[i];
+      const int uu = snd & 0xFFFFFF;
+      const int jri = (snd >> 24) & 0x7F;
+      const bool isGray = snd < 0;
+      const uint64_t rl = sRelay[i], pb = sPub[i];
+      const int n = min(4, sLn[i] - 4 * kb[r]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (c >= n) break;
+        const uint32_t ent = c == 0 ? q[r].x : (c == 1 ? q[r].y : (c == 2 ? q[r].z : q[r].w));
+        const int slot = (int)(ent & 0xFFFF);
+        const int tag = (int)(ent >> 16);
+        const int t = (int)__umulhi((unsigned)slot, d.stMagic);
+        bool sent = tag == 255 ? ((pb >> t) & 1) : ((rl >> t) & 1);
+        sent = sent && tag != jri;  // ReceivedFrom exclusion (gossipsub.go:1003)
+        if (sent && d.router == 1) sent = (d.sel[(int64_t)uu * d.S + slot] >> jri) & 1;
+        if (sent && authV && d.slotSrc[slot] == v) sent = false;  // never to the author
+        if (!sent) continue;
+        ++nSent;
+        if (isGray) ++nGray;  // one RPC per relayed message, all dropped
+        deliver(i, slot, isGray);
+      }
+    }
+  }
+  // ---- pass 1b: IWANT responses (one list per sender, rare)
+  for (int k = 0; k < irN; ++k) {
+    const int slot = d.pool[prv][irOff + k];
+    ++nSent;
+    deliver(lane, slot, gray);
   }
   __syncthreads();
 

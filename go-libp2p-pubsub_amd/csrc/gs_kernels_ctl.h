@@ -20,6 +20,7 @@ __device__ __forceinline__ bool graft_one(const Dev& d, int64_t e, int v, int t,
       d.bp[e] += 1.0;
       const int64_t floodCutoff = be + (d.GraftFloodThreshold - d.PruneBackoff);
       if (now < floodCutoff) d.bp[e] += 1.0;
+      d.sdirty[e] = 1;
       dirty = true;
     }
     add_backoff(d, e, t, now, d.PruneBackoff);
@@ -410,7 +411,10 @@ __global__ __launch_bounds__(64) void k_hb_pre(Dev d, int64_t now, uint64_t tick
     const int pe = __shfl(edge, q);
     const unsigned long long same = __ballot(broken && edge == pe);
     bm &= ~same;
-    if (lane == 0) d.bp[base + pe] += (double)__popcll(same);
+    if (lane == 0) {
+      d.bp[base + pe] += (double)__popcll(same);
+      d.sdirty[base + pe] = 1;
+    }
   }
   // compact the surviving entries
   const unsigned long long lm = __ballot(live);
