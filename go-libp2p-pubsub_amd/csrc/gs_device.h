@@ -3,8 +3,11 @@
 // Layout: message slots are topic-segmented, slot s belongs to
 // topic s / St; a node bitset is W = T*Wt 64-bit words.  Per-node arrays are
 // row-major [node][word]; per-edge arrays are indexed by the CSR edge id e
-// (observer u = edge_src[e], neighbour col[e]); per-(edge,topic) score state
-// is topic-major [t*E + e] so a thread-per-edge pass is coalesced.
+// (observer u = edge_src[e], neighbour col[e]); per-(edge,topic) state
+// (score counters, backoff) is tiled [e/64][t][e%64] (tix): a wave of 64
+// consecutive edges reads one contiguous 512-byte row per topic, and all the
+// topics of a node's edges lie within a few KiB, so per-node passes stay
+// inside a handful of pages instead of touching T pages E*8 bytes apart.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -24,7 +27,7 @@ enum {
 // device error codes (first one wins)
 enum {
   E_NONE = 0, E_POOL = 1, E_PROMISES = 2, E_PEERTX = 3, E_LATE = 4, E_TRUNCATE = 5, E_DOUBLE = 6,
-  E_FCAP = 7
+  E_FCAP = 7, E_DELTA = 8
 };
 
 struct TopicP {  // TopicScoreParams (score_params.go:98-148) + scored flag
@@ -99,7 +102,9 @@ struct Dev {
   double* score1;  // after the message phase (S1) / heartbeat memo
   uint8_t* sdirty; // [E] a score-lowering change (graft/prune/penalty/refresh) since score0
   int64_t* backoff;  // [T][E], 0 = none
-  double *fmd, *mmd, *mfp, *imd;  // [T][E]
+  double *fmd, *mmd, *mfp, *imd;  // tiled (tix)
+  uint32_t* dlt;                  // tiled: deliveries not yet folded into fmd / mmd,
+                                  // (+1s to fmd) | (+1s to mmd) << 16 (see eff_counters)
   int64_t *graftTime, *meshTime;  // [T][E]
   uint8_t* flags;                 // [T][E] bit0 inMesh, bit1 P3 active
   double* bp;                     // [E] behaviourPenalty
@@ -128,11 +133,18 @@ struct Dev {
   const int32_t* mSlot;
   const int64_t* mId;
   // counters / error
+  unsigned long long* stamps;  // debug builds only (GS_STAMPS)
+  double* pad;                 // [256][64][2] scratch targets of branch-free predicated accesses
   unsigned long long* ctr;
   int32_t* err;
 };
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// index of (edge e, topic t) in the tiled per-(edge, topic) arrays
+__device__ __forceinline__ int64_t tix(const Dev& d, int t, int64_t e) {
+  return ((((e >> 6) * d.T) + t) << 6) | (e & 63);
+}
 
 __device__ __forceinline__ void set_err(const Dev& d, int code) { atomicCAS(d.err, 0, code); }
 // Event counters are spread over GS_CTR_SPREAD copies (by workgroup) so a
@@ -182,12 +194,26 @@ __device__ __forceinline__ double add_ones_capped(double x, int n, double cap) {
 // state index i = t*E + e.  kEager: every load is issued up front (latency-
 // bound callers); otherwise meshTime / mmd are read only when P1 / P3 apply
 // (the bandwidth-bound streaming pass).
+// Phase A records a hop's deliveries per (edge, topic) as counts in dlt and
+// leaves fmd / mmd untouched; the counts are folded in (the same "+1, cap"
+// steps, score.go:915-928, 960-963) by every reader that needs the exact
+// counter and for good at refreshScores, before the decay.  Applying n then m
+// steps equals applying n + m steps, so the result is independent of when
+// the fold happens as long as it precedes the decay.
+__device__ __forceinline__ double eff_fmd(const TopicP& tp, double fmd, uint32_t q) {
+  return (q & 0xFFFF) ? add_ones_capped(fmd, (int)(q & 0xFFFF), tp.FmdCap) : fmd;
+}
+__device__ __forceinline__ double eff_mmd(const TopicP& tp, double mmd, uint32_t q) {
+  return (q >> 16) ? add_ones_capped(mmd, (int)(q >> 16), tp.MmdCap) : mmd;
+}
+
 template <bool kEager>
 __device__ __forceinline__ double topic_term(const Dev& d, const TopicP& tp, int64_t i) {
   const uint8_t fl = d.flags[i];
+  const uint32_t q = d.dlt[i];
   const int64_t mt = (kEager || (fl & 1)) ? d.meshTime[i] : 0;
-  const double mm = (kEager || (fl & 2)) ? d.mmd[i] : 0.0;
-  const double fmd = d.fmd[i], mfp = d.mfp[i], im = d.imd[i];
+  const double mm = eff_mmd(tp, (kEager || (fl & 2)) ? d.mmd[i] : 0.0, q);
+  const double fmd = eff_fmd(tp, d.fmd[i], q), mfp = d.mfp[i], im = d.imd[i];
   double topicScore = 0.0;
   if (fl & 1) {
     double p1 = (double)(mt / tp.TimeInMeshQuantum);
@@ -229,7 +255,7 @@ __device__ __forceinline__ double edge_score(const Dev& d, int64_t e) {
   for (int t = 0; t < d.T; ++t) {
     const TopicP& tp = d.tp[t];
     if (!tp.scored) continue;
-    score += topic_term<false>(d, tp, (int64_t)t * d.E + e);
+    score += topic_term<false>(d, tp, tix(d, t, e));
   }
   return score_tail(d, e, score);
 }
@@ -241,7 +267,7 @@ __device__ __forceinline__ double edge_score_wave(const Dev& d, int64_t e, doubl
   if (!d.scoring) return 0.0;
   const int lane = lane_id();
   double term = 0.0;
-  if (lane < d.T && d.tp[lane].scored) term = topic_term<true>(d, d.tp[lane], (int64_t)lane * d.E + e);
+  if (lane < d.T && d.tp[lane].scored) term = topic_term<true>(d, d.tp[lane], tix(d, lane, e));
   __syncthreads();
   lds[lane] = term;
   __syncthreads();
@@ -254,7 +280,7 @@ __device__ __forceinline__ double edge_score_wave(const Dev& d, int64_t e, doubl
 // peerScore.Graft — score.go:640-658 (scored topics only)
 __device__ __forceinline__ void stats_graft(const Dev& d, int64_t e, int t, int64_t now) {
   if (!d.scoring || !d.tp[t].scored) return;
-  const int64_t i = (int64_t)t * d.E + e;
+  const int64_t i = tix(d, t, e);
   d.sdirty[e] = 1;
   d.flags[i] = 1;  // inMesh, P3 inactive
   d.graftTime[i] = now;
@@ -264,12 +290,20 @@ __device__ __forceinline__ void stats_graft(const Dev& d, int64_t e, int t, int6
 // peerScore.Prune — score.go:660-682
 __device__ __forceinline__ void stats_prune(const Dev& d, int64_t e, int t) {
   if (!d.scoring || !d.tp[t].scored) return;
-  const int64_t i = (int64_t)t * d.E + e;
+  const int64_t i = tix(d, t, e);
   d.sdirty[e] = 1;
   const uint8_t fl = d.flags[i];
-  const double thr = d.tp[t].MmdThreshold;
-  if ((fl & 2) && d.mmd[i] < thr) {
-    const double deficit = thr - d.mmd[i];
+  const TopicP& tp = d.tp[t];
+  const uint32_t q = d.dlt[i];
+  double mm = d.mmd[i];
+  if (q >> 16) {  // fold the pending mesh deliveries: the deficit reads the counter
+    mm = eff_mmd(tp, mm, q);
+    d.mmd[i] = mm;
+    d.dlt[i] = q & 0xFFFF;
+  }
+  const double thr = tp.MmdThreshold;
+  if ((fl & 2) && mm < thr) {
+    const double deficit = thr - mm;
     d.mfp[i] += deficit * deficit;
   }
   d.flags[i] = fl & ~1;
@@ -277,7 +311,7 @@ __device__ __forceinline__ void stats_prune(const Dev& d, int64_t e, int t) {
 
 // doAddBackoff — gossipsub.go:844-854 (0 = no entry)
 __device__ __forceinline__ void add_backoff(const Dev& d, int64_t e, int t, int64_t now, int64_t interval) {
-  const int64_t i = (int64_t)t * d.E + e;
+  const int64_t i = tix(d, t, e);
   const int64_t expire = now + interval;
   const int64_t cur = d.backoff[i];
   if (cur == 0 || cur < expire) d.backoff[i] = expire;

@@ -46,6 +46,7 @@ struct gs_engine {
   int64_t E = 0;
   int H = 16;  // hops per heartbeat (or a nominal 16 for floodsub/randomsub)
   int64_t retireHops = 0;
+  int64_t hopsSinceFold = 0, foldEvery = 1;  // pending-delivery fold cadence (dlt)
   int maxAge = 0;
   // host graph / attributes
   std::vector<int64_t> rowptr;
@@ -254,7 +255,7 @@ int gs_engine::start() {
   x.PruneRecv = (gp.PruneBackoff / kSec) > 0 ? (gp.PruneBackoff / kSec) * kSec : gp.PruneBackoff;
   x.OGT = gp.OpportunisticGraftTicks ? gp.OpportunisticGraftTicks : 1;
 
-  const size_t NW = (size_t)N * W, NS = (size_t)N * S, TE = (size_t)T * E;
+  const size_t NW = (size_t)N * W, NS = (size_t)N * S, TE = (size_t)T * (size_t)((E + 63) & ~63ll);
   bool ok = true;
   auto chk = [&](const void* p) { if (!p) ok = false; };
   int64_t* dRowptr = dalloc<int64_t>(N + 1); chk(dRowptr);
@@ -310,6 +311,7 @@ int gs_engine::start() {
   }
   x.maxDeg = std::max(1, maxdeg);
   x.stMagic = (uint32_t)(((1ull << 32) + (uint64_t)St - 1) / (uint64_t)St);
+  foldEvery = std::max<int64_t>(1, 65535 / (2 * (int64_t)St));  // a hop adds at most 2*St per (edge, topic)
   x.oldm = dalloc<uint64_t>(W); chk(x.oldm);
   x.nAuth = dalloc<int32_t>(N); chk(x.nAuth);
   x.sel = cfg.router == GS_ROUTER_RANDOMSUB ? dalloc<uint64_t>(NS) : nullptr;
@@ -340,6 +342,7 @@ int gs_engine::start() {
   x.sdirty = dalloc<uint8_t>(E, 1); chk(x.sdirty);
   x.backoff = dalloc<int64_t>(TE);
   x.fmd = dalloc<double>(TE); x.mmd = dalloc<double>(TE); x.mfp = dalloc<double>(TE); x.imd = dalloc<double>(TE);
+  x.dlt = dalloc<uint32_t>(TE); chk(x.dlt);
   x.graftTime = dalloc<int64_t>(TE); x.meshTime = dalloc<int64_t>(TE); x.flags = dalloc<uint8_t>(TE);
   x.bp = dalloc<double>(E); x.peerhave = dalloc<int32_t>(E); x.iasked = dalloc<int32_t>(E);
   chk(x.score0); chk(x.score1); chk(x.backoff); chk(x.fmd); chk(x.mmd); chk(x.mfp); chk(x.imd);
@@ -350,6 +353,10 @@ int gs_engine::start() {
   x.poolCnt = dalloc<unsigned long long>(2); chk(x.poolCnt);
   x.slotSrc = dalloc<int32_t>(S, 0xFF); x.slotPubHop = dalloc<int64_t>(S); x.slotMid = dalloc<int64_t>(S, 0xFF);
   chk(x.slotSrc); chk(x.slotPubHop); chk(x.slotMid);
+#ifdef GS_STAMPS
+  x.stamps = dalloc<unsigned long long>((size_t)(N / 1024 + 1) * 8);
+#endif
+  x.pad = dalloc<double>(256 * 64 * 2); chk(x.pad);
   x.ctr = dalloc<unsigned long long>((size_t)C_NCOUNTERS * GS_CTR_SPREAD); x.err = dalloc<int32_t>(1);
   chk(x.ctr); chk(x.err);
   dScoreTmp = dalloc<double>(E); chk(dScoreTmp);
@@ -502,7 +509,14 @@ int gs_engine::stepOne() {
     TIMED(this, GS_K_PHASE_B,
           launch_wpl(W, [&](auto wpl) { k_phase_b<decltype(wpl)::value><<<N, 64, 0, stream>>>(d, h, now, cur, head); }));
   }
-  if (refreshDue(now)) TIMED(this, GS_K_REFRESH, (k_refresh<<<eb, 256, 0, stream>>>(d, now)));
+  if (refreshDue(now)) {
+    TIMED(this, GS_K_REFRESH, (k_refresh<<<eb, 256, 0, stream>>>(d, now)));
+    hopsSinceFold = 0;
+  } else if (scoring && ++hopsSinceFold >= foldEvery) {
+    // pending delivery counts are 16-bit: fold them before they can overflow
+    k_fold<<<eb, 256, 0, stream>>>(d, -1);
+    hopsSinceFold = 0;
+  }
   if (heartbeatDue(now)) {
     ticks++;
     TIMED(this, GS_K_HB_PRE, (k_hb_pre<<<N, 64, 0, stream>>>(d, now, ticks)));
@@ -537,6 +551,9 @@ int gs_engine::checkDeviceError() {
       gs_set_error("more first deliveries (plus own publishes) at one node in one hop than its "
                    "frontier list holds (min(slots + 64, 2^31 / num_nodes) entries)");
       return GS_ECAPACITY;
+    case E_DELTA:
+      gs_set_error("pending delivery count of one (edge, topic) overflowed 65535 between two score refreshes");
+      return GS_ECAPACITY;
     case E_DOUBLE:
       gs_set_error("a peer sent the same message twice in one hop (outside the canonical model)");
       return GS_EUNSUPPORTED;
@@ -544,6 +561,26 @@ int gs_engine::checkDeviceError() {
   }
 }
 
+// Per-(edge, topic) arrays are tiled on the device (tix in gs_device.h);
+// readbacks return them topic-major [t*E + e].
+template <class X>
+static int copy_back_tiled(gs_engine* g, X* dst, const X* src) {
+  const size_t E = (size_t)g->E, T = (size_t)g->T, Ep = (E + 63) & ~(size_t)63;
+  if (!g->started) {
+    std::memset(dst, 0, T * E * sizeof(X));
+    return GS_OK;
+  }
+  std::vector<X> tmp(T * Ep);
+  HIPCHECK(hipStreamSynchronize(g->stream));
+  HIPCHECK(hipMemcpy(tmp.data(), src, tmp.size() * sizeof(X), hipMemcpyDeviceToHost));
+  for (size_t b = 0; b < Ep / 64; ++b)
+    for (size_t t = 0; t < T; ++t) {
+      const X* row = tmp.data() + (b * T + t) * 64;
+      const size_t e0 = b * 64, n = std::min<size_t>(64, E - e0);
+      std::memcpy(dst + t * E + e0, row, n * sizeof(X));
+    }
+  return GS_OK;
+}
 extern "C" {
 
 const char* gs_last_error(void) { return g_err.c_str(); }
@@ -764,6 +801,7 @@ int gs_set_topic_score_params(gs_engine* g, int32_t topic, const gs_topic_score_
   g->tscored[topic] = 1;
   if (!g->started) return GS_OK;
   TopicP tp = to_dev(*p, g->scoring);
+  if (g->scoring) k_fold<<<nblk(g->E, 256), 256, 0, g->stream>>>(g->d, topic);  // with the old caps
   HIPCHECK(hipMemcpyAsync(g->dTp + topic, &tp, sizeof(TopicP), hipMemcpyHostToDevice, g->stream));
   HIPCHECK(hipMemsetAsync(g->d.sdirty, 1, (size_t)g->E, g->stream));  // every score may have changed
   if (existed && g->scoring &&
@@ -833,20 +871,18 @@ static int copy_back(gs_engine* g, void* dst, const void* src, size_t bytes) {
 
 int gs_read_mesh(gs_engine* g, uint64_t* mesh) { return copy_back(g, mesh, g->d.mesh, g->E * 8); }
 int gs_read_fanout(gs_engine* g, uint64_t* fanout) { return copy_back(g, fanout, g->d.fanout, g->E * 8); }
-int gs_read_backoff(gs_engine* g, int64_t* expire) {
-  return copy_back(g, expire, g->d.backoff, (size_t)g->T * g->E * 8);
-}
+int gs_read_backoff(gs_engine* g, int64_t* expire) { return copy_back_tiled(g, expire, g->d.backoff); }
 int gs_read_topic_stats(gs_engine* g, double* fmd, double* mmd, double* mfp, double* imd, int64_t* mesh_time,
                         int64_t* graft_time, uint8_t* flags) {
-  const size_t n = (size_t)g->T * g->E;
   int rc;
-  if ((rc = copy_back(g, fmd, g->d.fmd, n * 8))) return rc;
-  if ((rc = copy_back(g, mmd, g->d.mmd, n * 8))) return rc;
-  if ((rc = copy_back(g, mfp, g->d.mfp, n * 8))) return rc;
-  if ((rc = copy_back(g, imd, g->d.imd, n * 8))) return rc;
-  if ((rc = copy_back(g, mesh_time, g->d.meshTime, n * 8))) return rc;
-  if ((rc = copy_back(g, graft_time, g->d.graftTime, n * 8))) return rc;
-  return copy_back(g, flags, g->d.flags, n);
+  if (g->started && g->scoring) k_fold<<<nblk(g->E, 256), 256, 0, g->stream>>>(g->d, -1);
+  if ((rc = copy_back_tiled(g, fmd, g->d.fmd))) return rc;
+  if ((rc = copy_back_tiled(g, mmd, g->d.mmd))) return rc;
+  if ((rc = copy_back_tiled(g, mfp, g->d.mfp))) return rc;
+  if ((rc = copy_back_tiled(g, imd, g->d.imd))) return rc;
+  if ((rc = copy_back_tiled(g, mesh_time, (const int64_t*)g->d.meshTime))) return rc;
+  if ((rc = copy_back_tiled(g, graft_time, (const int64_t*)g->d.graftTime))) return rc;
+  return copy_back_tiled(g, flags, (const uint8_t*)g->d.flags);
 }
 int gs_read_behaviour_penalty(gs_engine* g, double* bp) { return copy_back(g, bp, g->d.bp, g->E * 8); }
 
@@ -868,6 +904,15 @@ int gs_read_deliveries(gs_engine* g, int64_t id, int32_t* hop, int32_t* from) {
   HIPCHECK(hipStreamSynchronize(g->stream));
   return GS_OK;
 }
+
+#ifdef GS_STAMPS
+// Debug build: phase-A cycle stamps of the sampled nodes of the last hop.
+int gs_debug_stamps(gs_engine* g, unsigned long long* out, int n) {
+  HIPCHECK(hipStreamSynchronize(g->stream));
+  HIPCHECK(hipMemcpy(out, g->d.stamps, (size_t)n * 8, hipMemcpyDeviceToHost));
+  return GS_OK;
+}
+#endif
 
 int gs_set_profiling(gs_engine* g, int on) {
   if (g->started) {

@@ -62,11 +62,13 @@ __global__ void k_refresh(Dev d, int64_t now) {
   for (int t = 0; t < d.T; ++t) {
     const TopicP& tp = d.tp[t];
     if (!tp.scored) continue;
-    const int64_t i = (int64_t)t * d.E + e;
-    double x = d.fmd[i] * tp.FmdDecay;
+    const int64_t i = tix(d, t, e);
+    const uint32_t q = d.dlt[i];
+    if (q) d.dlt[i] = 0;
+    double x = eff_fmd(tp, d.fmd[i], q) * tp.FmdDecay;
     if (x < d.DecayToZero) x = 0;
     d.fmd[i] = x;
-    x = d.mmd[i] * tp.MmdDecay;
+    x = eff_mmd(tp, d.mmd[i], q) * tp.MmdDecay;
     if (x < d.DecayToZero) x = 0;
     d.mmd[i] = x;
     x = d.mfp[i] * tp.MfpDecay;
@@ -88,11 +90,26 @@ __global__ void k_refresh(Dev d, int64_t now) {
   d.sdirty[e] = 1;
 }
 
+// Folds the pending deliveries of topic t (t < 0: every topic) into fmd / mmd.
+__global__ void k_fold(Dev d, int t0) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.E) return;
+  for (int t = t0 < 0 ? 0 : t0; t < (t0 < 0 ? d.T : t0 + 1); ++t) {
+    const int64_t i = tix(d, t, e);
+    const uint32_t q = d.dlt[i];
+    if (!q) continue;
+    const TopicP& tp = d.tp[t];
+    d.fmd[i] = eff_fmd(tp, d.fmd[i], q);
+    d.mmd[i] = eff_mmd(tp, d.mmd[i], q);
+    d.dlt[i] = 0;
+  }
+}
+
 // SetTopicScoreParams recap — score.go:215-229
 __global__ void k_recap(Dev d, int t, double fmdCap, double mmdCap) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= d.E) return;
-  const int64_t i = (int64_t)t * d.E + e;
+  const int64_t i = tix(d, t, e);
   if (d.fmd[i] > fmdCap) d.fmd[i] = fmdCap;
   if (d.mmd[i] > mmdCap) d.mmd[i] = mmdCap;
 }
@@ -263,6 +280,19 @@ __device__ __forceinline__ int wave_min_int(int x) {
 
 #define GS_NO_SLOT 0x7FFFFFFF
 
+// Debug build only (-DGS_STAMPS): cycle stamps at pass boundaries of every
+// 1024th node, read with gs_debug_stamps.
+#ifdef GS_STAMPS
+#define GS_STAMP(k)                                                                            \
+  do {                                                                                         \
+    if ((blockIdx.x & 1023) == 0 && lane == 0) d.stamps[(blockIdx.x >> 10) * 8 + (k)] = clock64(); \
+  } while (0)
+#else
+#define GS_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
 // Phase A — handleIncomingRPC / pushMsg for the payload of every RPC sent to
 // node v in the previous hop (pubsub.go:946-1022, score.go:693-964).  One
 // wave per receiving node; lane i = in-edge i, i.e. sender u_i = col[base+i],
@@ -298,6 +328,8 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   __shared__ uint64_t sRelay[64], sPub[64];
   __shared__ int sSnd[64];        // sender node | jr << 24 | graylisted << 31
   __shared__ int sLn[64];
+  __shared__ double sFcap[64], sMcap[64];  // per-topic caps (pass 3), 0 cap flag = unscored
+  __shared__ int sScored[64];
   const int v = blockIdx.x;
   const int lane = lane_id();
   const int prv = cur ^ 1;
@@ -331,6 +363,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     gray = d.router == 2 && scoring && !d.direct[e] && d.score0[e] < d.graylistThr;
     if (relay | pub) Ln = d.fln[prv][u];
   }
+  GS_STAMP(0);
   const bool authV = d.nAuth[v] > 0;  // v authored a live message: author exclusion possible
   for (int k = lane; k < T * MD; k += 64) scnt[k] = 0;
   if (d.needAge)
@@ -350,7 +383,14 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   sPub[lane] = pub;
   sSnd[lane] = valid ? (u | (jr << 24) | (gray ? (1 << 31) : 0)) : 0;
   sLn[lane] = Ln;
+  if (lane < T) {
+    const TopicP& tpl = d.tp[lane];
+    sScored[lane] = scoring && tpl.scored;
+    sFcap[lane] = tpl.FmdCap;
+    sMcap[lane] = tpl.MmdCap;
+  }
   __syncthreads();
+  GS_STAMP(1);
 
   long long nSent = 0, nGray = 0;
   // One delivered copy of `slot` from sender i (already known to be sent).
@@ -380,6 +420,10 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     uint32_t* wp = (uint32_t*)(sFirst + (ix & ~3));
     const int sh = 8 * (ix & 3);
     uint32_t old = *wp;
+#ifdef GS_EXP_NOCAS
+    if ((int)((old >> sh) & 0xFF) > i) *wp = (old & ~(0xFFu << sh)) | ((uint32_t)i << sh);
+    if (0)
+#endif
     while ((int)((old >> sh) & 0xFF) > i) {
       const uint32_t nw = (old & ~(0xFFu << sh)) | ((uint32_t)i << sh);
       const uint32_t prev = atomicCAS(wp, old, nw);
@@ -446,23 +490,122 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   }
   __syncthreads();
 
-  // ---- pass 2 (lane = word of the active window): first deliveries
+  GS_STAMP(2);
+  // ---- pass 2 (lane = word of the active window): first deliveries.  All
+  // loads of the pass are issued before its first store (on gfx9 a load's
+  // wait also waits for every older store).
   uint32_t* Lv = d.fl[cur] + (int64_t)v * FC;
   long long nDeliv = 0;
-  int running = 0;  // rank of the next entry of v's own frontier list
-  for (int c0 = 0; c0 < W; c0 += 64) {
-    const int w = c0 + lane;
-    const bool act = w < W && wm_has(amR, w);
-    uint64_t U = 0, S = 0;
-    int ix0 = 0;
-    if (act) {
-      ix0 = wm_rank(amR, w) * 64;
-      const uint64_t D = sD[ix0 >> 6];
+  uint64_t Uw[WPL], Sw[WPL], Hw[WPL], Ow[WPL];
+  int ixw[WPL];
+#pragma unroll
+  for (int j = 0; j < WPL; ++j) {
+    const int w = lane + 64 * j;
+    Uw[j] = Sw[j] = Hw[j] = Ow[j] = 0;
+    ixw[j] = 0;
+    if (w < W && wm_has(amR, w)) {
+      ixw[j] = wm_rank(amR, w) * 64;
+      const uint64_t D = sD[ixw[j] >> 6];
       if (D) {
-        S = d.seen[(int64_t)v * W + w];
-        U = D & ~S;
+        Sw[j] = d.seen[(int64_t)v * W + w];
+        Uw[j] = D;  // & ~seen below
       }
     }
+  }
+#pragma unroll
+  for (int j = 0; j < WPL; ++j) {
+    const int w = lane + 64 * j;
+    Uw[j] &= ~Sw[j];
+    if (Uw[j]) {
+      Ow[j] = d.oldm[w];
+      if (d.router == 2) Hw[j] = d.hist[((int64_t)head * d.N + v) * W + w];
+    }
+  }
+  // first deliveries per (topic, first deliverer) for the counters of pass 3
+  if (scoring) {
+#pragma unroll
+    for (int j = 0; j < WPL; ++j) {
+      uint64_t y = Uw[j];
+      const int t = (int)__umulhi((unsigned)((lane + 64 * j) * 64), d.stMagic);
+      while (y) {
+        const int b = __ffsll((long long)y) - 1;
+        y &= y - 1;
+        atomicAdd(&scnt[t * MD + sFirst[ixw[j] + b]], 1u << 16);
+      }
+    }
+  }
+  __syncthreads();
+  GS_STAMP(3);
+  // ---- pass 3 (lane = in-edge): fmd += fresh, mmd += fresh + creditable
+  // duplicates while in the mesh (score.go:915-928, 945-963).  inMesh of a
+  // scored topic is the edge's mesh bit (tracer.Graft / tracer.Prune accompany
+  // every mesh change).  Batches of 8 topics, the next batch's loads issued
+  // before this batch's stores.
+  long long nCopies = 0;
+  int maxCopies = 0;
+  for (int t = 0; t < T; ++t) {
+    const int cc = valid ? (int)(scnt[t * MD + lane] & 0xFFFF) : 0;
+    nCopies += cc;
+    maxCopies = cc > maxCopies ? cc : maxCopies;
+  }
+#ifdef GS_STAMPS
+  {
+    const long long tc = (long long)wave_sum_ll(nCopies), td = (long long)wave_sum_ll(nDeliv);
+    int mc = maxCopies;
+    for (int o = 32; o > 0; o >>= 1) mc = max(mc, __shfl_xor(mc, o));
+    if ((blockIdx.x & 1023) == 0 && lane == 0) {
+      d.stamps[(blockIdx.x >> 10) * 8 + 5] = tc;
+      d.stamps[(blockIdx.x >> 10) * 8 + 6] = td;
+      d.stamps[(blockIdx.x >> 10) * 8 + 7] = mc;
+    }
+  }
+#endif
+  if (scoring && valid) {
+    const uint64_t meshE = d.mesh[base + lane];
+    const int64_t e0 = base + lane;
+    // The counts go to the pending-delivery words dlt (eff_counters): one
+    // coalesced, branch-free read-modify-write per topic and in-edge, so every
+    // load and store is counted exactly by the compiler (no full-queue drains)
+    // and the next 16 topics' loads are in flight before this batch's stores.
+    uint32_t qA[16], qB[16];
+    auto loadQ = [&](int t0, uint32_t (&q)[16]) {
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const int t = t0 + kk < T ? t0 + kk : T - 1;
+        q[kk] = d.dlt[tix(d, t, e0)];
+      }
+    };
+    auto storeQ = [&](int t0, const uint32_t (&q)[16]) {
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const int t = t0 + kk < T ? t0 + kk : T - 1;
+        const uint32_t c = (t0 + kk < T && sScored[t]) ? scnt[t * MD + lane] : 0u;
+        const int copies = (int)(c & 0xFFFF), nf = (int)(c >> 16);
+        int credited = copies - nf;
+        if (d.needAge) credited -= (int)sUnc[t * MD + lane];
+        const uint32_t addM = ((meshE >> t) & 1) ? (uint32_t)(nf + credited) : 0u;
+        const uint32_t nq = q[kk] + (uint32_t)nf + (addM << 16);
+        if ((q[kk] & 0xFFFF) + nf > 0xFFFF || (q[kk] >> 16) + addM > 0xFFFF) set_err(d, E_DELTA);
+        // topics past T (T not a multiple of 16) go to this lane's scratch word
+        uint32_t* dst = t0 + kk < T ? d.dlt + tix(d, t, e0) : (uint32_t*)(d.pad + ((int64_t)(blockIdx.x & 255) * 64 + lane) * 2);
+        *dst = nq;
+      }
+    };
+    loadQ(0, qA);
+    for (int t0 = 0; t0 < T; t0 += 32) {
+      if (t0 + 16 < T) loadQ(t0 + 16, qB);
+      storeQ(t0, qA);
+      if (t0 + 32 < T) loadQ(t0 + 32, qA);
+      if (t0 + 16 < T) storeQ(t0 + 16, qB);
+    }
+  }
+  // ---- pass 2b: the stores of the first deliveries (after pass 3's loads,
+  // which would otherwise wait for them)
+  int running = 0;  // rank of the next entry of v's own frontier list
+#pragma unroll
+  for (int j = 0; j < WPL; ++j) {
+    const int w = lane + 64 * j;
+    const uint64_t U = Uw[j];
     const int k = __popcll(U);
     int incl = k;
     for (int o = 1; o < 64; o <<= 1) {
@@ -472,21 +615,20 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     int rank = running + incl - k;
     running += __shfl(incl, 63);
     if (U) {
-      if ((U & d.oldm[w]) || !wm_has(amW, w)) set_err(d, E_LATE);
-      d.seen[(int64_t)v * W + w] = S | U;
-      if (d.router == 2) d.hist[((int64_t)head * d.N + v) * W + w] |= U;
+      if ((U & Ow[j]) || !wm_has(amW, w)) set_err(d, E_LATE);
+      d.seen[(int64_t)v * W + w] = Sw[j] | U;
+      if (d.router == 2) d.hist[((int64_t)head * d.N + v) * W + w] = Hw[j] | U;
       nDeliv += k;
-      const int t = w / d.Wt;
+      const int t = (int)__umulhi((unsigned)(w * 64), d.stMagic);
       uint64_t y = U;
       while (y) {
         const int b = __ffsll((long long)y) - 1;
         y &= y - 1;
         const int slot = w * 64 + b;
-        const int ff = sFirst[ix0 + b];
+        const int ff = sFirst[ixw[j] + b];
         if (rank < FC) Lv[rank] = (uint32_t)slot | ((uint32_t)ff << 16);
         else set_err(d, E_FCAP);
         ++rank;
-        if (scoring) atomicAdd(&scnt[t * MD + ff], 1u << 16);
         if (d.needAge || d.record) {
           const int64_t a = h - d.slotPubHop[slot];
           if (d.needAge) d.age[(int64_t)v * d.S + slot] = (int16_t)a;
@@ -500,8 +642,8 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
         const int src = __ffsll((long long)lanesWith) - 1;
         lanesWith &= lanesWith - 1;
         uint64_t y = shfl_u64(U, src);
-        const int wsrc = c0 + src;
-        const int ixs = __shfl(ix0, src);
+        const int wsrc = src + 64 * j;
+        const int ixs = __shfl(ixw[j], src);
         while (y) {
           const int b = __ffsll((long long)y) - 1;
           y &= y - 1;
@@ -510,44 +652,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
       }
     }
   }
-  __syncthreads();
-
-  // ---- pass 3 (lane = in-edge): fmd += fresh, mmd += fresh + creditable
-  // duplicates while in the mesh (score.go:915-928, 945-963)
-  long long nCopies = 0;
-  for (int t = 0; t < T; ++t) nCopies += valid ? (scnt[t * MD + lane] & 0xFFFF) : 0;
-  if (scoring && valid) {
-    for (int t0 = 0; t0 < T; t0 += 8) {
-      uint32_t c[8];
-      uint8_t fl[8];
-      double fm[8], mm[8];
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        const int t = t0 + kk;
-        c[kk] = (t < T && d.tp[t].scored) ? scnt[t * MD + lane] : 0u;
-        fl[kk] = 0;
-        fm[kk] = mm[kk] = 0.0;
-        if (c[kk]) {
-          const int64_t ti = (int64_t)t * d.E + base + lane;
-          fl[kk] = d.flags[ti];
-          fm[kk] = d.fmd[ti];
-          mm[kk] = d.mmd[ti];
-        }
-      }
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        if (!c[kk]) continue;
-        const int t = t0 + kk;
-        const TopicP& tp = d.tp[t];
-        const int copies = (int)(c[kk] & 0xFFFF), nf = (int)(c[kk] >> 16);
-        int credited = copies - nf;
-        const int64_t ti = (int64_t)t * d.E + base + lane;
-        if (d.needAge) credited -= (int)sUnc[t * MD + lane];
-        if (nf) d.fmd[ti] = add_ones_capped(fm[kk], nf, tp.FmdCap);
-        if (fl[kk] & 1) d.mmd[ti] = add_ones_capped(mm[kk], nf + credited, tp.MmdCap);
-      }
-    }
-  }
+  GS_STAMP(4);
   if (lane == 0) d.fln[cur][v] = running < FC ? running : FC;
   const long long deliv = (long long)wave_sum_ll(nDeliv);
   const unsigned long long copies = wave_sum_ll(nCopies), s2 = wave_sum_ll(nSent), s3 = wave_sum_ll(nGray);

@@ -13,7 +13,7 @@ __device__ __forceinline__ bool graft_one(const Dev& d, int64_t e, int v, int t,
   if (!((d.sub[v] >> t) & 1)) return false;  // unknown topic: ignore
   if ((meshE >> t) & 1) return false;         // already in mesh
   if (d.direct[e]) return true;
-  const int64_t bi = (int64_t)t * d.E + e;
+  const int64_t bi = tix(d, t, e);
   const int64_t be = d.backoff[bi];
   if (be != 0 && now < be) {
     if (d.scoring) {
@@ -379,7 +379,7 @@ __global__ __launch_bounds__(64) void k_hb_pre(Dev d, int64_t now, uint64_t tick
     d.iasked[e] = 0;
     if (ticks % 15 == 0) {
       for (int t = 0; t < d.T; ++t) {
-        const int64_t i = (int64_t)t * d.E + e;
+        const int64_t i = tix(d, t, e);
         const int64_t be = d.backoff[i];
         if (be != 0 && be + 2000000000LL < now) d.backoff[i] = 0;
       }
@@ -527,7 +527,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
     int cnt = __popcll(__ballot(m));
     // do we have enough peers?
     if (cnt < d.Dlo) {
-      const bool bo = valid && d.backoff[(int64_t)t * d.E + e] != 0;
+      const bool bo = valid && d.backoff[tix(d, t, e)] != 0;
       const bool cand = inTopic && !m && !bo && !dir && S >= 0;
       const uint64_t key = gs_key64(d.seed, GS_SITE_GP_DLO, v, hw, vcol, t);
       if (select_k(cand, key, d.D - cnt)) {
@@ -609,7 +609,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
     if (cnt >= d.Dlo) {
       const int outb = __popcll(__ballot(m && ob));
       if (outb < d.Dout) {
-        const bool bo = valid && d.backoff[(int64_t)t * d.E + e] != 0;
+        const bool bo = valid && d.backoff[tix(d, t, e)] != 0;
         const bool cand = inTopic && !m && !bo && !dir && ob && S >= 0;
         const uint64_t key = gs_key64(d.seed, GS_SITE_GP_DOUT, v, hw, vcol, t);
         if (select_k(cand, key, d.Dout - outb)) {
@@ -635,7 +635,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
       const unsigned long long ml = __ballot(m && rank == cnt / 2);
       const double median = __shfl(S, __ffsll((long long)ml) - 1);
       if (median < d.oppThr) {
-        const bool bo = valid && d.backoff[(int64_t)t * d.E + e] != 0;
+        const bool bo = valid && d.backoff[tix(d, t, e)] != 0;
         const bool cand = inTopic && !m && !bo && !dir && S > median;
         const uint64_t key = gs_key64(d.seed, GS_SITE_GP_OPPORTUNISTIC, v, hw, vcol, t);
         if (select_k(cand, key, d.OGP)) {

@@ -10,4 +10,5 @@ timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
     > "$OUT/pytest_gpu.log" 2>&1 &&
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 &&
 timeout -k 10 400 python -u bench.py --steps 3 --warmup 1 > "$OUT/bench.json" 2> "$OUT/bench.err" &&
+timeout -k 10 300 python3 -u scripts/stamps.py > "$OUT/stamps.txt" 2>&1 &&
 echo done
