@@ -60,275 +60,481 @@ __device__ __forceinline__ void prune_topics(const Dev& d, int64_t e, int v, uin
   }
 }
 
+#define GS_PTXH 1024  // LDS hash slots for a node's mcache.peertx table (>= 2 * GS_PTX)
+
+__device__ __forceinline__ int ptx_hash(uint64_t key) {
+  return (int)((key * 0x9E3779B97F4A7C15ull) >> 54);  // 10 bits
+}
+
+// k-th set bit (0-based) of m
+__device__ __forceinline__ int kth_bit(uint64_t m, int k) {
+  for (int i = 0; i < k; ++i) m &= m - 1;
+  return __ffsll((long long)m) - 1;
+}
+
+// ++peertx[slot][edge] (mcache.GetForPeer, mcache.go:66-80) in the LDS hash;
+// returns the new count, or 0 when the table is full (E_PEERTX raised).
+__device__ __forceinline__ int ptx_incr(const Dev& d, unsigned long long* sH, uint64_t key) {
+  int hsl = ptx_hash(key);
+  for (int probe = 0; probe < GS_PTXH; ++probe) {
+    unsigned long long cur = sH[hsl];
+    while (true) {
+      if (cur == 0) {
+        const unsigned long long prev = atomicCAS(&sH[hsl], 0ull, (unsigned long long)(key | 1));
+        if (prev == 0) return 1;
+        cur = prev;
+      }
+      if ((cur & ~0xFFull) != key) break;  // another key: probe on
+      const unsigned long long c = cur & 0xFF;
+      const unsigned long long nw = key | (c < 255 ? c + 1 : 255);
+      const unsigned long long prev = atomicCAS(&sH[hsl], cur, nw);
+      if (prev == cur) return (int)(nw & 0xFF);
+      cur = prev;
+    }
+    hsl = (hsl + 1) & (GS_PTXH - 1);
+  }
+  set_err(d, E_PEERTX);
+  return 0;
+}
+
+__device__ __forceinline__ int ptx_count(const unsigned long long* sH, uint64_t key) {
+  int hsl = ptx_hash(key);
+  for (int probe = 0; probe < GS_PTXH; ++probe) {
+    const unsigned long long cur = sH[hsl];
+    if (cur == 0) return 0;
+    if ((cur & ~0xFFull) == key) return (int)(cur & 0xFF);
+    hsl = (hsl + 1) & (GS_PTXH - 1);
+  }
+  return 0;
+}
+
+// Item b of a per-sender item space (sIt = exclusive prefix of item counts
+// over the 64 senders): returns the sender; k = item index within it.
+__device__ __forceinline__ int item_sender(const int* sIt, int b, int& k) {
+  int lo = 0, hi = 63;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (sIt[mid] <= b) lo = mid; else hi = mid - 1;
+  }
+  k = b - sIt[lo];
+  return lo;
+}
+
+// Exclusive prefix over the 64 lanes; *total gets the sum.
+__device__ __forceinline__ int lane_prefix(int x, int* total) {
+  const int lane = lane_id();
+  int incl = x;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  *total = __shfl(incl, 63);
+  return incl - x;
+}
+
+// Phase B — HandleRPC for every control RPC sent to node v in the previous
+// hop (gossipsub.go:591-838), one wave per node.
+//   step 1 (serial, senders ascending, RPCs in send order: join GRAFTs, reply
+//          RPCs, heartbeat RPC): everything whose outcome depends on order —
+//          GRAFT acceptance against the running mesh size, PRUNEs, backoff,
+//          the live score that gates IHAVE / IWANT handling, peerhave;
+//   step 2 (lane-parallel): handleIWant of the gated senders — request lists
+//          cut into 16-id items spread over the lanes; peertx counts in an LDS
+//          hash (every (message, requester) pair is a distinct key, so the
+//          order of the increments does not matter);
+//   step 3 (lane-parallel): handleIHave of the gated senders — one item per
+//          (sender, advertised subscribed topic); wants = IHAVE payload &
+//          ~seen; the promised message (gossip_tracer.go:53) is the sender's
+//          (key, mid)-smallest want;
+//   step 4: per-edge results and reply RPCs written once.
+// Id lists (IWANT requests / responses) are sets: their order in the arena is
+// irrelevant to every reader.
 template <int WPL>
 __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, int cur, int head) {
-  __shared__ unsigned long long reqb[64 * GS_MAX_WPL];
-  __shared__ unsigned long long ptx[GS_PTX];
+  __shared__ uint64_t sseen[64 * WPL];   // v's seen row (handleIHave)
+  __shared__ uint64_t scache[64 * WPL];  // v's mcache windows (handleIWant)
+  __shared__ unsigned long long sH[GS_PTXH];
   __shared__ double sterm[64];
+  __shared__ int sIt[64];                // per-sender exclusive item prefix
+  __shared__ int sReqOff[64], sReqN[64]; // step 2: request list of each sender
+  __shared__ int sOut[64];               // step 2/3: where each sender's id list starts
+  __shared__ int sNode[64];              // step 3: sender node
+  __shared__ uint64_t sTm[64];           // step 3: advertised subscribed topics
+  __shared__ int sCnt[64], sCur[64];     // per-sender id counts / write cursors
+  __shared__ unsigned long long sKey[64];
+  __shared__ long long sMid[64];
+  __shared__ int sSlot[64];
+  __shared__ unsigned long long sBase;
   const int v = blockIdx.x;
   const int lane = lane_id();
   const int prv = cur ^ 1;
   const int W = d.W;
+  const int Wt = d.Wt;
   const int64_t base = d.rowptr[v];
   const int deg = (int)(d.rowptr[v + 1] - base);
   const uint64_t sv = d.sub[v];
+  const bool valid = lane < deg;
+  const int64_t e = base + lane;
+  // ---- per-sender control words (lane = in-edge), read before any store
+  int64_t r = 0;
+  int npre = 0, hb = 0;
+  if (valid) {
+    r = d.rev[e];
+    npre = d.cPre[prv][r];
+    hb = d.cHb[prv][r];
+  }
+  const bool ctl = npre != 0 || hb != 0;
+  const unsigned long long cmask = __ballot(ctl);
+  if (!cmask) return;
+  uint64_t gJoin = 0, gHb = 0, pRep = 0, pHb = 0, ihaveT = 0, meshE = 0;
+  int64_t iwRec = -1;
+  int ph = 0, ia = 0, u = 0;
+  double sc = 0.0;
+  bool gl = false;
+  if (valid) meshE = d.mesh[e];
+  if (ctl) {
+    gJoin = d.cGraftJoin[prv][r];
+    gHb = d.cGraftHb[prv][r];
+    pRep = d.cPruneReply[prv][r];
+    pHb = d.cPruneHb[prv][r];
+    ihaveT = d.cIhave[prv][r];
+    iwRec = d.cIwant[prv][r];
+    ph = d.peerhave[e];
+    ia = d.iasked[e];
+    u = d.col[e];
+    if (d.scoring) {
+      sc = d.score1[e];
+      gl = !d.direct[e] && d.score0[e] < d.graylistThr;  // AcceptFrom on the hop-start memo
+    }
+  }
+  const unsigned long long glmask = __ballot(gl);
   // lane t: current mesh size of topic t
-  uint64_t myMesh = lane < deg ? d.mesh[base + lane] : 0;
   int meshcnt = 0;
   for (int t = 0; t < d.T; ++t) {
-    const int c = __popcll(__ballot((myMesh >> t) & 1));
+    const int c = __popcll(__ballot((meshE >> t) & 1));
     if (lane == t) meshcnt = c;
   }
-  // graylist (AcceptFrom) on the hop-start memo, as in phase A
-  bool gl = false;
-  if (lane < deg && d.scoring) gl = !d.direct[base + lane] && d.score0[base + lane] < d.graylistThr;
-  const unsigned long long glmask = __ballot(gl);
-  // node tables: lane q = entry q
-  int promN = d.promN[v];
-  int64_t pMid = lane < promN ? d.promMid[(int64_t)v * GS_TABLE + lane] : -1;
-  int64_t pExp = lane < promN ? d.promExp[(int64_t)v * GS_TABLE + lane] : 0;
-  int32_t pSlot = lane < promN ? d.promSlot[(int64_t)v * GS_TABLE + lane] : 0;
-  int pEdge = lane < promN ? d.promEdge[(int64_t)v * GS_TABLE + lane] : 0;
-  bool promDirty = false;
-  // mcache.peertx for this node: (slot, requester edge) -> count, staged in LDS
-  int ptxN = d.ptxN[v];
-  for (int q = lane; q < ptxN; q += 64) ptx[q] = d.ptx[(int64_t)v * GS_PTX + q];
-  __syncthreads();
-  bool ptxDirty = false;
-  long long cPrunes = 0, cIwantSent = 0, cServed = 0, cGray = 0;
-  // senders with control RPCs this hop (lane i = in-edge i), then visit only those
-  int64_t rL = 0;
-  int npreL = 0, hbL = 0;
-  if (lane < deg) {
-    rL = d.rev[base + lane];
-    npreL = d.cPre[prv][rL];
-    hbL = d.cHb[prv][rL];
-  }
-  unsigned long long cmask = __ballot(npreL != 0 || hbL != 0);
-  while (cmask) {
-    const int i = __ffsll((long long)cmask) - 1;
-    cmask &= cmask - 1;
-    const int64_t e = base + i;
-    const int u = d.col[e];
-    const int64_t r = (int64_t)shfl_u64((uint64_t)rL, i);
-    const int npre = __shfl(npreL, i);
-    const int hb = __shfl(hbL, i);
-    const uint64_t gJoin = d.cGraftJoin[prv][r];
-    const uint64_t gHb = d.cGraftHb[prv][r];
-    const uint64_t pRep = d.cPruneReply[prv][r];
-    const uint64_t pHb = d.cPruneHb[prv][r];
-    const uint64_t ihaveT = d.cIhave[prv][r];
-    const int64_t iwRec = d.cIwant[prv][r];
-    // consume the outbox entry (the sender re-writes it two hops later)
-    if (lane == 0) {
-      d.cPre[prv][r] = 0;
-      d.cHb[prv][r] = 0;
-      d.cGraftJoin[prv][r] = 0;
-      d.cGraftHb[prv][r] = 0;
-      d.cPruneReply[prv][r] = 0;
-      d.cPruneHb[prv][r] = 0;
-      d.cIhave[prv][r] = 0;
-      d.cIwant[prv][r] = -1;
-      d.cIresp[prv][r] = -1;
-    }
-    if ((glmask >> i) & 1) {  // AcceptNone: the whole RPC is dropped
-      cGray += npre + hb;
-      continue;
-    }
-    uint64_t meshE = __shfl(myMesh, i);
-    bool dirty = false;
-    double sc = d.scoring ? d.score1[e] : 0.0;
-    int ph = d.peerhave[e];
-    int ia = d.iasked[e];
-    uint64_t pruneOut = 0;
-    int nReplies = 0;
-    int64_t respRec = -1, iwantRec = -1;
-    // (1) Join RPCs: one GRAFT each (gossipsub.go:1080-1084)
-    const int nJoin = __popcll(gJoin);
-    {
-      uint64_t gj = gJoin;
+  // ---- step 1: order-dependent control, senders ascending
+  bool gateIWant = false, gateIHave = false, prunesHb = false;
+  uint64_t pruneOut = 0;
+  int nRep1 = 0;
+  long long cPrunes = 0, cGray = 0;
+  {
+    unsigned long long m = cmask;
+    while (m) {
+      const int i = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const int npre_i = __shfl(npre, i), hb_i = __shfl(hb, i);
+      if ((glmask >> i) & 1) {  // AcceptNone: the whole RPC is dropped
+        cGray += npre_i + hb_i;
+        continue;
+      }
+      const int64_t ei = base + i;
+      const uint64_t gJoin_i = shfl_u64(gJoin, i), gHb_i = shfl_u64(gHb, i);
+      const uint64_t pRep_i = shfl_u64(pRep, i), pHb_i = shfl_u64(pHb, i), ihaveT_i = shfl_u64(ihaveT, i);
+      const int64_t iwRec_i = (int64_t)shfl_u64((uint64_t)iwRec, i);
+      int ph_i = __shfl(ph, i);
+      const int ia_i = __shfl(ia, i);
+      double sc_i = __shfl(sc, i);
+      uint64_t mE = shfl_u64(meshE, i);
+      bool dirty = false;
+      uint64_t pOut = 0;
+      int nR = 0;
+      // (1) Join RPCs: one GRAFT each (gossipsub.go:1080-1084)
+      uint64_t gj = gJoin_i;
       while (gj) {
         const int t = __ffsll((long long)gj) - 1;
         gj &= gj - 1;
-        if (dirty) { sc = edge_score_wave(d, e, sterm); dirty = false; }
-        if (sc >= d.gossipThr) ph++;  // handleIHave's counter (no IHAVE entries)
-        if (graft_one(d, e, v, t, sc, now, meshcnt, meshE, dirty)) {
-          pruneOut |= 1ull << t;
-          nReplies++;
+        if (dirty) { sc_i = edge_score_wave(d, ei, sterm); dirty = false; }
+        if (sc_i >= d.gossipThr) ph_i++;  // handleIHave's counter (no IHAVE entries)
+        if (graft_one(d, ei, v, t, sc_i, now, meshcnt, mE, dirty)) {
+          pOut |= 1ull << t;
+          nR++;
         }
       }
-    }
-    // (2) reply RPCs: IWANT requests and PRUNEs answering our own control
-    const int nRep = npre - nJoin;
-    if (nRep > 0) {
-      if (dirty) { sc = edge_score_wave(d, e, sterm); dirty = false; }
-      const bool gossipOK = sc >= d.gossipThr;
-      if (gossipOK) ph += nRep;
-      if (gossipOK && iwRec >= 0) {
-        // handleIWant (gossipsub.go:674-711): serve cached messages, counting
-        // per-peer retransmissions (mcache.GetForPeer)
-        uint64_t served[WPL];
-        int nServed = 0;
-        arena_read(d, prv, iwRec, reqb);
-#pragma unroll
-        for (int j = 0; j < WPL; ++j) {
-          const int w = lane + 64 * j;
-          uint64_t req = 0, cache = 0;
-          if (w < W) {
-            req = reqb[w];
-            if (req)
-              for (int k = 0; k < d.HL; ++k) cache |= d.hist[((int64_t)((head + k) % d.R) * d.N + v) * W + w];
-          }
-          uint64_t cand = req & cache;
-          served[j] = 0;
-          // serialise the retransmission-table updates over the wave
-          unsigned long long lanesWith = __ballot(cand != 0);
-          while (lanesWith) {
-            const int src = __ffsll((long long)lanesWith) - 1;
-            lanesWith &= lanesWith - 1;
-            uint64_t cw = shfl_u64(cand, src);
-            while (cw) {
-              const int b = __ffsll((long long)cw) - 1;
-              cw &= cw - 1;
-              const int slot = (src + 64 * j) * 64 + b;
-              // GetForPeer (mcache.go:66-80): ++peertx[mid][p]
-              const uint64_t key = ((uint64_t)(uint32_t)slot << 32) | ((uint64_t)i << 8);
-              int found = -1;
-              for (int q = lane; q < ptxN; q += 64)
-                if ((ptx[q] & ~0xFFull) == key) found = q;
-              const unsigned long long hit = __ballot(found >= 0);
-              int count;
-              if (hit) {
-                const int fl = __ffsll((long long)hit) - 1;
-                const int q = __shfl(found, fl);
-                if (lane == 0) {
-                  const uint64_t c = ptx[q] & 0xFF;
-                  ptx[q] = key | (c < 255 ? c + 1 : 255);
-                }
-                __syncthreads();
-                count = (int)(ptx[q] & 0xFF);
-              } else {
-                if (ptxN >= GS_PTX) {
-                  if (lane == 0) set_err(d, E_PEERTX);
-                } else {
-                  if (lane == 0) ptx[ptxN] = key | 1;
-                  ptxN++;
-                  __syncthreads();
-                }
-                count = 1;
-              }
-              ptxDirty = true;
-              if (count <= d.GR && lane == src) served[j] |= 1ull << b;
-            }
-          }
-          nServed += __popcll(served[j]);
-        }
-        nServed = wave_sum_int(nServed);
-        if (nServed > 0) {
-          respRec = arena_write<WPL>(d, cur, served);
-          nReplies++;
-          cServed += nServed;
-        }
+      // (2) reply RPCs: IWANT requests and PRUNEs answering our own control
+      bool gIW = false;
+      const int nRep = npre_i - __popcll(gJoin_i);
+      if (nRep > 0) {
+        if (dirty) { sc_i = edge_score_wave(d, ei, sterm); dirty = false; }
+        const bool gossipOK = sc_i >= d.gossipThr;
+        if (gossipOK) ph_i += nRep;
+        gIW = gossipOK && iwRec_i >= 0;  // handleIWant (gossipsub.go:674-711): step 2
+        prune_topics(d, ei, v, pRep_i, now, meshcnt, mE, dirty);
       }
-      prune_topics(d, e, v, pRep, now, meshcnt, meshE, dirty);
-    }
-    // (3) heartbeat RPC: IHAVE, GRAFT, PRUNE (gossipsub.go:1618-1654 sends it last)
-    if (hb) {
-      if (dirty) { sc = edge_score_wave(d, e, sterm); dirty = false; }
-      bool iwantAny = false;
-      if (sc >= d.gossipThr) {
-        ph++;
-        if (ph <= d.MaxIHaveMessages && ia < d.MaxIHaveLength && ihaveT) {
-          // handleIHave (gossipsub.go:610-672): IHAVE payload = the sender's
-          // gossip windows at its heartbeat, now ring slots 1..HG after Shift
-          uint64_t want[WPL];
-          int nWant = 0, nMids = 0;
-          uint64_t bestKey = ~0ull;
-          int64_t bestMid = INT64_MAX;
-          int bestSlot = -1;
-#pragma unroll
-          for (int j = 0; j < WPL; ++j) {
-            const int w = lane + 64 * j;
-            want[j] = 0;
-            if (w >= W) continue;
-            const int tw = w / d.Wt;
-            if (!((ihaveT >> tw) & 1)) continue;
-            uint64_t mids = 0;
-            mids = d.gw[(int64_t)u * W + w];
-            nMids += __popcll(mids);
-            if (!((sv >> tw) & 1)) continue;  // topic not in our mesh map
-            want[j] = mids & ~d.seen[(int64_t)v * W + w];
-            nWant += __popcll(want[j]);
-            uint64_t y = want[j];
-            while (y) {
-              const int b = __ffsll((long long)y) - 1;
-              y &= y - 1;
-              const int64_t mid = d.slotMid[(int64_t)w * 64 + b];
-              const uint64_t k = gs_key64(d.seed, GS_SITE_IWANT, v, u, (uint32_t)mid, (uint32_t)h);
-              if (k < bestKey || (k == bestKey && mid < bestMid)) { bestKey = k; bestMid = mid; bestSlot = w * 64 + b; }
-            }
-          }
-          nWant = wave_sum_int(nWant);
-          nMids = wave_sum_int(nMids);
-          if (nMids > d.MaxIHaveLength * __popcll(ihaveT)) {
-            if (lane == 0) set_err(d, E_TRUNCATE);  // per-peer IHAVE truncation: not built yet
-          }
-          if (nWant > 0) {
-            int iask = nWant;
-            if (iask + ia > d.MaxIHaveLength) {
-              iask = d.MaxIHaveLength - ia;
-              if (lane == 0) set_err(d, E_TRUNCATE);
-            }
-            // wave argmin over (key, mid): the promised message (gossip_tracer.go:53)
-            for (int o = 32; o > 0; o >>= 1) {
-              const uint64_t ok = shfl_u64(bestKey, lane ^ o);
-              const int64_t om = (int64_t)shfl_u64((uint64_t)bestMid, lane ^ o);
-              const int os = __shfl(bestSlot, lane ^ o);
-              if (ok < bestKey || (ok == bestKey && om < bestMid)) { bestKey = ok; bestMid = om; bestSlot = os; }
-            }
-            iwantRec = arena_write<WPL>(d, cur, want);
-            ia += iask;
-            cIwantSent += iask;
-            iwantAny = true;
-            if (d.scoring) {  // gossipTracer.AddPromise (gossip_tracer.go:48-75)
-              const unsigned long long ex = __ballot(lane < promN && pMid == bestMid && pEdge == i);
-              if (!ex) {
-                if (promN >= GS_TABLE) {
-                  if (lane == 0) set_err(d, E_PROMISES);
-                } else {
-                  if (lane == promN) {
-                    pMid = bestMid;
-                    pSlot = bestSlot;
-                    pEdge = i;
-                    pExp = now + d.IWantFollowupTime;
-                  }
-                  promN++;
-                  promDirty = true;
-                }
-              }
-            }
-          }
+      // (3) heartbeat RPC: IHAVE (step 3), GRAFT, PRUNE
+      bool gIH = false;
+      uint64_t prunes = 0;
+      if (hb_i) {
+        if (dirty) { sc_i = edge_score_wave(d, ei, sterm); dirty = false; }
+        if (sc_i >= d.gossipThr) {
+          ph_i++;
+          // handleIHave gates (gossipsub.go:612-628); only topics in our mesh map count (:633)
+          gIH = ph_i <= d.MaxIHaveMessages && ia_i < d.MaxIHaveLength && (ihaveT_i & sv) != 0;
         }
-      }
-      {
-        uint64_t g = gHb;
-        uint64_t prunes = 0;
+        uint64_t g = gHb_i;
         while (g) {
           const int t = __ffsll((long long)g) - 1;
           g &= g - 1;
-          if (graft_one(d, e, v, t, sc, now, meshcnt, meshE, dirty)) prunes |= 1ull << t;
+          if (graft_one(d, ei, v, t, sc_i, now, meshcnt, mE, dirty)) prunes |= 1ull << t;
         }
-        prune_topics(d, e, v, pHb, now, meshcnt, meshE, dirty);
-        pruneOut |= prunes;
-        if (iwantAny || prunes) nReplies++;
+        prune_topics(d, ei, v, pHb_i, now, meshcnt, mE, dirty);
+      }
+      pOut |= prunes;
+      if (lane == i) {
+        meshE = mE;
+        ph = ph_i;
+        pruneOut = pOut;
+        nRep1 = nR;
+        gateIWant = gIW;
+        gateIHave = gIH;
+        prunesHb = prunes != 0;
+      }
+      cPrunes += __popcll(pOut);
+    }
+  }
+
+  // ---- step 2: handleIWant — serve cached messages at most GossipRetransmission times per peer
+  int64_t respRec = -1;
+  long long cServed = 0;
+  bool ptxDirty = false;
+  if (__ballot(gateIWant)) {
+    ptxDirty = true;
+    for (int w = lane; w < W; w += 64) {
+      uint64_t x = 0;
+      for (int k = 0; k < d.HL; ++k) x |= d.hist[((int64_t)((head + k) % d.R) * d.N + v) * W + w];
+      scache[w] = x;
+    }
+    for (int k = lane; k < GS_PTXH; k += 64) sH[k] = 0ull;
+    const int n = gateIWant ? (int)(iwRec & 0xFFFFFF) : 0;
+    int totalItems;
+    sIt[lane] = lane_prefix((n + 15) >> 4, &totalItems);
+    sReqOff[lane] = gateIWant ? (int)(iwRec >> 24) : 0;
+    sReqN[lane] = n;
+    sCnt[lane] = 0;
+    sCur[lane] = 0;
+    __syncthreads();
+    const int ptxN = d.ptxN[v];
+    for (int q = lane; q < ptxN; q += 64) {
+      const unsigned long long ent = d.ptx[(int64_t)v * GS_PTX + q];
+      int hsl = ptx_hash(ent & ~0xFFull);
+      while (atomicCAS(&sH[hsl], 0ull, ent) != 0ull) hsl = (hsl + 1) & (GS_PTXH - 1);
+    }
+    __syncthreads();
+    // pass a: increments and per-sender served counts
+    for (int b = lane; b < totalItems; b += 64) {
+      int k;
+      const int i = item_sender(sIt, b, k);
+      const int off = sReqOff[i] + 16 * k, cnt = min(16, sReqN[i] - 16 * k);
+      int c = 0;
+      for (int q = 0; q < cnt; ++q) {
+        const int slot = d.pool[prv][off + q];
+        if (!((scache[slot >> 6] >> (slot & 63)) & 1)) continue;  // not in the cache
+        const uint64_t key = ((uint64_t)(uint32_t)slot << 32) | ((uint64_t)i << 8);
+        const int count = ptx_incr(d, sH, key);
+        if (count >= 1 && count <= d.GR) ++c;
+      }
+      if (c) atomicAdd(&sCnt[i], c);
+    }
+    __syncthreads();
+    int totalServed;
+    const int myServed = sCnt[lane];
+    const int myOff = lane_prefix(myServed, &totalServed);
+    if (lane == 0 && totalServed) sBase = atomicAdd(&d.poolCnt[cur], (unsigned long long)totalServed);
+    __syncthreads();
+    if (totalServed) {
+      const unsigned long long poolBase = sBase;
+      if (poolBase + totalServed > (unsigned long long)d.poolCap) {
+        if (lane == 0) set_err(d, E_POOL);
+      } else {
+        sOut[lane] = (int)poolBase + myOff;
+        if (myServed) respRec = ((int64_t)(poolBase + myOff) << 24) | (int64_t)myServed;
+        cServed = totalServed;
+        __syncthreads();
+        // pass b: write the served ids (the counts are final now)
+        for (int b = lane; b < totalItems; b += 64) {
+          int k;
+          const int i = item_sender(sIt, b, k);
+          const int off = sReqOff[i] + 16 * k, cnt = min(16, sReqN[i] - 16 * k);
+          for (int q = 0; q < cnt; ++q) {
+            const int slot = d.pool[prv][off + q];
+            if (!((scache[slot >> 6] >> (slot & 63)) & 1)) continue;
+            const uint64_t key = ((uint64_t)(uint32_t)slot << 32) | ((uint64_t)i << 8);
+            const int count = ptx_count(sH, key);
+            if (count >= 1 && count <= d.GR) d.pool[cur][sOut[i] + atomicAdd(&sCur[i], 1)] = slot;
+          }
+        }
       }
     }
-    // write back per-edge state and our reply RPCs to u
-    if (lane == i) myMesh = meshE;
-    if (lane == 0) {
+    __syncthreads();
+  }
+
+  // ---- step 3: handleIHave — IWANT the unseen advertised messages of our topics
+  int64_t iwantRec = -1;
+  bool iwantAny = false;
+  long long cIwantSent = 0;
+  const unsigned long long ihMask = __ballot(gateIHave);
+  if (ihMask) {
+    for (int w = lane; w < W; w += 64) sseen[w] = d.seen[(int64_t)v * W + w];
+    const uint64_t tm = gateIHave ? (ihaveT & sv) : 0ull;
+    int totalItems;
+    sIt[lane] = lane_prefix(__popcll(tm), &totalItems);
+    sTm[lane] = tm;
+    sNode[lane] = u;
+    sCnt[lane] = 0;
+    sCur[lane] = 0;
+    sKey[lane] = ~0ull;
+    sMid[lane] = INT64_MAX;
+    sSlot[lane] = -1;
+    __syncthreads();
+    // pass a: want counts and the per-sender smallest promise key
+    for (int b = lane; b < totalItems; b += 64) {
+      int k;
+      const int i = item_sender(sIt, b, k);
+      const int t = kth_bit(sTm[i], k);
+      const int uu = sNode[i];
+      int c = 0;
+      uint64_t bestKey = ~0ull;
+      for (int w = t * Wt; w < (t + 1) * Wt; ++w) {
+        const uint64_t want = d.gw[(int64_t)uu * W + w] & ~sseen[w];
+        c += __popcll(want);
+        uint64_t y = want;
+        while (y) {
+          const int bb = __ffsll((long long)y) - 1;
+          y &= y - 1;
+          const int64_t mid = d.slotMid[(int64_t)w * 64 + bb];
+          const uint64_t key = gs_key64(d.seed, GS_SITE_IWANT, v, uu, (uint32_t)mid, (uint32_t)h);
+          bestKey = key < bestKey ? key : bestKey;
+        }
+      }
+      if (c) {
+        atomicAdd(&sCnt[i], c);
+        atomicMin(&sKey[i], bestKey);
+      }
+    }
+    __syncthreads();
+    // pass a2: the smallest mid among the wants holding the smallest key
+    for (int b = lane; b < totalItems; b += 64) {
+      int k;
+      const int i = item_sender(sIt, b, k);
+      const int t = kth_bit(sTm[i], k);
+      const int uu = sNode[i];
+      const uint64_t best = sKey[i];
+      for (int w = t * Wt; w < (t + 1) * Wt; ++w) {
+        uint64_t y = d.gw[(int64_t)uu * W + w] & ~sseen[w];
+        while (y) {
+          const int bb = __ffsll((long long)y) - 1;
+          y &= y - 1;
+          const int64_t mid = d.slotMid[(int64_t)w * 64 + bb];
+          if (gs_key64(d.seed, GS_SITE_IWANT, v, uu, (uint32_t)mid, (uint32_t)h) == best)
+            atomicMin(&sMid[i], (long long)mid);
+        }
+      }
+    }
+    __syncthreads();
+    int totalWant;
+    const int myWant = sCnt[lane];
+    const int myOff = lane_prefix(myWant, &totalWant);
+    if (lane == 0 && totalWant) sBase = atomicAdd(&d.poolCnt[cur], (unsigned long long)totalWant);
+    __syncthreads();
+    if (totalWant) {
+      const unsigned long long poolBase = sBase;
+      if (poolBase + totalWant > (unsigned long long)d.poolCap) {
+        if (lane == 0) set_err(d, E_POOL);
+      } else {
+        sOut[lane] = (int)poolBase + myOff;
+        __syncthreads();
+        // pass b: write the request lists; the promised message's slot
+        for (int b = lane; b < totalItems; b += 64) {
+          int k;
+          const int i = item_sender(sIt, b, k);
+          const int t = kth_bit(sTm[i], k);
+          const int uu = sNode[i];
+          const long long bestMid = sMid[i];
+          for (int w = t * Wt; w < (t + 1) * Wt; ++w) {
+            uint64_t y = d.gw[(int64_t)uu * W + w] & ~sseen[w];
+            while (y) {
+              const int bb = __ffsll((long long)y) - 1;
+              y &= y - 1;
+              const int slot = w * 64 + bb;
+              d.pool[cur][sOut[i] + atomicAdd(&sCur[i], 1)] = slot;
+              if (d.slotMid[slot] == bestMid) sSlot[i] = slot;
+            }
+          }
+        }
+        if (myWant) {
+          int iask = myWant;
+          if (iask + ia > d.MaxIHaveLength) {
+            iask = d.MaxIHaveLength - ia;
+            set_err(d, E_TRUNCATE);  // per-peer IWANT truncation is not built
+          }
+          iwantRec = ((int64_t)(poolBase + myOff) << 24) | (int64_t)myWant;
+          ia += iask;
+          cIwantSent = iask;
+          iwantAny = true;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  cIwantSent = (long long)wave_sum_ll(cIwantSent);
+
+  // ---- gossipTracer.AddPromise (gossip_tracer.go:48-75) for every sender we
+  // sent an IWANT, senders ascending; table lane q = entry q
+  if (d.scoring) {
+    const unsigned long long pm = __ballot(iwantAny);
+    if (pm) {
+      int promN = d.promN[v];
+      int64_t pMid = lane < promN ? d.promMid[(int64_t)v * GS_TABLE + lane] : -1;
+      int64_t pExp = lane < promN ? d.promExp[(int64_t)v * GS_TABLE + lane] : 0;
+      int32_t pSlot = lane < promN ? d.promSlot[(int64_t)v * GS_TABLE + lane] : 0;
+      int pEdge = lane < promN ? d.promEdge[(int64_t)v * GS_TABLE + lane] : 0;
+      unsigned long long m = pm;
+      while (m) {
+        const int i = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const int64_t bm = sMid[i];
+        const int bs = sSlot[i];
+        const unsigned long long ex = __ballot(lane < promN && pMid == bm && pEdge == i);
+        if (ex) continue;
+        if (promN >= GS_TABLE) {
+          if (lane == 0) set_err(d, E_PROMISES);
+          continue;
+        }
+        if (lane == promN) {
+          pMid = bm;
+          pSlot = bs;
+          pEdge = i;
+          pExp = now + d.IWantFollowupTime;
+        }
+        promN++;
+      }
+      if (lane < promN && lane < GS_TABLE) {
+        d.promMid[(int64_t)v * GS_TABLE + lane] = pMid;
+        d.promExp[(int64_t)v * GS_TABLE + lane] = pExp;
+        d.promSlot[(int64_t)v * GS_TABLE + lane] = pSlot;
+        d.promEdge[(int64_t)v * GS_TABLE + lane] = (uint8_t)pEdge;
+      }
+      if (lane == 0) d.promN[v] = promN < GS_TABLE ? promN : GS_TABLE;
+    }
+  }
+
+  // ---- step 4: consume the outbox entries, per-edge state, reply RPCs
+  if (ctl) {
+    d.cPre[prv][r] = 0;
+    d.cHb[prv][r] = 0;
+    d.cGraftJoin[prv][r] = 0;
+    d.cGraftHb[prv][r] = 0;
+    d.cPruneReply[prv][r] = 0;
+    d.cPruneHb[prv][r] = 0;
+    d.cIhave[prv][r] = 0;
+    d.cIwant[prv][r] = -1;
+    d.cIresp[prv][r] = -1;
+    if (!gl) {
       d.mesh[e] = meshE;
       d.peerhave[e] = ph;
       d.iasked[e] = ia;
+      const int nReplies = nRep1 + (respRec >= 0 ? 1 : 0) + ((iwantAny || prunesHb) ? 1 : 0);
       if (nReplies) {
         d.cPre[cur][e] = (uint8_t)(d.cPre[cur][e] + nReplies);
         d.cPruneReply[cur][e] |= pruneOut;
@@ -336,22 +542,19 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
         if (respRec >= 0) d.cIresp[cur][e] = respRec;
       }
     }
-    cPrunes += __popcll(pruneOut);
   }
-  if (promDirty) {
-    if (lane < promN && lane < GS_TABLE) {
-      d.promMid[(int64_t)v * GS_TABLE + lane] = pMid;
-      d.promExp[(int64_t)v * GS_TABLE + lane] = pExp;
-      d.promSlot[(int64_t)v * GS_TABLE + lane] = pSlot;
-      d.promEdge[(int64_t)v * GS_TABLE + lane] = (uint8_t)pEdge;
-    }
-    if (lane == 0) d.promN[v] = promN < GS_TABLE ? promN : GS_TABLE;
-  }
-  if (ptxDirty) {
+  if (ptxDirty) {  // peertx table back to its list form
     __syncthreads();
-    const int n = ptxN < GS_PTX ? ptxN : GS_PTX;
-    for (int q = lane; q < n; q += 64) d.ptx[(int64_t)v * GS_PTX + q] = ptx[q];
-    if (lane == 0) d.ptxN[v] = n;
+    int kept = 0;
+    for (int q0 = 0; q0 < GS_PTXH; q0 += 64) {
+      const unsigned long long ent = sH[q0 + lane];
+      int tot;
+      const int pos = kept + lane_prefix(ent != 0ull ? 1 : 0, &tot);
+      if (ent && pos < GS_PTX) d.ptx[(int64_t)v * GS_PTX + pos] = ent;
+      kept += tot;
+    }
+    if (kept > GS_PTX && lane == 0) set_err(d, E_PEERTX);
+    if (lane == 0) d.ptxN[v] = kept < GS_PTX ? kept : GS_PTX;
   }
   if (lane == 0) {
     if (cPrunes) ctr_add(d, C_PRUNES, (unsigned long long)cPrunes);
