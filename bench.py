@@ -55,32 +55,54 @@ def build_engine(wl, rounds, seed, device, lib=None, n=None, msgs_per_round=MSGS
     src = rng.integers(0, n, len(hops)).astype(np.int32)
     top = (np.arange(len(hops)) % T).astype(np.int32)
     eng.publish(src, top, hops)
+    eng.schedule = (top, hops)
     return eng, g
 
 
-def algorithmic_bytes(kernel, eng, wl, launches_per_round):
-    """Algorithmic HBM bytes of ONE launch (DESIGN.md §5 lists the formulas)."""
+def active_words(eng, wl, hop):
+    """Words of the message window phase A touches at `hop` (the engine's amR:
+    words holding a message published within the last 3 heartbeats + 1 hop,
+    slots assigned round-robin per topic as gs_publish does)."""
+    top, hops = eng.schedule
+    if not hasattr(eng, "sched_slots"):
+        St = wl["slots"]
+        slots = np.empty(len(top), dtype=np.int64)
+        for t in range(wl["topics"]):
+            idx = np.nonzero(top == t)[0]  # publish order (hops are non-decreasing)
+            slots[idx] = t * St + np.arange(len(idx)) % St
+        eng.sched_slots = slots
+    slots = eng.sched_slots
+    max_age = 3 * HOPS_PER_ROUND
+    live = (hops >= hop - 1 - max_age) & (hops <= hop - 1)
+    return len(np.unique(slots[live] // 64))
+
+
+def algorithmic_bytes(kernel, eng, wl, per_hop):
+    """Algorithmic HBM bytes of ONE launch of `kernel`: the data
+    the algorithm must move with the engine's representation, not what the
+    caches end up fetching.  per_hop: measured averages over the timed hops."""
     N, E, T = eng.N, eng.E, wl["topics"]
-    W = T * wl["slots"] // 64
-    Wt = wl["slots"] // 64
     if kernel == "phase_a":
-        # read the forwarded topics' frontier words of every forwarding edge,
-        # read+write seen, write the next frontier: (E_fwd_words + 3 N W) * 8
         mesh = eng.mesh()
-        fwd_topic_edges = int(np.unpackbits(mesh.view(np.uint8)).sum())
-        return (fwd_topic_edges * Wt + 3 * N * W) * 8, dict(fwd_topic_edges=fwd_topic_edges, W=W)
-    if kernel == "score":
-        # per (edge, topic): flags 1 + fmd/mmd/mfp/imd 32 + meshTime 8; per edge:
-        # col 4 + app[col] 8 + p6 8 + bp 8 + score write 8
-        return E * (41 * T + 36), dict(E=E, T=T)
+        fwd_edges = int((mesh != 0).sum())          # edges with a forwarding topic
+        items = per_hop["deliveries"] + per_hop["published"]   # frontier-list entries written per hop
+        list_reads = 4.0 * items * fwd_edges / N     # each list is read by the neighbours it forwards to
+        list_writes = 4.0 * items
+        pending = 8.0 * T * E                        # pending-delivery counts, read + write per (edge, topic)
+        seen = 16.0 * N * per_hop["active_words"]    # seen words of the active window, read + write
+        meta = 49.0 * E                              # rev, col, fwd masks, IWANT ref, S0 memo, direct, mesh
+        b = list_reads + list_writes + pending + seen + meta
+        return b, dict(fwd_edges=fwd_edges, list_entries_per_hop=items, active_words=per_hop["active_words"],
+                       bytes_lists=int(list_reads + list_writes), bytes_pending=int(pending),
+                       bytes_seen=int(seen), bytes_meta=int(meta))
     if kernel == "refresh":
-        # per (edge, topic): 4 counters r+w 64 + flags r+w 2 + graftTime r 8 + meshTime w 8; per edge bp r+w 16
-        return E * (82 * T + 16), dict(E=E, T=T)
-    if kernel == "heartbeat":
-        # per (edge, topic): backoff 8 + flags 1 (+ stats touched on graft/prune);
-        # per edge: mesh r+w 16, fanout r+w 16, score 8, col 4, sub[col] 8, direct+outbound 2,
-        # control outbox writes 25; per node: mcache windows of all topics (HG*W*8) + clear W*8
-        return E * (9 * T + 79) + N * W * 8 * 6, dict(E=E, T=T)
+        # per (edge, topic): fmd/mmd/mfp/imd r+w 64, pending counts r 4, flags r 1,
+        # graftTime r 8 + meshTime w 8 (mesh edges); per edge: bp r+w 16, dirty w 1
+        return E * (77.0 * T + 17), dict(E=E, T=T)
+    if kernel == "score":
+        # full pass: per (edge, topic) flags 1 + fmd/mfp/imd 24 + pending 4 (+ mmd, meshTime when
+        # active); per edge col 4 + app 8 + p6 8 + bp 8 + out 8
+        return E * (29.0 * T + 36), dict(E=E, T=T)
     return None, {}
 
 
@@ -141,6 +163,7 @@ def main():
         eng.sync()
 
     c0 = eng.counters()
+    hop0 = eng.hop
     eng.set_profiling(True)
     barrier()
     t0 = time.perf_counter()
@@ -168,7 +191,11 @@ def main():
     dom = max(kstats, key=lambda k: kstats[k][0])
     total_ms, launches = kstats[dom]
     avg_ms = total_ms / max(1, launches)
-    bytes_per_launch, bytes_info = algorithmic_bytes(dom, eng, wl, launches / args.steps)
+    nh = args.steps * HOPS_PER_ROUND
+    per_hop = {"deliveries": (c1["deliveries"] - c0["deliveries"]) / nh,
+               "published": (c1["published"] - c0["published"]) / nh,
+               "active_words": float(np.mean([active_words(eng, wl, hop0 + i) for i in range(nh)]))}
+    bytes_per_launch, bytes_info = algorithmic_bytes(dom, eng, wl, per_hop)
     roofline = None
     if bytes_per_launch:
         achieved = bytes_per_launch / (avg_ms / 1e3) / 1e9
@@ -199,6 +226,9 @@ def main():
         "rounds_per_sec": rounds_per_s * world,
         "hops_per_sec": rounds_per_s * HOPS_PER_ROUND,
         "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kstats.items() if v[1]},
+        "events_per_step": {k: (c1[k] - c0[k]) // args.steps for k in
+                            ("deliveries", "duplicates", "transmissions", "grafts_sent", "prunes_sent",
+                             "ihave_sent", "iwant_sent", "iwant_served", "promises_broken", "graylisted")},
         "roofline": roofline,
         "setup_s": round(setup_s, 1),
     }

@@ -1,0 +1,28 @@
+"""Golden vectors (tests/golden/scenarios.json, made by make_golden.py): the
+oracle on CPU and the HIP engine on the GPU must both reproduce every counter
+and every readback digest of every parity scenario."""
+import json
+import os
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+
+import scenarios  # noqa: E402
+from make_golden import digest  # noqa: E402
+
+GOLDEN = json.load(open(os.path.join(HERE, "golden", "scenarios.json")))
+
+
+@pytest.mark.parametrize("name", sorted(GOLDEN))
+def test_oracle_reproduces_golden(oracle_path, name):
+    assert digest(scenarios.run(oracle_path, name)) == GOLDEN[name]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(GOLDEN))
+def test_gpu_reproduces_golden(name):
+    from pubsub_amd import PRODUCT_LIB
+    assert digest(scenarios.run(PRODUCT_LIB, name)) == GOLDEN[name]
