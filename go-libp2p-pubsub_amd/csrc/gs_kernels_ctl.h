@@ -641,7 +641,7 @@ __global__ __launch_bounds__(64) void k_hb_pre(Dev d, int64_t now, uint64_t tick
 // changed earlier in this heartbeat.
 __device__ __forceinline__ uint64_t emit_gossip(const Dev& d, int v, int t, int64_t hop, int head, bool valid,
                                                 int vcol, bool inTopic, bool excl, bool dir, double& Slive,
-                                                bool& dirty, int64_t rowBase, double* lds,
+                                                bool& dirty, bool& dirtyUp, int64_t rowBase, double* lds,
                                                 const uint64_t* sgw) {
   const int lane = lane_id();
   int nm = 0;
@@ -650,7 +650,10 @@ __device__ __forceinline__ uint64_t emit_gossip(const Dev& d, int v, int t, int6
   if (nm == 0) return 0;
   if (nm > d.MaxIHaveLength && lane == 0) set_err(d, E_TRUNCATE);
   const bool base = valid && inTopic && !excl && !dir;
-  unsigned long long dm = __ballot(base && dirty);
+  // A graft never lowers a score (P1 is 0 at meshTime 0, the P3 deficit term
+  // is switched off; weights validated w1 >= 0, w3 <= 0), so a cached score
+  // already at or above the threshold stays a correct decision after one.
+  unsigned long long dm = __ballot(base && (dirty || (dirtyUp && !(Slive >= d.gossipThr))));
   while (dm) {
     const int j = __ffsll((long long)dm) - 1;
     dm &= dm - 1;
@@ -658,6 +661,7 @@ __device__ __forceinline__ uint64_t emit_gossip(const Dev& d, int v, int t, int6
     if (lane == j) {
       Slive = s;
       dirty = false;
+      dirtyUp = false;
     }
   }
   const bool cand = base && Slive >= d.gossipThr;
@@ -709,7 +713,8 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
   double Slive = S;  // live Score(p) for emitGossip
   const bool dir = valid && d.direct[e];
   const bool ob = valid && d.outbound[e];
-  bool dirty = false;
+  bool dirty = false;    // a PRUNE lowered the peer's score since Slive
+  bool dirtyUp = false;  // a GRAFT (never lowers it) changed it since Slive
   uint64_t tograft = 0, toprune = 0, ihave = 0;
   const uint64_t joined = d.sub[v];
   const uint32_t hw = (uint32_t)hop;
@@ -737,7 +742,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
         stats_graft(d, e, t, now);
         meshl |= bit;
         tograft |= bit;
-        dirty = true;
+        dirtyUp = true;
         m = true;
       }
       cnt = __popcll(__ballot(m));
@@ -819,7 +824,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
           stats_graft(d, e, t, now);
           meshl |= bit;
           tograft |= bit;
-          dirty = true;
+          dirtyUp = true;
           m = true;
         }
         cnt = __popcll(__ballot(m));
@@ -845,12 +850,12 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
           stats_graft(d, e, t, now);
           meshl |= bit;
           tograft |= bit;
-          dirty = true;
+          dirtyUp = true;
           m = true;
         }
       }
     }
-    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, m, dir, Slive, dirty, base, sterm, sgw);
+    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, m, dir, Slive, dirty, dirtyUp, base, sterm, sgw);
   }
   // expire fanout for topics we haven't published to in a while
   uint64_t fpres = d.fanoutPresent[v];
@@ -881,7 +886,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
         f = true;
       }
     }
-    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, f, dir, Slive, dirty, base, sterm, sgw);
+    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, f, dir, Slive, dirty, dirtyUp, base, sterm, sgw);
   }
   // sendGraftPrune + flush: one heartbeat RPC per peer with any control
   if (valid) {
