@@ -330,12 +330,13 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   __shared__ int sLn[64];
   __shared__ double sFcap[64], sMcap[64];  // per-topic caps (pass 3), 0 cap flag = unscored
   __shared__ int sScored[64];
+  __shared__ uint32_t sQ[GS_QRING];        // sent copies awaiting delivery: slot | sender << 16
+  __shared__ uint16_t sRk[64 * GS_MAX_WPL];  // rank of word w in amR, 0xFFFF = outside
   const int v = blockIdx.x;
   const int lane = lane_id();
   const int prv = cur ^ 1;
   const int W = d.W;
   const int T = d.T;
-  const int St = d.St;
   const int MD = d.maxDeg;
   const int FC = d.FC;
   const int64_t base = d.rowptr[v];
@@ -369,6 +370,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   if (d.needAge)
     for (int k = lane; k < T * MD; k += 64) sUnc[k] = 0;
   for (int k = lane; k < nR; k += 64) sD[k] = 0;
+  for (int k = lane; k < W; k += 64) sRk[k] = wm_has(amR, k) ? (uint16_t)wm_rank(amR, k) : (uint16_t)0xFFFF;
   for (int k = lane; k < nR * 16; k += 64) ((uint32_t*)sFirst)[k] = 0xFFFFFFFFu;
   // per-sender view for the block-parallel walk
   const int nb = (Ln + 3) >> 2;  // 16-byte blocks of the sender's list
@@ -393,13 +395,15 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   GS_STAMP(1);
 
   long long nSent = 0, nGray = 0;
-  // One delivered copy of `slot` from sender i (already known to be sent).
-  auto deliver = [&](int i, int slot, bool isGray) {
-    if (isGray) return;
+  // One delivered copy of `slot` from sender i (sent, not graylisted).
+  auto deliver = [&](int i, int slot) {
     const int w = slot >> 6;
     const int t = (int)__umulhi((unsigned)slot, d.stMagic);
+#ifndef GS_EXP_NOADD
     atomicAdd(&scnt[t * MD + i], 1u);
-    if (d.needAge || !wm_has(amR, w)) {
+#endif
+    const int rk = sRk[w];
+    if (d.needAge || rk == 0xFFFF) {
       const bool had = (d.seen[(int64_t)v * W + w] >> (slot & 63)) & 1;
       // markDuplicateMessageDelivery window (score.go:955): a copy of a message
       // first delivered before this hop is credited only within the window
@@ -407,14 +411,14 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
         const int64_t firstHop = d.slotPubHop[slot] + d.age[(int64_t)v * d.S + slot];
         if ((h - firstHop) * d.hop_ns > d.tp[t].MmdWindow) atomicAdd(&sUnc[t * MD + i], 1u);
       }
-      if (!wm_has(amR, w)) {
+      if (rk == 0xFFFF) {
         // outside the window only an old duplicate is possible; a first
         // delivery there is later than the engine's window allows
         if (!had) set_err(d, E_LATE);
         return;
       }
     }
-    const int ix = wm_rank(amR, w) * 64 + (slot & 63);
+    const int ix = rk * 64 + (slot & 63);
     atomicOr((unsigned long long*)&sD[ix >> 6], 1ull << (slot & 63));
     // byte-wise min of the lowest deliverer (senders ascending)
     uint32_t* wp = (uint32_t*)(sFirst + (ix & ~3));
@@ -432,7 +436,10 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     }
   };
   // ---- pass 1a: every 16-byte block of every sender's list is one work item;
-  // lane l takes items l, l+64, ...  (four loads in flight per lane)
+  // lane l takes items l, l+64, ...  (four loads in flight per lane).  The
+  // entries actually sent (about a quarter: the sender's per-edge topic masks)
+  // are compacted into an LDS ring and delivered 64 at a time by all lanes.
+  int qh = 0, qt = 0;  // ring head / tail (wave-uniform)
   for (int b0 = 0; b0 < totalBlk; b0 += 256) {
     int si[4], kb[4];
     uint4 q[4];
@@ -456,37 +463,62 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      if (si[r] < 0) continue;
-      const int i = si[r];
-      const int snd = sSnd[i];
-      const int uu = snd & 0xFFFFFF;
-      const int jri = (snd >> 24) & 0x7F;
-      const bool isGray = snd < 0;
-      const uint64_t rl = sRelay[i], pb = sPub[i];
-      const int n = min(4, sLn[i] - 4 * kb[r]);
+      uint32_t en[4];
+      bool sn[4];
+      int k = 0;
+      {
+        const int i = si[r] < 0 ? 0 : si[r];
+        const int snd = sSnd[i];
+        const int uu = snd & 0xFFFFFF;
+        const int jri = (snd >> 24) & 0x7F;
+        const bool isGray = snd < 0;
+        const uint64_t rl = sRelay[i], pb = sPub[i];
+        const int n = si[r] < 0 ? 0 : min(4, sLn[i] - 4 * kb[r]);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        if (c >= n) break;
-        const uint32_t ent = c == 0 ? q[r].x : (c == 1 ? q[r].y : (c == 2 ? q[r].z : q[r].w));
-        const int slot = (int)(ent & 0xFFFF);
-        const int tag = (int)(ent >> 16);
-        const int t = (int)__umulhi((unsigned)slot, d.stMagic);
-        bool sent = tag == 255 ? ((pb >> t) & 1) : ((rl >> t) & 1);
-        sent = sent && tag != jri;  // ReceivedFrom exclusion (gossipsub.go:1003)
-        if (sent && d.router == 1) sent = (d.sel[(int64_t)uu * d.S + slot] >> jri) & 1;
-        if (sent && authV && d.slotSrc[slot] == v) sent = false;  // never to the author
-        if (!sent) continue;
-        ++nSent;
-        if (isGray) ++nGray;  // one RPC per relayed message, all dropped
-        deliver(i, slot, isGray);
+        for (int c = 0; c < 4; ++c) {
+          const uint32_t ent = c == 0 ? q[r].x : (c == 1 ? q[r].y : (c == 2 ? q[r].z : q[r].w));
+          const int slot = (int)(ent & 0xFFFF);
+          const int tag = (int)(ent >> 16);
+          const int t = (int)__umulhi((unsigned)slot, d.stMagic);
+          bool sent = c < n && (tag == 255 ? ((pb >> t) & 1) : ((rl >> t) & 1));
+          sent = sent && tag != jri;  // ReceivedFrom exclusion (gossipsub.go:1003)
+          if (sent && d.router == 1) sent = (d.sel[(int64_t)uu * d.S + slot] >> jri) & 1;
+          if (sent && authV && d.slotSrc[slot] == v) sent = false;  // never to the author
+          nSent += sent;
+          if (sent && isGray) ++nGray;  // one RPC per relayed message, all dropped
+          sn[c] = sent && !isGray;
+          en[c] = (uint32_t)slot | ((uint32_t)i << 16);
+          k += sn[c];
+        }
       }
+      int incl = k;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+      }
+      int p = qt + incl - k;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (sn[c]) sQ[(p++) & (GS_QRING - 1)] = en[c];
+      qt += __shfl(incl, 63);
+      __syncthreads();
+      while (qt - qh >= 64) {
+        const uint32_t ent = sQ[(qh + lane) & (GS_QRING - 1)];
+        deliver((int)(ent >> 16), (int)(ent & 0xFFFF));
+        qh += 64;
+      }
+      __syncthreads();
     }
+  }
+  if (qt > qh && lane < qt - qh) {
+    const uint32_t ent = sQ[(qh + lane) & (GS_QRING - 1)];
+    deliver((int)(ent >> 16), (int)(ent & 0xFFFF));
   }
   // ---- pass 1b: IWANT responses (one list per sender, rare)
   for (int k = 0; k < irN; ++k) {
     const int slot = d.pool[prv][irOff + k];
     ++nSent;
-    deliver(lane, slot, gray);
+    if (!gray) deliver(lane, slot);
   }
   __syncthreads();
 
@@ -619,7 +651,6 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
       d.seen[(int64_t)v * W + w] = Sw[j] | U;
       if (d.router == 2) d.hist[((int64_t)head * d.N + v) * W + w] = Hw[j] | U;
       nDeliv += k;
-      const int t = (int)__umulhi((unsigned)(w * 64), d.stMagic);
       uint64_t y = U;
       while (y) {
         const int b = __ffsll((long long)y) - 1;
