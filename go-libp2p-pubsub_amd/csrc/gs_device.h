@@ -16,7 +16,7 @@
 
 #define GS_WAVE 64
 #define GS_MAX_WPL 4   // words per lane in the node-wave kernels: W <= 256
-#define GS_QRING 512   // phase A delivery ring (>= 63 pending + 256 appended per sub-round)
+#define GS_QCAP 320    // phase A delivery queue (>= 63 pending + 256 appended per sub-round)
 #define GS_TABLE 64    // promise table entries per node (one per lane)
 #define GS_PTX 512     // IWANT-retransmission (mcache peertx) entries per node
 

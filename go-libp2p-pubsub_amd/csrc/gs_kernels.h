@@ -17,6 +17,8 @@
 //   k_heartbeat    wave/node     mesh maintenance, emitGossip, fanout, mcache.Shift
 //                                                           gossipsub.go:1299-1552, 1658-1712
 #pragma once
+#include <type_traits>
+
 #include "gs_device.h"
 
 // ---------------------------------------------------------------- score
@@ -328,9 +330,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   __shared__ uint64_t sRelay[64], sPub[64];
   __shared__ int sSnd[64];        // sender node | jr << 24 | graylisted << 31
   __shared__ int sLn[64];
-  __shared__ double sFcap[64], sMcap[64];  // per-topic caps (pass 3), 0 cap flag = unscored
-  __shared__ int sScored[64];
-  __shared__ uint32_t sQ[GS_QRING];        // sent copies awaiting delivery: slot | sender << 16
+  __shared__ uint32_t sQ[GS_QCAP];         // sent copies awaiting delivery: slot | sender << 16
   __shared__ uint16_t sRk[64 * GS_MAX_WPL];  // rank of word w in amR, 0xFFFF = outside
   const int v = blockIdx.x;
   const int lane = lane_id();
@@ -366,12 +366,21 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   }
   GS_STAMP(0);
   const bool authV = d.nAuth[v] > 0;  // v authored a live message: author exclusion possible
-  for (int k = lane; k < T * MD; k += 64) scnt[k] = 0;
+  for (int k = lane; k < nCnt / 4; k += 64) ((uint4*)scnt)[k] = make_uint4(0, 0, 0, 0);
   if (d.needAge)
-    for (int k = lane; k < T * MD; k += 64) sUnc[k] = 0;
+    for (int k = lane; k < nCnt / 4; k += 64) ((uint4*)sUnc)[k] = make_uint4(0, 0, 0, 0);
   for (int k = lane; k < nR; k += 64) sD[k] = 0;
-  for (int k = lane; k < W; k += 64) sRk[k] = wm_has(amR, k) ? (uint16_t)wm_rank(amR, k) : (uint16_t)0xFFFF;
-  for (int k = lane; k < nR * 16; k += 64) ((uint32_t*)sFirst)[k] = 0xFFFFFFFFu;
+  {
+    int rb = 0;  // rank of word 64 j + lane in amR
+#pragma unroll
+    for (int j = 0; j < GS_MAX_WPL; ++j) {
+      const uint64_t m = amR.m[j];
+      if (64 * j + lane < W)
+        sRk[64 * j + lane] = ((m >> lane) & 1) ? (uint16_t)(rb + __popcll(m & ((1ull << lane) - 1))) : (uint16_t)0xFFFF;
+      rb += __popcll(m);
+    }
+  }
+  for (int k = lane; k < nR * 4; k += 64) ((uint4*)sFirst)[k] = make_uint4(~0u, ~0u, ~0u, ~0u);
   // per-sender view for the block-parallel walk
   const int nb = (Ln + 3) >> 2;  // 16-byte blocks of the sender's list
   int bincl = nb;
@@ -385,12 +394,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   sPub[lane] = pub;
   sSnd[lane] = valid ? (u | (jr << 24) | (gray ? (1 << 31) : 0)) : 0;
   sLn[lane] = Ln;
-  if (lane < T) {
-    const TopicP& tpl = d.tp[lane];
-    sScored[lane] = scoring && tpl.scored;
-    sFcap[lane] = tpl.FmdCap;
-    sMcap[lane] = tpl.MmdCap;
-  }
+  const uint64_t scoredT = __ballot(lane < T && scoring && d.tp[lane].scored);  // scored topics
   __syncthreads();
   GS_STAMP(1);
 
@@ -436,15 +440,16 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     }
   };
   // ---- pass 1a: every 16-byte block of every sender's list is one work item;
-  // lane l takes items l, l+64, ...  (four loads in flight per lane).  The
+  // lane l takes items l, l+64, ...  (PB loads in flight per lane).  The
   // entries actually sent (about a quarter: the sender's per-edge topic masks)
-  // are compacted into an LDS ring and delivered 64 at a time by all lanes.
-  int qh = 0, qt = 0;  // ring head / tail (wave-uniform)
-  for (int b0 = 0; b0 < totalBlk; b0 += 256) {
-    int si[4], kb[4];
-    uint4 q[4];
+  // are compacted into an LDS queue and delivered 64 at a time by all lanes.
+  int qh = 0, qt = 0;  // queue head / tail (wave-uniform)
+  constexpr int PB = 8;
+  for (int b0 = 0; b0 < totalBlk; b0 += 64 * PB) {
+    int si[PB], kb[PB];
+    uint4 q[PB];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < PB; ++r) {
       const int bidx = b0 + r * 64 + lane;
       si[r] = -1;
       kb[r] = 0;
@@ -462,7 +467,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
       }
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < PB; ++r) {
       uint32_t en[4];
       bool sn[4];
       int k = 0;
@@ -499,19 +504,27 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
       int p = qt + incl - k;
 #pragma unroll
       for (int c = 0; c < 4; ++c)
-        if (sn[c]) sQ[(p++) & (GS_QRING - 1)] = en[c];
+        if (sn[c]) sQ[p++] = en[c];
       qt += __shfl(incl, 63);
       __syncthreads();
-      while (qt - qh >= 64) {
-        const uint32_t ent = sQ[(qh + lane) & (GS_QRING - 1)];
-        deliver((int)(ent >> 16), (int)(ent & 0xFFFF));
-        qh += 64;
+      if (qt >= 64) {
+        while (qt - qh >= 64) {
+          const uint32_t ent = sQ[qh + lane];
+          deliver((int)(ent >> 16), (int)(ent & 0xFFFF));
+          qh += 64;
+        }
+        // move the (< 64) pending copies to the front
+        const uint32_t rest = lane < qt - qh ? sQ[qh + lane] : 0u;
+        __syncthreads();
+        if (lane < qt - qh) sQ[lane] = rest;
+        qt -= qh;
+        qh = 0;
+        __syncthreads();
       }
-      __syncthreads();
     }
   }
-  if (qt > qh && lane < qt - qh) {
-    const uint32_t ent = sQ[(qh + lane) & (GS_QRING - 1)];
+  if (lane < qt - qh) {
+    const uint32_t ent = sQ[qh + lane];
     deliver((int)(ent >> 16), (int)(ent & 0xFFFF));
   }
   // ---- pass 1b: IWANT responses (one list per sender, rare)
@@ -599,37 +612,43 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     // coalesced, branch-free read-modify-write per topic and in-edge, so every
     // load and store is counted exactly by the compiler (no full-queue drains)
     // and the next 16 topics' loads are in flight before this batch's stores.
-    uint32_t qA[16], qB[16];
-    auto loadQ = [&](int t0, uint32_t (&q)[16]) {
+    // All loads of a batch of BS topics are issued before its first store
+    // (BS = 64 when T > 16: one round trip for the usual topic counts).
+    // tiled words of in-edge e0: topic t at p0[64 t]
+    uint32_t* const p0 = d.dlt + ((((e0 >> 6) * T) << 6) | (e0 & 63));
+    auto upd = [&](int t, uint32_t q) -> uint32_t {
+      const uint32_t c = ((scoredT >> t) & 1) ? scnt[t * MD + lane] : 0u;
+      const int copies = (int)(c & 0xFFFF), nf = (int)(c >> 16);
+      int credited = copies - nf;
+      if (d.needAge) credited -= (int)sUnc[t * MD + lane];
+      const uint32_t addM = ((meshE >> t) & 1) ? (uint32_t)(nf + credited) : 0u;
+      if ((q & 0xFFFF) + nf > 0xFFFF || (q >> 16) + addM > 0xFFFF) set_err(d, E_DELTA);
+      return q + (uint32_t)nf + (addM << 16);
+    };
+    auto rmw = [&](auto bsC) {
+      constexpr int BS = decltype(bsC)::value;
+      uint32_t q[BS];
+      int t0 = 0;
+      for (; t0 + BS <= T; t0 += BS) {
+        uint32_t* p = p0 + ((int64_t)t0 << 6);
 #pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        const int t = t0 + kk < T ? t0 + kk : T - 1;
-        q[kk] = d.dlt[tix(d, t, e0)];
+        for (int kk = 0; kk < BS; ++kk) q[kk] = p[kk << 6];
+#pragma unroll
+        for (int kk = 0; kk < BS; ++kk) p[kk << 6] = upd(t0 + kk, q[kk]);
+      }
+      if (t0 < T) {  // the last T % BS topics; the rest of the batch goes to this lane's scratch word
+        uint32_t* const scr = (uint32_t*)(d.pad + ((int64_t)(blockIdx.x & 255) * 64 + lane) * 2);
+#pragma unroll
+        for (int kk = 0; kk < BS; ++kk) q[kk] = p0[(int64_t)min(t0 + kk, T - 1) << 6];
+#pragma unroll
+        for (int kk = 0; kk < BS; ++kk) {
+          const uint32_t nq = upd(min(t0 + kk, T - 1), q[kk]);
+          *(t0 + kk < T ? p0 + ((int64_t)(t0 + kk) << 6) : scr) = nq;
+        }
       }
     };
-    auto storeQ = [&](int t0, const uint32_t (&q)[16]) {
-#pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        const int t = t0 + kk < T ? t0 + kk : T - 1;
-        const uint32_t c = (t0 + kk < T && sScored[t]) ? scnt[t * MD + lane] : 0u;
-        const int copies = (int)(c & 0xFFFF), nf = (int)(c >> 16);
-        int credited = copies - nf;
-        if (d.needAge) credited -= (int)sUnc[t * MD + lane];
-        const uint32_t addM = ((meshE >> t) & 1) ? (uint32_t)(nf + credited) : 0u;
-        const uint32_t nq = q[kk] + (uint32_t)nf + (addM << 16);
-        if ((q[kk] & 0xFFFF) + nf > 0xFFFF || (q[kk] >> 16) + addM > 0xFFFF) set_err(d, E_DELTA);
-        // topics past T (T not a multiple of 16) go to this lane's scratch word
-        uint32_t* dst = t0 + kk < T ? d.dlt + tix(d, t, e0) : (uint32_t*)(d.pad + ((int64_t)(blockIdx.x & 255) * 64 + lane) * 2);
-        *dst = nq;
-      }
-    };
-    loadQ(0, qA);
-    for (int t0 = 0; t0 < T; t0 += 32) {
-      if (t0 + 16 < T) loadQ(t0 + 16, qB);
-      storeQ(t0, qA);
-      if (t0 + 32 < T) loadQ(t0 + 32, qA);
-      if (t0 + 16 < T) storeQ(t0 + 16, qB);
-    }
+    if (T > 16) rmw(std::integral_constant<int, 64>{});
+    else rmw(std::integral_constant<int, 16>{});
   }
   // ---- pass 2b: the stores of the first deliveries (after pass 3's loads,
   // which would otherwise wait for them)
