@@ -322,6 +322,24 @@ __device__ __forceinline__ void add_backoff(const Dev& d, int64_t e, int t, int6
 // Writes the set bits of a wave-distributed bitset (word w = lane + 64*j) as
 // slot ids in ascending slot order (phase A walks them with a cursor);
 // returns the packed record (off << 24 | count) or -1 when empty.
+// Inclusive prefix sum over the 64 lanes with DPP row shifts and row
+// broadcasts (no LDS permutes).  Call with all 64 lanes active.
+__device__ __forceinline__ int wave_incl_sum(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return x;
+}
+// Number of set bits of the wave mask m below this lane.
+__device__ __forceinline__ int lane_rank(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+// Value of lane 63 (wave-uniform).
+__device__ __forceinline__ int wave_last(int x) { return __builtin_amdgcn_readlane(x, 63); }
+
 template <int WPL>
 __device__ __forceinline__ int64_t arena_write(const Dev& d, int buf, const uint64_t (&bits)[WPL]) {
   const int lane = lane_id();
@@ -330,13 +348,9 @@ __device__ __forceinline__ int64_t arena_write(const Dev& d, int buf, const uint
 #pragma unroll
   for (int j = 0; j < WPL; ++j) {
     const int c = __popcll(bits[j]);
-    int s = c;  // inclusive prefix over lanes of word row j
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(s, o);
-      if (lane >= o) s += y;
-    }
+    const int s = wave_incl_sum(c);  // inclusive prefix over lanes of word row j
     incl[j] = s - c;
-    tot[j] = __shfl(s, 63);
+    tot[j] = wave_last(s);
     total += tot[j];
   }
   if (total == 0) return -1;

@@ -383,12 +383,8 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   for (int k = lane; k < nR * 4; k += 64) ((uint4*)sFirst)[k] = make_uint4(~0u, ~0u, ~0u, ~0u);
   // per-sender view for the block-parallel walk
   const int nb = (Ln + 3) >> 2;  // 16-byte blocks of the sender's list
-  int bincl = nb;
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(bincl, o);
-    if (lane >= o) bincl += y;
-  }
-  const int totalBlk = __shfl(bincl, 63);
+  const int bincl = wave_incl_sum(nb);
+  const int totalBlk = wave_last(bincl);
   sBlk[lane] = bincl - nb;
   sRelay[lane] = relay;
   sPub[lane] = pub;
@@ -398,7 +394,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   __syncthreads();
   GS_STAMP(1);
 
-  long long nSent = 0, nGray = 0;
+  int nSent = 0, nGray = 0;
   // One delivered copy of `slot` from sender i (sent, not graylisted).
   auto deliver = [&](int i, int slot) {
     const int w = slot >> 6;
@@ -444,8 +440,15 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   // entries actually sent (about a quarter: the sender's per-edge topic masks)
   // are compacted into an LDS queue and delivered 64 at a time by all lanes.
   int qh = 0, qt = 0;  // queue head / tail (wave-uniform)
+#ifdef GS_STAMPS
+  long long accDel = 0;  // cycles in the delivery drains
+  long long accLd = 0;   // cycles from a round's start to its list blocks' arrival
+#endif
   constexpr int PB = 8;
   for (int b0 = 0; b0 < totalBlk; b0 += 64 * PB) {
+#ifdef GS_STAMPS
+    const long long tl0 = clock64();
+#endif
     int si[PB], kb[PB];
     uint4 q[PB];
 #pragma unroll
@@ -466,11 +469,14 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
         q[r] = *(const uint4*)(d.fl[prv] + (int64_t)uu * FC + 4 * kb[r]);
       }
     }
+#ifdef GS_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    accLd += clock64() - tl0;
+#endif
 #pragma unroll
     for (int r = 0; r < PB; ++r) {
       uint32_t en[4];
       bool sn[4];
-      int k = 0;
       {
         const int i = si[r] < 0 ? 0 : si[r];
         const int snd = sSnd[i];
@@ -493,21 +499,21 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
           if (sent && isGray) ++nGray;  // one RPC per relayed message, all dropped
           sn[c] = sent && !isGray;
           en[c] = (uint32_t)slot | ((uint32_t)i << 16);
-          k += sn[c];
         }
       }
-      int incl = k;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-      }
-      int p = qt + incl - k;
+      // c-major positions (delivery order does not matter: every update is
+      // a commutative LDS atomic)
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if (sn[c]) sQ[p++] = en[c];
-      qt += __shfl(incl, 63);
+      for (int c = 0; c < 4; ++c) {
+        const uint64_t m = __ballot(sn[c]);
+        if (sn[c]) sQ[qt + lane_rank(m)] = en[c];
+        qt += __popcll(m);
+      }
       __syncthreads();
       if (qt >= 64) {
+#ifdef GS_STAMPS
+        const long long tq0 = clock64();
+#endif
         while (qt - qh >= 64) {
           const uint32_t ent = sQ[qh + lane];
           deliver((int)(ent >> 16), (int)(ent & 0xFFFF));
@@ -520,6 +526,9 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
         qt -= qh;
         qh = 0;
         __syncthreads();
+#ifdef GS_STAMPS
+        accDel += clock64() - tq0;
+#endif
       }
     }
   }
@@ -595,12 +604,11 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   }
 #ifdef GS_STAMPS
   {
-    const long long tc = (long long)wave_sum_ll(nCopies), td = (long long)wave_sum_ll(nDeliv);
-    int mc = maxCopies;
-    for (int o = 32; o > 0; o >>= 1) mc = max(mc, __shfl_xor(mc, o));
+    const long long tc = (long long)wave_sum_ll(nCopies);
+    const long long mc = accDel;
     if ((blockIdx.x & 1023) == 0 && lane == 0) {
       d.stamps[(blockIdx.x >> 10) * 8 + 5] = tc;
-      d.stamps[(blockIdx.x >> 10) * 8 + 6] = td;
+      d.stamps[(blockIdx.x >> 10) * 8 + 6] = accLd;
       d.stamps[(blockIdx.x >> 10) * 8 + 7] = mc;
     }
   }
@@ -658,13 +666,9 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     const int w = lane + 64 * j;
     const uint64_t U = Uw[j];
     const int k = __popcll(U);
-    int incl = k;
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(incl, o);
-      if (lane >= o) incl += y;
-    }
+    const int incl = wave_incl_sum(k);
     int rank = running + incl - k;
-    running += __shfl(incl, 63);
+    running += wave_last(incl);
     if (U) {
       if ((U & Ow[j]) || !wm_has(amW, w)) set_err(d, E_LATE);
       d.seen[(int64_t)v * W + w] = Sw[j] | U;

@@ -122,13 +122,8 @@ __device__ __forceinline__ int item_sender(const int* sIt, int b, int& k) {
 
 // Exclusive prefix over the 64 lanes; *total gets the sum.
 __device__ __forceinline__ int lane_prefix(int x, int* total) {
-  const int lane = lane_id();
-  int incl = x;
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(incl, o);
-    if (lane >= o) incl += y;
-  }
-  *total = __shfl(incl, 63);
+  const int incl = wave_incl_sum(x);
+  *total = wave_last(incl);
   return incl - x;
 }
 
