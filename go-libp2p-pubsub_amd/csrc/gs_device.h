@@ -158,6 +158,17 @@ __device__ __forceinline__ void ctr_add(const Dev& d, int k, unsigned long long 
 __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
   return (uint64_t)__shfl((unsigned long long)v, src);
 }
+// Value of lane i for a wave-uniform i (v_readlane into a scalar register,
+// no LDS permute).
+__device__ __forceinline__ int lane_get(int x, int i) { return __builtin_amdgcn_readlane(x, i); }
+__device__ __forceinline__ uint64_t lane_get64(uint64_t x, int i) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, i);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), i);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ double lane_getf(double x, int i) {
+  return __longlong_as_double((long long)lane_get64((uint64_t)__double_as_longlong(x), i));
+}
 
 __device__ __forceinline__ int wave_sum_int(int v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -174,7 +185,7 @@ __device__ __forceinline__ bool select_k(bool cand, uint64_t key, int k) {
   while (m) {
     int j = __ffsll((long long)m) - 1;
     m &= m - 1;
-    uint64_t kj = shfl_u64(key, j);
+    uint64_t kj = lane_get64(key, j);
     if (kj < key || (kj == key && j < lane)) rank++;
   }
   return cand && rank < k;
@@ -356,7 +367,7 @@ __device__ __forceinline__ int64_t arena_write(const Dev& d, int buf, const uint
   if (total == 0) return -1;
   unsigned long long off = 0;
   if (lane == 0) off = atomicAdd(&d.poolCnt[buf], (unsigned long long)total);
-  off = __shfl(off, 0);
+  off = lane_get64(off, 0);
   if ((int64_t)(off + total) > d.poolCap) {
     if (lane == 0) set_err(d, E_POOL);
     return -1;

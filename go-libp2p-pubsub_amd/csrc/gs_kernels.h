@@ -695,9 +695,9 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
       while (lanesWith) {
         const int src = __ffsll((long long)lanesWith) - 1;
         lanesWith &= lanesWith - 1;
-        uint64_t y = shfl_u64(U, src);
+        uint64_t y = lane_get64(U, src);
         const int wsrc = src + 64 * j;
-        const int ixs = __shfl(ixw[j], src);
+        const int ixs = lane_get(ixw[j], src);
         while (y) {
           const int b = __ffsll((long long)y) - 1;
           y &= y - 1;

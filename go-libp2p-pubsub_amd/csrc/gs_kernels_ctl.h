@@ -30,7 +30,7 @@ __device__ __forceinline__ bool graft_one(const Dev& d, int64_t e, int v, int t,
     add_backoff(d, e, t, now, d.PruneBackoff);
     return true;
   }
-  const int mc = __shfl(meshcnt_lane, t);
+  const int mc = lane_get(meshcnt_lane, t);
   if (mc >= d.Dhi && !d.outbound[e]) {
     add_backoff(d, e, t, now, d.PruneBackoff);
     return true;
@@ -219,19 +219,19 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     while (m) {
       const int i = __ffsll((long long)m) - 1;
       m &= m - 1;
-      const int npre_i = __shfl(npre, i), hb_i = __shfl(hb, i);
+      const int npre_i = lane_get(npre, i), hb_i = lane_get(hb, i);
       if ((glmask >> i) & 1) {  // AcceptNone: the whole RPC is dropped
         cGray += npre_i + hb_i;
         continue;
       }
       const int64_t ei = base + i;
-      const uint64_t gJoin_i = shfl_u64(gJoin, i), gHb_i = shfl_u64(gHb, i);
-      const uint64_t pRep_i = shfl_u64(pRep, i), pHb_i = shfl_u64(pHb, i), ihaveT_i = shfl_u64(ihaveT, i);
-      const int64_t iwRec_i = (int64_t)shfl_u64((uint64_t)iwRec, i);
-      int ph_i = __shfl(ph, i);
-      const int ia_i = __shfl(ia, i);
-      double sc_i = __shfl(sc, i);
-      uint64_t mE = shfl_u64(meshE, i);
+      const uint64_t gJoin_i = lane_get64(gJoin, i), gHb_i = lane_get64(gHb, i);
+      const uint64_t pRep_i = lane_get64(pRep, i), pHb_i = lane_get64(pHb, i), ihaveT_i = lane_get64(ihaveT, i);
+      const int64_t iwRec_i = (int64_t)lane_get64((uint64_t)iwRec, i);
+      int ph_i = lane_get(ph, i);
+      const int ia_i = lane_get(ia, i);
+      double sc_i = lane_getf(sc, i);
+      uint64_t mE = lane_get64(meshE, i);
       bool dirty = false;
       uint64_t pOut = 0;
       int nR = 0;
@@ -606,7 +606,7 @@ __global__ __launch_bounds__(64) void k_hb_pre(Dev d, int64_t now, uint64_t tick
   int total = __popcll(bm);
   while (bm) {
     const int q = __ffsll((long long)bm) - 1;
-    const int pe = __shfl(edge, q);
+    const int pe = lane_get(edge, q);
     const unsigned long long same = __ballot(broken && edge == pe);
     bm &= ~same;
     if (lane == 0) {
@@ -750,8 +750,8 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
       while (mm) {
         const int j = __ffsll((long long)mm) - 1;
         mm &= mm - 1;
-        const double sj = __shfl(S, j);
-        const uint64_t kj = shfl_u64(k1, j);
+        const double sj = lane_getf(S, j);
+        const uint64_t kj = lane_get64(k1, j);
         if (sj > S || (sj == S && (kj < k1 || (kj == k1 && j < lane)))) rank1++;
       }
       const bool tail = m && rank1 >= d.Dscore;
@@ -761,7 +761,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
       while (mm) {
         const int j = __ffsll((long long)mm) - 1;
         mm &= mm - 1;
-        const uint64_t kj = shfl_u64(k2, j);
+        const uint64_t kj = lane_get64(k2, j);
         if (kj < k2 || (kj == k2 && j < lane)) rank2++;
       }
       const int pos = tail ? d.Dscore + rank2 : rank1;
@@ -832,11 +832,11 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
       while (mm) {
         const int j = __ffsll((long long)mm) - 1;
         mm &= mm - 1;
-        const double sj = __shfl(S, j);
+        const double sj = lane_getf(S, j);
         if (sj < S || (sj == S && j < lane)) rank++;
       }
       const unsigned long long ml = __ballot(m && rank == cnt / 2);
-      const double median = __shfl(S, __ffsll((long long)ml) - 1);
+      const double median = lane_getf(S, __ffsll((long long)ml) - 1);
       if (median < d.oppThr) {
         const bool bo = valid && d.backoff[tix(d, t, e)] != 0;
         const bool cand = inTopic && !m && !bo && !dir && S > median;
