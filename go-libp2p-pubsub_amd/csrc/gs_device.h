@@ -80,6 +80,7 @@ struct Dev {
   int32_t* fln[2]; // [N] list lengths
   int32_t FC;      // list capacity per node (multiple of 4)
   uint32_t stMagic; // ceil(2^32 / St): topic of slot s = umulhi(s, stMagic) (s < 2^16)
+  uint64_t tDivM;   // ceil(2^64 / T) (0 when T == 1): edge of pair p = umul64hi(p, tDivM)
   int32_t maxDeg;  // largest node degree (<= 64)
   uint64_t* oldm;  // [W] slots whose message is too old to be first-delivered this hop
   int32_t* nAuth;  // [N] live message slots authored by the node
@@ -103,7 +104,8 @@ struct Dev {
   double* score1;  // after the message phase (S1) / heartbeat memo
   uint8_t* sdirty; // [E] a score-lowering change (graft/prune/penalty/refresh) since score0
   int64_t* backoff;  // [T][E], 0 = none
-  double *fmd, *mmd, *mfp, *imd;  // tiled (tix)
+  double *fmd, *mmd, *mfp, *imd;  // per-(edge, topic) rows (tix)
+  int32_t anyImd;                 // 0: no invalid delivery ever recorded, imd is all 0 (P4 = 0)
   uint32_t* dlt;                  // tiled: deliveries not yet folded into fmd / mmd,
                                   // (+1s to fmd) | (+1s to mmd) << 16 (see eff_counters)
   int64_t *graftTime, *meshTime;  // [T][E]
@@ -142,9 +144,15 @@ struct Dev {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
-// index of (edge e, topic t) in the tiled per-(edge, topic) arrays
-__device__ __forceinline__ int64_t tix(const Dev& d, int t, int64_t e) {
-  return ((((e >> 6) * d.T) + t) << 6) | (e & 63);
+// Index of (edge e, topic t) in the per-(edge, topic) arrays: one row of T
+// topics per edge, so one edge's state is contiguous (a wave with lane =
+// topic reads it in full lines) and one node's in-edges are one contiguous
+// range [rowptr[v] * T, rowptr[v + 1] * T) of pairs.
+__device__ __forceinline__ int64_t tix(const Dev& d, int t, int64_t e) { return e * d.T + t; }
+// (edge, topic) of pair index p (exact for p < 2^58)
+__device__ __forceinline__ void pair_split(const Dev& d, int64_t p, int64_t& e, int& t) {
+  e = d.T == 1 ? p : (int64_t)__umul64hi((unsigned long long)p, (unsigned long long)d.tDivM);
+  t = (int)(p - e * d.T);
 }
 
 __device__ __forceinline__ void set_err(const Dev& d, int code) { atomicCAS(d.err, 0, code); }
@@ -219,29 +227,48 @@ __device__ __forceinline__ double eff_mmd(const TopicP& tp, double mmd, uint32_t
   return (q >> 16) ? add_ones_capped(mmd, (int)(q >> 16), tp.MmdCap) : mmd;
 }
 
-template <bool kEager>
-__device__ __forceinline__ double topic_term(const Dev& d, const TopicP& tp, int64_t i) {
-  const uint8_t fl = d.flags[i];
-  const uint32_t q = d.dlt[i];
-  const int64_t mt = (kEager || (fl & 1)) ? d.meshTime[i] : 0;
-  const double mm = eff_mmd(tp, (kEager || (fl & 2)) ? d.mmd[i] : 0.0, q);
-  const double fmd = eff_fmd(tp, d.fmd[i], q), mfp = d.mfp[i], im = d.imd[i];
+// One topic's contribution topicScore * TopicWeight (score.go:265-311) of
+// pair i, split into its loads (all issued at once) and its arithmetic.
+struct TermIn {
+  double fmd, mm, mfp, im;
+  int64_t mt;
+  uint32_t q;
+  uint8_t fl;
+};
+__device__ __forceinline__ TermIn term_load(const Dev& d, int64_t i) {
+  TermIn x;
+  x.fl = d.flags[i];
+  x.q = d.dlt[i];
+  x.mt = d.meshTime[i];
+  x.mm = d.mmd[i];
+  x.fmd = d.fmd[i];
+  x.mfp = d.mfp[i];
+  x.im = d.anyImd ? d.imd[i] : 0.0;
+  return x;
+}
+__device__ __forceinline__ double term_eval(const TopicP& tp, const TermIn& x) {
   double topicScore = 0.0;
-  if (fl & 1) {
-    double p1 = (double)(mt / tp.TimeInMeshQuantum);
+  if (x.fl & 1) {
+    double p1 = (double)(x.mt / tp.TimeInMeshQuantum);
     if (p1 > tp.TimeInMeshCap) p1 = tp.TimeInMeshCap;
     topicScore += p1 * tp.TimeInMeshWeight;
   }
-  topicScore += fmd * tp.FmdWeight;
-  if ((fl & 2) && mm < tp.MmdThreshold) {
-    const double deficit = tp.MmdThreshold - mm;
-    const double p3 = deficit * deficit;
-    topicScore += p3 * tp.MmdWeight;
+  topicScore += eff_fmd(tp, x.fmd, x.q) * tp.FmdWeight;
+  if (x.fl & 2) {
+    const double mm = eff_mmd(tp, x.mm, x.q);
+    if (mm < tp.MmdThreshold) {
+      const double deficit = tp.MmdThreshold - mm;
+      const double p3 = deficit * deficit;
+      topicScore += p3 * tp.MmdWeight;
+    }
   }
-  topicScore += mfp * tp.MfpWeight;
-  const double p4 = im * im;
+  topicScore += x.mfp * tp.MfpWeight;
+  const double p4 = x.im * x.im;
   topicScore += p4 * tp.ImdWeight;
   return topicScore * tp.TopicWeight;
+}
+__device__ __forceinline__ double topic_term(const Dev& d, const TopicP& tp, int64_t i) {
+  return term_eval(tp, term_load(d, i));
 }
 
 // The topic-independent tail of score(): cap, P5, P6, P7 (score.go:313-332).
@@ -258,20 +285,6 @@ __device__ __forceinline__ double score_tail(const Dev& d, int64_t e, double sco
   return score;
 }
 
-// peerScore.score — score.go:256-333, topics summed in ascending order.
-// Compiled with -ffp-contract=off: every product/sum rounds as in Go.
-__device__ __forceinline__ double edge_score(const Dev& d, int64_t e) {
-  if (!d.scoring) return 0.0;
-  double score = 0.0;
-#pragma unroll 4
-  for (int t = 0; t < d.T; ++t) {
-    const TopicP& tp = d.tp[t];
-    if (!tp.scored) continue;
-    score += topic_term<false>(d, tp, tix(d, t, e));
-  }
-  return score_tail(d, e, score);
-}
-
 // Score of ONE edge computed by the whole wave (e wave-uniform): lane t loads
 // topic t's state, so every load is in flight at once; the terms are then
 // added in ascending topic order exactly as edge_score does.  lds: 64 doubles.
@@ -279,7 +292,7 @@ __device__ __forceinline__ double edge_score_wave(const Dev& d, int64_t e, doubl
   if (!d.scoring) return 0.0;
   const int lane = lane_id();
   double term = 0.0;
-  if (lane < d.T && d.tp[lane].scored) term = topic_term<true>(d, d.tp[lane], tix(d, lane, e));
+  if (lane < d.T && d.tp[lane].scored) term = topic_term(d, d.tp[lane], tix(d, lane, e));
   __syncthreads();
   lds[lane] = term;
   __syncthreads();

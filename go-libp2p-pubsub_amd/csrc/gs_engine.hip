@@ -47,6 +47,7 @@ struct gs_engine {
   int H = 16;  // hops per heartbeat (or a nominal 16 for floodsub/randomsub)
   int64_t retireHops = 0;
   int64_t hopsSinceFold = 0, foldEvery = 1;  // pending-delivery fold cadence (dlt)
+  int64_t refreshedHop = -1;                 // hop of the last refreshScores (S0 exact after it)
   int maxAge = 0;
   // host graph / attributes
   std::vector<int64_t> rowptr;
@@ -311,6 +312,7 @@ int gs_engine::start() {
   }
   x.maxDeg = std::max(1, maxdeg);
   x.stMagic = (uint32_t)(((1ull << 32) + (uint64_t)St - 1) / (uint64_t)St);
+  x.tDivM = T == 1 ? 0 : ~0ull / (uint64_t)T + 1;  // ceil(2^64 / T)
   foldEvery = std::max<int64_t>(1, 65535 / (2 * (int64_t)St));  // a hop adds at most 2*St per (edge, topic)
   x.oldm = dalloc<uint64_t>(W); chk(x.oldm);
   x.nAuth = dalloc<int32_t>(N); chk(x.nAuth);
@@ -445,7 +447,8 @@ int gs_engine::stepOne() {
   HIPCHECK(hipMemsetAsync(d.pubmask[cur], 0, (size_t)W * 8, stream));
   HIPCHECK(hipMemsetAsync(d.poolCnt + cur, 0, 8, stream));
   const unsigned eb = nblk(E, 256);
-  if (scoring) TIMED(this, GS_K_SCORE, (k_score0<<<eb, 256, 0, stream>>>(d)));
+  const unsigned sgb = nblk(E, GS_SG), pb = nblk((int64_t)E * T, 256);
+  if (scoring) TIMED(this, GS_K_SCORE, (k_score_rows<1><<<sgb, 64, 0, stream>>>(d, nullptr)));
   if (h == 0 && gossip) TIMED(this, GS_K_JOIN, (k_join<<<N, 64, 0, stream>>>(d, h, now, cur)));
   if (gossip && !floodPublish && n > 0) {
     // Publish to a topic we have not joined: fanout (gossipsub.go:977-994)
@@ -505,22 +508,27 @@ int gs_engine::stepOne() {
     if (cfg.router == GS_ROUTER_RANDOMSUB) k_publish_rs<<<n, 64, 0, stream>>>(d, (int)b);
   }
   if (gossip) {
-    if (scoring) TIMED(this, GS_K_SCORE, (k_score1<<<eb, 256, 0, stream>>>(d)));
+    if (scoring) TIMED(this, GS_K_SCORE, (k_score_rows<2><<<sgb, 64, 0, stream>>>(d, nullptr)));
     TIMED(this, GS_K_PHASE_B,
           launch_wpl(W, [&](auto wpl) { k_phase_b<decltype(wpl)::value><<<N, 64, 0, stream>>>(d, h, now, cur, head); }));
   }
   if (refreshDue(now)) {
-    TIMED(this, GS_K_REFRESH, (k_refresh<<<eb, 256, 0, stream>>>(d, now)));
+    TIMED(this, GS_K_REFRESH, (k_refresh_rows<<<sgb, 64, 0, stream>>>(d, now)));
+    refreshedHop = h;
     hopsSinceFold = 0;
   } else if (scoring && ++hopsSinceFold >= foldEvery) {
     // pending delivery counts are 16-bit: fold them before they can overflow
-    k_fold<<<eb, 256, 0, stream>>>(d, -1);
+    k_fold_all<<<pb, 256, 0, stream>>>(d);
     hopsSinceFold = 0;
   }
   if (heartbeatDue(now)) {
     ticks++;
     TIMED(this, GS_K_HB_PRE, (k_hb_pre<<<N, 64, 0, stream>>>(d, now, ticks)));
-    if (scoring) TIMED(this, GS_K_SCORE, (k_score<<<eb, 256, 0, stream>>>(d, d.score1)));
+    // right after a refresh S0 holds exact scores: recompute only what hb_pre dirtied
+    if (scoring && refreshedHop == h)
+      TIMED(this, GS_K_SCORE, (k_score_rows<3><<<sgb, 64, 0, stream>>>(d, nullptr)));
+    else if (scoring)
+      TIMED(this, GS_K_SCORE, (k_score_rows<0><<<sgb, 64, 0, stream>>>(d, d.score1)));
     const int newhead = (head + R - 1) % R;
     TIMED(this, GS_K_HEARTBEAT, (k_heartbeat<<<N, 64, 0, stream>>>(d, h, now, ticks, cur, head, newhead)));
     head = newhead;
@@ -561,24 +569,20 @@ int gs_engine::checkDeviceError() {
   }
 }
 
-// Per-(edge, topic) arrays are tiled on the device (tix in gs_device.h);
-// readbacks return them topic-major [t*E + e].
+// Per-(edge, topic) arrays are edge-major rows [e*T + t] on the device (tix
+// in gs_device.h); readbacks return them topic-major [t*E + e].
 template <class X>
-static int copy_back_tiled(gs_engine* g, X* dst, const X* src) {
-  const size_t E = (size_t)g->E, T = (size_t)g->T, Ep = (E + 63) & ~(size_t)63;
+static int copy_back_pairs(gs_engine* g, X* dst, const X* src) {
+  const size_t E = (size_t)g->E, T = (size_t)g->T;
   if (!g->started) {
     std::memset(dst, 0, T * E * sizeof(X));
     return GS_OK;
   }
-  std::vector<X> tmp(T * Ep);
+  std::vector<X> tmp(T * E);
   HIPCHECK(hipStreamSynchronize(g->stream));
   HIPCHECK(hipMemcpy(tmp.data(), src, tmp.size() * sizeof(X), hipMemcpyDeviceToHost));
-  for (size_t b = 0; b < Ep / 64; ++b)
-    for (size_t t = 0; t < T; ++t) {
-      const X* row = tmp.data() + (b * T + t) * 64;
-      const size_t e0 = b * 64, n = std::min<size_t>(64, E - e0);
-      std::memcpy(dst + t * E + e0, row, n * sizeof(X));
-    }
+  for (size_t e = 0; e < E; ++e)
+    for (size_t t = 0; t < T; ++t) dst[t * E + e] = tmp[e * T + t];
   return GS_OK;
 }
 extern "C" {
@@ -853,7 +857,7 @@ int gs_read_counters(gs_engine* g, gs_counters* out) {
 int gs_read_scores(gs_engine* g, double* score) {
   if (!g->graphSet) { gs_set_error("graph not set"); return GS_ESTATE; }
   NEED_STARTED(g);
-  k_score<<<nblk(g->E, 256), 256, 0, g->stream>>>(g->d, g->dScoreTmp);
+  k_score_rows<0><<<nblk(g->E, GS_SG), 64, 0, g->stream>>>(g->d, g->dScoreTmp);
   HIPCHECK(hipMemcpyAsync(score, g->dScoreTmp, g->E * 8, hipMemcpyDeviceToHost, g->stream));
   HIPCHECK(hipStreamSynchronize(g->stream));
   return GS_OK;
@@ -871,18 +875,18 @@ static int copy_back(gs_engine* g, void* dst, const void* src, size_t bytes) {
 
 int gs_read_mesh(gs_engine* g, uint64_t* mesh) { return copy_back(g, mesh, g->d.mesh, g->E * 8); }
 int gs_read_fanout(gs_engine* g, uint64_t* fanout) { return copy_back(g, fanout, g->d.fanout, g->E * 8); }
-int gs_read_backoff(gs_engine* g, int64_t* expire) { return copy_back_tiled(g, expire, g->d.backoff); }
+int gs_read_backoff(gs_engine* g, int64_t* expire) { return copy_back_pairs(g, expire, g->d.backoff); }
 int gs_read_topic_stats(gs_engine* g, double* fmd, double* mmd, double* mfp, double* imd, int64_t* mesh_time,
                         int64_t* graft_time, uint8_t* flags) {
   int rc;
-  if (g->started && g->scoring) k_fold<<<nblk(g->E, 256), 256, 0, g->stream>>>(g->d, -1);
-  if ((rc = copy_back_tiled(g, fmd, g->d.fmd))) return rc;
-  if ((rc = copy_back_tiled(g, mmd, g->d.mmd))) return rc;
-  if ((rc = copy_back_tiled(g, mfp, g->d.mfp))) return rc;
-  if ((rc = copy_back_tiled(g, imd, g->d.imd))) return rc;
-  if ((rc = copy_back_tiled(g, mesh_time, (const int64_t*)g->d.meshTime))) return rc;
-  if ((rc = copy_back_tiled(g, graft_time, (const int64_t*)g->d.graftTime))) return rc;
-  return copy_back_tiled(g, flags, (const uint8_t*)g->d.flags);
+  if (g->started && g->scoring) k_fold_all<<<nblk((int64_t)g->E * g->T, 256), 256, 0, g->stream>>>(g->d);
+  if ((rc = copy_back_pairs(g, fmd, g->d.fmd))) return rc;
+  if ((rc = copy_back_pairs(g, mmd, g->d.mmd))) return rc;
+  if ((rc = copy_back_pairs(g, mfp, g->d.mfp))) return rc;
+  if ((rc = copy_back_pairs(g, imd, g->d.imd))) return rc;
+  if ((rc = copy_back_pairs(g, mesh_time, (const int64_t*)g->d.meshTime))) return rc;
+  if ((rc = copy_back_pairs(g, graft_time, (const int64_t*)g->d.graftTime))) return rc;
+  return copy_back_pairs(g, flags, (const uint8_t*)g->d.flags);
 }
 int gs_read_behaviour_penalty(gs_engine* g, double* bp) { return copy_back(g, bp, g->d.bp, g->E * 8); }
 

@@ -1,8 +1,8 @@
 // gs_kernels.h — HIP kernels of the gossip engine (gfx950, wave64).
 //
 // Kernel map (one hop):
-//   k_score        thread/edge   peerScore.score            score.go:256-333
-//   k_refresh      thread/edge   refreshScores              score.go:495-556
+//   k_score_rows   wave/32 edges peerScore.score (+ memos)  score.go:256-333
+//   k_refresh_rows wave/32 edges refreshScores (+ exact S0) score.go:495-556
 //   k_join         wave/node     Join at hop 0              gossipsub.go:1011-1060
 //   k_fanout_pub   wave/pair     Publish fanout creation    gossipsub.go:977-994
 //   k_fwd          thread/edge   forwarding-target snapshot gossipsub.go:953-999, floodsub.go:85, randomsub.go:115
@@ -22,89 +22,203 @@
 #include "gs_device.h"
 
 // ---------------------------------------------------------------- score
-__global__ void k_score(Dev d, double* __restrict__ out) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= d.E) return;
-  out[e] = edge_score(d, e);
+// peerScore.score (score.go:256-333) of a group of GS_SG consecutive edges per
+// wave.  Lane = topic: the topic terms of one edge are one contiguous row of
+// each state array (full lines); terms go to LDS and lane j then adds edge j's
+// terms in ascending topic order, exactly as the reference's loop does.
+// Only the edges that need it are computed, so a sparse recompute costs the
+// rows it touches, not the whole table.
+//   MODE 0: every edge -> out
+//   MODE 1: memo S0.  Every consumer of S0 only asks "score >= threshold" for
+//     thresholds <= PublishThreshold (AcceptFrom graylist, publish / fanout
+//     filters; thresholds are <= 0 by validation, score_params.go:34-51), and
+//     between two recomputations the score can only rise unless a graft,
+//     prune, penalty or refresh touched the edge (message deliveries raise P2
+//     and lower the P3 deficit; FirstMessageDeliveriesWeight >= 0 and
+//     MeshMessageDeliveriesWeight <= 0 by validation).  So a memo that is
+//     >= PublishThreshold and not dirty gives the same decisions as the exact
+//     score; everything else is recomputed exactly.
+//   MODE 2: memo S1 for HandleRPC (after the message phase): its decisions
+//     compare with 0 and GossipThreshold (<= 0), and only deliveries happened
+//     since S0, so a non-negative S0 decides exactly like the exact score.
+//   MODE 3: every edge exact -> score1, right after k_refresh_rows left exact
+//     scores in S0: only the edges dirtied since (penalties) are recomputed.
+#define GS_SG 16  // edges per wave
+#define GS_SB 8   // edges per load batch
+template <int MODE>
+__global__ __launch_bounds__(64) void k_score_rows(Dev d, double* __restrict__ out) {
+  __shared__ double sT[GS_SG * 65];  // [edge][topic], row stride 65: conflict-free column reads
+  const int lane = lane_id();
+  const int64_t e0 = (int64_t)blockIdx.x * GS_SG;
+  const int64_t e = e0 + lane;
+  const bool in = lane < GS_SG && e < d.E;
+  double s0 = 0.0;
+  bool need = false;
+  if (in) {
+    if (MODE == 0) {
+      need = true;
+    } else {
+      s0 = d.score0[e];
+      need = MODE == 1 ? (d.sdirty[e] != 0 || !(s0 >= d.publishThr))
+                       : MODE == 2 ? !(s0 >= 0.0) : d.sdirty[e] != 0;
+    }
+  }
+  if (!d.scoring) {
+    if (in) {
+      if (MODE == 0) out[e] = 0.0;
+      if (MODE == 1) { d.score0[e] = 0.0; d.sdirty[e] = 0; }
+      if (MODE >= 2) d.score1[e] = 0.0;
+    }
+    return;
+  }
+  if (MODE >= 2 && in && !need) d.score1[e] = s0;
+  unsigned long long m = __ballot(need);
+  if (!m) return;
+  const int T = d.T;
+  const int tl = lane < T ? lane : 0;
+  const bool scoredL = lane < T && d.tp[tl].scored;
+  const uint64_t scoredT = __ballot(scoredL);
+  while (m) {
+    // GS_SB edges per batch: every load of the batch in flight at once
+    int js[GS_SB];
+#pragma unroll
+    for (int k = 0; k < GS_SB; ++k) {
+      js[k] = m ? __ffsll((long long)m) - 1 : -1;
+      m &= m - 1;
+    }
+    TermIn x[GS_SB];
+#pragma unroll
+    for (int k = 0; k < GS_SB; ++k) x[k] = term_load(d, (e0 + (js[k] < 0 ? js[0] : js[k])) * T + tl);
+#pragma unroll
+    for (int k = 0; k < GS_SB; ++k)
+      if (js[k] >= 0) sT[js[k] * 65 + lane] = scoredL ? term_eval(d.tp[tl], x[k]) : 0.0;
+  }
+  __syncthreads();
+  if (lane < GS_SG && need) {
+    double score = 0.0;
+    for (int t = 0; t < T; ++t)
+      if ((scoredT >> t) & 1) score += sT[lane * 65 + t];
+    score = score_tail(d, e, score);
+    if (MODE == 0) out[e] = score;
+    if (MODE == 1 || MODE == 3) { d.score0[e] = score; d.sdirty[e] = 0; }
+    if (MODE >= 2) d.score1[e] = score;
+  }
 }
 
-// Hop-start memo S0.  Every consumer of S0 only asks "score >= threshold" for
-// thresholds <= PublishThreshold (AcceptFrom graylist, publish / fanout
-// filters; thresholds are <= 0 by validation, score_params.go:34-51), and
-// between two recomputations the score can only rise unless a graft, prune,
-// penalty or refresh touched the edge (message deliveries raise P2 and lower
-// the P3 deficit; FirstMessageDeliveriesWeight >= 0 and MeshMessageDeliveries-
-// Weight <= 0 by validation).  So a memo that is >= PublishThreshold and not
-// dirty gives the same decisions as the exact score; everything else is
-// recomputed exactly.
-__global__ void k_score0(Dev d) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= d.E) return;
-  const double s = d.score0[e];
-  if (d.sdirty[e] || !(s >= d.publishThr)) {
-    d.score0[e] = edge_score(d, e);
+// refreshScores — score.go:495-556 (every peer is connected: no retention
+// path), GS_SG edges per wave, lane = topic, and the exact score of every
+// edge from the refreshed state into S0 (sdirty cleared): nothing but
+// refreshScores changed the state since the hop's message phase, so this is
+// the value the next S0 pass would compute.
+__global__ __launch_bounds__(64) void k_refresh_rows(Dev d, int64_t now) {
+  __shared__ double sT[GS_SG * 65];
+  const int lane = lane_id();
+  const int64_t e0 = (int64_t)blockIdx.x * GS_SG;
+  const int ng = (int)min((int64_t)GS_SG, d.E - e0);
+  const int T = d.T;
+  const int tl = lane < T ? lane : 0;
+  const TopicP& tp = d.tp[tl];
+  const bool act = lane < T && tp.scored;
+  const uint64_t scoredT = __ballot(act);
+  for (int j0 = 0; j0 < ng; j0 += GS_SB) {
+    uint32_t q[GS_SB];
+    double fmd[GS_SB], mmd[GS_SB], mfp[GS_SB], imd[GS_SB];
+    int64_t gt[GS_SB];
+    uint8_t fl[GS_SB];
+#pragma unroll
+    for (int k = 0; k < GS_SB; ++k) {
+      const int64_t i = (e0 + min(j0 + k, ng - 1)) * T + tl;
+      q[k] = d.dlt[i];
+      fmd[k] = d.fmd[i];
+      mmd[k] = d.mmd[i];
+      mfp[k] = d.mfp[i];
+      imd[k] = d.anyImd ? d.imd[i] : 0.0;
+      gt[k] = d.graftTime[i];
+      fl[k] = d.flags[i];
+    }
+#pragma unroll
+    for (int k = 0; k < GS_SB; ++k) {
+      if (j0 + k >= ng) break;
+      const int64_t i = (e0 + j0 + k) * T + tl;
+      double term = 0.0;
+      if (act) {
+        TermIn x;
+        x.q = 0;
+        double v = eff_fmd(tp, fmd[k], q[k]) * tp.FmdDecay;
+        if (v < d.DecayToZero) v = 0;
+        x.fmd = v;
+        v = eff_mmd(tp, mmd[k], q[k]) * tp.MmdDecay;
+        if (v < d.DecayToZero) v = 0;
+        x.mm = v;
+        v = mfp[k] * tp.MfpDecay;
+        if (v < d.DecayToZero) v = 0;
+        x.mfp = v;
+        v = imd[k] * tp.ImdDecay;
+        if (v < d.DecayToZero) v = 0;
+        x.im = v;
+        x.fl = fl[k];
+        x.mt = 0;
+        if (q[k]) d.dlt[i] = 0;
+        d.fmd[i] = x.fmd;
+        d.mmd[i] = x.mm;
+        d.mfp[i] = x.mfp;
+        if (d.anyImd) d.imd[i] = x.im;
+        if (x.fl & 1) {
+          x.mt = now - gt[k];
+          d.meshTime[i] = x.mt;
+          if (x.mt > tp.MmdActivation) {
+            x.fl |= 2;
+            d.flags[i] = x.fl;
+          }
+        }
+        term = term_eval(tp, x);
+      }
+      sT[(j0 + k) * 65 + lane] = term;
+    }
+  }
+  __syncthreads();
+  if (lane < ng) {
+    const int64_t e = e0 + lane;
+    double b = d.bp[e] * d.BPDecay;
+    if (b < d.DecayToZero) b = 0;
+    d.bp[e] = b;
+    double score = 0.0;
+    if (d.scoring) {
+      for (int t = 0; t < T; ++t)
+        if ((scoredT >> t) & 1) score += sT[lane * 65 + t];
+      score = score_tail(d, e, score);
+    }
+    d.score0[e] = score;
     d.sdirty[e] = 0;
   }
 }
 
-// Memo S1 for HandleRPC (after the message phase): its decisions compare with
-// 0 and GossipThreshold (<= 0), and only deliveries happened since S0, so a
-// non-negative S0 decides exactly like the exact score.
-__global__ void k_score1(Dev d) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= d.E) return;
-  const double s = d.score0[e];
-  d.score1[e] = s >= 0.0 ? s : edge_score(d, e);
+// Folds the pending deliveries of every pair into fmd / mmd.
+__global__ void k_fold_all(Dev d) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= d.E * d.T) return;
+  const uint32_t q = d.dlt[p];
+  if (!q) return;
+  int64_t e;
+  int t;
+  pair_split(d, p, e, t);
+  const TopicP& tp = d.tp[t];
+  d.fmd[p] = eff_fmd(tp, d.fmd[p], q);
+  d.mmd[p] = eff_mmd(tp, d.mmd[p], q);
+  d.dlt[p] = 0;
 }
 
-// refreshScores — score.go:495-556 (every peer is connected: no retention path)
-__global__ void k_refresh(Dev d, int64_t now) {
+// Folds the pending deliveries of topic t into fmd / mmd.
+__global__ void k_fold(Dev d, int t) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= d.E) return;
-  for (int t = 0; t < d.T; ++t) {
-    const TopicP& tp = d.tp[t];
-    if (!tp.scored) continue;
-    const int64_t i = tix(d, t, e);
-    const uint32_t q = d.dlt[i];
-    if (q) d.dlt[i] = 0;
-    double x = eff_fmd(tp, d.fmd[i], q) * tp.FmdDecay;
-    if (x < d.DecayToZero) x = 0;
-    d.fmd[i] = x;
-    x = eff_mmd(tp, d.mmd[i], q) * tp.MmdDecay;
-    if (x < d.DecayToZero) x = 0;
-    d.mmd[i] = x;
-    x = d.mfp[i] * tp.MfpDecay;
-    if (x < d.DecayToZero) x = 0;
-    d.mfp[i] = x;
-    x = d.imd[i] * tp.ImdDecay;
-    if (x < d.DecayToZero) x = 0;
-    d.imd[i] = x;
-    const uint8_t fl = d.flags[i];
-    if (fl & 1) {
-      const int64_t mt = now - d.graftTime[i];
-      d.meshTime[i] = mt;
-      if (mt > tp.MmdActivation) d.flags[i] = fl | 2;
-    }
-  }
-  double b = d.bp[e] * d.BPDecay;
-  if (b < d.DecayToZero) b = 0;
-  d.bp[e] = b;
-  d.sdirty[e] = 1;
-}
-
-// Folds the pending deliveries of topic t (t < 0: every topic) into fmd / mmd.
-__global__ void k_fold(Dev d, int t0) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= d.E) return;
-  for (int t = t0 < 0 ? 0 : t0; t < (t0 < 0 ? d.T : t0 + 1); ++t) {
-    const int64_t i = tix(d, t, e);
-    const uint32_t q = d.dlt[i];
-    if (!q) continue;
-    const TopicP& tp = d.tp[t];
-    d.fmd[i] = eff_fmd(tp, d.fmd[i], q);
-    d.mmd[i] = eff_mmd(tp, d.mmd[i], q);
-    d.dlt[i] = 0;
-  }
+  const int64_t i = tix(d, t, e);
+  const uint32_t q = d.dlt[i];
+  if (!q) return;
+  const TopicP& tp = d.tp[t];
+  d.fmd[i] = eff_fmd(tp, d.fmd[i], q);
+  d.mmd[i] = eff_mmd(tp, d.mmd[i], q);
+  d.dlt[i] = 0;
 }
 
 // SetTopicScoreParams recap — score.go:215-229
@@ -322,10 +436,10 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
                                                 int nR) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
   const int nCnt = (d.T * d.maxDeg + 3) & ~3;
-  uint32_t* scnt = smem32;                                // [T][MD] copies | fresh << 16
+  uint32_t* scnt = smem32;                                // [MD][T] copies | fresh << 16
   uint64_t* sD = (uint64_t*)(smem32 + nCnt);              // [nR] delivered slots (non-graylisted)
   uint8_t* sFirst = (uint8_t*)(sD + nR);                  // [nR * 64] lowest deliverer
-  uint32_t* sUnc = (uint32_t*)(sFirst + nR * 64);         // [T][MD] uncredited duplicates (needAge)
+  uint32_t* sUnc = (uint32_t*)(sFirst + nR * 64);         // [MD][T] uncredited duplicates (needAge)
   __shared__ int sBlk[64];        // first list block of each sender
   __shared__ uint64_t sRelay[64], sPub[64];
   __shared__ int sSnd[64];        // sender node | jr << 24 | graylisted << 31
@@ -337,7 +451,6 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   const int prv = cur ^ 1;
   const int W = d.W;
   const int T = d.T;
-  const int MD = d.maxDeg;
   const int FC = d.FC;
   const int64_t base = d.rowptr[v];
   const int deg = (int)(d.rowptr[v + 1] - base);
@@ -395,12 +508,14 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   GS_STAMP(1);
 
   int nSent = 0, nGray = 0;
+  long long nCopies = 0;  // delivered copies (non-graylisted)
   // One delivered copy of `slot` from sender i (sent, not graylisted).
   auto deliver = [&](int i, int slot) {
     const int w = slot >> 6;
     const int t = (int)__umulhi((unsigned)slot, d.stMagic);
 #ifndef GS_EXP_NOADD
-    atomicAdd(&scnt[t * MD + i], 1u);
+    atomicAdd(&scnt[i * T + t], 1u);
+    ++nCopies;
 #endif
     const int rk = sRk[w];
     if (d.needAge || rk == 0xFFFF) {
@@ -409,7 +524,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
       // first delivered before this hop is credited only within the window
       if (had && d.needAge) {
         const int64_t firstHop = d.slotPubHop[slot] + d.age[(int64_t)v * d.S + slot];
-        if ((h - firstHop) * d.hop_ns > d.tp[t].MmdWindow) atomicAdd(&sUnc[t * MD + i], 1u);
+        if ((h - firstHop) * d.hop_ns > d.tp[t].MmdWindow) atomicAdd(&sUnc[i * T + t], 1u);
       }
       if (rk == 0xFFFF) {
         // outside the window only an old duplicate is possible; a first
@@ -549,6 +664,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   // loads of the pass are issued before its first store (on gfx9 a load's
   // wait also waits for every older store).
   uint32_t* Lv = d.fl[cur] + (int64_t)v * FC;
+  if (scoring) sRelay[lane] = valid ? d.mesh[base + lane] : 0ull;  // pass 3: in-edge mesh words
   long long nDeliv = 0;
   uint64_t Uw[WPL], Sw[WPL], Hw[WPL], Ow[WPL];
   int ixw[WPL];
@@ -584,7 +700,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
       while (y) {
         const int b = __ffsll((long long)y) - 1;
         y &= y - 1;
-        atomicAdd(&scnt[t * MD + sFirst[ixw[j] + b]], 1u << 16);
+        atomicAdd(&scnt[sFirst[ixw[j] + b] * T + t], 1u << 16);
       }
     }
   }
@@ -595,17 +711,10 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   // scored topic is the edge's mesh bit (tracer.Graft / tracer.Prune accompany
   // every mesh change).  Batches of 8 topics, the next batch's loads issued
   // before this batch's stores.
-  long long nCopies = 0;
-  int maxCopies = 0;
-  for (int t = 0; t < T; ++t) {
-    const int cc = valid ? (int)(scnt[t * MD + lane] & 0xFFFF) : 0;
-    nCopies += cc;
-    maxCopies = cc > maxCopies ? cc : maxCopies;
-  }
 #ifdef GS_STAMPS
   {
     const long long tc = (long long)wave_sum_ll(nCopies);
-    const long long mc = accDel;
+    const long long mc = accDel;  // delivery-drain cycles
     if ((blockIdx.x & 1023) == 0 && lane == 0) {
       d.stamps[(blockIdx.x >> 10) * 8 + 5] = tc;
       d.stamps[(blockIdx.x >> 10) * 8 + 6] = accLd;
@@ -613,49 +722,51 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     }
   }
 #endif
-  if (scoring && valid) {
-    const uint64_t meshE = d.mesh[base + lane];
-    const int64_t e0 = base + lane;
-    // The counts go to the pending-delivery words dlt (eff_counters): one
-    // coalesced, branch-free read-modify-write per topic and in-edge, so every
-    // load and store is counted exactly by the compiler (no full-queue drains)
-    // and the next 16 topics' loads are in flight before this batch's stores.
-    // All loads of a batch of BS topics are issued before its first store
-    // (BS = 64 when T > 16: one round trip for the usual topic counts).
-    // tiled words of in-edge e0: topic t at p0[64 t]
-    uint32_t* const p0 = d.dlt + ((((e0 >> 6) * T) << 6) | (e0 & 63));
-    auto upd = [&](int t, uint32_t q) -> uint32_t {
-      const uint32_t c = ((scoredT >> t) & 1) ? scnt[t * MD + lane] : 0u;
+  if (scoring) {
+    // The counts go to the pending-delivery words dlt (eff_counters).  v's
+    // in-edges own the contiguous pairs [base*T, (base+deg)*T), pair index
+    // pl = i*T + t (== the scnt index): lane l takes pairs l, l+64, ... — one
+    // coalesced, branch-free read-modify-write per pair, every load of a batch
+    // issued before its first store (no full-queue drains).
+    const int nP = deg * T;
+    uint32_t* const pv = d.dlt + base * T;
+    uint32_t* const scr = (uint32_t*)(d.pad + ((int64_t)(blockIdx.x & 255) * 64 + lane) * 2);
+    const int q64 = 64 / T, r64 = 64 - q64 * T;
+    int ic = lane / T, tc = lane - (lane / T) * T;  // (in-edge, topic) of the lane's next pair
+    auto upd = [&](int pl, int i, int t, uint32_t q) -> uint32_t {
+      const uint32_t c = ((scoredT >> t) & 1) ? scnt[pl] : 0u;
       const int copies = (int)(c & 0xFFFF), nf = (int)(c >> 16);
       int credited = copies - nf;
-      if (d.needAge) credited -= (int)sUnc[t * MD + lane];
-      const uint32_t addM = ((meshE >> t) & 1) ? (uint32_t)(nf + credited) : 0u;
+      if (d.needAge) credited -= (int)sUnc[pl];
+      const uint32_t addM = ((sRelay[i] >> t) & 1) ? (uint32_t)(nf + credited) : 0u;
       if ((q & 0xFFFF) + nf > 0xFFFF || (q >> 16) + addM > 0xFFFF) set_err(d, E_DELTA);
       return q + (uint32_t)nf + (addM << 16);
     };
     auto rmw = [&](auto bsC) {
       constexpr int BS = decltype(bsC)::value;
       uint32_t q[BS];
-      int t0 = 0;
-      for (; t0 + BS <= T; t0 += BS) {
-        uint32_t* p = p0 + ((int64_t)t0 << 6);
-#pragma unroll
-        for (int kk = 0; kk < BS; ++kk) q[kk] = p[kk << 6];
-#pragma unroll
-        for (int kk = 0; kk < BS; ++kk) p[kk << 6] = upd(t0 + kk, q[kk]);
-      }
-      if (t0 < T) {  // the last T % BS topics; the rest of the batch goes to this lane's scratch word
-        uint32_t* const scr = (uint32_t*)(d.pad + ((int64_t)(blockIdx.x & 255) * 64 + lane) * 2);
-#pragma unroll
-        for (int kk = 0; kk < BS; ++kk) q[kk] = p0[(int64_t)min(t0 + kk, T - 1) << 6];
+      int iv[BS], tv[BS];
+      for (int k0 = 0; 64 * k0 < nP; k0 += BS) {
 #pragma unroll
         for (int kk = 0; kk < BS; ++kk) {
-          const uint32_t nq = upd(min(t0 + kk, T - 1), q[kk]);
-          *(t0 + kk < T ? p0 + ((int64_t)(t0 + kk) << 6) : scr) = nq;
+          const int pl = lane + 64 * (k0 + kk);
+          q[kk] = pv[pl < nP ? pl : nP - 1];
+          iv[kk] = ic;
+          tv[kk] = tc;
+          ic += q64;
+          tc += r64;
+          if (tc >= T) { tc -= T; ++ic; }
+        }
+#pragma unroll
+        for (int kk = 0; kk < BS; ++kk) {
+          const int pl = lane + 64 * (k0 + kk);
+          const bool ok = pl < nP;
+          const uint32_t nq = upd(ok ? pl : 0, ok ? iv[kk] : 0, ok ? tv[kk] : 0, q[kk]);
+          *(ok ? pv + pl : scr) = nq;
         }
       }
     };
-    if (T > 16) rmw(std::integral_constant<int, 64>{});
+    if (nP > 16 * 64) rmw(std::integral_constant<int, 32>{});
     else rmw(std::integral_constant<int, 16>{});
   }
   // ---- pass 2b: the stores of the first deliveries (after pass 3's loads,

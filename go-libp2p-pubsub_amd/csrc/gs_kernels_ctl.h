@@ -575,12 +575,11 @@ __global__ __launch_bounds__(64) void k_hb_pre(Dev d, int64_t now, uint64_t tick
   if (valid) {
     d.peerhave[e] = 0;
     d.iasked[e] = 0;
-    if (ticks % 15 == 0) {
-      for (int t = 0; t < d.T; ++t) {
-        const int64_t i = tix(d, t, e);
-        const int64_t be = d.backoff[i];
-        if (be != 0 && be + 2000000000LL < now) d.backoff[i] = 0;
-      }
+  }
+  if (ticks % 15 == 0) {  // v's in-edges own the contiguous pairs [base*T, (base+deg)*T)
+    for (int64_t i = base * d.T + lane; i < (base + deg) * d.T; i += 64) {
+      const int64_t be = d.backoff[i];
+      if (be != 0 && be + 2000000000LL < now) d.backoff[i] = 0;
     }
   }
   if (!d.scoring) return;
