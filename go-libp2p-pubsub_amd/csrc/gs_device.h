@@ -272,6 +272,17 @@ __device__ __forceinline__ double topic_term(const Dev& d, const TopicP& tp, int
 }
 
 // The topic-independent tail of score(): cap, P5, P6, P7 (score.go:313-332).
+__device__ __forceinline__ double score_tail_v(const Dev& d, double score, double app, double p6, double b) {
+  if (d.TopicScoreCap > 0 && score > d.TopicScoreCap) score = d.TopicScoreCap;
+  score += app * d.AppW;
+  score += p6 * d.IPW;
+  if (b > d.BPThr) {
+    const double excess = b - d.BPThr;
+    const double p7 = excess * excess;
+    score += p7 * d.BPW;
+  }
+  return score;
+}
 __device__ __forceinline__ double score_tail(const Dev& d, int64_t e, double score) {
   if (d.TopicScoreCap > 0 && score > d.TopicScoreCap) score = d.TopicScoreCap;
   score += d.app[d.col[e]] * d.AppW;
@@ -291,15 +302,20 @@ __device__ __forceinline__ double score_tail(const Dev& d, int64_t e, double sco
 __device__ __forceinline__ double edge_score_wave(const Dev& d, int64_t e, double* lds) {
   if (!d.scoring) return 0.0;
   const int lane = lane_id();
-  double term = 0.0;
-  if (lane < d.T && d.tp[lane].scored) term = topic_term(d, d.tp[lane], tix(d, lane, e));
+  const int tl = lane < d.T ? lane : 0;
+  const bool sc = lane < d.T && d.tp[tl].scored;
+  const uint64_t scoredT = __ballot(sc);
+  // every load of the score at once: the row of the edge and the tail inputs
+  const TermIn x = term_load(d, tix(d, tl, e));
+  const double app = d.app[d.col[e]], p6 = d.p6[e], b = d.bp[e];
+  const double term = sc ? term_eval(d.tp[tl], x) : 0.0;
   __syncthreads();
   lds[lane] = term;
   __syncthreads();
   double score = 0.0;
   for (int t = 0; t < d.T; ++t)
-    if (d.tp[t].scored) score += lds[t];
-  return score_tail(d, e, score);
+    if ((scoredT >> t) & 1) score += lds[t];
+  return score_tail_v(d, score, app, p6, b);
 }
 
 // peerScore.Graft — score.go:640-658 (scored topics only)

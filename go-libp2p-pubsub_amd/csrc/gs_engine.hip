@@ -356,7 +356,7 @@ int gs_engine::start() {
   x.slotSrc = dalloc<int32_t>(S, 0xFF); x.slotPubHop = dalloc<int64_t>(S); x.slotMid = dalloc<int64_t>(S, 0xFF);
   chk(x.slotSrc); chk(x.slotPubHop); chk(x.slotMid);
 #ifdef GS_STAMPS
-  x.stamps = dalloc<unsigned long long>((size_t)(N / 1024 + 1) * 8);
+  x.stamps = dalloc<unsigned long long>((size_t)(N / 1024 + 1) * 16);  // phase A | phase B
 #endif
   x.pad = dalloc<double>(256 * 64 * 2); chk(x.pad);
   x.ctr = dalloc<unsigned long long>((size_t)C_NCOUNTERS * GS_CTR_SPREAD); x.err = dalloc<int32_t>(1);

@@ -403,9 +403,17 @@ __device__ __forceinline__ int wave_min_int(int x) {
   do {                                                                                         \
     if ((blockIdx.x & 1023) == 0 && lane == 0) d.stamps[(blockIdx.x >> 10) * 8 + (k)] = clock64(); \
   } while (0)
+#define GS_STAMPB(k)                                                                           \
+  do {                                                                                         \
+    if ((blockIdx.x & 1023) == 0 && lane == 0)                                                 \
+      d.stamps[((int64_t)d.N / 1024 + 1) * 8 + (blockIdx.x >> 10) * 8 + (k)] = clock64();      \
+  } while (0)
 #else
 #define GS_STAMP(k) \
   do {              \
+  } while (0)
+#define GS_STAMPB(k) \
+  do {               \
   } while (0)
 #endif
 

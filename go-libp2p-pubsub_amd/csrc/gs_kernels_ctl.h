@@ -9,7 +9,7 @@
 // Scalar (wave-uniform) code; meshcnt is held by lane t.  Returns true when a
 // PRUNE for t must be sent back.
 __device__ __forceinline__ bool graft_one(const Dev& d, int64_t e, int v, int t, double sc, int64_t now,
-                                          int& meshcnt_lane, uint64_t& meshE, bool& dirty) {
+                                          int& meshcnt_lane, uint64_t& meshE, bool& dirty, bool& dirtyUp) {
   if (!((d.sub[v] >> t) & 1)) return false;  // unknown topic: ignore
   if ((meshE >> t) & 1) return false;         // already in mesh
   if (d.direct[e]) return true;
@@ -36,7 +36,7 @@ __device__ __forceinline__ bool graft_one(const Dev& d, int64_t e, int v, int t,
     return true;
   }
   stats_graft(d, e, t, now);
-  dirty = true;
+  dirtyUp = true;  // a graft never lowers the score (P1 = 0 at meshTime 0, P3 switched off)
   meshE |= 1ull << t;
   if (lane_id() == t) meshcnt_lane++;
   return false;
@@ -160,6 +160,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
   __shared__ long long sMid[64];
   __shared__ int sSlot[64];
   __shared__ unsigned long long sBase;
+  __shared__ uint32_t sHas[64 * 64 / 32];  // step 3: items with a want (<= 64 senders x 64 topics)
   const int v = blockIdx.x;
   const int lane = lane_id();
   const int prv = cur ^ 1;
@@ -203,27 +204,41 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     }
   }
   const unsigned long long glmask = __ballot(gl);
+  GS_STAMPB(0);
   // lane t: current mesh size of topic t
   int meshcnt = 0;
   for (int t = 0; t < d.T; ++t) {
     const int c = __popcll(__ballot((meshE >> t) & 1));
     if (lane == t) meshcnt = c;
   }
-  // ---- step 1: order-dependent control, senders ascending
+  // ---- step 1: order-dependent control, senders ascending.  Only GRAFTs and
+  // PRUNEs depend on the order (the running mesh size, backoff, the live
+  // score); a sender whose RPCs carry neither is handled in its own lane.
   bool gateIWant = false, gateIHave = false, prunesHb = false;
   uint64_t pruneOut = 0;
   int nRep1 = 0;
   long long cPrunes = 0, cGray = 0;
+  const bool heavy = ctl && !gl && (gJoin | gHb | pRep | pHb) != 0;
+  if (ctl && gl) cGray = npre + hb;  // AcceptNone: the whole RPC is dropped
+  if (ctl && !gl && !heavy) {
+    // (2) reply RPCs (IWANT requests), (3) heartbeat RPC (IHAVE)
+    if (npre > 0) {
+      const bool gossipOK = sc >= d.gossipThr;
+      if (gossipOK) ph += npre;
+      gateIWant = gossipOK && iwRec >= 0;  // handleIWant (gossipsub.go:674-711): step 2
+    }
+    if (hb && sc >= d.gossipThr) {
+      ph++;
+      // handleIHave gates (gossipsub.go:612-628); only topics in our mesh map count (:633)
+      gateIHave = ph <= d.MaxIHaveMessages && ia < d.MaxIHaveLength && (ihaveT & sv) != 0;
+    }
+  }
   {
-    unsigned long long m = cmask;
+    unsigned long long m = __ballot(heavy);
     while (m) {
       const int i = __ffsll((long long)m) - 1;
       m &= m - 1;
       const int npre_i = lane_get(npre, i), hb_i = lane_get(hb, i);
-      if ((glmask >> i) & 1) {  // AcceptNone: the whole RPC is dropped
-        cGray += npre_i + hb_i;
-        continue;
-      }
       const int64_t ei = base + i;
       const uint64_t gJoin_i = lane_get64(gJoin, i), gHb_i = lane_get64(gHb, i);
       const uint64_t pRep_i = lane_get64(pRep, i), pHb_i = lane_get64(pHb, i), ihaveT_i = lane_get64(ihaveT, i);
@@ -232,7 +247,14 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
       const int ia_i = lane_get(ia, i);
       double sc_i = lane_getf(sc, i);
       uint64_t mE = lane_get64(meshE, i);
-      bool dirty = false;
+      bool dirty = false;    // the score may have dropped since sc_i
+      bool dirtyUp = false;  // the score may have risen since sc_i (grafts)
+      // every decision below compares sc_i with 0 or GossipThreshold (<= 0): a
+      // stale value >= 0 that can only have risen decides exactly
+      auto fresh = [&]() {
+        if (dirty || (dirtyUp && !(sc_i >= 0.0))) sc_i = edge_score_wave(d, ei, sterm);
+        dirty = dirtyUp = false;
+      };
       uint64_t pOut = 0;
       int nR = 0;
       // (1) Join RPCs: one GRAFT each (gossipsub.go:1080-1084)
@@ -240,9 +262,11 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
       while (gj) {
         const int t = __ffsll((long long)gj) - 1;
         gj &= gj - 1;
-        if (dirty) { sc_i = edge_score_wave(d, ei, sterm); dirty = false; }
+        fresh();
         if (sc_i >= d.gossipThr) ph_i++;  // handleIHave's counter (no IHAVE entries)
-        if (graft_one(d, ei, v, t, sc_i, now, meshcnt, mE, dirty)) {
+        bool pr;
+        pr = graft_one(d, ei, v, t, sc_i, now, meshcnt, mE, dirty, dirtyUp);
+        if (pr) {
           pOut |= 1ull << t;
           nR++;
         }
@@ -251,7 +275,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
       bool gIW = false;
       const int nRep = npre_i - __popcll(gJoin_i);
       if (nRep > 0) {
-        if (dirty) { sc_i = edge_score_wave(d, ei, sterm); dirty = false; }
+        fresh();
         const bool gossipOK = sc_i >= d.gossipThr;
         if (gossipOK) ph_i += nRep;
         gIW = gossipOK && iwRec_i >= 0;  // handleIWant (gossipsub.go:674-711): step 2
@@ -261,7 +285,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
       bool gIH = false;
       uint64_t prunes = 0;
       if (hb_i) {
-        if (dirty) { sc_i = edge_score_wave(d, ei, sterm); dirty = false; }
+        fresh();
         if (sc_i >= d.gossipThr) {
           ph_i++;
           // handleIHave gates (gossipsub.go:612-628); only topics in our mesh map count (:633)
@@ -271,7 +295,9 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
         while (g) {
           const int t = __ffsll((long long)g) - 1;
           g &= g - 1;
-          if (graft_one(d, ei, v, t, sc_i, now, meshcnt, mE, dirty)) prunes |= 1ull << t;
+          bool pr;
+          pr = graft_one(d, ei, v, t, sc_i, now, meshcnt, mE, dirty, dirtyUp);
+          if (pr) prunes |= 1ull << t;
         }
         prune_topics(d, ei, v, pHb_i, now, meshcnt, mE, dirty);
       }
@@ -289,6 +315,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     }
   }
 
+  GS_STAMPB(1);
   // ---- step 2: handleIWant — serve cached messages at most GossipRetransmission times per peer
   int64_t respRec = -1;
   long long cServed = 0;
@@ -364,6 +391,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     __syncthreads();
   }
 
+  GS_STAMPB(2);
   // ---- step 3: handleIHave — IWANT the unseen advertised messages of our topics
   int64_t iwantRec = -1;
   bool iwantAny = false;
@@ -382,7 +410,26 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     sMid[lane] = INT64_MAX;
     sSlot[lane] = -1;
     __syncthreads();
-    // pass a: want counts and the per-sender smallest promise key
+    // The wanted words of item (sender i, topic t): the advertised window of
+    // the sender minus v's seen row, four words loaded at once.
+    const int nHas = (totalItems + 31) >> 5;
+    for (int k = lane; k < nHas; k += 64) sHas[k] = 0u;
+    __syncthreads();
+    auto wants = [&](int uu, int t, auto&& fn) {
+      const int wEnd = (t + 1) * Wt;
+      for (int w0 = t * Wt; w0 < wEnd; w0 += 4) {
+        uint64_t g[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) g[q] = d.gw[(int64_t)uu * W + min(w0 + q, wEnd - 1)];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint64_t want = w0 + q < wEnd ? g[q] & ~sseen[w0 + q] : 0ull;
+          if (want) fn(w0 + q, want);
+        }
+      }
+    };
+    // pass a: want counts and the per-sender smallest promise key; items with
+    // a want are flagged for passes a2 / b
     for (int b = lane; b < totalItems; b += 64) {
       int k;
       const int i = item_sender(sIt, b, k);
@@ -390,8 +437,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
       const int uu = sNode[i];
       int c = 0;
       uint64_t bestKey = ~0ull;
-      for (int w = t * Wt; w < (t + 1) * Wt; ++w) {
-        const uint64_t want = d.gw[(int64_t)uu * W + w] & ~sseen[w];
+      wants(uu, t, [&](int w, uint64_t want) {
         c += __popcll(want);
         uint64_t y = want;
         while (y) {
@@ -401,22 +447,25 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
           const uint64_t key = gs_key64(d.seed, GS_SITE_IWANT, v, uu, (uint32_t)mid, (uint32_t)h);
           bestKey = key < bestKey ? key : bestKey;
         }
-      }
+      });
       if (c) {
         atomicAdd(&sCnt[i], c);
         atomicMin(&sKey[i], bestKey);
+        atomicOr(&sHas[b >> 5], 1u << (b & 31));
       }
     }
     __syncthreads();
+    GS_STAMPB(5);
     // pass a2: the smallest mid among the wants holding the smallest key
     for (int b = lane; b < totalItems; b += 64) {
+      if (!((sHas[b >> 5] >> (b & 31)) & 1)) continue;
       int k;
       const int i = item_sender(sIt, b, k);
       const int t = kth_bit(sTm[i], k);
       const int uu = sNode[i];
       const uint64_t best = sKey[i];
-      for (int w = t * Wt; w < (t + 1) * Wt; ++w) {
-        uint64_t y = d.gw[(int64_t)uu * W + w] & ~sseen[w];
+      wants(uu, t, [&](int w, uint64_t want) {
+        uint64_t y = want;
         while (y) {
           const int bb = __ffsll((long long)y) - 1;
           y &= y - 1;
@@ -424,9 +473,10 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
           if (gs_key64(d.seed, GS_SITE_IWANT, v, uu, (uint32_t)mid, (uint32_t)h) == best)
             atomicMin(&sMid[i], (long long)mid);
         }
-      }
+      });
     }
     __syncthreads();
+    GS_STAMPB(6);
     int totalWant;
     const int myWant = sCnt[lane];
     const int myOff = lane_prefix(myWant, &totalWant);
@@ -441,13 +491,14 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
         __syncthreads();
         // pass b: write the request lists; the promised message's slot
         for (int b = lane; b < totalItems; b += 64) {
+          if (!((sHas[b >> 5] >> (b & 31)) & 1)) continue;
           int k;
           const int i = item_sender(sIt, b, k);
           const int t = kth_bit(sTm[i], k);
           const int uu = sNode[i];
           const long long bestMid = sMid[i];
-          for (int w = t * Wt; w < (t + 1) * Wt; ++w) {
-            uint64_t y = d.gw[(int64_t)uu * W + w] & ~sseen[w];
+          wants(uu, t, [&](int w, uint64_t want) {
+            uint64_t y = want;
             while (y) {
               const int bb = __ffsll((long long)y) - 1;
               y &= y - 1;
@@ -455,7 +506,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
               d.pool[cur][sOut[i] + atomicAdd(&sCur[i], 1)] = slot;
               if (d.slotMid[slot] == bestMid) sSlot[i] = slot;
             }
-          }
+          });
         }
         if (myWant) {
           int iask = myWant;
@@ -471,6 +522,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
       }
     }
     __syncthreads();
+    GS_STAMPB(7);
   }
   cIwantSent = (long long)wave_sum_ll(cIwantSent);
 
@@ -514,6 +566,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     }
   }
 
+  GS_STAMPB(3);
   // ---- step 4: consume the outbox entries, per-edge state, reply RPCs
   if (ctl) {
     d.cPre[prv][r] = 0;
@@ -557,6 +610,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     if (cServed) ctr_add(d, C_IWANT_SERVED, (unsigned long long)cServed);
     if (cGray) ctr_add(d, C_GRAYLISTED, (unsigned long long)cGray);
   }
+  GS_STAMPB(4);
 }
 
 // ---------------------------------------------------------------- heartbeat prelude

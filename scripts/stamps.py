@@ -15,14 +15,15 @@ LIB = os.path.join(REPO, "go-libp2p-pubsub_amd", "build", os.environ.get("GS_STA
 def main():
     wl = bench.WORKLOADS[sys.argv[1] if len(sys.argv) > 1 else "config4"]
     eng, _ = bench.build_engine(wl, 4, 3, 0, lib=LIB)
-    eng.step(1 + 2 * bench.HOPS_PER_ROUND + 3)
+    hops = int(sys.argv[2]) if len(sys.argv) > 2 else 1 + 2 * bench.HOPS_PER_ROUND + 3
+    eng.step(hops)
     raw = C.CDLL(LIB)
-    n = (eng.N // 1024 + 1) * 8
+    n = (eng.N // 1024 + 1) * 16
     buf = np.zeros(n, dtype=np.uint64)
     raw.gs_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]
     rc = raw.gs_debug_stamps(eng.h, buf.ctypes.data_as(C.POINTER(C.c_uint64)), n)
     assert rc == 0
-    s = buf.reshape(-1, 8)[:, :5].astype(np.int64)
+    s = buf.reshape(-1, 8)[: len(buf) // 16, :5].astype(np.int64)
     s = s[(s[:, 0] > 0) & (s[:, 4] > 0)]
     d = np.diff(s, axis=1)
     names = ["setup", "pass1", "pass2", "pass3"]
@@ -30,9 +31,24 @@ def main():
     for i, nm in enumerate(names):
         print(f"{nm}: mean {d[:, i].mean():.0f} cycles  p50 {np.median(d[:, i]):.0f}  p99 {np.percentile(d[:, i], 99):.0f}")
     print("total mean", d.sum(1).mean())
-    c = buf.reshape(-1, 8)[:, 5:8].astype(np.int64)
+    c = buf.reshape(-1, 8)[: len(buf) // 16, 5:8].astype(np.int64)
     print("copies/node mean", c[:, 0].mean(), "pass-1 list-load cycles mean", c[:, 1].mean(), "pass-1 delivery-drain cycles mean",
           c[:, 2].mean())
+    bb = buf.reshape(-1, 8)[len(buf) // 16:].astype(np.int64)
+    bb = bb[(bb[:, 0] > 0) & (bb[:, 4] > 0)]
+    b = bb[:, :5]
+    if len(b):
+        db = np.diff(b, axis=1)
+        print("phase B samples", len(b))
+        for i, nm in enumerate(["step1", "step2 iwant", "step3 ihave", "step4"]):
+            print(f"  {nm}: mean {db[:, i].mean():.0f} cycles  p50 {np.median(db[:, i]):.0f}  p99 {np.percentile(db[:, i], 99):.0f}")
+        sub = bb[(bb[:, 5] > 0) & (bb[:, 7] > 0)]
+        if len(sub):
+            print("  step3 (nodes with IHAVE work, %d): setup %.0f, pass a %.0f, pass a2 %.0f, pass b + arena %.0f" % (
+                len(sub), (sub[:, 5] - sub[:, 2]).mean() - (sub[:, 5] - sub[:, 5]).mean(), 0, 0, 0)
+                  if False else "  step3 (nodes with IHAVE work, %d): to pass a end %.0f, pass a2 %.0f, pass b + arena %.0f, promises + rest %.0f" % (
+                len(sub), (sub[:, 5] - sub[:, 2]).mean(), (sub[:, 6] - sub[:, 5]).mean(), (sub[:, 7] - sub[:, 6]).mean(),
+                (sub[:, 3] - sub[:, 7]).mean()))
 
 
 if __name__ == "__main__":
