@@ -10,9 +10,13 @@ IHAVE emission, mcache shift).  `--workload config3` runs BASELINE configs[2]
 (1M peers, 1 topic) instead.
 
 Contract: python bench.py --gpus N --steps K --warmup W; with N > 1 it is
-launched by torch.distributed.run and every rank runs its own replica of the
-workload on its GPU ("replicas", weak scaling: the partitioned multi-GPU
-exchange over RCCL is not built yet).  Prints one JSON line.
+launched by torch.distributed.run, one rank per GPU.  By default the ranks
+PARTITION the one 1M-peer graph: rank r simulates a contiguous
+node range and exchanges its nodes' RPCs with the other ranks once per hop over
+RCCL (all-gather of frontier lists / IWANT arena / IHAVE rows, all-to-all-v of
+per-edge forwarding + control records; pubsub_amd.transport).  The total work
+is fixed, so scaling is "strong".  `--mode replicas` runs N independent copies
+instead (weak scaling).  Prints one JSON line.
 """
 import argparse
 import json
@@ -26,7 +30,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "go-libp2p-pubsub_amd"))
 
 from pubsub_amd import (Millisecond, NewGossipSub, WithDevice, WithHop, WithMessageWindow,  # noqa: E402
-                        WithPeerScore, WithSeed, eth2_peer_score_params, eth2_thresholds)
+                        WithPartition, WithPeerScore, WithSeed, eth2_peer_score_params, eth2_thresholds)
 from pubsub_amd import graphs  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
@@ -39,7 +43,7 @@ WORKLOADS = {
 }
 
 
-def build_engine(wl, rounds, seed, device, lib=None, n=None, msgs_per_round=MSGS_PER_ROUND):
+def build_engine(wl, rounds, seed, device, lib=None, n=None, msgs_per_round=MSGS_PER_ROUND, extra=()):
     n = n or wl["n"]
     T = wl["topics"]
     g = graphs.random_regular_fast(n, wl["k"], seed)
@@ -48,7 +52,7 @@ def build_engine(wl, rounds, seed, device, lib=None, n=None, msgs_per_round=MSGS
             WithMessageWindow(wl["slots"]), WithSeed(seed)]
     if lib is None:
         opts.append(WithDevice(device))
-    eng = NewGossipSub(n, T, g, subs, *opts, lib=lib)
+    eng = NewGossipSub(n, T, g, subs, *opts, *extra, lib=lib)
     per_hop = msgs_per_round // HOPS_PER_ROUND
     hops = np.repeat(np.arange(1, rounds * HOPS_PER_ROUND + 1, dtype=np.int64), per_hop)
     rng = np.random.default_rng(seed + 7)
@@ -81,9 +85,11 @@ def algorithmic_bytes(kernel, eng, wl, per_hop):
     """Algorithmic HBM bytes of ONE launch of `kernel`: the data
     the algorithm must move with the engine's representation, not what the
     caches end up fetching.  per_hop: measured averages over the timed hops."""
-    N, E, T = eng.N, eng.E, wl["topics"]
+    # a partitioned rank's kernels cover its own nodes [n0, n1) and edges [e0, e1)
+    (n0, n1), (e0, e1) = eng.node_range, eng.edge_range
+    N, E, T = n1 - n0, e1 - e0, wl["topics"]
     if kernel == "phase_a":
-        mesh = eng.mesh()
+        mesh = eng.mesh()[e0:e1]
         fwd_edges = int((mesh != 0).sum())          # edges with a forwarding topic
         items = per_hop["deliveries"] + per_hop["published"]   # frontier-list entries written per hop
         list_reads = 4.0 * items * fwd_edges / N     # each list is read by the neighbours it forwards to
@@ -137,22 +143,39 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="config4", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", default="partition", choices=["partition", "replicas"])
+    ap.add_argument("--peers", type=int, default=0, help="override the workload's peer count (rehearsals)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    extra = ()
+    partitioned = world > 1 and args.mode == "partition"
     if world > 1:
         import torch
         import torch.distributed as dist
+        # GS_DIST_BACKEND=gloo + several ranks per GPU: a rehearsal of the
+        # partitioned path on a 1-GPU box (host-staged exchange)
+        backend = os.environ.get("GS_DIST_BACKEND", "nccl")
+        local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+        if partitioned:
+            from pubsub_amd.transport import TorchTransport
+            extra = (WithPartition(rank, world, TorchTransport(memory="device")),)
 
-    wl = WORKLOADS[args.workload]
+    wl = dict(WORKLOADS[args.workload])
+    if args.peers:
+        wl["n"] = args.peers
     rounds = args.warmup + args.steps + 1
     t_setup = time.perf_counter()
-    eng, g = build_engine(wl, rounds, 3 + rank, local)
+    # partitioned ranks simulate ONE graph and schedule (same seed); replicas differ
+    eng, g = build_engine(wl, rounds, 3 if partitioned else 3 + rank, local, extra=extra)
     # hop 0 (Join) + warm-up rounds: meshes form, the message window fills
     eng.step(1 + args.warmup * HOPS_PER_ROUND)
     setup_s = time.perf_counter() - t_setup
@@ -163,6 +186,7 @@ def main():
         eng.sync()
 
     c0 = eng.counters()
+    x0 = eng.exchange_stats()
     hop0 = eng.hop
     eng.set_profiling(True)
     barrier()
@@ -173,17 +197,22 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     c1 = eng.counters()
+    x1 = eng.exchange_stats()
     kstats = eng.kernel_stats()
     eng.set_profiling(False)
-    deliveries = c1["deliveries"] - c0["deliveries"]
+    ev_keys = ("deliveries", "duplicates", "transmissions", "grafts_sent", "prunes_sent",
+               "ihave_sent", "iwant_sent", "iwant_served", "promises_broken", "graylisted")
+    events = {k: c1[k] - c0[k] for k in ev_keys}
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        cdev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        dv = torch.tensor([deliveries], dtype=torch.float64, device="cuda")
+        dv = torch.tensor([events[k] for k in ev_keys], dtype=torch.int64, device=cdev)
         dist.all_reduce(dv, op=dist.ReduceOp.SUM)
-        deliveries = int(dv.item())
+        events = dict(zip(ev_keys, (int(x) for x in dv.tolist())))
+    deliveries = events["deliveries"]
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -213,7 +242,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if partitioned else "weak",
         "vs_baseline": None,
         "dtype": "f64+u64",
         "data": "synthetic (seeded random 32-regular graph, seeded publish schedule)",
@@ -222,17 +251,19 @@ def main():
                    ", k=32, gossipsub v1.1 + Eth2 scoring, 1000 msgs/round, 10 hops/round",
                    "peers": wl["n"], "topics": wl["topics"], "degree": wl["k"],
                    "msgs_per_round": MSGS_PER_ROUND, "hops_per_round": HOPS_PER_ROUND,
-                   "parallelism": f"replicas{world}"},
-        "rounds_per_sec": rounds_per_s * world,
+                   "parallelism": f"partition{world}" if partitioned else f"replicas{world}"},
+        "rounds_per_sec": rounds_per_s * (1 if partitioned else world),
         "hops_per_sec": rounds_per_s * HOPS_PER_ROUND,
         "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kstats.items() if v[1]},
-        "events_per_step": {k: (c1[k] - c0[k]) // args.steps for k in
-                            ("deliveries", "duplicates", "transmissions", "grafts_sent", "prunes_sent",
-                             "ihave_sent", "iwant_sent", "iwant_served", "promises_broken", "graylisted")},
+        "events_per_step": {k: v // args.steps for k, v in events.items()},
         "roofline": roofline,
         "setup_s": round(setup_s, 1),
     }
-    if not args.no_cpu_baseline:
+    if partitioned:
+        out["exchange"] = {"rank0_host_ms_per_step": round((x1[0] - x0[0]) / args.steps, 3),
+                           "rank0_bytes_in_per_step": (x1[1] - x0[1]) // args.steps,
+                           "rank0_nodes": eng.node_range[1] - eng.node_range[0]}
+    if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(wl)
     print(json.dumps(out))
     if dist is not None:

@@ -48,6 +48,14 @@ struct Dev {
   int32_t N, T, Wt, W, St, S, R, HL, HG;
   int64_t E;
   int32_t router, scoring, floodPublish, rsTarget, maxAge;
+  // partition (gs_set_partition): this rank owns nodes [n0, n1) and their CSR
+  // rows, i.e. edges [e0, e1).  Node kernels run one wave per owned node, edge
+  // kernels one lane per owned edge; per-(edge, topic) state is allocated for
+  // the owned edges only.  Unpartitioned: n0 = 0, n1 = N, e0 = 0, e1 = E.
+  int32_t n0, n1, rank, world;
+  int64_t e0, e1;
+  uint8_t* xmark;   // [E] forwarding set changed since its parity was exchanged (world > 1)
+  const uint8_t* nodeRank;  // [N] owning rank of every node (world > 1)
   uint32_t seed;
   int64_t hop_ns;
   // graph (static)

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -19,6 +20,7 @@
 #include "gs_host.h"
 #include "gs_kernels.h"
 #include "gs_kernels_ctl.h"
+#include "gs_exchange.h"
 
 static thread_local std::string g_err;
 void gs_set_error(const std::string& msg) { g_err = msg; }
@@ -78,6 +80,23 @@ struct gs_engine {
   int retireCap = 0;
   double* dScoreTmp = nullptr;
   int32_t *dHopOut = nullptr, *dFromOut = nullptr;
+  // partition (gs_set_partition; world == 1: the whole graph)
+  int rank = 0, world = 1;
+  gs_transport tr{};
+  std::vector<int32_t> part;  // [world + 1] node boundaries
+  int32_t n0 = 0, n1 = 0;
+  int64_t e0 = 0, e1 = 0, poolSeg = 0;
+  // exchange buffers (device) and the pinned host staging of the counts
+  uint8_t *xSend = nullptr, *xRecv = nullptr, *xSendE = nullptr, *xRecvE = nullptr;
+  size_t xSendCap = 0, xRecvCap = 0, xSendECap = 0, xRecvECap = 0;
+  unsigned long long* xCnt = nullptr;  // device: [world] record counts, [world] cursors, bump
+  int64_t* xOff = nullptr;             // device: [world] record offsets
+  unsigned long long* xHost = nullptr; // pinned: world counts, bump, poolCnt
+  double xMs = 0.0;                    // host wall time spent in exchanges
+  int64_t xBytes = 0;                  // bytes received by this rank
+  int exchange(int cur, bool hb);
+  int64_t x_poolEnd() const { return (int64_t)(rank + 1) * poolSeg; }
+  int growDev(uint8_t*& p, size_t& cap, size_t need, size_t keep = 0);
   // kernel timing: (kernel id, start event, end event) pending until a sync
   bool profiling = false;
   std::vector<hipEvent_t> evPool;
@@ -105,6 +124,8 @@ struct gs_engine {
 
   ~gs_engine() {
     for (hipEvent_t ev : evPool) (void)hipEventDestroy(ev);
+    for (uint8_t* p : {xSend, xRecv, xSendE, xRecvE}) if (p) (void)hipFree(p);
+    if (xHost) (void)hipHostFree(xHost);
     for (void* p : allocs) (void)hipFree(p);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -133,6 +154,18 @@ struct gs_engine {
   int uploadMessages();
   int checkDeviceError();
 };
+
+// Contiguous node ranges balanced by edges: rank r owns the nodes whose CSR
+// rows start in [E*r/world, E*(r+1)/world).  Identical on every rank.
+static std::vector<int32_t> partition_bounds(const std::vector<int64_t>& rowptr, int N, int world) {
+  const int64_t E = rowptr[N];
+  std::vector<int32_t> part(world + 1, N);
+  part[0] = 0;
+  for (int r = 1; r < world; ++r)
+    part[r] = (int32_t)(std::lower_bound(rowptr.begin(), rowptr.begin() + N, (E * r) / world) - rowptr.begin());
+  for (int r = 1; r <= world; ++r) part[r] = std::max(part[r], part[r - 1]);
+  return part;
+}
 
 static TopicP to_dev(const gs_topic_score_params& p, bool scored) {
   TopicP t{};
@@ -203,6 +236,15 @@ int gs_engine::start() {
     gs_set_error("this build supports < 2^31 edges per engine");
     return GS_EUNSUPPORTED;
   }
+  part = partition_bounds(rowptr, N, world);
+  n0 = part[rank];
+  n1 = part[rank + 1];
+  e0 = rowptr[n0];
+  e1 = rowptr[n1];
+  if (world > 1 && cfg.router == GS_ROUTER_RANDOMSUB) {
+    gs_set_error("a partitioned engine supports floodsub and gossipsub (randomsub target masks are not exchanged)");
+    return GS_EUNSUPPORTED;
+  }
   std::vector<double> p6(E, 0.0);
   if (scoring && sp.IPColocationFactorWeight != 0 && !ipv4.empty()) {
     // ipColocationFactor (score.go:335-379): peers per IP among the observer's peers
@@ -241,6 +283,7 @@ int gs_engine::start() {
     x.rsTarget = std::max(6, sq);
   }
   x.maxAge = maxAge; x.seed = cfg.seed; x.hop_ns = cfg.hop_ns;
+  x.n0 = n0; x.n1 = n1; x.e0 = e0; x.e1 = e1; x.rank = rank; x.world = world;
   x.TopicScoreCap = sp.TopicScoreCap; x.AppW = sp.AppSpecificWeight; x.IPW = sp.IPColocationFactorWeight;
   x.BPW = sp.BehaviourPenaltyWeight; x.BPThr = sp.BehaviourPenaltyThreshold; x.BPDecay = sp.BehaviourPenaltyDecay;
   x.DecayToZero = sp.DecayToZero;
@@ -256,7 +299,11 @@ int gs_engine::start() {
   x.PruneRecv = (gp.PruneBackoff / kSec) > 0 ? (gp.PruneBackoff / kSec) * kSec : gp.PruneBackoff;
   x.OGT = gp.OpportunisticGraftTicks ? gp.OpportunisticGraftTicks : 1;
 
-  const size_t NW = (size_t)N * W, NS = (size_t)N * S, TE = (size_t)T * (size_t)((E + 63) & ~63ll);
+  const size_t NW = (size_t)N * W, NS = (size_t)N * S;
+  // per-(edge, topic) state exists for the owned edges only: rows e*T + t,
+  // addressed through a base shifted by e0*T
+  const size_t TE = (size_t)T * (size_t)(e1 - e0) + 64;
+  const int64_t shift = e0 * T;
   bool ok = true;
   auto chk = [&](const void* p) { if (!p) ok = false; };
   int64_t* dRowptr = dalloc<int64_t>(N + 1); chk(dRowptr);
@@ -346,12 +393,19 @@ int gs_engine::start() {
   x.fmd = dalloc<double>(TE); x.mmd = dalloc<double>(TE); x.mfp = dalloc<double>(TE); x.imd = dalloc<double>(TE);
   x.dlt = dalloc<uint32_t>(TE); chk(x.dlt);
   x.graftTime = dalloc<int64_t>(TE); x.meshTime = dalloc<int64_t>(TE); x.flags = dalloc<uint8_t>(TE);
+  chk(x.backoff); chk(x.fmd); chk(x.mmd); chk(x.mfp); chk(x.imd); chk(x.graftTime); chk(x.meshTime); chk(x.flags);
+  if (!ok) { gs_set_error("device allocation failed (per-(edge, topic) state)"); return GS_ENOMEM; }
+  x.backoff -= shift; x.fmd -= shift; x.mmd -= shift; x.mfp -= shift; x.imd -= shift;
+  x.dlt -= shift; x.graftTime -= shift; x.meshTime -= shift; x.flags -= shift;
   x.bp = dalloc<double>(E); x.peerhave = dalloc<int32_t>(E); x.iasked = dalloc<int32_t>(E);
   chk(x.score0); chk(x.score1); chk(x.backoff); chk(x.fmd); chk(x.mmd); chk(x.mfp); chk(x.imd);
   chk(x.graftTime); chk(x.meshTime); chk(x.flags); chk(x.bp); chk(x.peerhave); chk(x.iasked);
-  // IWANT payload arena (slot ids): 4 ids per edge per hop, >= 16M
-  x.poolCap = cfg.router == GS_ROUTER_GOSSIPSUB ? std::max<int64_t>(1 << 24, 4 * E) : 16;
-  for (int k = 0; k < 2; ++k) { x.pool[k] = dalloc<int32_t>((size_t)x.poolCap); chk(x.pool[k]); }
+  // IWANT payload arena (slot ids): 4 ids per owned edge per hop, >= 16M in
+  // total; rank r allocates from its own segment [r*seg, (r+1)*seg)
+  poolSeg = cfg.router == GS_ROUTER_GOSSIPSUB ? std::max<int64_t>((1 << 24) / world, 4 * (e1 - e0)) : 16;
+  poolSeg = (poolSeg + 63) & ~63ll;
+  x.poolCap = (int64_t)(rank + 1) * poolSeg;
+  for (int k = 0; k < 2; ++k) { x.pool[k] = dalloc<int32_t>((size_t)poolSeg * world); chk(x.pool[k]); }
   x.poolCnt = dalloc<unsigned long long>(2); chk(x.poolCnt);
   x.slotSrc = dalloc<int32_t>(S, 0xFF); x.slotPubHop = dalloc<int64_t>(S); x.slotMid = dalloc<int64_t>(S, 0xFF);
   chk(x.slotSrc); chk(x.slotPubHop); chk(x.slotMid);
@@ -363,6 +417,23 @@ int gs_engine::start() {
   chk(x.ctr); chk(x.err);
   dScoreTmp = dalloc<double>(E); chk(dScoreTmp);
   dHopOut = dalloc<int32_t>(N); dFromOut = dalloc<int32_t>(N); chk(dHopOut); chk(dFromOut);
+  x.xmark = nullptr;
+  x.nodeRank = nullptr;
+  if (world > 1) {
+    x.xmark = dalloc<uint8_t>(E); chk(x.xmark);
+    uint8_t* nr = dalloc<uint8_t>(N); chk(nr);
+    xCnt = dalloc<unsigned long long>(2 * world + 1); chk(xCnt);
+    xOff = dalloc<int64_t>(world); chk(xOff);
+    if (ok) {
+      std::vector<uint8_t> h(N);
+      for (int r = 0; r < world; ++r)
+        for (int v = part[r]; v < part[r + 1]; ++v) h[v] = (uint8_t)r;
+      HIPCHECK(hipMemcpyAsync(nr, h.data(), N, hipMemcpyHostToDevice, stream));
+      HIPCHECK(hipStreamSynchronize(stream));
+    }
+    x.nodeRank = nr;
+    HIPCHECK(hipHostMalloc((void**)&xHost, (size_t)(world + 2) * 8, hipHostMallocDefault));
+  }
   if (!ok) {
     gs_set_error("device allocation failed (state); reduce num_nodes or slots_per_topic");
     return GS_ENOMEM;
@@ -445,17 +516,20 @@ int gs_engine::stepOne() {
     if (std::find(retireWords.begin(), retireWords.end(), w) == retireWords.end()) retireWords.push_back(w);
   }
   HIPCHECK(hipMemsetAsync(d.pubmask[cur], 0, (size_t)W * 8, stream));
-  HIPCHECK(hipMemsetAsync(d.poolCnt + cur, 0, 8, stream));
-  const unsigned eb = nblk(E, 256);
-  const unsigned sgb = nblk(E, GS_SG), pb = nblk((int64_t)E * T, 256);
+  k_set_u64<<<1, 1, 0, stream>>>(d.poolCnt + cur, (unsigned long long)rank * (unsigned long long)poolSeg);
+  const int nOwn = n1 - n0;
+  const int64_t eOwn = e1 - e0;
+  const unsigned eb = nblk(eOwn, 256);
+  const unsigned sgb = nblk(eOwn, GS_SG), pb = nblk(eOwn * T, 256);
   if (scoring) TIMED(this, GS_K_SCORE, (k_score_rows<1><<<sgb, 64, 0, stream>>>(d, nullptr)));
-  if (h == 0 && gossip) TIMED(this, GS_K_JOIN, (k_join<<<N, 64, 0, stream>>>(d, h, now, cur)));
+  if (h == 0 && gossip && nOwn) TIMED(this, GS_K_JOIN, (k_join<<<nOwn, 64, 0, stream>>>(d, h, now, cur)));
   if (gossip && !floodPublish && n > 0) {
     // Publish to a topic we have not joined: fanout (gossipsub.go:977-994)
     std::vector<int32_t> pairs;
     std::vector<uint64_t> seenPair;
     for (size_t i = b; i < e; ++i) {
       const int src = mSrc[i], t = mTopic[i];
+      if (src < n0 || src >= n1) continue;  // another rank's publisher
       if ((sub[src] >> t) & 1) continue;
       const uint64_t key = ((uint64_t)src << 6) | (uint64_t)t;
       if (std::find(seenPair.begin(), seenPair.end(), key) != seenPair.end()) continue;
@@ -477,7 +551,7 @@ int gs_engine::stepOne() {
       HIPCHECK(hipStreamSynchronize(stream));  // `pairs` is pageable host memory
     }
   }
-  TIMED(this, GS_K_FWD, (k_fwd<<<eb, 256, 0, stream>>>(d, cur)));
+  if (eOwn) TIMED(this, GS_K_FWD, (k_fwd<<<eb, 256, 0, stream>>>(d, cur)));
   if (n > 0) k_pubmask<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, cur);
   k_oldmask<<<nblk(S, 256), 256, 0, stream>>>(d, h);
   {
@@ -486,7 +560,7 @@ int gs_engine::stepOne() {
     const size_t nCnt = ((size_t)T * d.maxDeg + 3) & ~(size_t)3;
     const size_t lds = 4 * nCnt + 8 * (size_t)nR + 64 * (size_t)nR + (d.needAge ? 4 * nCnt : 0);
     TIMED(this, GS_K_PHASE_A, launch_wpl(W, [&](auto w) {
-            k_phase_a<decltype(w)::value><<<N, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR);
+            if (nOwn) k_phase_a<decltype(w)::value><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR);
           }));
   }
   if (!retireWords.empty()) {
@@ -499,7 +573,7 @@ int gs_engine::stepOne() {
     }
     HIPCHECK(hipMemcpyAsync(dRetire, retireWords.data(), retireWords.size() * 4, hipMemcpyHostToDevice, stream));
     const int nw = (int)retireWords.size();
-    k_retire<<<nblk((int64_t)N * nw, 256), 256, 0, stream>>>(d, cur, dRetire, nw);
+    if (nOwn) k_retire<<<nblk((int64_t)nOwn * nw, 256), 256, 0, stream>>>(d, cur, dRetire, nw);
     HIPCHECK(hipStreamSynchronize(stream));  // retireWords is pageable host memory
   }
   if (n > 0) {
@@ -510,7 +584,9 @@ int gs_engine::stepOne() {
   if (gossip) {
     if (scoring) TIMED(this, GS_K_SCORE, (k_score_rows<2><<<sgb, 64, 0, stream>>>(d, nullptr)));
     TIMED(this, GS_K_PHASE_B,
-          launch_wpl(W, [&](auto wpl) { k_phase_b<decltype(wpl)::value><<<N, 64, 0, stream>>>(d, h, now, cur, head); }));
+          launch_wpl(W, [&](auto wpl) {
+            if (nOwn) k_phase_b<decltype(wpl)::value><<<nOwn, 64, 0, stream>>>(d, h, now, cur, head);
+          }));
   }
   if (refreshDue(now)) {
     TIMED(this, GS_K_REFRESH, (k_refresh_rows<<<sgb, 64, 0, stream>>>(d, now)));
@@ -523,18 +599,22 @@ int gs_engine::stepOne() {
   }
   if (heartbeatDue(now)) {
     ticks++;
-    TIMED(this, GS_K_HB_PRE, (k_hb_pre<<<N, 64, 0, stream>>>(d, now, ticks)));
+    if (nOwn) TIMED(this, GS_K_HB_PRE, (k_hb_pre<<<nOwn, 64, 0, stream>>>(d, now, ticks)));
     // right after a refresh S0 holds exact scores: recompute only what hb_pre dirtied
     if (scoring && refreshedHop == h)
       TIMED(this, GS_K_SCORE, (k_score_rows<3><<<sgb, 64, 0, stream>>>(d, nullptr)));
     else if (scoring)
       TIMED(this, GS_K_SCORE, (k_score_rows<0><<<sgb, 64, 0, stream>>>(d, d.score1)));
     const int newhead = (head + R - 1) % R;
-    TIMED(this, GS_K_HEARTBEAT, (k_heartbeat<<<N, 64, 0, stream>>>(d, h, now, ticks, cur, head, newhead)));
+    if (nOwn) TIMED(this, GS_K_HEARTBEAT, (k_heartbeat<<<nOwn, 64, 0, stream>>>(d, h, now, ticks, cur, head, newhead)));
     head = newhead;
     heartbeats++;
   }
   HIPCHECK(hipGetLastError());
+  if (world > 1) {
+    const int rc = exchange(cur, heartbeatDue(now));
+    if (rc) return rc;
+  }
   hop++;
   return GS_OK;
 }
@@ -569,6 +649,153 @@ int gs_engine::checkDeviceError() {
   }
 }
 
+// Grows a device buffer to `need` bytes, keeping its first `keep` bytes.
+int gs_engine::growDev(uint8_t*& p, size_t& cap, size_t need, size_t keep) {
+  if (need <= cap) return GS_OK;
+  uint8_t* q = nullptr;
+  const size_t ncap = std::max<size_t>(need + need / 4, 1 << 20);
+  if (hipMalloc(&q, ncap) != hipSuccess) {
+    gs_set_error("device allocation failed (exchange buffer)");
+    return GS_ENOMEM;
+  }
+  if (p && keep) HIPCHECK(hipMemcpyAsync(q, p, std::min(keep, cap), hipMemcpyDeviceToDevice, stream));
+  if (p) {
+    HIPCHECK(hipStreamSynchronize(stream));
+    HIPCHECK(hipFree(p));
+  }
+  p = q;
+  cap = ncap;
+  return GS_OK;
+}
+
+static inline size_t align8(size_t x) { return (x + 7) & ~(size_t)7; }
+
+// End-of-hop exchange of a partitioned engine (gs_exchange.h): pack what this
+// rank's nodes sent in hop h, hand it to the host transport, unpack what the
+// other ranks' nodes sent to ours.
+int gs_engine::exchange(int cur, bool hb) {
+  const int nOwn = n1 - n0;
+  const int64_t eOwn = e1 - e0;
+  const size_t hdrBytes = align8((size_t)nOwn * 8);
+  unsigned long long* cnt = xCnt;             // [world]
+  unsigned long long* cursor = xCnt + world;  // [world]
+  unsigned long long* bump = xCnt + 2 * world;
+  // 1. counts + lists (into a buffer that usually suffices; re-packed if not)
+  HIPCHECK(hipMemsetAsync(xCnt, 0, (size_t)(2 * world + 1) * 8, stream));
+  if (eOwn) k_x_count<<<nblk(eOwn, 256), 256, 0, stream>>>(d, cur, cnt);
+  if (xSendCap < hdrBytes + (16u << 20)) {
+    int rc = growDev(xSend, xSendCap, hdrBytes + (16u << 20));
+    if (rc) return rc;
+  }
+  auto packLists = [&]() {
+    const int64_t capEnt = (int64_t)((xSendCap - hdrBytes) / 4);
+    if (nOwn)
+      k_x_lists<<<nOwn, 64, 0, stream>>>(d, cur, bump, (int64_t*)xSend, (uint32_t*)(xSend + hdrBytes), capEnt);
+  };
+  packLists();
+  HIPCHECK(hipMemcpyAsync(xHost, xCnt, (size_t)world * 8, hipMemcpyDeviceToHost, stream));
+  HIPCHECK(hipMemcpyAsync(xHost + world, bump, 8, hipMemcpyDeviceToHost, stream));
+  HIPCHECK(hipMemcpyAsync(xHost + world + 1, d.poolCnt + cur, 8, hipMemcpyDeviceToHost, stream));
+  HIPCHECK(hipStreamSynchronize(stream));
+  const int64_t nEnt = (int64_t)xHost[world];
+  const int64_t poolBase = (int64_t)rank * poolSeg;
+  const int64_t nPool = std::max<int64_t>(0, std::min<int64_t>((int64_t)xHost[world + 1], x_poolEnd()) - poolBase);
+  const size_t entBytes = align8((size_t)nEnt * 4), poolBytes = align8((size_t)nPool * 4);
+  const size_t gwBytes = hb ? (size_t)nOwn * W * 8 : 0;
+  const size_t bcast = hdrBytes + entBytes + poolBytes + gwBytes;
+  if (bcast > xSendCap) {  // grow (keeps nothing) and pack the lists again
+    int rc = growDev(xSend, xSendCap, bcast);
+    if (rc) return rc;
+    HIPCHECK(hipMemsetAsync(bump, 0, 8, stream));
+    packLists();
+  }
+  if (nPool)
+    HIPCHECK(hipMemcpyAsync(xSend + hdrBytes + entBytes, d.pool[cur] + poolBase, (size_t)nPool * 4,
+                            hipMemcpyDeviceToDevice, stream));
+  if (gwBytes)
+    HIPCHECK(hipMemcpyAsync(xSend + hdrBytes + entBytes + poolBytes, d.gw + (size_t)n0 * W, gwBytes,
+                            hipMemcpyDeviceToDevice, stream));
+  // 2. edge records, one block per destination rank
+  std::vector<int64_t> sendRec(world), sendOff(world);
+  int64_t totRec = 0;
+  for (int r = 0; r < world; ++r) {
+    sendRec[r] = (int64_t)xHost[r];
+    sendOff[r] = totRec;
+    totRec += sendRec[r];
+  }
+  {
+    int rc = growDev(xSendE, xSendECap, (size_t)std::max<int64_t>(totRec, 1) * sizeof(XRec));
+    if (rc) return rc;
+  }
+  if (totRec) {
+    HIPCHECK(hipMemcpyAsync(xOff, sendOff.data(), (size_t)world * 8, hipMemcpyHostToDevice, stream));
+    k_x_pack<<<nblk(eOwn, 256), 256, 0, stream>>>(d, cur, xOff, cursor, (XRec*)xSendE);
+  }
+  HIPCHECK(hipStreamSynchronize(stream));  // sendOff is pageable; the transport reads the buffers
+  // 3. sizes of every rank: [bcast bytes, list entries, arena ids, gw rows?, records to rank 0..world-1]
+  const int nS = 4 + world;
+  std::vector<int64_t> mine(nS), all((size_t)nS * world);
+  mine[0] = (int64_t)bcast; mine[1] = nEnt; mine[2] = nPool; mine[3] = hb ? 1 : 0;
+  for (int r = 0; r < world; ++r) mine[4 + r] = sendRec[r];
+  const auto t0 = std::chrono::steady_clock::now();
+  if (tr.allgather_i64(tr.user, mine.data(), nS, all.data()) != 0) {
+    gs_set_error("transport allgather_i64 failed");
+    return GS_EDEVICE;
+  }
+  int64_t chunk = 8;
+  for (int r = 0; r < world; ++r) chunk = std::max<int64_t>(chunk, all[(size_t)r * nS]);
+  chunk = (int64_t)align8((size_t)chunk);
+  {
+    int rc = growDev(xSend, xSendCap, (size_t)chunk, bcast);  // the transport reads `chunk` bytes
+    if (rc) return rc;
+    rc = growDev(xRecv, xRecvCap, (size_t)chunk * world);
+    if (rc) return rc;
+  }
+  if (tr.allgather(tr.user, xSend, xRecv, chunk) != 0) {
+    gs_set_error("transport allgather failed");
+    return GS_EDEVICE;
+  }
+  std::vector<int64_t> sendB(world), recvB(world);
+  int64_t totIn = 0;
+  for (int r = 0; r < world; ++r) {
+    sendB[r] = sendRec[r] * (int64_t)sizeof(XRec);
+    recvB[r] = all[(size_t)r * nS + 4 + rank] * (int64_t)sizeof(XRec);
+    totIn += recvB[r];
+  }
+  {
+    int rc = growDev(xRecvE, xRecvECap, (size_t)std::max<int64_t>(totIn, 1));
+    if (rc) return rc;
+  }
+  if (tr.alltoallv(tr.user, xSendE, sendB.data(), xRecvE, recvB.data()) != 0) {
+    gs_set_error("transport alltoallv failed");
+    return GS_EDEVICE;
+  }
+  xMs += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  // 4. unpack the other ranks' parts into the mirrors
+  for (int r = 0; r < world; ++r) {
+    if (r == rank) continue;
+    const int nr = part[r + 1] - part[r];
+    const int64_t* a = &all[(size_t)r * nS];
+    const size_t hB = align8((size_t)nr * 8), eB = align8((size_t)a[1] * 4), pB = align8((size_t)a[2] * 4);
+    const uint8_t* c = xRecv + (size_t)r * chunk;
+    xBytes += a[0];
+    if (nr) k_x_unlists<<<nr, 64, 0, stream>>>(d, cur, (const int64_t*)c, (const uint32_t*)(c + hB), part[r]);
+    if (a[2])
+      HIPCHECK(hipMemcpyAsync(d.pool[cur] + (size_t)r * poolSeg, c + hB + eB, (size_t)a[2] * 4,
+                              hipMemcpyDeviceToDevice, stream));
+    if (a[3] && nr)
+      HIPCHECK(hipMemcpyAsync(d.gw + (size_t)part[r] * W, c + hB + eB + pB, (size_t)nr * W * 8,
+                              hipMemcpyDeviceToDevice, stream));
+  }
+  xBytes += totIn;
+  if (totIn) {
+    const int64_t n = totIn / (int64_t)sizeof(XRec);
+    k_x_unpack<<<nblk(n, 256), 256, 0, stream>>>(d, cur, (const XRec*)xRecvE, n);
+  }
+  HIPCHECK(hipGetLastError());
+  return GS_OK;
+}
+
 // Per-(edge, topic) arrays are edge-major rows [e*T + t] on the device (tix
 // in gs_device.h); readbacks return them topic-major [t*E + e].
 template <class X>
@@ -578,11 +805,14 @@ static int copy_back_pairs(gs_engine* g, X* dst, const X* src) {
     std::memset(dst, 0, T * E * sizeof(X));
     return GS_OK;
   }
-  std::vector<X> tmp(T * E);
+  // only the owned edges [e0, e1) have per-(edge, topic) state on this rank
+  const size_t e0 = (size_t)g->e0, e1 = (size_t)g->e1;
+  std::vector<X> tmp(T * (e1 - e0));
   HIPCHECK(hipStreamSynchronize(g->stream));
-  HIPCHECK(hipMemcpy(tmp.data(), src, tmp.size() * sizeof(X), hipMemcpyDeviceToHost));
-  for (size_t e = 0; e < E; ++e)
-    for (size_t t = 0; t < T; ++t) dst[t * E + e] = tmp[e * T + t];
+  HIPCHECK(hipMemcpy(tmp.data(), src + e0 * T, tmp.size() * sizeof(X), hipMemcpyDeviceToHost));
+  std::memset(dst, 0, T * E * sizeof(X));
+  for (size_t e = e0; e < e1; ++e)
+    for (size_t t = 0; t < T; ++t) dst[t * E + e] = tmp[(e - e0) * T + t];
   return GS_OK;
 }
 extern "C" {
@@ -814,6 +1044,33 @@ int gs_set_topic_score_params(gs_engine* g, int32_t topic, const gs_topic_score_
     k_recap<<<nblk(g->E, 256), 256, 0, g->stream>>>(g->d, topic, p->FirstMessageDeliveriesCap,
                                                     p->MeshMessageDeliveriesCap);
   HIPCHECK(hipStreamSynchronize(g->stream));
+  return GS_OK;
+}
+
+int gs_set_partition(gs_engine* g, int32_t rank, int32_t world, const gs_transport* tr) {
+  if (g->started) { gs_set_error("the partition must be set before the first step"); return GS_ESTATE; }
+  if (world < 1 || world > 255 || rank < 0 || rank >= world) { gs_set_error("bad rank / world"); return GS_EINVAL; }
+  if (world > 1 && (!tr || !tr->allgather_i64 || !tr->allgather || !tr->alltoallv)) {
+    gs_set_error("a partitioned engine needs a transport with allgather_i64, allgather and alltoallv");
+    return GS_EINVAL;
+  }
+  g->rank = rank;
+  g->world = world;
+  if (tr) g->tr = *tr;
+  return GS_OK;
+}
+
+int gs_partition_range(const gs_engine* g, int32_t* node_begin, int32_t* node_end) {
+  if (!g->graphSet) { gs_set_error("graph not set"); return GS_ESTATE; }
+  const std::vector<int32_t> part = partition_bounds(g->rowptr, g->N, g->world);
+  *node_begin = part[g->rank];
+  *node_end = part[g->rank + 1];
+  return GS_OK;
+}
+
+int gs_read_exchange_stats(gs_engine* g, double* host_ms, int64_t* bytes_in) {
+  *host_ms = g->xMs;
+  *bytes_in = g->xBytes;
   return GS_OK;
 }
 

@@ -49,9 +49,9 @@ template <int MODE>
 __global__ __launch_bounds__(64) void k_score_rows(Dev d, double* __restrict__ out) {
   __shared__ double sT[GS_SG * 65];  // [edge][topic], row stride 65: conflict-free column reads
   const int lane = lane_id();
-  const int64_t e0 = (int64_t)blockIdx.x * GS_SG;
+  const int64_t e0 = d.e0 + (int64_t)blockIdx.x * GS_SG;
   const int64_t e = e0 + lane;
-  const bool in = lane < GS_SG && e < d.E;
+  const bool in = lane < GS_SG && e < d.e1;
   double s0 = 0.0;
   bool need = false;
   if (in) {
@@ -113,8 +113,8 @@ __global__ __launch_bounds__(64) void k_score_rows(Dev d, double* __restrict__ o
 __global__ __launch_bounds__(64) void k_refresh_rows(Dev d, int64_t now) {
   __shared__ double sT[GS_SG * 65];
   const int lane = lane_id();
-  const int64_t e0 = (int64_t)blockIdx.x * GS_SG;
-  const int ng = (int)min((int64_t)GS_SG, d.E - e0);
+  const int64_t e0 = d.e0 + (int64_t)blockIdx.x * GS_SG;
+  const int ng = (int)min((int64_t)GS_SG, d.e1 - e0);
   const int T = d.T;
   const int tl = lane < T ? lane : 0;
   const TopicP& tp = d.tp[tl];
@@ -195,8 +195,8 @@ __global__ __launch_bounds__(64) void k_refresh_rows(Dev d, int64_t now) {
 
 // Folds the pending deliveries of every pair into fmd / mmd.
 __global__ void k_fold_all(Dev d) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= d.E * d.T) return;
+  const int64_t p = d.e0 * d.T + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= d.e1 * d.T) return;
   const uint32_t q = d.dlt[p];
   if (!q) return;
   int64_t e;
@@ -210,8 +210,8 @@ __global__ void k_fold_all(Dev d) {
 
 // Folds the pending deliveries of topic t into fmd / mmd.
 __global__ void k_fold(Dev d, int t) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= d.E) return;
+  const int64_t e = d.e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.e1) return;
   const int64_t i = tix(d, t, e);
   const uint32_t q = d.dlt[i];
   if (!q) return;
@@ -223,8 +223,8 @@ __global__ void k_fold(Dev d, int t) {
 
 // SetTopicScoreParams recap — score.go:215-229
 __global__ void k_recap(Dev d, int t, double fmdCap, double mmdCap) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= d.E) return;
+  const int64_t e = d.e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.e1) return;
   const int64_t i = tix(d, t, e);
   if (d.fmd[i] > fmdCap) d.fmd[i] = fmdCap;
   if (d.mmd[i] > mmdCap) d.mmd[i] = mmdCap;
@@ -234,7 +234,7 @@ __global__ void k_recap(Dev d, int t, double fmdCap, double mmdCap) {
 // GossipSubRouter.Join for every subscribed topic, ascending (gossipsub.go:1011-1060).
 // At hop 0 no fanout exists, so Join takes getPeers(D, !direct && score >= 0).
 __global__ __launch_bounds__(64) void k_join(Dev d, int64_t hop, int64_t now, int cur) {
-  const int u = blockIdx.x;
+  const int u = d.n0 + blockIdx.x;
   const int lane = lane_id();
   const int64_t base = d.rowptr[u];
   const int deg = (int)(d.rowptr[u + 1] - base);
@@ -302,8 +302,8 @@ __global__ __launch_bounds__(64) void k_fanout_pub(Dev d, const int32_t* __restr
 // Topics for which the owner of edge e forwards to col[e] during this hop:
 // relay = messages first delivered here, pub = the owner's own publishes.
 __global__ void k_fwd(Dev d, int cur) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= d.E) return;
+  const int64_t e = d.e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.e1) return;
   const int u = d.esrc[e];
   const uint64_t sv = d.sub[d.col[e]];
   uint64_t relay, pub;
@@ -321,6 +321,9 @@ __global__ void k_fwd(Dev d, int cur) {
       pub = (dir ? sv : 0) | (m & joined) | (d.fanout[e] & ~joined);
     }
   }
+  // partitioned engine: a forwarding set that changed since this parity was
+  // last exchanged must reach the receiver's rank (gs_exchange.h)
+  if (d.xmark && (d.fwdRelay[cur][e] != relay || d.fwdPub[cur][e] != pub)) d.xmark[e] = 1;
   d.fwdRelay[cur][e] = relay;
   d.fwdPub[cur][e] = pub;
 }
@@ -454,7 +457,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   __shared__ int sLn[64];
   __shared__ uint32_t sQ[GS_QCAP];         // sent copies awaiting delivery: slot | sender << 16
   __shared__ uint16_t sRk[64 * GS_MAX_WPL];  // rank of word w in amR, 0xFFFF = outside
-  const int v = blockIdx.x;
+  const int v = d.n0 + blockIdx.x;
   const int lane = lane_id();
   const int prv = cur ^ 1;
   const int W = d.W;
@@ -851,8 +854,8 @@ __global__ void k_oldmask(Dev d, int64_t h) {
 // (node, word) of the words[] list.
 __global__ void k_retire(Dev d, int cur, const int32_t* __restrict__ words, int nwords) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= (int64_t)d.N * nwords) return;
-  const int v = (int)(k / nwords);
+  if (k >= (int64_t)(d.n1 - d.n0) * nwords) return;
+  const int v = d.n0 + (int)(k / nwords);
   const int w = words[k % nwords];
   d.seen[(int64_t)v * d.W + w] &= ~d.pubmask[cur][w];
 }
@@ -866,11 +869,13 @@ __global__ void k_publish(Dev d, int b, int n, int64_t h, int cur, int head) {
   const int slot = d.mSlot[b + i];
   const int src = d.mSrc[b + i];
   const int prevAuthor = d.slotSrc[slot];  // the retired message of this slot
-  if (prevAuthor >= 0) atomicSub(&d.nAuth[prevAuthor], 1);
-  atomicAdd(&d.nAuth[src], 1);
+  // slot metadata is replicated on every rank; the rest belongs to src's rank
+  if (prevAuthor >= d.n0 && prevAuthor < d.n1) atomicSub(&d.nAuth[prevAuthor], 1);
   d.slotSrc[slot] = src;
   d.slotPubHop[slot] = h;
   d.slotMid[slot] = d.mId[b + i];
+  if (src < d.n0 || src >= d.n1) return;
+  atomicAdd(&d.nAuth[src], 1);
   const int w = slot >> 6;
   const unsigned long long bit = 1ull << (slot & 63);
   atomicOr((unsigned long long*)&d.seen[(int64_t)src * d.W + w], bit);
@@ -888,6 +893,7 @@ __global__ void k_publist(Dev d, int b, int n, int cur) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int src = d.mSrc[b + i];
+  if (src < d.n0 || src >= d.n1) return;
   for (int j = 0; j < i; ++j)
     if (d.mSrc[b + j] == src) return;
   uint32_t* L = d.fl[cur] + (int64_t)src * d.FC;

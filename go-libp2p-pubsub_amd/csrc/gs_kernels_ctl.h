@@ -161,7 +161,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
   __shared__ int sSlot[64];
   __shared__ unsigned long long sBase;
   __shared__ uint32_t sHas[64 * 64 / 32];  // step 3: items with a want (<= 64 senders x 64 topics)
-  const int v = blockIdx.x;
+  const int v = d.n0 + blockIdx.x;
   const int lane = lane_id();
   const int prv = cur ^ 1;
   const int W = d.W;
@@ -203,7 +203,6 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
       gl = !d.direct[e] && d.score0[e] < d.graylistThr;  // AcceptFrom on the hop-start memo
     }
   }
-  const unsigned long long glmask = __ballot(gl);
   GS_STAMPB(0);
   // lane t: current mesh size of topic t
   int meshcnt = 0;
@@ -620,7 +619,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
 // A promise is fulfilled iff its message has been delivered since (it was
 // unseen when promised), so "fulfilled" == "seen now".
 __global__ __launch_bounds__(64) void k_hb_pre(Dev d, int64_t now, uint64_t ticks) {
-  const int v = blockIdx.x;
+  const int v = d.n0 + blockIdx.x;
   const int lane = lane_id();
   const int64_t base = d.rowptr[v];
   const int deg = (int)(d.rowptr[v + 1] - base);
@@ -738,7 +737,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
   __shared__ int posOf[64];
   __shared__ double sterm[64];
   __shared__ uint64_t sgw[64 * GS_MAX_WPL];
-  const int v = blockIdx.x;
+  const int v = d.n0 + blockIdx.x;
   const int lane = lane_id();
   const int64_t base = d.rowptr[v];
   const int deg = (int)(d.rowptr[v + 1] - base);
@@ -989,6 +988,7 @@ __global__ void k_read_deliv(Dev d, int slot, int64_t pubhop, int32_t* hop, int3
   // needs GS_FLAG_RECORD_DELIVERIES (age / ffrom kept per slot)
   const int v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= d.N) return;
+  if (v < d.n0 || v >= d.n1) { hop[v] = -1; from[v] = -1; return; }  // another rank's node
   const bool s = (d.seen[(int64_t)v * d.W + (slot >> 6)] >> (slot & 63)) & 1;
   if (!s) { hop[v] = -1; from[v] = -1; return; }
   hop[v] = (int32_t)(pubhop + d.age[(int64_t)v * d.S + slot]);

@@ -12,4 +12,5 @@ from .params import (DefaultGossipSubParams, DefaultPeerGaterParams, GossipSubPa
                      eth2_thresholds, eth2_topic_score_params)
 from .engine import (PRODUCT_LIB, Engine, GossipEngineError, NewFloodSub, NewGossipSub,  # noqa: F401
                      NewRandomSub, WithDevice, WithDirectPeers, WithFloodPublish, WithGossipSubParams,
-                     WithHop, WithMessageWindow, WithPeerScore, WithRecordDeliveries, WithSeed, load)
+                     WithHop, WithMessageWindow, WithPartition, WithPeerScore, WithRecordDeliveries, WithSeed,
+                     load)

@@ -99,6 +99,18 @@ class CountersC(C.Structure):
 
 
 P = C.c_void_p
+
+# gs_transport callbacks (gossip_engine.h)
+ALLGATHER_I64 = C.CFUNCTYPE(C.c_int, P, C.POINTER(i64), i32, C.POINTER(i64))
+ALLGATHER = C.CFUNCTYPE(C.c_int, P, P, P, i64)
+ALLTOALLV = C.CFUNCTYPE(C.c_int, P, P, C.POINTER(i64), P, C.POINTER(i64))
+
+
+class TransportC(C.Structure):
+    _fields_ = [("user", P), ("allgather_i64", ALLGATHER_I64), ("allgather", ALLGATHER),
+                ("alltoallv", ALLTOALLV)]
+
+
 # (name, restype, argtypes) for every function declared in gossip_engine.h
 ABI_FUNCTIONS = [
     ("gs_abi_version", C.c_int, []),
@@ -125,6 +137,9 @@ ABI_FUNCTIONS = [
     ("gs_step", C.c_int, [P, i64]),
     ("gs_sync", C.c_int, [P]),
     ("gs_set_topic_score_params", C.c_int, [P, i32, C.POINTER(TopicScoreParamsC)]),
+    ("gs_set_partition", C.c_int, [P, i32, i32, C.POINTER(TransportC)]),
+    ("gs_partition_range", C.c_int, [P, C.POINTER(i32), C.POINTER(i32)]),
+    ("gs_read_exchange_stats", C.c_int, [P, C.POINTER(f64), C.POINTER(i64)]),
     ("gs_num_edges", i64, [P]),
     ("gs_current_hop", i64, [P]),
     ("gs_read_counters", C.c_int, [P, C.POINTER(CountersC)]),

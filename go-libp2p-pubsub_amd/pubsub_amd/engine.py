@@ -88,6 +88,13 @@ def WithDevice(dev):
     return ("device", int(dev))
 
 
+def WithPartition(rank, world, transport):
+    """Simulate only this rank's node range; exchange RPCs with the other
+    ranks through `transport` (a pubsub_amd.transport.TorchTransport) once per
+    hop.  Every rank makes the same calls (graph, subscriptions, publishes)."""
+    return ("partition", (int(rank), int(world), transport))
+
+
 class Engine:
     """One batched simulation of N routers (see module docstring)."""
 
@@ -138,6 +145,14 @@ class Engine:
         direct = np.ascontiguousarray(direct, dtype=np.uint8) if direct is not None else None
         _check(self.lib, self.lib.gs_set_graph(h, _ptr(self.rowptr, C.c_int64), _ptr(self.col, C.c_int32),
                                                _ptr(ob, C.c_uint8), _ptr(direct, C.c_uint8)))
+        self.rank, self.world, self.transport = opts.get("partition", (0, 1, None))
+        if self.world > 1:
+            _check(self.lib, self.lib.gs_set_partition(h, self.rank, self.world, C.byref(self.transport.c)))
+        b, e = C.c_int32(), C.c_int32()
+        _check(self.lib, self.lib.gs_partition_range(h, C.byref(b), C.byref(e)))
+        self.node_range = (b.value, e.value)
+        self.n_published = 0  # messages scheduled by publish() (all ranks)
+        self.edge_range = (int(self.rowptr[b.value]), int(self.rowptr[e.value]))
         subs = np.ascontiguousarray(subscriptions, dtype=np.uint64)
         _check(self.lib, self.lib.gs_set_subscriptions(h, _ptr(subs, C.c_uint64)))
         app = np.ascontiguousarray(app_score, dtype=np.float64) if app_score is not None else None
@@ -164,7 +179,14 @@ class Engine:
         ids = np.empty(len(src), dtype=np.int64)
         _check(self.lib, self.lib.gs_publish(self.h, len(src), _ptr(src, C.c_int32), _ptr(topic, C.c_int32),
                                              _ptr(hop, C.c_int64), _ptr(ids, C.c_int64)))
+        self.n_published += len(src)
         return ids
+
+    def exchange_stats(self):
+        """(host ms spent in the transport, bytes received from other ranks)."""
+        ms, nb = C.c_double(), C.c_int64()
+        _check(self.lib, self.lib.gs_read_exchange_stats(self.h, C.byref(ms), C.byref(nb)))
+        return ms.value, nb.value
 
     def step(self, hops=1):
         _check(self.lib, self.lib.gs_step(self.h, int(hops)))

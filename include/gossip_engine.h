@@ -238,7 +238,43 @@ int gs_sync(gs_engine* eng);
  * peerScore.SetTopicScoreParams, score.go:192-232, including the recap). */
 int gs_set_topic_score_params(gs_engine* eng, int32_t topic, const gs_topic_score_params* p);
 
+/* ---- partitioned engines: one rank per GPU ------------ */
+/* The reference runs one router per host and its only cross-host traffic is
+ * RPCs (handleIncomingRPC / sendRPC, pubsub.go:902-970, gossipsub.go:1092-
+ * 1156).  A partitioned engine owns a contiguous node range (balanced by
+ * edges, gs_partition_range) and simulates only those routers; at the end of
+ * every hop the RPCs its nodes sent to other ranks' nodes are exchanged
+ * through the host transport below (RCCL all-gather / all-to-all over xGMI in
+ * the Python host; any transport with the same semantics works).  Every rank
+ * must make the same sequence of set_graph / set_subscriptions / publish /
+ * step calls.  Callbacks return 0 on success and are called from gs_step on
+ * the calling thread, with no device work of the engine pending. */
+typedef struct gs_transport {
+  void* user;
+  /* all[r*n + i] = rank r's mine[i] (host memory, n int64 per rank). */
+  int (*allgather_i64)(void* user, const int64_t* mine, int32_t n, int64_t* all);
+  /* Device buffers: recv[r*bytes .. (r+1)*bytes) = rank r's send[0..bytes). */
+  int (*allgather)(void* user, const void* send, void* recv, int64_t bytes);
+  /* Device buffers: send holds the blocks for ranks 0..world-1 back to back
+   * (send_bytes[r] each); recv receives rank r's block for this rank at the
+   * prefix offset of recv_bytes[0..r). */
+  int (*alltoallv)(void* user, const void* send, const int64_t* send_bytes, void* recv,
+                   const int64_t* recv_bytes);
+} gs_transport;
+/* Before the first step.  world == 1 (the default) simulates the whole graph;
+ * the transport is copied (it may be NULL then).  The oracle supports
+ * world == 1 only. */
+int gs_set_partition(gs_engine* eng, int32_t rank, int32_t world, const gs_transport* tr);
+/* Nodes [node_begin, node_end) owned by this rank (after gs_set_graph). */
+int gs_partition_range(const gs_engine* eng, int32_t* node_begin, int32_t* node_end);
+/* Host time spent in the transport and bytes received from other ranks. */
+int gs_read_exchange_stats(gs_engine* eng, double* host_ms, int64_t* bytes_in);
+
 /* ---- readbacks (host arrays sized by the caller) ----------------------- */
+/* A partitioned engine reports its own nodes / edges only: counters count its
+ * nodes' events, per-edge arrays are valid on its edges [rowptr[node_begin],
+ * rowptr[node_end]) and zero elsewhere, per-node arrays on its nodes (-1
+ * elsewhere). */
 int64_t gs_num_edges(const gs_engine* eng);
 int64_t gs_current_hop(const gs_engine* eng);
 int gs_read_counters(gs_engine* eng, gs_counters* out);

@@ -1035,4 +1035,20 @@ int gs_read_kernel_stats(gs_engine*, double* total_ms, int64_t* launches) {
   return GS_OK;
 }
 
+// The oracle simulates the whole graph: world == 1 only (gossip_engine.h).
+int gs_set_partition(gs_engine*, int32_t rank, int32_t world, const gs_transport*) {
+  if (world == 1 && rank == 0) return GS_OK;
+  return GS_EUNSUPPORTED;
+}
+int gs_partition_range(const gs_engine* g, int32_t* node_begin, int32_t* node_end) {
+  *node_begin = 0;
+  *node_end = g->sim.N;
+  return GS_OK;
+}
+int gs_read_exchange_stats(gs_engine*, double* host_ms, int64_t* bytes_in) {
+  *host_ms = 0;
+  *bytes_in = 0;
+  return GS_OK;
+}
+
 }  // extern "C"

@@ -22,40 +22,40 @@ def _publish_schedule(n, topics, count, start, every, seed, srcs=None):
     return src.astype(np.int32), top.astype(np.int32), np.asarray(hops, dtype=np.int64)
 
 
-def floodsub_dense(lib, seed=1):
+def floodsub_dense(lib, seed=1, extra=()):
     """TestFloodsubDense-like: 20 hosts, denseConnect, 100 messages."""
     n = 20
     g = graphs.dense_connect(n, seed)
     e = NewFloodSub(n, 1, g, graphs.all_subscribed(n, 1), WithRecordDeliveries(), WithSeed(seed),
-                    WithMessageWindow(128), lib=lib)
+                    WithMessageWindow(128), *extra, lib=lib)
     src, top, hops = _publish_schedule(n, 1, 100, 1, 2, seed)
     e.publish(src, top, hops)
     return e, int(hops[-1]) + 20
 
 
-def randomsub(lib, size, n=200, k=16, seed=2, msgs=60):
+def randomsub(lib, size, n=200, k=16, seed=2, msgs=60, extra=()):
     g = graphs.random_regular(n, k, seed)
     e = NewRandomSub(n, 1, g, graphs.all_subscribed(n, 1), size, WithRecordDeliveries(), WithSeed(seed),
-                     WithMessageWindow(128), lib=lib)
+                     WithMessageWindow(128), *extra, lib=lib)
     src, top, hops = _publish_schedule(n, 1, msgs, 0, 1, seed)
     e.publish(src, top, hops)
     return e, int(hops[-1]) + 20
 
 
-def gossipsub_dense(lib, seed=1, msgs=100):
+def gossipsub_dense(lib, seed=1, msgs=100, extra=()):
     """TestDenseGossipsub (gossipsub_test.go:84-123): 20 hosts, denseConnect,
     2 s of heartbeats, then 100 messages from random owners."""
     n = 20
     g = graphs.dense_connect(n, seed)
     e = NewGossipSub(n, 1, g, graphs.all_subscribed(n, 1), WithRecordDeliveries(), WithSeed(seed),
-                     WithHop(HOP), WithMessageWindow(256), lib=lib)
+                     WithHop(HOP), WithMessageWindow(256), *extra, lib=lib)
     src, top, hops = _publish_schedule(n, 1, msgs, 20, 1, seed)
     e.publish(src, top, hops)
     return e, int(hops[-1]) + 40
 
 
 def gossipsub_scored(lib, n=300, k=20, topics=1, seed=3, msgs=300, hb=12, flood=False, sub_frac=1.0,
-                     app_neg_frac=0.0, ip_groups=0, params=None, window=1024):
+                     app_neg_frac=0.0, ip_groups=0, params=None, window=1024, extra=()):
     """gossipsub v1.1 with Eth2-derived scoring over a random regular graph."""
     rng = np.random.default_rng(seed)
     g = graphs.random_regular(n, k, seed)
@@ -79,7 +79,7 @@ def gossipsub_scored(lib, n=300, k=20, topics=1, seed=3, msgs=300, hb=12, flood=
         opts.append(WithGossipSubParams(params))
     if flood:
         opts.append(WithFloodPublish(True))
-    e = NewGossipSub(n, topics, g, subs, *opts, app_score=app, ipv4=ipv4, lib=lib)
+    e = NewGossipSub(n, topics, g, subs, *opts, *extra, app_score=app, ipv4=ipv4, lib=lib)
     rng2 = np.random.default_rng(seed + 100)
     src = rng2.integers(0, n, msgs).astype(np.int32)
     top = rng2.integers(0, topics, msgs).astype(np.int32)
@@ -89,15 +89,15 @@ def gossipsub_scored(lib, n=300, k=20, topics=1, seed=3, msgs=300, hb=12, flood=
 
 
 SCENARIOS = {
-    "floodsub_dense": lambda lib: floodsub_dense(lib),
-    "randomsub_100": lambda lib: randomsub(lib, 100),
-    "randomsub_N": lambda lib: randomsub(lib, 200),
-    "gossipsub_dense": lambda lib: gossipsub_dense(lib),
-    "gossipsub_scored": lambda lib: gossipsub_scored(lib),
-    "gossipsub_flood_publish": lambda lib: gossipsub_scored(lib, n=200, flood=True, seed=5),
-    "gossipsub_multitopic": lambda lib: gossipsub_scored(lib, n=200, topics=3, sub_frac=0.7, seed=7, msgs=240),
-    "gossipsub_negative_app": lambda lib: gossipsub_scored(lib, n=200, app_neg_frac=0.2, ip_groups=40, seed=9),
-    "gossipsub_dense_dhi": lambda lib: gossipsub_scored(lib, n=120, k=40, seed=11, hb=20, msgs=200),
+    "floodsub_dense": lambda lib, x=(): floodsub_dense(lib, extra=x),
+    "randomsub_100": lambda lib, x=(): randomsub(lib, 100, extra=x),
+    "randomsub_N": lambda lib, x=(): randomsub(lib, 200, extra=x),
+    "gossipsub_dense": lambda lib, x=(): gossipsub_dense(lib, extra=x),
+    "gossipsub_scored": lambda lib, x=(): gossipsub_scored(lib, extra=x),
+    "gossipsub_flood_publish": lambda lib, x=(): gossipsub_scored(lib, n=200, flood=True, seed=5, extra=x),
+    "gossipsub_multitopic": lambda lib, x=(): gossipsub_scored(lib, n=200, topics=3, sub_frac=0.7, seed=7, msgs=240, extra=x),
+    "gossipsub_negative_app": lambda lib, x=(): gossipsub_scored(lib, n=200, app_neg_frac=0.2, ip_groups=40, seed=9, extra=x),
+    "gossipsub_dense_dhi": lambda lib, x=(): gossipsub_scored(lib, n=120, k=40, seed=11, hb=20, msgs=200, extra=x),
 }
 
 
@@ -109,11 +109,30 @@ def snapshot(e, msg_ids):
     return out
 
 
-def run(lib, name, extra_hops=0):
-    e, hops = SCENARIOS[name](lib)
+def run(lib, name, extra_hops=0, extra=()):
+    e, hops = SCENARIOS[name](lib, extra)
     e.step(hops + extra_hops)
-    ids = range(int(e.counters()["published"]))
-    return snapshot(e, ids)
+    snap = snapshot(e, range(e.n_published))
+    snap["node_range"], snap["edge_range"] = e.node_range, e.edge_range
+    return snap
+
+
+def restrict(s, T):
+    """The part of a snapshot a partitioned rank owns (its nodes and their
+    edges); counters are left out (they are per rank, compared summed)."""
+    n0, n1 = s["node_range"]
+    e0, e1 = s["edge_range"]
+    out = {}
+    for k, v in s.items():
+        if k in ("counters", "node_range", "edge_range"):
+            continue
+        if k == "deliv":
+            out[k] = [(h[n0:n1], f[n0:n1]) for h, f in v]
+        elif k in ("backoff",) or k.startswith("ts_"):
+            out[k] = np.asarray(v).reshape(T, -1)[:, e0:e1]
+        else:
+            out[k] = np.asarray(v)[e0:e1]
+    return out
 
 
 def _bits(a):
@@ -125,6 +144,8 @@ def compare(a, b):
     """Returns a list of human-readable mismatches (empty = bit-exact)."""
     bad = []
     for k in a:
+        if k in ("node_range", "edge_range"):
+            continue
         if k == "counters":
             if a[k] != b[k]:
                 bad.append(f"counters: {a[k]} != {b[k]}")
