@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/gossip_engine.h"
 #include "../../include/gs_rng.h"
 
 #define GS_WAVE 64
@@ -28,7 +29,7 @@ enum {
 // device error codes (first one wins)
 enum {
   E_NONE = 0, E_POOL = 1, E_PROMISES = 2, E_PEERTX = 3, E_LATE = 4, E_TRUNCATE = 5, E_DOUBLE = 6,
-  E_FCAP = 7, E_DELTA = 8
+  E_FCAP = 7, E_DELTA = 8, E_TRACE = 9
 };
 
 struct TopicP {  // TopicScoreParams (score_params.go:98-148) + scored flag
@@ -55,6 +56,11 @@ struct Dev {
   int32_t n0, n1, rank, world;
   int64_t e0, e1;
   uint8_t* xmark;   // [E] forwarding set changed since its parity was exchanged (world > 1)
+  // EventTracer of the hosts with traced[u] != 0 (gs_set_trace); nullptr = off
+  const uint8_t* traced;
+  gs_trace_event* trace;
+  unsigned long long* traceN;
+  int64_t traceCap;
   const uint8_t* nodeRank;  // [N] owning rank of every node (world > 1)
   uint32_t seed;
   int64_t hop_ns;
@@ -151,6 +157,29 @@ struct Dev {
 };
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// ---- trace events (gossip_engine.h gs_trace_event) -----------------------
+#define GS_TRACE_COPY 100  // internal: one delivered copy; the host turns every
+                           // copy but the delivering one into DUPLICATE_MESSAGE
+__device__ __forceinline__ bool is_traced(const Dev& d, int v) { return d.traced != nullptr && d.traced[v] != 0; }
+__device__ __forceinline__ void set_err(const Dev& d, int code);
+__device__ __forceinline__ void trace_emit(const Dev& d, int64_t hop, int type, int node, int peer, int topic,
+                                           int64_t msg, int phase) {
+  const unsigned long long k = atomicAdd(d.traceN, 1ull);
+  if ((int64_t)k >= d.traceCap) {
+    set_err(d, E_TRACE);
+    return;
+  }
+  gs_trace_event e;
+  e.hop = hop;
+  e.msg = msg;
+  e.type = type;
+  e.node = node;
+  e.peer = peer;
+  e.topic = (int16_t)topic;
+  e.phase = (int16_t)phase;
+  d.trace[k] = e;
+}
 
 // Index of (edge e, topic t) in the per-(edge, topic) arrays: one row of T
 // topics per edge, so one edge's state is contiguous (a wave with lane =

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <tuple>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -17,6 +18,7 @@
 #include <vector>
 
 #include "../../include/gossip_engine.h"
+#include "../../include/gs_trace.h"
 #include "gs_host.h"
 #include "gs_kernels.h"
 #include "gs_kernels_ctl.h"
@@ -95,6 +97,12 @@ struct gs_engine {
   double xMs = 0.0;                    // host wall time spent in exchanges
   int64_t xBytes = 0;                  // bytes received by this rank
   int exchange(int cur, bool hb);
+  // trace events (gs_set_trace / gs_trace_read)
+  std::vector<uint8_t> traceMask;
+  int64_t traceCap = 0;
+  std::vector<gs_trace_event> tracePending;  // converted, canonical order from traceOut
+  size_t traceOut = 0;
+  int drainTrace();
   int64_t x_poolEnd() const { return (int64_t)(rank + 1) * poolSeg; }
   int growDev(uint8_t*& p, size_t& cap, size_t need, size_t keep = 0);
   // kernel timing: (kernel id, start event, end event) pending until a sync
@@ -419,6 +427,30 @@ int gs_engine::start() {
   dHopOut = dalloc<int32_t>(N); dFromOut = dalloc<int32_t>(N); chk(dHopOut); chk(dFromOut);
   x.xmark = nullptr;
   x.nodeRank = nullptr;
+  x.traced = nullptr;
+  x.trace = nullptr;
+  x.traceN = nullptr;
+  x.traceCap = 0;
+  if (!traceMask.empty()) {
+    uint8_t* tm = dalloc<uint8_t>(N); chk(tm);
+    x.trace = dalloc<gs_trace_event>((size_t)traceCap); chk(x.trace);
+    x.traceN = dalloc<unsigned long long>(1); chk(x.traceN);
+    x.traceCap = traceCap;
+    if (ok) {
+      HIPCHECK(hipMemcpyAsync(tm, traceMask.data(), N, hipMemcpyHostToDevice, stream));
+      HIPCHECK(hipStreamSynchronize(stream));
+    }
+    x.traced = tm;
+    // AddPeer (gossipsub.go:507, floodsub.go:45) and Join (gossipsub.go:1018,
+    // floodsub.go:103) of the traced hosts at time 0, recorded on the host
+    for (int u = n0; u < n1; ++u) {
+      if (!traceMask[u]) continue;
+      for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e)
+        tracePending.push_back(gs_trace_event{0, -1, GS_TRACE_ADD_PEER, u, col[e], -1, 0});
+      for (int t = 0; t < T; ++t)
+        if ((sub[u] >> t) & 1) tracePending.push_back(gs_trace_event{0, -1, GS_TRACE_JOIN, u, -1, (int16_t)t, 0});
+    }
+  }
   if (world > 1) {
     x.xmark = dalloc<uint8_t>(E); chk(x.xmark);
     uint8_t* nr = dalloc<uint8_t>(N); chk(nr);
@@ -642,6 +674,9 @@ int gs_engine::checkDeviceError() {
     case E_DELTA:
       gs_set_error("pending delivery count of one (edge, topic) overflowed 65535 between two score refreshes");
       return GS_ECAPACITY;
+    case E_TRACE:
+      gs_set_error("more trace events between two gs_trace_read calls than the capacity given to gs_set_trace");
+      return GS_ECAPACITY;
     case E_DOUBLE:
       gs_set_error("a peer sent the same message twice in one hop (outside the canonical model)");
       return GS_EUNSUPPORTED;
@@ -793,6 +828,44 @@ int gs_engine::exchange(int cur, bool hb) {
     k_x_unpack<<<nblk(n, 256), 256, 0, stream>>>(d, cur, (const XRec*)xRecvE, n);
   }
   HIPCHECK(hipGetLastError());
+  return GS_OK;
+}
+
+// Moves the device's trace records to tracePending in canonical order.  The
+// kernels record every delivered copy (GS_TRACE_COPY); the copy from the
+// first deliverer of a fresh message is its DeliverMessage, every other copy
+// a DuplicateMessage (pubsub.go:1010-1013).
+int gs_engine::drainTrace() {
+  if (!started || !d.traceN) return GS_OK;
+  unsigned long long cnt = 0;
+  HIPCHECK(hipStreamSynchronize(stream));
+  HIPCHECK(hipMemcpy(&cnt, d.traceN, 8, hipMemcpyDeviceToHost));
+  const int64_t k = std::min<int64_t>((int64_t)cnt, traceCap);
+  std::vector<gs_trace_event> ev((size_t)k);
+  if (k) HIPCHECK(hipMemcpy(ev.data(), d.trace, (size_t)k * sizeof(gs_trace_event), hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemset(d.traceN, 0, 8));
+  struct Key {
+    int64_t hop, msg;
+    int32_t node, peer;
+    bool operator<(const Key& o) const {
+      return std::tie(hop, msg, node, peer) < std::tie(o.hop, o.msg, o.node, o.peer);
+    }
+  };
+  std::vector<Key> delivered;
+  for (const auto& e : ev)
+    if (e.type == GS_TRACE_DELIVER_MESSAGE && e.phase == 2) delivered.push_back(Key{e.hop, e.msg, e.node, e.peer});
+  std::sort(delivered.begin(), delivered.end());
+  std::vector<gs_trace_event> keep(tracePending.begin() + traceOut, tracePending.end());
+  for (auto e : ev) {
+    if (e.type == GS_TRACE_COPY) {
+      if (std::binary_search(delivered.begin(), delivered.end(), Key{e.hop, e.msg, e.node, e.peer})) continue;
+      e.type = GS_TRACE_DUPLICATE_MESSAGE;
+    }
+    keep.push_back(e);
+  }
+  std::stable_sort(keep.begin(), keep.end(), gs_trace_less);
+  tracePending.swap(keep);
+  traceOut = 0;
   return GS_OK;
 }
 
@@ -1065,6 +1138,32 @@ int gs_partition_range(const gs_engine* g, int32_t* node_begin, int32_t* node_en
   const std::vector<int32_t> part = partition_bounds(g->rowptr, g->N, g->world);
   *node_begin = part[g->rank];
   *node_end = part[g->rank + 1];
+  return GS_OK;
+}
+
+int gs_set_trace(gs_engine* g, const uint8_t* node_mask, int64_t capacity) {
+  if (g->started) { gs_set_error("tracing must be set before the first step"); return GS_ESTATE; }
+  if (node_mask && capacity <= 0) { gs_set_error("trace capacity must be positive"); return GS_EINVAL; }
+  if (node_mask) g->traceMask.assign(node_mask, node_mask + g->N);
+  else g->traceMask.clear();
+  g->traceCap = capacity;
+  return GS_OK;
+}
+
+int gs_trace_read(gs_engine* g, gs_trace_event* out, int64_t cap, int64_t* n) {
+  *n = 0;
+  if (g->traceOut == 0 || g->traceOut == g->tracePending.size()) {
+    int rc = g->drainTrace();
+    if (rc) return rc;
+  }
+  const int64_t k = std::min<int64_t>(cap, (int64_t)(g->tracePending.size() - g->traceOut));
+  std::copy(g->tracePending.begin() + g->traceOut, g->tracePending.begin() + g->traceOut + k, out);
+  g->traceOut += (size_t)k;
+  if (g->traceOut == g->tracePending.size()) {
+    g->tracePending.clear();
+    g->traceOut = 0;
+  }
+  *n = k;
   return GS_OK;
 }
 

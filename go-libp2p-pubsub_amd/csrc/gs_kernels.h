@@ -255,6 +255,7 @@ __global__ __launch_bounds__(64) void k_join(Dev d, int64_t hop, int64_t now, in
       meshl |= 1ull << t;
       gj |= 1ull << t;
       stats_graft(d, e, t, now);
+      if (is_traced(d, u)) trace_emit(d, hop, GS_TRACE_GRAFT, u, v, t, -1, 0);  // gossipsub.go:1057
     }
   }
   if (valid) {
@@ -521,9 +522,11 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   int nSent = 0, nGray = 0;
   long long nCopies = 0;  // delivered copies (non-graylisted)
   // One delivered copy of `slot` from sender i (sent, not graylisted).
+  const bool trv = is_traced(d, v);
   auto deliver = [&](int i, int slot) {
     const int w = slot >> 6;
     const int t = (int)__umulhi((unsigned)slot, d.stMagic);
+    if (trv) trace_emit(d, h, GS_TRACE_COPY, v, d.col[base + i], t, d.slotMid[slot], 2);
 #ifndef GS_EXP_NOADD
     atomicAdd(&scnt[i * T + t], 1u);
     ++nCopies;
@@ -802,6 +805,9 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
         y &= y - 1;
         const int slot = w * 64 + b;
         const int ff = sFirst[ixw[j] + b];
+        if (trv)  // pubsub.go:1057, ReceivedFrom = the first deliverer
+          trace_emit(d, h, GS_TRACE_DELIVER_MESSAGE, v, d.col[base + ff], (int)__umulhi((unsigned)slot, d.stMagic),
+                     d.slotMid[slot], 2);
         if (rank < FC) Lv[rank] = (uint32_t)slot | ((uint32_t)ff << 16);
         else set_err(d, E_FCAP);
         ++rank;
@@ -876,6 +882,10 @@ __global__ void k_publish(Dev d, int b, int n, int64_t h, int cur, int head) {
   d.slotMid[slot] = d.mId[b + i];
   if (src < d.n0 || src >= d.n1) return;
   atomicAdd(&d.nAuth[src], 1);
+  if (is_traced(d, src)) {  // validation.go:217, then pubsub.go:1057 with ReceivedFrom = self
+    trace_emit(d, h, GS_TRACE_PUBLISH_MESSAGE, src, -1, d.mTopic[b + i], d.mId[b + i], 1);
+    trace_emit(d, h, GS_TRACE_DELIVER_MESSAGE, src, src, d.mTopic[b + i], d.mId[b + i], 1);
+  }
   const int w = slot >> 6;
   const unsigned long long bit = 1ull << (slot & 63);
   atomicOr((unsigned long long*)&d.seen[(int64_t)src * d.W + w], bit);

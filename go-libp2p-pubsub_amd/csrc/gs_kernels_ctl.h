@@ -38,6 +38,7 @@ __device__ __forceinline__ bool graft_one(const Dev& d, int64_t e, int v, int t,
   stats_graft(d, e, t, now);
   dirtyUp = true;  // a graft never lowers the score (P1 = 0 at meshTime 0, P3 switched off)
   meshE |= 1ull << t;
+  if (lane_id() == 0 && is_traced(d, v)) trace_emit(d, now / d.hop_ns, GS_TRACE_GRAFT, v, d.col[e], t, -1, 3);
   if (lane_id() == t) meshcnt_lane++;
   return false;
 }
@@ -50,6 +51,8 @@ __device__ __forceinline__ void prune_topics(const Dev& d, int64_t e, int v, uin
     const int t = __ffsll((long long)topics) - 1;
     topics &= topics - 1;
     if (!((d.sub[v] >> t) & 1)) continue;
+    if (lane_id() == 0 && is_traced(d, v))  // gossipsub.go:817, whether or not p is in the mesh
+      trace_emit(d, now / d.hop_ns, GS_TRACE_PRUNE, v, d.col[e], t, -1, 3);
     stats_prune(d, e, t);
     if (d.scoring) dirty = true;
     if ((meshE >> t) & 1) {
@@ -936,6 +939,10 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
     ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, f, dir, Slive, dirty, dirtyUp, base, sterm, sgw);
   }
   // sendGraftPrune + flush: one heartbeat RPC per peer with any control
+  if (valid && is_traced(d, v)) {  // prunePeer / graftPeer, gossipsub.go:1334, 1343
+    for (uint64_t m = toprune; m; m &= m - 1) trace_emit(d, hop, GS_TRACE_PRUNE, v, vcol, __ffsll((long long)m) - 1, -1, 4);
+    for (uint64_t m = tograft; m; m &= m - 1) trace_emit(d, hop, GS_TRACE_GRAFT, v, vcol, __ffsll((long long)m) - 1, -1, 4);
+  }
   if (valid) {
     d.mesh[e] = meshl;
     d.fanout[e] = fanl;

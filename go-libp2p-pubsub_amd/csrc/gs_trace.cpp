@@ -1,0 +1,160 @@
+// gs_trace.cpp — encodes gs_trace_event records as the reference's event
+// tracers write pb.TraceEvent (pb/trace.proto, generated code pb/trace.pb.go):
+//   GS_TRACE_FORMAT_PB    PBTracer (tracer.go:141-181): each event marshalled
+//                         (gogo: fields in ascending field-number order, a
+//                         sub-message as tag + length + body) and written
+//                         through a uvarint-delimited protoio writer;
+//   GS_TRACE_FORMAT_JSON  JSONTracer (tracer.go:79-139): encoding/json of the
+//                         Go struct, one object + '\n' per event: struct field
+//                         order, omitempty, []byte as padded standard base64,
+//                         the enum Type as its number.
+// Host code only; no device involvement.
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gossip_engine.h"
+#include "gs_host.h"
+
+namespace {
+
+std::string peer_bytes(int32_t p) { return "n" + std::to_string(p); }
+std::string msg_bytes(int64_t m) { return std::to_string(m); }
+
+// ---- protobuf wire format
+void put_varint(std::string& o, uint64_t v) {
+  while (v >= 0x80) {
+    o.push_back((char)(v | 0x80));
+    v >>= 7;
+  }
+  o.push_back((char)v);
+}
+void put_bytes(std::string& o, int field, const std::string& b) {
+  put_varint(o, ((uint64_t)field << 3) | 2);
+  put_varint(o, b.size());
+  o += b;
+}
+void put_int(std::string& o, int field, int64_t v) {
+  put_varint(o, ((uint64_t)field << 3) | 0);
+  put_varint(o, (uint64_t)v);  // int64 varint: two's complement for negatives
+}
+
+// ---- JSON
+std::string b64(const std::string& s) {
+  static const char* A = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  std::string o;
+  size_t i = 0;
+  for (; i + 2 < s.size(); i += 3) {
+    const uint32_t x = ((uint8_t)s[i] << 16) | ((uint8_t)s[i + 1] << 8) | (uint8_t)s[i + 2];
+    o += A[x >> 18]; o += A[(x >> 12) & 63]; o += A[(x >> 6) & 63]; o += A[x & 63];
+  }
+  if (i + 1 == s.size()) {
+    const uint32_t x = (uint8_t)s[i] << 16;
+    o += A[x >> 18]; o += A[(x >> 12) & 63]; o += "==";
+  } else if (i + 2 == s.size()) {
+    const uint32_t x = ((uint8_t)s[i] << 16) | ((uint8_t)s[i + 1] << 8);
+    o += A[x >> 18]; o += A[(x >> 12) & 63]; o += A[(x >> 6) & 63]; o += '=';
+  }
+  return o;
+}
+std::string jstr(const std::string& s) {  // encoding/json string escaping (HTML-safe)
+  std::string o = "\"";
+  for (unsigned char c : s) {
+    if (c == '"' || c == '\\') { o += '\\'; o += (char)c; }
+    else if (c < 0x20 || c == '<' || c == '>' || c == '&') {
+      char buf[8];
+      std::snprintf(buf, sizeof buf, "\\u%04x", c);
+      o += buf;
+    } else o += (char)c;
+  }
+  return o + "\"";
+}
+
+struct Field {  // one field of a sub-message: bytes (base64 in JSON) or string
+  int num;
+  const char* name;
+  std::string val;
+  bool isBytes;
+};
+
+// pb.TraceEvent field number / JSON name of the sub-message of each type
+const int kSubField[13] = {4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+const char* kSubName[13] = {"publishMessage", "rejectMessage", "duplicateMessage", "deliverMessage", "addPeer",
+                            "removePeer", "recvRPC", "sendRPC", "dropRPC", "join", "leave", "graft", "prune"};
+
+std::vector<Field> sub_fields(const gs_trace_event& e, const std::string& topic, const char* proto) {
+  switch (e.type) {
+    case GS_TRACE_PUBLISH_MESSAGE:  // trace.proto PublishMessage {messageID=1, topic=2}
+      return {{1, "messageID", msg_bytes(e.msg), true}, {2, "topic", topic, false}};
+    case GS_TRACE_DUPLICATE_MESSAGE:  // {messageID=1, receivedFrom=2, topic=3}
+      return {{1, "messageID", msg_bytes(e.msg), true}, {2, "receivedFrom", peer_bytes(e.peer), true},
+              {3, "topic", topic, false}};
+    case GS_TRACE_DELIVER_MESSAGE:  // {messageID=1, topic=2, receivedFrom=3}
+      return {{1, "messageID", msg_bytes(e.msg), true}, {2, "topic", topic, false},
+              {3, "receivedFrom", peer_bytes(e.peer), true}};
+    case GS_TRACE_ADD_PEER:  // {peerID=1, proto=2}
+      return {{1, "peerID", peer_bytes(e.peer), true}, {2, "proto", proto ? proto : "", false}};
+    case GS_TRACE_JOIN:  // {topic=1}
+      return {{1, "topic", topic, false}};
+    case GS_TRACE_GRAFT:
+    case GS_TRACE_PRUNE:  // {peerID=1, topic=2}
+      return {{1, "peerID", peer_bytes(e.peer), true}, {2, "topic", topic, false}};
+    default:
+      return {};
+  }
+}
+
+}  // namespace
+
+extern "C" int gs_trace_encode(const gs_trace_event* ev, int64_t n, int32_t format, int64_t hop_ns,
+                               const char* const* topic_names, const char* proto, uint8_t* buf, int64_t cap,
+                               int64_t* written) {
+  if (!written || n < 0 || (n > 0 && !ev) || (format != GS_TRACE_FORMAT_PB && format != GS_TRACE_FORMAT_JSON)) {
+    gs_set_error("gs_trace_encode: bad arguments");
+    return GS_EINVAL;
+  }
+  std::string out;
+  for (int64_t i = 0; i < n; ++i) {
+    const gs_trace_event& e = ev[i];
+    if (e.type < 0 || e.type > GS_TRACE_PRUNE) {
+      gs_set_error("gs_trace_encode: unknown event type");
+      return GS_EINVAL;
+    }
+    const std::string topic =
+        e.topic < 0 ? std::string() : (topic_names ? std::string(topic_names[e.topic]) : std::to_string(e.topic));
+    const std::string peer = peer_bytes(e.node);
+    const int64_t ts = e.hop * hop_ns;
+    const std::vector<Field> fs = sub_fields(e, topic, proto);
+    if (format == GS_TRACE_FORMAT_PB) {
+      std::string body;
+      for (const Field& f : fs) put_bytes(body, f.num, f.val);  // trace.go sets every field
+      std::string m;
+      put_int(m, 1, e.type);
+      put_bytes(m, 2, peer);
+      put_int(m, 3, ts);
+      put_bytes(m, kSubField[e.type], body);
+      put_varint(out, m.size());
+      out += m;
+    } else {
+      std::string j = "{\"type\":" + std::to_string(e.type) + ",\"peerID\":\"" + b64(peer) +
+                      "\",\"timestamp\":" + std::to_string(ts) + ",\"" + kSubName[e.type] + "\":{";
+      bool first = true;
+      for (const Field& f : fs) {
+        if (f.isBytes && f.val.empty()) continue;  // omitempty: nil/empty []byte (a *string is always set)
+        if (!first) j += ",";
+        first = false;
+        j += "\"" + std::string(f.name) + "\":" + (f.isBytes ? "\"" + b64(f.val) + "\"" : jstr(f.val));
+      }
+      j += "}}\n";
+      out += j;
+    }
+  }
+  *written = (int64_t)out.size();
+  if ((int64_t)out.size() > cap) {
+    gs_set_error("gs_trace_encode: buffer too small (see *written)");
+    return GS_ECAPACITY;
+  }
+  if (!out.empty()) std::memcpy(buf, out.data(), out.size());
+  return GS_OK;
+}

@@ -11,6 +11,6 @@ from .params import (DefaultGossipSubParams, DefaultPeerGaterParams, GossipSubPa
                      ScoreParameterDecayWithBase, Second, TopicScoreParams, eth2_peer_score_params,
                      eth2_thresholds, eth2_topic_score_params)
 from .engine import (PRODUCT_LIB, Engine, GossipEngineError, NewFloodSub, NewGossipSub,  # noqa: F401
-                     NewRandomSub, WithDevice, WithDirectPeers, WithFloodPublish, WithGossipSubParams,
+                     NewRandomSub, PROTOCOLS, WithDevice, WithEventTracer, encode_trace, WithDirectPeers, WithFloodPublish, WithGossipSubParams,
                      WithHop, WithMessageWindow, WithPartition, WithPeerScore, WithRecordDeliveries, WithSeed,
                      load)

@@ -5,6 +5,8 @@ whichever library exports the ABI: the product (libgossip_engine.so, HIP) or,
 in tests only, the CPU oracle (oracle/_build/libgossip_oracle.so).
 """
 import ctypes as C
+
+import numpy as np
 import os
 
 GS_OK = 0
@@ -86,6 +88,14 @@ class ConfigC(C.Structure):
     ]
 
 
+# gs_trace_event (gossip_engine.h): 32 bytes
+TRACE_EVENT_DTYPE = np.dtype([("hop", "<i8"), ("msg", "<i8"), ("type", "<i4"), ("node", "<i4"),
+                              ("peer", "<i4"), ("topic", "<i2"), ("phase", "<i2")])
+TRACE_TYPES = ["PUBLISH_MESSAGE", "REJECT_MESSAGE", "DUPLICATE_MESSAGE", "DELIVER_MESSAGE", "ADD_PEER",
+               "REMOVE_PEER", "RECV_RPC", "SEND_RPC", "DROP_RPC", "JOIN", "LEAVE", "GRAFT", "PRUNE"]
+GS_TRACE_FORMAT_PB, GS_TRACE_FORMAT_JSON = 0, 1
+
+
 class CountersC(C.Structure):
     _fields_ = [
         ("hops", i64), ("heartbeats", i64), ("published", i64), ("deliveries", i64),
@@ -152,6 +162,9 @@ ABI_FUNCTIONS = [
       C.POINTER(i64), C.POINTER(u8)]),
     ("gs_read_behaviour_penalty", C.c_int, [P, C.POINTER(f64)]),
     ("gs_read_deliveries", C.c_int, [P, i64, C.POINTER(i32), C.POINTER(i32)]),
+    ("gs_set_trace", C.c_int, [P, C.POINTER(u8), i64]),
+    ("gs_trace_read", C.c_int, [P, P, i64, C.POINTER(i64)]),
+    ("gs_trace_encode", C.c_int, [P, i64, i32, i64, C.POINTER(C.c_char_p), C.c_char_p, P, i64, C.POINTER(i64)]),
     ("gs_set_profiling", C.c_int, [P, C.c_int]),
     ("gs_read_kernel_stats", C.c_int, [P, C.POINTER(f64), C.POINTER(i64)]),
 ]

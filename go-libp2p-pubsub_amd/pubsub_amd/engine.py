@@ -88,6 +88,13 @@ def WithDevice(dev):
     return ("device", int(dev))
 
 
+def WithEventTracer(nodes, capacity=1 << 22):
+    """EventTracer (pubsub.go:418, trace.go) for the hosts in `nodes` (indices
+    or a bool mask): their PublishMessage / DeliverMessage / DuplicateMessage /
+    AddPeer / Join / Graft / Prune events, read with Engine.trace_events()."""
+    return ("trace", (nodes, int(capacity)))
+
+
 def WithPartition(rank, world, transport):
     """Simulate only this rank's node range; exchange RPCs with the other
     ranks through `transport` (a pubsub_amd.transport.TorchTransport) once per
@@ -145,6 +152,15 @@ class Engine:
         direct = np.ascontiguousarray(direct, dtype=np.uint8) if direct is not None else None
         _check(self.lib, self.lib.gs_set_graph(h, _ptr(self.rowptr, C.c_int64), _ptr(self.col, C.c_int32),
                                                _ptr(ob, C.c_uint8), _ptr(direct, C.c_uint8)))
+        tr = opts.get("trace")
+        if tr is not None:
+            nodes, cap = tr
+            mask = np.zeros(num_nodes, dtype=np.uint8)
+            nodes = np.asarray(nodes)
+            mask[np.nonzero(nodes)[0] if nodes.dtype == bool else nodes] = 1
+            _check(self.lib, self.lib.gs_set_trace(h, _ptr(mask, C.c_uint8), cap))
+        self.router = router
+        self.hop_ns = cfg.hop_ns
         self.rank, self.world, self.transport = opts.get("partition", (0, 1, None))
         if self.world > 1:
             _check(self.lib, self.lib.gs_set_partition(h, self.rank, self.world, C.byref(self.transport.c)))
@@ -256,12 +272,47 @@ class Engine:
         _check(self.lib, self.lib.gs_read_kernel_stats(self.h, _ptr(ms, C.c_double), _ptr(cnt, C.c_int64)))
         return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(_abi.KERNEL_NAMES)}
 
+    def trace_events(self, chunk=1 << 16):
+        """Every recorded event since the last call, in canonical order
+        (include/gs_trace.h), as a structured array (_abi.TRACE_EVENT_DTYPE)."""
+        parts = []
+        n = C.c_int64()
+        while True:
+            buf = np.empty(chunk, dtype=_abi.TRACE_EVENT_DTYPE)
+            _check(self.lib, self.lib.gs_trace_read(self.h, buf.ctypes.data, chunk, C.byref(n)))
+            parts.append(buf[:n.value])
+            if n.value < chunk:
+                return np.concatenate(parts)
+
     def deliveries(self, msg_id):
         hop = np.empty(self.N, dtype=np.int32)
         frm = np.empty(self.N, dtype=np.int32)
         _check(self.lib, self.lib.gs_read_deliveries(self.h, int(msg_id), _ptr(hop, C.c_int32),
                                                      _ptr(frm, C.c_int32)))
         return hop, frm
+
+
+PROTOCOLS = {_abi.GS_ROUTER_FLOODSUB: "/floodsub/1.0.0", _abi.GS_ROUTER_RANDOMSUB: "/randomsub/1.0.0",
+             _abi.GS_ROUTER_GOSSIPSUB: "/meshsub/1.1.0"}  # floodsub.go:15, randomsub.go:16, gossipsub.go:25
+
+
+def encode_trace(events, fmt=_abi.GS_TRACE_FORMAT_PB, hop_ns=100 * Millisecond, topic_names=None,
+                 proto="/meshsub/1.1.0", lib=None):
+    """The reference tracers' output for `events` (Engine.trace_events()):
+    uvarint-delimited pb.TraceEvent (PBTracer) or JSON lines (JSONTracer)."""
+    lib = load(lib)
+    ev = np.ascontiguousarray(events, dtype=_abi.TRACE_EVENT_DTYPE)
+    names = None
+    if topic_names is not None:
+        names = (C.c_char_p * len(topic_names))(*[t.encode() for t in topic_names])
+    need = C.c_int64()
+    rc = lib.gs_trace_encode(ev.ctypes.data, len(ev), fmt, hop_ns, names, proto.encode(), None, 0, C.byref(need))
+    if rc not in (_abi.GS_OK, _abi.GS_ECAPACITY):
+        _check(lib, rc)
+    buf = (C.c_uint8 * max(1, need.value))()
+    _check(lib, lib.gs_trace_encode(ev.ctypes.data, len(ev), fmt, hop_ns, names, proto.encode(),
+                                    C.cast(buf, C.c_void_p), need.value, C.byref(need)))
+    return bytes(buf[:need.value])
 
 
 def NewFloodSub(num_nodes, num_topics, graph, subscriptions, *options, **kw):

@@ -296,6 +296,56 @@ int gs_read_behaviour_penalty(gs_engine* eng, double* bp /*[E]*/);
 int gs_read_deliveries(gs_engine* eng, int64_t id, int32_t* hop /*[N]*/,
                        int32_t* from /*[N]*/);
 
+/* ---- trace events (EventTracer, trace.go:61-499 + pb/trace.proto) ------ */
+/* Event types: the values of pb.TraceEvent.Type (pb/trace.proto:28-42). */
+#define GS_TRACE_PUBLISH_MESSAGE 0
+#define GS_TRACE_REJECT_MESSAGE 1
+#define GS_TRACE_DUPLICATE_MESSAGE 2
+#define GS_TRACE_DELIVER_MESSAGE 3
+#define GS_TRACE_ADD_PEER 4
+#define GS_TRACE_REMOVE_PEER 5
+#define GS_TRACE_RECV_RPC 6
+#define GS_TRACE_SEND_RPC 7
+#define GS_TRACE_DROP_RPC 8
+#define GS_TRACE_JOIN 9
+#define GS_TRACE_LEAVE 10
+#define GS_TRACE_GRAFT 11
+#define GS_TRACE_PRUNE 12
+/* One traced event of host `node` (32 bytes).  Recorded: PUBLISH_MESSAGE
+ * (validation.go:217), DELIVER_MESSAGE / DUPLICATE_MESSAGE (pubsub.go:1011,
+ * 1057; receivedFrom = peer), ADD_PEER (gossipsub.go:507, floodsub.go:45),
+ * JOIN (gossipsub.go:1018, floodsub.go:103), GRAFT / PRUNE (gossipsub.go:790,
+ * 817, 1057, 1334, 1343).  The RPC events (RECV/SEND/DROP_RPC) are not
+ * recorded.  `phase` orders the events of one (hop, node): 0 connection and
+ * Join, 1 local publish, 2 received messages, 3 received control, 4 heartbeat;
+ * gs_trace_read returns events in the canonical order of include/gs_trace.h. */
+typedef struct gs_trace_event {
+  int64_t hop;   /* virtual time: timestamp = hop * hop_ns */
+  int64_t msg;   /* message id, -1 = none */
+  int32_t type;  /* GS_TRACE_* */
+  int32_t node;  /* the tracing host */
+  int32_t peer;  /* peer / receivedFrom, -1 = none */
+  int16_t topic; /* -1 = none */
+  int16_t phase;
+} gs_trace_event;
+/* Before the first step: trace the hosts with node_mask[u] != 0 (NULL: off),
+ * keeping up to `capacity` events between two gs_trace_read calls (more is a
+ * GS_ECAPACITY error of gs_step). */
+int gs_set_trace(gs_engine* eng, const uint8_t* node_mask, int64_t capacity);
+/* Moves up to `cap` recorded events, in canonical order, into out; *n = the
+ * number written.  Call until *n < cap to drain. */
+int gs_trace_read(gs_engine* eng, gs_trace_event* out, int64_t cap, int64_t* n);
+#define GS_TRACE_FORMAT_PB 0   /* uvarint-delimited pb.TraceEvent (PBTracer, tracer.go:141-181) */
+#define GS_TRACE_FORMAT_JSON 1 /* one JSON object per line (JSONTracer, tracer.go:79-139) */
+/* Encodes events as the reference's tracers write them.  peerID bytes are
+ * "n<index>", messageID bytes the decimal id, topic names topic_names[t]
+ * (NULL: the decimal index), timestamp hop * hop_ns, AddPeer.proto `proto`.
+ * Writes at most cap bytes; *written = bytes needed (GS_ECAPACITY if > cap).
+ * Product library only (the oracle returns GS_EUNSUPPORTED). */
+int gs_trace_encode(const gs_trace_event* ev, int64_t n, int32_t format, int64_t hop_ns,
+                    const char* const* topic_names, const char* proto, uint8_t* buf, int64_t cap,
+                    int64_t* written);
+
 /* ---- kernel timing (HIP events on the engine's stream) ----------------- */
 /* Kernel classes timed when profiling is on (gs_set_profiling(eng, 1)). */
 #define GS_K_SCORE 0     /* peerScore.score over all edges              */

@@ -23,6 +23,7 @@
 #include <unordered_map>
 
 #include "oracle_core.hpp"
+#include "../include/gs_trace.h"
 
 namespace oracle {
 
@@ -117,6 +118,17 @@ struct Sim {
   std::vector<std::unordered_map<int64_t, std::pair<int32_t, int32_t>>> deliv;  // per node
   gs_counters ctr{};
   int64_t now() const { return hop * cfg.hop_ns; }
+  // EventTracer (trace.go:61-499) of the hosts with traced[u] != 0
+  std::vector<uint8_t> traced;
+  std::vector<gs_trace_event> events;
+  size_t traceRead = 0;
+  void emit(int type, int node, int peer, int topic, int64_t msg, int phase) {
+    if (traced.empty() || !traced[node]) return;
+    gs_trace_event e;
+    e.hop = hop; e.msg = msg; e.type = type; e.node = node; e.peer = peer;
+    e.topic = (int16_t)topic; e.phase = (int16_t)phase;
+    events.push_back(e);
+  }
 
   int edgeIndex(int u, int v) const {
     auto b = col.begin() + rowptr[u], e = col.begin() + rowptr[u + 1];
@@ -194,6 +206,7 @@ void Node::join(int topic) {
   }
   mesh[topic] = gmap;
   for (int p : gmap) {
+    sim->emit(GS_TRACE_GRAFT, id, p, topic, -1, 0);        // tracer.Graft gossipsub.go:1057
     if (sim->scoring) score.Graft(p, topic, sim->now());  // tracer.Graft
     RPC r; r.hasCtl = true; r.ctl.graft.push_back(topic);  // sendGraft gossipsub.go:1080
     sendRPC(p, std::move(r));
@@ -204,6 +217,8 @@ void Node::join(int topic) {
 // (topic.go:207-245, validation.go:216-226, pubsub.go:1056-1060).  Raw tracers
 // skip self-originated messages (trace.go:89,101,132,162).
 void Node::localPublish(const Msg& m) {
+  sim->emit(GS_TRACE_PUBLISH_MESSAGE, id, -1, m.topic, m.id, 1);  // validation.go:217
+  sim->emit(GS_TRACE_DELIVER_MESSAGE, id, id, m.topic, m.id, 1);  // pubsub.go:1057
   seen.insert(m.id);
   sim->ctr.published++;
   if (sim->record) sim->deliv[id][m.id] = {(int32_t)sim->hop, -1};
@@ -219,11 +234,13 @@ void Node::handleMessage(int from, const Msg& m) {
     return;
   }
   if (seen.count(m.id)) {                   // duplicate (pubsub.go:1010-1013)
+    sim->emit(GS_TRACE_DUPLICATE_MESSAGE, id, from, m.topic, m.id, 2);
     sim->ctr.duplicates++;
     if (sim->scoring) score.DuplicateMessage(m, from, sim->now());
     return;
   }
   seen.insert(m.id);                        // markSeen
+  sim->emit(GS_TRACE_DELIVER_MESSAGE, id, from, m.topic, m.id, 2);
   sim->ctr.deliveries++;
   if (sim->record) sim->deliv[id][m.id] = {(int32_t)sim->hop, from};
   if (sim->scoring) {                       // tracer.DeliverMessage -> raw tracers
@@ -408,6 +425,7 @@ std::vector<PruneEntry> Node::handleGraft(int p, const Control& ctl) {
       addBackoff(p, topic);
       continue;
     }
+    sim->emit(GS_TRACE_GRAFT, id, p, topic, -1, 3);  // gossipsub.go:790
     if (sim->scoring) score.Graft(p, topic, now);
     peers.insert(p);
   }
@@ -421,6 +439,7 @@ void Node::handlePrune(int p, const Control& ctl) {
   for (const PruneEntry& pr : ctl.prune) {
     auto pm = mesh.find(pr.topic);
     if (pm == mesh.end()) continue;
+    sim->emit(GS_TRACE_PRUNE, id, p, pr.topic, -1, 3);  // gossipsub.go:817
     if (sim->scoring) score.Prune(p, pr.topic);
     pm->second.erase(p);
     if (pr.hasBackoff && pr.backoff > 0)
@@ -533,12 +552,14 @@ void Node::heartbeat() {
     const int topic = mt.first;
     std::set<int>& peers = mt.second;
     auto prunePeer = [&](int p) {
+      sim->emit(GS_TRACE_PRUNE, id, p, topic, -1, 4);  // gossipsub.go:1334
       if (sim->scoring) this->score.Prune(p, topic);
       peers.erase(p);
       addBackoff(p, topic);
       toprune[p].push_back(topic);
     };
     auto graftPeer = [&](int p) {
+      sim->emit(GS_TRACE_GRAFT, id, p, topic, -1, 4);  // gossipsub.go:1343
       if (sim->scoring) this->score.Graft(p, topic, now);
       peers.insert(p);
       tograft[p].push_back(topic);
@@ -700,6 +721,7 @@ void Sim::start() {
     nd.gtracer.followUpTime = gp.IWantFollowupTime;
     for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) {
       int v = col[e];
+      emit(GS_TRACE_ADD_PEER, u, v, -1, -1, 0);  // AddPeer gossipsub.go:507, floodsub.go:45
       nd.nbrs.push_back(v);
       nd.outbound[v] = outboundE.empty() ? false : outboundE[e] != 0;  // AddPeer gossipsub.go:505-532
       if (!directE.empty() && directE[e]) nd.direct.insert(v);
@@ -724,7 +746,10 @@ void Sim::step() {
   if (hop == 0) {  // Join: the GRAFTs it sends arrive in hop 1
     for (int u = 0; u < N; ++u)
       for (int tp = 0; tp < T; ++tp)
-        if ((nodes[u].mySubs >> tp) & 1) nodes[u].join(tp);
+        if ((nodes[u].mySubs >> tp) & 1) {
+          emit(GS_TRACE_JOIN, u, -1, tp, -1, 0);  // tracer.Join gossipsub.go:1018, floodsub.go:103
+          nodes[u].join(tp);
+        }
   }
   // S0 memo
   if (scoring)
@@ -1044,6 +1069,29 @@ int gs_partition_range(const gs_engine* g, int32_t* node_begin, int32_t* node_en
   *node_begin = 0;
   *node_end = g->sim.N;
   return GS_OK;
+}
+int gs_set_trace(gs_engine* g, const uint8_t* node_mask, int64_t capacity) {
+  (void)capacity;  // the oracle keeps every event
+  if (g->sim.started) { set_error("tracing must be set before the first step"); return GS_ESTATE; }
+  if (node_mask) g->sim.traced.assign(node_mask, node_mask + g->sim.N);
+  else g->sim.traced.clear();
+  return GS_OK;
+}
+int gs_trace_read(gs_engine* g, gs_trace_event* out, int64_t cap, int64_t* n) {
+  Sim& s = g->sim;
+  if (s.traceRead == 0) std::stable_sort(s.events.begin(), s.events.end(), gs_trace_less);
+  const int64_t k = std::min<int64_t>(cap, (int64_t)(s.events.size() - s.traceRead));
+  for (int64_t i = 0; i < k; ++i) out[i] = s.events[s.traceRead + i];
+  s.traceRead += (size_t)k;
+  if (s.traceRead == s.events.size()) { s.events.clear(); s.traceRead = 0; }
+  *n = k;
+  return GS_OK;
+}
+int gs_trace_encode(const gs_trace_event*, int64_t, int32_t, int64_t, const char* const*, const char*, uint8_t*,
+                    int64_t, int64_t* written) {
+  *written = 0;
+  set_error("gs_trace_encode is in the product library");
+  return GS_EUNSUPPORTED;
 }
 int gs_read_exchange_stats(gs_engine*, double* host_ms, int64_t* bytes_in) {
   *host_ms = 0;
