@@ -226,10 +226,19 @@ def main():
                "active_words": float(np.mean([active_words(eng, wl, hop0 + i) for i in range(nh)]))}
     bytes_per_launch, bytes_info = algorithmic_bytes(dom, eng, wl, per_hop)
     roofline = None
+    traffic, traffic_src = None, None
+    pmc = os.path.join(REPO, "profiles", f"pmc_traffic_{args.workload}.json")
+    if os.path.exists(pmc) and not partitioned:
+        # rocprofv3 PMC passes of this workload (scripts/gpu_pmc.sh + pmc_summary.py):
+        # FETCH_SIZE x 2 (gfx950 wide-read correction, MI355X_MICROARCH.md) + WRITE_SIZE
+        rec = json.load(open(pmc)).get(f"void k_{dom}<4>") or json.load(open(pmc)).get(f"k_{dom}")
+        if rec:
+            traffic, traffic_src = rec["traffic_bytes_est"], os.path.relpath(pmc, REPO)
     if bytes_per_launch:
         achieved = bytes_per_launch / (avg_ms / 1e3) / 1e9
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                    "kernel": dom,
                     "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": int(bytes_per_launch),
                     **{k: v for k, v in bytes_info.items()}}
     rounds_per_s = args.steps / elapsed
