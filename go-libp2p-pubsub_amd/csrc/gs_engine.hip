@@ -632,13 +632,23 @@ int gs_engine::stepOne() {
   if (heartbeatDue(now)) {
     ticks++;
     if (nOwn) TIMED(this, GS_K_HB_PRE, (k_hb_pre<<<nOwn, 64, 0, stream>>>(d, now, ticks)));
-    // right after a refresh S0 holds exact scores: recompute only what hb_pre dirtied
+    // right after a refresh S0 holds exact scores: recompute only what hb_pre
+    // dirtied; opportunistic grafting (every OGT ticks) ranks every mesh
+    // score, so it gets the full exact pass; otherwise the threshold-exact
+    // memo pass (k_score_rows<4>)
+    int allExact = 1;
     if (scoring && refreshedHop == h)
       TIMED(this, GS_K_SCORE, (k_score_rows<3><<<sgb, 64, 0, stream>>>(d, nullptr)));
-    else if (scoring)
+    else if (scoring && ticks % (uint64_t)d.OGT == 0)
       TIMED(this, GS_K_SCORE, (k_score_rows<0><<<sgb, 64, 0, stream>>>(d, d.score1)));
+    else if (scoring) {
+      TIMED(this, GS_K_SCORE, (k_score_rows<4><<<sgb, 64, 0, stream>>>(d, nullptr)));
+      allExact = 0;
+    }
     const int newhead = (head + R - 1) % R;
-    if (nOwn) TIMED(this, GS_K_HEARTBEAT, (k_heartbeat<<<nOwn, 64, 0, stream>>>(d, h, now, ticks, cur, head, newhead)));
+    if (nOwn)
+      TIMED(this, GS_K_HEARTBEAT,
+            (k_heartbeat<<<nOwn, 64, 0, stream>>>(d, h, now, ticks, cur, head, newhead, allExact)));
     head = newhead;
     heartbeats++;
   }

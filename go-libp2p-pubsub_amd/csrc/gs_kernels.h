@@ -43,6 +43,11 @@
 //     since S0, so a non-negative S0 decides exactly like the exact score.
 //   MODE 3: every edge exact -> score1, right after k_refresh_rows left exact
 //     scores in S0: only the edges dirtied since (penalties) are recomputed.
+//   MODE 4: heartbeat memo -> score1 without a refresh in this hop: exact where
+//     a score-lowering change happened or S0 < 0, else S0 (a lower bound >= 0
+//     of the exact score, so every heartbeat threshold test — 0, Gossip- and
+//     PublishThreshold, all <= 0 — decides exactly).  k_heartbeat recomputes
+//     the few scores it needs as values (Dhi ranking) from the same rule.
 #define GS_SG 16  // edges per wave
 #define GS_SB 8   // edges per load batch
 template <int MODE>
@@ -60,7 +65,9 @@ __global__ __launch_bounds__(64) void k_score_rows(Dev d, double* __restrict__ o
     } else {
       s0 = d.score0[e];
       need = MODE == 1 ? (d.sdirty[e] != 0 || !(s0 >= d.publishThr))
-                       : MODE == 2 ? !(s0 >= 0.0) : d.sdirty[e] != 0;
+             : MODE == 2 ? !(s0 >= 0.0)
+             : MODE == 4 ? (d.sdirty[e] != 0 || !(s0 >= 0.0))
+                         : d.sdirty[e] != 0;
     }
   }
   if (!d.scoring) {

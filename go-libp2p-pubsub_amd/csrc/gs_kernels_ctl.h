@@ -734,7 +734,7 @@ __device__ __forceinline__ uint64_t emit_gossip(const Dev& d, int v, int t, int6
 // heartbeat memo (score1, computed after applyIwantPenalties); emitGossip
 // re-scores peers whose stats changed during this heartbeat (live Score()).
 __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t now, uint64_t ticks, int cur,
-                                                  int head, int newhead) {
+                                                  int head, int newhead, int allExact) {
   __shared__ int plst[64];
   __shared__ int obs[64];
   __shared__ int posOf[64];
@@ -759,14 +759,33 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
   const uint64_t subv = valid ? d.sub[vcol] : 0;
   uint64_t meshl = valid ? d.mesh[e] : 0;
   uint64_t fanl = valid ? d.fanout[e] : 0;
-  const double S = valid ? d.score1[e] : 0.0;
+  double S = valid ? d.score1[e] : 0.0;
+  const uint64_t joined = d.sub[v];
+  if (d.scoring && !allExact) {
+    // score1 is exact only where k_score_rows<4> recomputed it; the Dhi
+    // ranking compares scores as values, so the mesh members of a topic that
+    // may exceed Dhi get their exact heartbeat-start score now, before any
+    // stats change in this heartbeat
+    bool needX = false;
+    for (int t = 0; t < d.T; ++t) {
+      const bool mt = valid && ((meshl >> t) & 1) && ((joined >> t) & 1);
+      if (__popcll(__ballot(mt)) > d.Dhi) needX |= mt;
+    }
+    const bool exact = valid && (d.sdirty[e] != 0 || !(d.score0[e] >= 0.0));
+    unsigned long long xm = __ballot(needX && !exact);
+    while (xm) {
+      const int j = __ffsll((long long)xm) - 1;
+      xm &= xm - 1;
+      const double sj = edge_score_wave(d, base + j, sterm);
+      if (lane == j) S = sj;
+    }
+  }
   double Slive = S;  // live Score(p) for emitGossip
   const bool dir = valid && d.direct[e];
   const bool ob = valid && d.outbound[e];
   bool dirty = false;    // a PRUNE lowered the peer's score since Slive
   bool dirtyUp = false;  // a GRAFT (never lowers it) changed it since Slive
   uint64_t tograft = 0, toprune = 0, ihave = 0;
-  const uint64_t joined = d.sub[v];
   const uint32_t hw = (uint32_t)hop;
   for (int t = 0; t < d.T; ++t) {
     if (!((joined >> t) & 1)) continue;
