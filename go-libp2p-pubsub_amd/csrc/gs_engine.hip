@@ -50,6 +50,7 @@ struct gs_engine {
   int64_t E = 0;
   int H = 16;  // hops per heartbeat (or a nominal 16 for floodsub/randomsub)
   int64_t retireHops = 0;
+  std::vector<int32_t> topicLive;  // per-topic live message count (phase-A counter width)
   int64_t hopsSinceFold = 0, foldEvery = 1;  // pending-delivery fold cadence (dlt)
   int64_t refreshedHop = -1;                 // hop of the last refreshScores (S0 exact after it)
   int maxAge = 0;
@@ -589,10 +590,24 @@ int gs_engine::stepOne() {
   {
     const int nR = __builtin_popcountll(amR.m[0]) + __builtin_popcountll(amR.m[1]) +
                    __builtin_popcountll(amR.m[2]) + __builtin_popcountll(amR.m[3]);
-    const size_t nCnt = ((size_t)T * d.maxDeg + 3) & ~(size_t)3;
-    const size_t lds = 4 * nCnt + 8 * (size_t)nR + 64 * (size_t)nR + (d.needAge ? 4 * nCnt : 0);
+    // 8-bit (sender, topic) counters when no topic has more than 255 live
+    // message slots: a sender delivers each message at most once per hop
+    // (E_DOUBLE), so it cannot deliver more copies of one topic than that
+    bool narrow = true;
+    {
+      auto it = std::lower_bound(mHop.begin(), mHop.end(), h - retireHops);
+      std::fill(topicLive.begin(), topicLive.end(), 0);
+      for (size_t k = (size_t)(it - mHop.begin()); k < mHop.size() && mHop[k] <= h; ++k)
+        if (++topicLive[mTopic[k]] > 255) { narrow = false; break; }
+    }
+    const size_t nCnt = ((size_t)T * d.maxDeg + 7) & ~(size_t)7;
+    const size_t lds = (narrow ? 2 : 4) * nCnt + 8 * (size_t)nR + 64 * (size_t)nR + (d.needAge ? 4 * nCnt : 0);
     TIMED(this, GS_K_PHASE_A, launch_wpl(W, [&](auto w) {
-            if (nOwn) k_phase_a<decltype(w)::value><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR);
+            if (!nOwn) return;
+            if (narrow)
+              k_phase_a<decltype(w)::value, true><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR);
+            else
+              k_phase_a<decltype(w)::value, false><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR);
           }));
   }
   if (!retireWords.empty()) {
@@ -986,6 +1001,7 @@ int gs_engine_create(const gs_config* cfg, const gs_gossipsub_params* gsp, const
     for (int t = 0; t < g->T; ++t) { g->tps[t] = topics[t]; g->tscored[t] = topic_scored[t]; }
   }
   g->topicCounter.assign(g->T, 0);
+  g->topicLive.assign(g->T, 0);
   g->slotOwnerHop.assign(g->S, INT64_MIN);
   g->slotOwnerId.assign(g->S, -1);
   *out = g.release();

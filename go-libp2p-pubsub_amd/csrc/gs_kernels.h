@@ -450,13 +450,18 @@ __device__ __forceinline__ int wave_min_int(int x) {
 //   pass 3 (lane = edge):   fmd / mmd of every (topic, in-edge) updated once.
 // LDS slot tables cover the words of the active window amR (messages young
 // enough to be in flight), indexed by the word's rank in amR.
-template <int WPL>
+// NARROW: the host proved that no sender can deliver more than 255 copies of
+// one topic in this hop (every topic has <= 255 live message slots), so the
+// (sender, topic) counters are 8-bit copies | 8-bit first deliveries, two per
+// LDS word: half the counter table, more waves per CU.
+template <int WPL, bool NARROW>
 __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int head, WMask amR, WMask amW,
                                                 int nR) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
-  const int nCnt = (d.T * d.maxDeg + 3) & ~3;
-  uint32_t* scnt = smem32;                                // [MD][T] copies | fresh << 16
-  uint64_t* sD = (uint64_t*)(smem32 + nCnt);              // [nR] delivered slots (non-graylisted)
+  const int nCnt = (d.T * d.maxDeg + 7) & ~7;
+  const int nCntW = NARROW ? nCnt / 2 : nCnt;             // LDS words of the counter table
+  uint32_t* scnt = smem32;  // [MD][T] copies | fresh << 16 (NARROW: u16 copies | fresh << 8)
+  uint64_t* sD = (uint64_t*)(smem32 + nCntW);             // [nR] delivered slots (non-graylisted)
   uint8_t* sFirst = (uint8_t*)(sD + nR);                  // [nR * 64] lowest deliverer
   uint32_t* sUnc = (uint32_t*)(sFirst + nR * 64);         // [MD][T] uncredited duplicates (needAge)
   __shared__ int sBlk[64];        // first list block of each sender
@@ -498,7 +503,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   }
   GS_STAMP(0);
   const bool authV = d.nAuth[v] > 0;  // v authored a live message: author exclusion possible
-  for (int k = lane; k < nCnt / 4; k += 64) ((uint4*)scnt)[k] = make_uint4(0, 0, 0, 0);
+  for (int k = lane; k < nCntW / 4; k += 64) ((uint4*)scnt)[k] = make_uint4(0, 0, 0, 0);
   if (d.needAge)
     for (int k = lane; k < nCnt / 4; k += 64) ((uint4*)sUnc)[k] = make_uint4(0, 0, 0, 0);
   for (int k = lane; k < nR; k += 64) sD[k] = 0;
@@ -535,7 +540,13 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     const int t = (int)__umulhi((unsigned)slot, d.stMagic);
     if (trv) trace_emit(d, h, GS_TRACE_COPY, v, d.col[base + i], t, d.slotMid[slot], 2);
 #ifndef GS_EXP_NOADD
-    atomicAdd(&scnt[i * T + t], 1u);
+    if (NARROW) {
+      const int pl = i * T + t;
+      const uint32_t old = atomicAdd(&scnt[pl >> 1], 1u << (16 * (pl & 1)));
+      if (((old >> (16 * (pl & 1))) & 0xFF) == 0xFF) set_err(d, E_DELTA);  // never: see the host's bound
+    } else {
+      atomicAdd(&scnt[i * T + t], 1u);
+    }
     ++nCopies;
 #endif
     const int rk = sRk[w];
@@ -721,7 +732,9 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
       while (y) {
         const int b = __ffsll((long long)y) - 1;
         y &= y - 1;
-        atomicAdd(&scnt[sFirst[ixw[j] + b] * T + t], 1u << 16);
+        const int pl = sFirst[ixw[j] + b] * T + t;
+        if (NARROW) atomicAdd(&scnt[pl >> 1], 1u << (16 * (pl & 1) + 8));
+        else atomicAdd(&scnt[pl], 1u << 16);
       }
     }
   }
@@ -755,8 +768,10 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     const int q64 = 64 / T, r64 = 64 - q64 * T;
     int ic = lane / T, tc = lane - (lane / T) * T;  // (in-edge, topic) of the lane's next pair
     auto upd = [&](int pl, int i, int t, uint32_t q) -> uint32_t {
-      const uint32_t c = ((scoredT >> t) & 1) ? scnt[pl] : 0u;
-      const int copies = (int)(c & 0xFFFF), nf = (int)(c >> 16);
+      uint32_t c = ((scoredT >> t) & 1) ? scnt[NARROW ? pl >> 1 : pl] : 0u;
+      if (NARROW) c = (c >> (16 * (pl & 1))) & 0xFFFF;
+      const int copies = NARROW ? (int)(c & 0xFF) : (int)(c & 0xFFFF);
+      const int nf = NARROW ? (int)(c >> 8) : (int)(c >> 16);
       int credited = copies - nf;
       if (d.needAge) credited -= (int)sUnc[pl];
       const uint32_t addM = ((sRelay[i] >> t) & 1) ? (uint32_t)(nf + credited) : 0u;
