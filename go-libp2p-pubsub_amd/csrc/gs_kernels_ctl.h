@@ -65,8 +65,18 @@ __device__ __forceinline__ void prune_topics(const Dev& d, int64_t e, int v, uin
 
 #define GS_PTXH 1024  // LDS hash slots for a node's mcache.peertx table (>= 2 * GS_PTX)
 
-__device__ __forceinline__ int ptx_hash(uint64_t key) {
-  return (int)((key * 0x9E3779B97F4A7C15ull) >> 54);  // 10 bits
+// The LDS hash holds 32-bit entries slot << 14 | in-edge << 8 | count (slot <
+// 2^14, in-edge < 64); the node's list in HBM keeps the 64-bit form
+// slot << 32 | in-edge << 8 | count.  Keys (count bits 0) are passed as u64.
+__device__ __forceinline__ uint32_t ptx_key32(uint64_t key) {
+  return ((uint32_t)(key >> 32) << 14) | ((uint32_t)((key >> 8) & 0x3F) << 8);
+}
+__device__ __forceinline__ uint32_t ptx_to32(uint64_t ent) { return ptx_key32(ent) | (uint32_t)(ent & 0xFF); }
+__device__ __forceinline__ uint64_t ptx_to64(uint32_t e) {
+  return ((uint64_t)(e >> 14) << 32) | ((uint64_t)((e >> 8) & 0x3F) << 8) | (uint64_t)(e & 0xFF);
+}
+__device__ __forceinline__ int ptx_hash(uint32_t key) {
+  return (int)((key * 0x9E3779B1u) >> 22);  // 10 bits
 }
 
 // k-th set bit (0-based) of m
@@ -77,20 +87,21 @@ __device__ __forceinline__ int kth_bit(uint64_t m, int k) {
 
 // ++peertx[slot][edge] (mcache.GetForPeer, mcache.go:66-80) in the LDS hash;
 // returns the new count, or 0 when the table is full (E_PEERTX raised).
-__device__ __forceinline__ int ptx_incr(const Dev& d, unsigned long long* sH, uint64_t key) {
+__device__ __forceinline__ int ptx_incr(const Dev& d, unsigned int* sH, uint64_t key64) {
+  const uint32_t key = ptx_key32(key64);
   int hsl = ptx_hash(key);
   for (int probe = 0; probe < GS_PTXH; ++probe) {
-    unsigned long long cur = sH[hsl];
+    unsigned int cur = sH[hsl];
     while (true) {
       if (cur == 0) {
-        const unsigned long long prev = atomicCAS(&sH[hsl], 0ull, (unsigned long long)(key | 1));
+        const unsigned int prev = atomicCAS(&sH[hsl], 0u, key | 1u);
         if (prev == 0) return 1;
         cur = prev;
       }
-      if ((cur & ~0xFFull) != key) break;  // another key: probe on
-      const unsigned long long c = cur & 0xFF;
-      const unsigned long long nw = key | (c < 255 ? c + 1 : 255);
-      const unsigned long long prev = atomicCAS(&sH[hsl], cur, nw);
+      if ((cur & ~0xFFu) != key) break;  // another key: probe on
+      const unsigned int c = cur & 0xFF;
+      const unsigned int nw = key | (c < 255 ? c + 1 : 255);
+      const unsigned int prev = atomicCAS(&sH[hsl], cur, nw);
       if (prev == cur) return (int)(nw & 0xFF);
       cur = prev;
     }
@@ -100,12 +111,13 @@ __device__ __forceinline__ int ptx_incr(const Dev& d, unsigned long long* sH, ui
   return 0;
 }
 
-__device__ __forceinline__ int ptx_count(const unsigned long long* sH, uint64_t key) {
+__device__ __forceinline__ int ptx_count(const unsigned int* sH, uint64_t key64) {
+  const uint32_t key = ptx_key32(key64);
   int hsl = ptx_hash(key);
   for (int probe = 0; probe < GS_PTXH; ++probe) {
-    const unsigned long long cur = sH[hsl];
+    const unsigned int cur = sH[hsl];
     if (cur == 0) return 0;
-    if ((cur & ~0xFFull) == key) return (int)(cur & 0xFF);
+    if ((cur & ~0xFFu) == key) return (int)(cur & 0xFF);
     hsl = (hsl + 1) & (GS_PTXH - 1);
   }
   return 0;
@@ -149,9 +161,9 @@ __device__ __forceinline__ int lane_prefix(int x, int* total) {
 // irrelevant to every reader.
 template <int WPL>
 __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, int cur, int head) {
-  __shared__ uint64_t sseen[64 * WPL];   // v's seen row (handleIHave)
-  __shared__ uint64_t scache[64 * WPL];  // v's mcache windows (handleIWant)
-  __shared__ unsigned long long sH[GS_PTXH];
+  __shared__ uint64_t scache[64 * WPL];  // v's mcache windows (handleIWant, step 2)
+  uint64_t* const sseen = scache;        // then v's seen row (handleIHave, step 3)
+  __shared__ unsigned int sH[GS_PTXH];
   __shared__ double sterm[64];
   __shared__ int sIt[64];                // per-sender exclusive item prefix
   __shared__ int sReqOff[64], sReqN[64]; // step 2: request list of each sender
@@ -329,7 +341,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
       for (int k = 0; k < d.HL; ++k) x |= d.hist[((int64_t)((head + k) % d.R) * d.N + v) * W + w];
       scache[w] = x;
     }
-    for (int k = lane; k < GS_PTXH; k += 64) sH[k] = 0ull;
+    for (int k = lane; k < GS_PTXH; k += 64) sH[k] = 0u;
     const int n = gateIWant ? (int)(iwRec & 0xFFFFFF) : 0;
     int totalItems;
     sIt[lane] = lane_prefix((n + 15) >> 4, &totalItems);
@@ -341,8 +353,9 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     const int ptxN = d.ptxN[v];
     for (int q = lane; q < ptxN; q += 64) {
       const unsigned long long ent = d.ptx[(int64_t)v * GS_PTX + q];
-      int hsl = ptx_hash(ent & ~0xFFull);
-      while (atomicCAS(&sH[hsl], 0ull, ent) != 0ull) hsl = (hsl + 1) & (GS_PTXH - 1);
+      const unsigned int e32 = ptx_to32(ent);
+      int hsl = ptx_hash(e32 & ~0xFFu);
+      while (atomicCAS(&sH[hsl], 0u, e32) != 0u) hsl = (hsl + 1) & (GS_PTXH - 1);
     }
     __syncthreads();
     // pass a: increments and per-sender served counts
@@ -597,10 +610,10 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     __syncthreads();
     int kept = 0;
     for (int q0 = 0; q0 < GS_PTXH; q0 += 64) {
-      const unsigned long long ent = sH[q0 + lane];
+      const unsigned int e32 = sH[q0 + lane];
       int tot;
-      const int pos = kept + lane_prefix(ent != 0ull ? 1 : 0, &tot);
-      if (ent && pos < GS_PTX) d.ptx[(int64_t)v * GS_PTX + pos] = ent;
+      const int pos = kept + lane_prefix(e32 != 0u ? 1 : 0, &tot);
+      if (e32 && pos < GS_PTX) d.ptx[(int64_t)v * GS_PTX + pos] = ptx_to64(e32);
       kept += tot;
     }
     if (kept > GS_PTX && lane == 0) set_err(d, E_PEERTX);
