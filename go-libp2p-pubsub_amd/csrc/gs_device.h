@@ -414,6 +414,26 @@ __device__ __forceinline__ int wave_incl_sum(int x) {
 __device__ __forceinline__ int lane_rank(uint64_t m) {
   return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
+// select_k for wave-uniform call sites that can spare 64 u64 of LDS (skey):
+// the candidates' keys are compacted in lane order, and every lane counts the
+// smaller ones in one broadcast-read loop (no per-candidate scalar work).
+// Same result as select_k: ties by lane, since compaction keeps lane order.
+__device__ __forceinline__ bool select_k_lds(bool cand, uint64_t key, int k, uint64_t* skey) {
+  const unsigned long long m = __ballot(cand);
+  const int n = __popcll(m);
+  if (k <= 0 || n <= k) return cand;
+  const int pos = lane_rank(m);
+  __syncthreads();  // previous users of skey are done
+  if (cand) skey[pos] = key;
+  __syncthreads();
+  int rank = 0;
+  for (int q = 0; q < n; ++q) {
+    const uint64_t kq = skey[q];
+    rank += (kq < key || (kq == key && q < pos)) ? 1 : 0;
+  }
+  return cand && rank < k;
+}
+
 // Value of lane 63 (wave-uniform).
 __device__ __forceinline__ int wave_last(int x) { return __builtin_amdgcn_readlane(x, 63); }
 

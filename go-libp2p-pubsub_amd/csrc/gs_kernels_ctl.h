@@ -705,12 +705,9 @@ __global__ __launch_bounds__(64) void k_hb_pre(Dev d, int64_t now, uint64_t tick
 __device__ __forceinline__ uint64_t emit_gossip(const Dev& d, int v, int t, int64_t hop, int head, bool valid,
                                                 int vcol, bool inTopic, bool excl, bool dir, double& Slive,
                                                 bool& dirty, bool& dirtyUp, int64_t rowBase, double* lds,
-                                                const uint64_t* sgw) {
+                                                int nm) {
   const int lane = lane_id();
-  int nm = 0;
-  for (int w = t * d.Wt + lane; w < (t + 1) * d.Wt; w += 64) nm += __popcll(sgw[w]);
-  nm = wave_sum_int(nm);
-  if (nm == 0) return 0;
+  if (nm == 0) return 0;  // nm: message ids of topic t in the gossip windows
   if (nm > d.MaxIHaveLength && lane == 0) set_err(d, E_TRUNCATE);
   const bool base = valid && inTopic && !excl && !dir;
   // A graft never lowers a score (P1 is 0 at meshTime 0, the P3 deficit term
@@ -735,7 +732,7 @@ __device__ __forceinline__ uint64_t emit_gossip(const Dev& d, int v, int t, int6
   bool sel = cand;
   if (target < n) {
     const uint64_t key = gs_key64(d.seed, GS_SITE_EMIT_PEERS, v, (uint32_t)hop, vcol, t);
-    sel = select_k(cand, key, target);
+    sel = select_k_lds(cand, key, target, (uint64_t*)lds);
   }
   return sel ? (1ull << t) : 0;
 }
@@ -769,6 +766,10 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
     d.gw[(int64_t)v * d.W + w] = x;
   }
   __syncthreads();
+  // lane t: message ids of topic t in the gossip windows (emitGossip's mids)
+  int nmT = 0;
+  if (lane < d.T)
+    for (int w = lane * d.Wt; w < (lane + 1) * d.Wt; ++w) nmT += __popcll(sgw[w]);
   const uint64_t subv = valid ? d.sub[vcol] : 0;
   uint64_t meshl = valid ? d.mesh[e] : 0;
   uint64_t fanl = valid ? d.fanout[e] : 0;
@@ -820,7 +821,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
       const bool bo = valid && d.backoff[tix(d, t, e)] != 0;
       const bool cand = inTopic && !m && !bo && !dir && S >= 0;
       const uint64_t key = gs_key64(d.seed, GS_SITE_GP_DLO, v, hw, vcol, t);
-      if (select_k(cand, key, d.D - cnt)) {
+      if (select_k_lds(cand, key, d.D - cnt, (uint64_t*)sterm)) {
         stats_graft(d, e, t, now);
         meshl |= bit;
         tograft |= bit;
@@ -902,7 +903,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
         const bool bo = valid && d.backoff[tix(d, t, e)] != 0;
         const bool cand = inTopic && !m && !bo && !dir && ob && S >= 0;
         const uint64_t key = gs_key64(d.seed, GS_SITE_GP_DOUT, v, hw, vcol, t);
-        if (select_k(cand, key, d.Dout - outb)) {
+        if (select_k_lds(cand, key, d.Dout - outb, (uint64_t*)sterm)) {
           stats_graft(d, e, t, now);
           meshl |= bit;
           tograft |= bit;
@@ -928,7 +929,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
         const bool bo = valid && d.backoff[tix(d, t, e)] != 0;
         const bool cand = inTopic && !m && !bo && !dir && S > median;
         const uint64_t key = gs_key64(d.seed, GS_SITE_GP_OPPORTUNISTIC, v, hw, vcol, t);
-        if (select_k(cand, key, d.OGP)) {
+        if (select_k_lds(cand, key, d.OGP, (uint64_t*)sterm)) {
           stats_graft(d, e, t, now);
           meshl |= bit;
           tograft |= bit;
@@ -937,7 +938,8 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
         }
       }
     }
-    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, m, dir, Slive, dirty, dirtyUp, base, sterm, sgw);
+    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, m, dir, Slive, dirty, dirtyUp, base, sterm,
+                         lane_get(nmT, t));
   }
   // expire fanout for topics we haven't published to in a while
   uint64_t fpres = d.fanoutPresent[v];
@@ -963,12 +965,13 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
     if (cnt < d.D) {
       const bool cand = inTopic && !f && !dir && S >= d.publishThr;
       const uint64_t key = gs_key64(d.seed, GS_SITE_GP_FANOUT_HB, v, hw, vcol, t);
-      if (select_k(cand, key, d.D - cnt)) {
+      if (select_k_lds(cand, key, d.D - cnt, (uint64_t*)sterm)) {
         fanl |= bit;
         f = true;
       }
     }
-    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, f, dir, Slive, dirty, dirtyUp, base, sterm, sgw);
+    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, f, dir, Slive, dirty, dirtyUp, base, sterm,
+                         lane_get(nmT, t));
   }
   // sendGraftPrune + flush: one heartbeat RPC per peer with any control
   if (valid && is_traced(d, v)) {  // prunePeer / graftPeer, gossipsub.go:1334, 1343
