@@ -18,7 +18,8 @@ def main():
     print("kernel,dispatches_in_window,avg_ms")
     for k, v in sorted(by.items()):
         v.sort()
-        per_hop = k.endswith("k_phase_a<4>") or k.endswith("k_phase_b<4>") or k in ("k_fwd", "k_score0", "k_score1")
+        per_hop = "k_phase_a<" in k or "k_phase_b<" in k or k in ("k_fwd", "void k_score_rows<1>",
+                                                                   "void k_score_rows<2>")
         w = v[-a.hops:] if per_hop else v[-max(1, a.hops // 10):]
         print(f"{k},{len(w)},{sum(e - s for s, e in w) / len(w) / 1e6:.4f}")
 
