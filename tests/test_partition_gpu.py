@@ -22,6 +22,9 @@ def _free_port():
         return s.getsockname()[1]
 
 
+TRACED = [0, 3, 17, 42, 99, 150]
+
+
 def _worker(rank, world, port, name, oracle, q):
     try:
         sys.path.insert(0, HERE)
@@ -35,9 +38,18 @@ def _worker(rank, world, port, name, oracle, q):
         from pubsub_amd.transport import TorchTransport
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        from pubsub_amd import WithEventTracer
         tr = TorchTransport(memory="device")
-        got = scenarios.run(PRODUCT_LIB, name, extra=(WithPartition(rank, world, tr),))
-        ref = scenarios.run(oracle, name)
+        traced = [u for u in TRACED if u < 20]
+        e, hops = scenarios.SCENARIOS[name](PRODUCT_LIB, (WithPartition(rank, world, tr), WithEventTracer(traced)))
+        e.step(hops)
+        got = scenarios.snapshot(e, range(e.n_published))
+        got["node_range"], got["edge_range"] = e.node_range, e.edge_range
+        ev = e.trace_events()
+        eo, _ = scenarios.SCENARIOS[name](oracle, (WithEventTracer(traced),))
+        eo.step(hops)
+        ref = scenarios.snapshot(eo, range(eo.n_published))
+        evo = eo.trace_events()
         T = got["ts_fmd"].shape[0]
         ref_part = dict(ref, node_range=got["node_range"], edge_range=got["edge_range"])
         bad = scenarios.compare(scenarios.restrict(ref_part, T), scenarios.restrict(got, T))
@@ -48,6 +60,11 @@ def _worker(rank, world, port, name, oracle, q):
         want = {k: ref["counters"][k] for k in keys}
         if summed != want:
             bad.append(f"summed counters {summed} != oracle {want}")
+        # trace events: this rank records its own traced hosts only
+        n0, n1 = got["node_range"]
+        want_ev = evo[(evo["node"] >= n0) & (evo["node"] < n1)]
+        if len(ev) != len(want_ev) or (len(ev) and not np.array_equal(ev, want_ev)):
+            bad.append(f"trace events differ: {len(ev)} vs {len(want_ev)}")
         if tr.calls == 0:
             bad.append("the transport was never called")
         q.put((rank, bad, got["node_range"]))
@@ -93,3 +110,24 @@ def test_partitioned_engine_matches_oracle(world, name, oracle_path):
     assert ranges[0][0] == 0 and all(ranges[i][1] == ranges[i + 1][0] for i in range(world - 1))
     bad = [f"rank {r}: {m}" for r, ms, _ in res for m in ms]
     assert not bad, "\n".join(bad)
+
+
+class _NoTransport:
+    """gs_transport whose callbacks fail (never reached in this test)."""
+
+    def __init__(self):
+        from pubsub_amd import _abi
+        self._cb = (_abi.ALLGATHER_I64(lambda *a: -1), _abi.ALLGATHER(lambda *a: -1),
+                    _abi.ALLTOALLV(lambda *a: -1))
+        self.c = _abi.TransportC(None, *self._cb)
+
+
+@pytest.mark.gpu
+def test_partitioned_randomsub_is_refused():
+    """Randomsub's per-message target masks are not exchanged: refused loudly."""
+    from pubsub_amd import GossipEngineError, NewRandomSub, WithPartition, _abi, graphs
+    g = graphs.random_regular(40, 8, 1)
+    e = NewRandomSub(40, 1, g, graphs.all_subscribed(40, 1), 10, WithPartition(0, 2, _NoTransport()))
+    with pytest.raises(GossipEngineError) as ei:
+        e.step(1)
+    assert ei.value.code == _abi.GS_EUNSUPPORTED
