@@ -241,6 +241,17 @@ def main():
                     "kernel": dom,
                     "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": int(bytes_per_launch),
                     **{k: v for k, v in bytes_info.items()}}
+    # the score kernels' rooflines too (north-star target: >= 50% of HBM on
+    # score / propagation): refreshScores streams every (edge, topic) record
+    rooflines = {}
+    for k in ("refresh",):
+        if k in kstats and kstats[k][1]:
+            b_k, _ = algorithmic_bytes(k, eng, wl, per_hop)
+            ms_k = kstats[k][0] / kstats[k][1]
+            ach = b_k / (ms_k / 1e3) / 1e9
+            rooflines[k] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(ach / HBM_PEAK_GBS, 4), "avg_launch_ms": round(ms_k, 4),
+                            "bytes_per_launch": int(b_k)}
     rounds_per_s = args.steps / elapsed
     out = {
         "metric": "peer-message deliveries/sec + gossipsub rounds/sec (node), 1M peers 64 topics",
@@ -266,6 +277,7 @@ def main():
         "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kstats.items() if v[1]},
         "events_per_step": {k: v // args.steps for k, v in events.items()},
         "roofline": roofline,
+        "rooflines_other": rooflines,
         "setup_s": round(setup_s, 1),
     }
     if partitioned:

@@ -165,11 +165,12 @@ __global__ __launch_bounds__(64) void k_refresh_rows(Dev d, int64_t now) {
         x.im = v;
         x.fl = fl[k];
         x.mt = 0;
+        // unchanged counters (mostly zeros staying zero) are not written back
         if (q[k]) d.dlt[i] = 0;
-        d.fmd[i] = x.fmd;
-        d.mmd[i] = x.mm;
-        d.mfp[i] = x.mfp;
-        if (d.anyImd) d.imd[i] = x.im;
+        if (x.fmd != fmd[k]) d.fmd[i] = x.fmd;
+        if (x.mm != mmd[k]) d.mmd[i] = x.mm;
+        if (x.mfp != mfp[k]) d.mfp[i] = x.mfp;
+        if (d.anyImd && x.im != imd[k]) d.imd[i] = x.im;
         if (x.fl & 1) {
           x.mt = now - gt[k];
           d.meshTime[i] = x.mt;
