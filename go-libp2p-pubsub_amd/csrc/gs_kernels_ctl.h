@@ -163,19 +163,22 @@ template <int WPL>
 __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, int cur, int head) {
   __shared__ uint64_t scache[64 * WPL];  // v's mcache windows (handleIWant, step 2)
   uint64_t* const sseen = scache;        // then v's seen row (handleIHave, step 3)
-  __shared__ unsigned int sH[GS_PTXH];
+  // step 2's peertx hash; the step-3 arrays below live in the same LDS once
+  // step 2 has written the table back to its list form
+  __shared__ __attribute__((aligned(16))) unsigned int sH[GS_PTXH];
   __shared__ double sterm[64];
   __shared__ int sIt[64];                // per-sender exclusive item prefix
   __shared__ int sReqOff[64], sReqN[64]; // step 2: request list of each sender
   __shared__ int sOut[64];               // step 2/3: where each sender's id list starts
-  __shared__ int sNode[64];              // step 3: sender node
-  __shared__ uint64_t sTm[64];           // step 3: advertised subscribed topics
   __shared__ int sCnt[64], sCur[64];     // per-sender id counts / write cursors
-  __shared__ unsigned long long sKey[64];
-  __shared__ long long sMid[64];
-  __shared__ int sSlot[64];
   __shared__ unsigned long long sBase;
-  __shared__ uint32_t sHas[64 * 64 / 32];  // step 3: items with a want (<= 64 senders x 64 topics)
+  int* const sNode = (int*)sH;                                  // step 3: sender node
+  uint64_t* const sTm = (uint64_t*)(sH + 64);                   // step 3: advertised subscribed topics
+  unsigned long long* const sKey = (unsigned long long*)(sH + 192);
+  long long* const sMid = (long long*)(sH + 320);
+  int* const sSlot = (int*)(sH + 448);
+  uint32_t* const sHas = (uint32_t*)(sH + 512);  // step 3: items with a want (<= 64 senders x 64 topics)
+  static_assert(512 + 64 * 64 / 32 <= GS_PTXH, "step-3 arrays must fit in the peertx hash");
   const int v = d.n0 + blockIdx.x;
   const int lane = lane_id();
   const int prv = cur ^ 1;
@@ -333,9 +336,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
   // ---- step 2: handleIWant — serve cached messages at most GossipRetransmission times per peer
   int64_t respRec = -1;
   long long cServed = 0;
-  bool ptxDirty = false;
   if (__ballot(gateIWant)) {
-    ptxDirty = true;
     for (int w = lane; w < W; w += 64) {
       uint64_t x = 0;
       for (int k = 0; k < d.HL; ++k) x |= d.hist[((int64_t)((head + k) % d.R) * d.N + v) * W + w];
@@ -404,6 +405,20 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
       }
     }
     __syncthreads();
+    {  // peertx table back to its list form
+      __syncthreads();
+      int kept = 0;
+      for (int q0 = 0; q0 < GS_PTXH; q0 += 64) {
+        const unsigned int e32 = sH[q0 + lane];
+        int tot;
+        const int pos = kept + lane_prefix(e32 != 0u ? 1 : 0, &tot);
+        if (e32 && pos < GS_PTX) d.ptx[(int64_t)v * GS_PTX + pos] = ptx_to64(e32);
+        kept += tot;
+      }
+      if (kept > GS_PTX && lane == 0) set_err(d, E_PEERTX);
+      if (lane == 0) d.ptxN[v] = kept < GS_PTX ? kept : GS_PTX;
+    }
+    __syncthreads();  // sH is reused by step 3
   }
 
   GS_STAMPB(2);
@@ -605,19 +620,6 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
         if (respRec >= 0) d.cIresp[cur][e] = respRec;
       }
     }
-  }
-  if (ptxDirty) {  // peertx table back to its list form
-    __syncthreads();
-    int kept = 0;
-    for (int q0 = 0; q0 < GS_PTXH; q0 += 64) {
-      const unsigned int e32 = sH[q0 + lane];
-      int tot;
-      const int pos = kept + lane_prefix(e32 != 0u ? 1 : 0, &tot);
-      if (e32 && pos < GS_PTX) d.ptx[(int64_t)v * GS_PTX + pos] = ptx_to64(e32);
-      kept += tot;
-    }
-    if (kept > GS_PTX && lane == 0) set_err(d, E_PEERTX);
-    if (lane == 0) d.ptxN[v] = kept < GS_PTX ? kept : GS_PTX;
   }
   if (lane == 0) {
     if (cPrunes) ctr_add(d, C_PRUNES, (unsigned long long)cPrunes);
