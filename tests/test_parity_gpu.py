@@ -28,3 +28,29 @@ def test_gpu_stepwise_equals_one_call(oracle_path):
     e2.step(hops)
     ids = range(e1.counters()["published"])
     assert scenarios.compare(scenarios.snapshot(e1, ids), scenarios.snapshot(e2, ids)) == []
+
+
+def _retuned(lib):
+    """Topic.SetScoreParams mid-run (score.go:192-232): topic 1 gets lower
+    first/mesh delivery caps (the recap clamps existing counters) and new
+    weights; topic 2, unscored so far, becomes scored."""
+    from pubsub_amd import eth2_topic_score_params
+    e, hops = scenarios.SCENARIOS["gossipsub_multitopic"](lib)
+    e.step(hops // 2)
+    p = eth2_topic_score_params()
+    p.FirstMessageDeliveriesCap = 3.0
+    p.MeshMessageDeliveriesCap = 4.0
+    p.MeshMessageDeliveriesThreshold = 2.0
+    p.TopicWeight = 0.5
+    e.set_topic_score_params(1, p)
+    e.step(3)
+    q = eth2_topic_score_params()
+    q.TimeInMeshWeight = 0.01
+    e.set_topic_score_params(2, q)
+    e.step(hops - hops // 2)
+    return scenarios.snapshot(e, range(e.n_published))
+
+
+def test_gpu_set_topic_score_params_matches_oracle(oracle_path):
+    bad = scenarios.compare(_retuned(oracle_path), _retuned(PRODUCT_LIB))
+    assert bad == [], "\n".join(bad)
