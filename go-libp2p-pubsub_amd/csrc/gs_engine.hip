@@ -52,6 +52,7 @@ struct gs_engine {
   int64_t retireHops = 0;
   std::vector<int32_t> topicLive;  // per-topic live message count (phase-A counter width)
   int64_t hopsSinceFold = 0, foldEvery = 1;  // pending-delivery fold cadence (dlt)
+  std::vector<uint64_t> yWord, yTabH;          // phase A young-slot tables (per hop)
   int64_t refreshedHop = -1;                 // hop of the last refreshScores (S0 exact after it)
   int maxAge = 0;
   // host graph / attributes
@@ -371,6 +372,7 @@ int gs_engine::start() {
   x.tDivM = T == 1 ? 0 : ~0ull / (uint64_t)T + 1;  // ceil(2^64 / T)
   foldEvery = std::max<int64_t>(1, 65535 / (2 * (int64_t)St));  // a hop adds at most 2*St per (edge, topic)
   x.oldm = dalloc<uint64_t>(W); chk(x.oldm);
+  x.yTab = dalloc<uint64_t>(2 * (size_t)W); chk(x.yTab);
   x.nAuth = dalloc<int32_t>(N); chk(x.nAuth);
   x.sel = cfg.router == GS_ROUTER_RANDOMSUB ? dalloc<uint64_t>(NS) : nullptr;
   if (cfg.router == GS_ROUTER_RANDOMSUB) chk(x.sel);
@@ -532,16 +534,34 @@ int gs_engine::stepOne() {
   // (what this hop's frontier may hold), amR = the previous hop's (what the
   // senders' frontiers hold)
   WMask amR{}, amW{};
+  // phase A's young slots (the messages of amR): per amR word (by rank) the
+  // slot mask, then the number of young slots in the words before it
+  yWord.assign((size_t)W, 0);
+  yTabH.assign(2 * (size_t)W, 0);
+  int nY = 0;
   {
-    auto build = [&](int64_t lo, int64_t hi, WMask& m) {
+    auto build = [&](int64_t lo, int64_t hi, WMask& m, bool young) {
       auto it = std::lower_bound(mHop.begin(), mHop.end(), lo);
       for (size_t k = (size_t)(it - mHop.begin()); k < mHop.size() && mHop[k] <= hi; ++k) {
         const int w = mSlot[k] >> 6;
         m.m[w >> 6] |= 1ull << (w & 63);
+        if (young) yWord[w] |= 1ull << (mSlot[k] & 63);
       }
     };
-    build(h - 1 - maxAge, h - 1, amR);
-    build(h - maxAge, h, amW);
+    build(h - 1 - maxAge, h - 1, amR, true);
+    build(h - maxAge, h, amW, false);
+    int rk = 0;
+    for (int w = 0; w < W; ++w) {
+      if (!((amR.m[w >> 6] >> (w & 63)) & 1)) continue;
+      yTabH[rk] = yWord[w];
+      yTabH[(size_t)W + rk] = (uint64_t)nY;
+      nY += __builtin_popcountll(yWord[w]);
+      ++rk;
+    }
+    if (rk) {
+      HIPCHECK(hipMemcpyAsync(d.yTab, yTabH.data(), yTabH.size() * 8, hipMemcpyHostToDevice, stream));
+      HIPCHECK(hipStreamSynchronize(stream));  // yTabH is pageable host memory
+    }
   }
   std::vector<int32_t> retireWords;
   for (size_t k = b; k < e; ++k) {
@@ -601,13 +621,14 @@ int gs_engine::stepOne() {
         if (++topicLive[mTopic[k]] > 255) { narrow = false; break; }
     }
     const size_t nCnt = ((size_t)T * d.maxDeg + 7) & ~(size_t)7;
-    const size_t lds = (narrow ? 2 : 4) * nCnt + 8 * (size_t)nR + 64 * (size_t)nR + (d.needAge ? 4 * nCnt : 0);
+    const int nYp = (nY + 15) & ~15;
+    const size_t lds = (narrow ? 2 : 4) * nCnt + 16 * (size_t)nR + (size_t)nYp + (d.needAge ? 4 * nCnt : 0);
     TIMED(this, GS_K_PHASE_A, launch_wpl(W, [&](auto w) {
             if (!nOwn) return;
             if (narrow)
-              k_phase_a<decltype(w)::value, true><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR);
+              k_phase_a<decltype(w)::value, true><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR, nYp);
             else
-              k_phase_a<decltype(w)::value, false><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR);
+              k_phase_a<decltype(w)::value, false><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR, nYp);
           }));
   }
   if (!retireWords.empty()) {

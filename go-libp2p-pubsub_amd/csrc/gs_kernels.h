@@ -450,27 +450,34 @@ __device__ __forceinline__ int wave_min_int(int x) {
 //          every other copy); seen, mcache and v's own frontier list are written;
 //   pass 3 (lane = edge):   fmd / mmd of every (topic, in-edge) updated once.
 // LDS slot tables cover the words of the active window amR (messages young
-// enough to be in flight), indexed by the word's rank in amR.
+// enough to be in flight), indexed by the word's rank in amR; the lowest-
+// deliverer table holds one byte per YOUNG slot only (published in the last
+// maxAge + 1 hops: d.yTab gives each amR word's young-slot mask and prefix),
+// which halves it at config4 (about half of an amR word's slots hold older
+// messages): less LDS per wave, more waves per CU.  A copy of an older slot
+// can only be a duplicate (or E_LATE).
 // NARROW: the host proved that no sender can deliver more than 255 copies of
 // one topic in this hop (every topic has <= 255 live message slots), so the
 // (sender, topic) counters are 8-bit copies | 8-bit first deliveries, two per
 // LDS word: half the counter table, more waves per CU.
 template <int WPL, bool NARROW>
 __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int head, WMask amR, WMask amW,
-                                                int nR) {
+                                                int nR, int nY) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
   const int nCnt = (d.T * d.maxDeg + 7) & ~7;
   const int nCntW = NARROW ? nCnt / 2 : nCnt;             // LDS words of the counter table
   uint32_t* scnt = smem32;  // [MD][T] copies | fresh << 16 (NARROW: u16 copies | fresh << 8)
-  uint64_t* sD = (uint64_t*)(smem32 + nCntW);             // [nR] delivered slots (non-graylisted)
-  uint8_t* sFirst = (uint8_t*)(sD + nR);                  // [nR * 64] lowest deliverer
-  uint32_t* sUnc = (uint32_t*)(sFirst + nR * 64);         // [MD][T] uncredited duplicates (needAge)
+  uint64_t* sD = (uint64_t*)(smem32 + nCntW);             // [nR] delivered young slots (non-graylisted)
+  uint64_t* sYm = sD + nR;                                // [nR] young-slot mask of each amR word
+  uint8_t* sFirst = (uint8_t*)(sYm + nR);                 // [nY] lowest deliverer per young slot
+  uint32_t* sUnc = (uint32_t*)(sFirst + nY);              // [MD][T] uncredited duplicates (needAge)
   __shared__ int sBlk[64];        // first list block of each sender
   __shared__ uint64_t sRelay[64], sPub[64];
   __shared__ int sSnd[64];        // sender node | jr << 24 | graylisted << 31
   __shared__ int sLn[64];
   __shared__ uint32_t sQ[GS_QCAP];         // sent copies awaiting delivery: slot | sender << 16
   __shared__ uint16_t sRk[64 * GS_MAX_WPL];  // rank of word w in amR, 0xFFFF = outside
+  __shared__ uint16_t sYp[64 * GS_MAX_WPL];  // [rank] young slots in the amR words before it
   const int v = d.n0 + blockIdx.x;
   const int lane = lane_id();
   const int prv = cur ^ 1;
@@ -507,7 +514,11 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   for (int k = lane; k < nCntW / 4; k += 64) ((uint4*)scnt)[k] = make_uint4(0, 0, 0, 0);
   if (d.needAge)
     for (int k = lane; k < nCnt / 4; k += 64) ((uint4*)sUnc)[k] = make_uint4(0, 0, 0, 0);
-  for (int k = lane; k < nR; k += 64) sD[k] = 0;
+  for (int k = lane; k < nR; k += 64) {
+    sD[k] = 0;
+    sYm[k] = d.yTab[k];
+    sYp[k] = (uint16_t)d.yTab[d.W + k];
+  }
   {
     int rb = 0;  // rank of word 64 j + lane in amR
 #pragma unroll
@@ -518,7 +529,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
       rb += __popcll(m);
     }
   }
-  for (int k = lane; k < nR * 4; k += 64) ((uint4*)sFirst)[k] = make_uint4(~0u, ~0u, ~0u, ~0u);
+  for (int k = lane; k < nY / 16; k += 64) ((uint4*)sFirst)[k] = make_uint4(~0u, ~0u, ~0u, ~0u);
   // per-sender view for the block-parallel walk
   const int nb = (Ln + 3) >> 2;  // 16-byte blocks of the sender's list
   const int bincl = wave_incl_sum(nb);
@@ -551,7 +562,9 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     ++nCopies;
 #endif
     const int rk = sRk[w];
-    if (d.needAge || rk == 0xFFFF) {
+    const uint64_t ym = rk == 0xFFFF ? 0ull : sYm[rk];
+    const bool young = (ym >> (slot & 63)) & 1;
+    if (d.needAge || !young) {
       const bool had = (d.seen[(int64_t)v * W + w] >> (slot & 63)) & 1;
       // markDuplicateMessageDelivery window (score.go:955): a copy of a message
       // first delivered before this hop is credited only within the window
@@ -559,15 +572,15 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
         const int64_t firstHop = d.slotPubHop[slot] + d.age[(int64_t)v * d.S + slot];
         if ((h - firstHop) * d.hop_ns > d.tp[t].MmdWindow) atomicAdd(&sUnc[i * T + t], 1u);
       }
-      if (rk == 0xFFFF) {
-        // outside the window only an old duplicate is possible; a first
+      if (!young) {
+        // outside the young slots only an old duplicate is possible; a first
         // delivery there is later than the engine's window allows
         if (!had) set_err(d, E_LATE);
         return;
       }
     }
-    const int ix = rk * 64 + (slot & 63);
-    atomicOr((unsigned long long*)&sD[ix >> 6], 1ull << (slot & 63));
+    const int ix = sYp[rk] + __popcll(ym & ((1ull << (slot & 63)) - 1));
+    atomicOr((unsigned long long*)&sD[rk], 1ull << (slot & 63));
     // byte-wise min of the lowest deliverer (senders ascending)
     uint32_t* wp = (uint32_t*)(sFirst + (ix & ~3));
     const int sh = 8 * (ix & 3);
@@ -700,15 +713,17 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   if (scoring) sRelay[lane] = valid ? d.mesh[base + lane] : 0ull;  // pass 3: in-edge mesh words
   long long nDeliv = 0;
   uint64_t Uw[WPL], Sw[WPL], Hw[WPL], Ow[WPL];
-  int ixw[WPL];
+  int rkw[WPL];  // rank of the lane's word in amR
+  // index of young slot b of the amR word of rank rk in sFirst
+  auto fidx = [&](int rk, int b) -> int { return sYp[rk] + __popcll(sYm[rk] & ((1ull << b) - 1)); };
 #pragma unroll
   for (int j = 0; j < WPL; ++j) {
     const int w = lane + 64 * j;
     Uw[j] = Sw[j] = Hw[j] = Ow[j] = 0;
-    ixw[j] = 0;
+    rkw[j] = 0;
     if (w < W && wm_has(amR, w)) {
-      ixw[j] = wm_rank(amR, w) * 64;
-      const uint64_t D = sD[ixw[j] >> 6];
+      rkw[j] = wm_rank(amR, w);
+      const uint64_t D = sD[rkw[j]];
       if (D) {
         Sw[j] = d.seen[(int64_t)v * W + w];
         Uw[j] = D;  // & ~seen below
@@ -733,7 +748,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
       while (y) {
         const int b = __ffsll((long long)y) - 1;
         y &= y - 1;
-        const int pl = sFirst[ixw[j] + b] * T + t;
+        const int pl = sFirst[fidx(rkw[j], b)] * T + t;
         if (NARROW) atomicAdd(&scnt[pl >> 1], 1u << (16 * (pl & 1) + 8));
         else atomicAdd(&scnt[pl], 1u << 16);
       }
@@ -827,7 +842,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
         const int b = __ffsll((long long)y) - 1;
         y &= y - 1;
         const int slot = w * 64 + b;
-        const int ff = sFirst[ixw[j] + b];
+        const int ff = sFirst[fidx(rkw[j], b)];
         if (trv)  // pubsub.go:1057, ReceivedFrom = the first deliverer
           trace_emit(d, h, GS_TRACE_DELIVER_MESSAGE, v, d.col[base + ff], (int)__umulhi((unsigned)slot, d.stMagic),
                      d.slotMid[slot], 2);
@@ -848,11 +863,11 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
         lanesWith &= lanesWith - 1;
         uint64_t y = lane_get64(U, src);
         const int wsrc = src + 64 * j;
-        const int ixs = lane_get(ixw[j], src);
+        const int rks = lane_get(rkw[j], src);
         while (y) {
           const int b = __ffsll((long long)y) - 1;
           y &= y - 1;
-          rs_select(d, v, deg, valid ? u : -1, valid ? d.sub[u] : 0, wsrc * 64 + b, sFirst[ixs + b]);
+          rs_select(d, v, deg, valid ? u : -1, valid ? d.sub[u] : 0, wsrc * 64 + b, sFirst[fidx(rks, b)]);
         }
       }
     }
