@@ -657,7 +657,7 @@ int gs_engine::stepOne() {
           }));
   }
   if (refreshDue(now)) {
-    TIMED(this, GS_K_REFRESH, (k_refresh_rows<<<sgb, 64, 0, stream>>>(d, now)));
+    TIMED(this, GS_K_REFRESH, (k_refresh_rows<<<nblk(eOwn, GS_RG), 64, 0, stream>>>(d, now)));
     refreshedHop = h;
     hopsSinceFold = 0;
   } else if (scoring && ++hopsSinceFold >= foldEvery) {

@@ -50,6 +50,11 @@
 //     the few scores it needs as values (Dhi ranking) from the same rule.
 #define GS_SG 16  // edges per wave
 #define GS_SB 8   // edges per load batch
+// refresh: one load batch per wave, so no wave issues a batch's loads behind
+// its own previous batch's stores (on gfx9 vmcnt counts both)
+#ifndef GS_RG
+#define GS_RG 16
+#endif
 template <int MODE>
 __global__ __launch_bounds__(64) void k_score_rows(Dev d, double* __restrict__ out) {
   __shared__ double sT[GS_SG * 65];  // [edge][topic], row stride 65: conflict-free column reads
@@ -113,15 +118,15 @@ __global__ __launch_bounds__(64) void k_score_rows(Dev d, double* __restrict__ o
 }
 
 // refreshScores — score.go:495-556 (every peer is connected: no retention
-// path), GS_SG edges per wave, lane = topic, and the exact score of every
+// path), GS_RG edges per wave, lane = topic, and the exact score of every
 // edge from the refreshed state into S0 (sdirty cleared): nothing but
 // refreshScores changed the state since the hop's message phase, so this is
 // the value the next S0 pass would compute.
 __global__ __launch_bounds__(64) void k_refresh_rows(Dev d, int64_t now) {
-  __shared__ double sT[GS_SG * 65];
+  __shared__ double sT[GS_RG * 65];
   const int lane = lane_id();
-  const int64_t e0 = d.e0 + (int64_t)blockIdx.x * GS_SG;
-  const int ng = (int)min((int64_t)GS_SG, d.e1 - e0);
+  const int64_t e0 = d.e0 + (int64_t)blockIdx.x * GS_RG;
+  const int ng = (int)min((int64_t)GS_RG, d.e1 - e0);
   const int T = d.T;
   const int tl = lane < T ? lane : 0;
   const TopicP& tp = d.tp[tl];
