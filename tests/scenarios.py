@@ -85,6 +85,14 @@ def gossipsub_scored(lib, n=300, k=20, topics=1, seed=3, msgs=300, hb=12, flood=
     top = rng2.integers(0, topics, msgs).astype(np.int32)
     hops = (5 + (np.arange(msgs) * (hb * 10 - 20)) // msgs).astype(np.int64)
     e.publish(src, top, hops)
+    st = window // topics
+    if msgs > st:
+        # the engine reads back only messages whose slot is not recycled yet:
+        # each topic's last `st` messages (slots are a ring per topic)
+        keep = []
+        for t in range(topics):
+            keep += list(np.flatnonzero(top == t)[-st:])
+        e.snapshot_ids = sorted(int(i) for i in keep)
     return e, hb * 10 + 5
 
 
@@ -98,6 +106,13 @@ SCENARIOS = {
     "gossipsub_multitopic": lambda lib, x=(): gossipsub_scored(lib, n=200, topics=3, sub_frac=0.7, seed=7, msgs=240, extra=x),
     "gossipsub_negative_app": lambda lib, x=(): gossipsub_scored(lib, n=200, app_neg_frac=0.2, ip_groups=40, seed=9, extra=x),
     "gossipsub_dense_dhi": lambda lib, x=(): gossipsub_scored(lib, n=120, k=40, seed=11, hb=20, msgs=200, extra=x),
+    # message windows smaller than the message count: slots are recycled, and
+    # every active word mixes young slots with older or retired ones (phase A's
+    # young-slot tables)
+    "gossipsub_slot_reuse": lambda lib, x=(): gossipsub_scored(lib, n=200, seed=13, msgs=400, hb=16, window=320,
+                                                               extra=x),
+    "gossipsub_slot_reuse_4t": lambda lib, x=(): gossipsub_scored(lib, n=200, topics=4, seed=17, msgs=600, hb=16,
+                                                                  window=512, extra=x),
 }
 
 
@@ -112,7 +127,7 @@ def snapshot(e, msg_ids):
 def run(lib, name, extra_hops=0, extra=()):
     e, hops = SCENARIOS[name](lib, extra)
     e.step(hops + extra_hops)
-    snap = snapshot(e, range(e.n_published))
+    snap = snapshot(e, getattr(e, "snapshot_ids", range(e.n_published)))
     snap["node_range"], snap["edge_range"] = e.node_range, e.edge_range
     return snap
 
