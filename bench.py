@@ -226,14 +226,20 @@ def main():
                "active_words": float(np.mean([active_words(eng, wl, hop0 + i) for i in range(nh)]))}
     bytes_per_launch, bytes_info = algorithmic_bytes(dom, eng, wl, per_hop)
     roofline = None
-    traffic, traffic_src = None, None
     pmc = os.path.join(REPO, "profiles", f"pmc_traffic_{args.workload}.json")
-    if os.path.exists(pmc) and not partitioned:
+    pmc_recs = json.load(open(pmc)) if os.path.exists(pmc) and not partitioned else {}
+
+    def pmc_traffic(kernel):
         # rocprofv3 PMC passes of this workload (scripts/gpu_pmc.sh + pmc_summary.py):
-        # FETCH_SIZE x 2 (gfx950 wide-read correction, MI355X_MICROARCH.md) + WRITE_SIZE
-        rec = json.load(open(pmc)).get(f"void k_{dom}<4>") or json.load(open(pmc)).get(f"k_{dom}")
-        if rec:
-            traffic, traffic_src = rec["traffic_bytes_est"], os.path.relpath(pmc, REPO)
+        # FETCH_SIZE x 2 (gfx950 wide-read correction, MI355X_MICROARCH.md) + WRITE_SIZE,
+        # per launch; kernel names carry template arguments ("void k_phase_a<4, true>")
+        base = {"refresh": "k_refresh_rows"}.get(kernel, f"k_{kernel}")
+        for name, rec in pmc_recs.items():
+            if name == base or name.startswith(f"void {base}<"):
+                return rec["traffic_bytes_est"], os.path.relpath(pmc, REPO)
+        return None, None
+
+    traffic, traffic_src = pmc_traffic(dom)
     if bytes_per_launch:
         achieved = bytes_per_launch / (avg_ms / 1e3) / 1e9
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -252,6 +258,7 @@ def main():
             rooflines[k] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": round(ach / HBM_PEAK_GBS, 4), "avg_launch_ms": round(ms_k, 4),
                             "bytes_per_launch": int(b_k)}
+            rooflines[k]["traffic"], rooflines[k]["traffic_source"] = pmc_traffic(k)
     rounds_per_s = args.steps / elapsed
     out = {
         "metric": "peer-message deliveries/sec + gossipsub rounds/sec (node), 1M peers 64 topics",

@@ -33,6 +33,18 @@ def test_library_exports_every_symbol(which, oracle_path):
         assert hasattr(lib, name), f"{which} library does not export {name}"
 
 
+def test_product_exports_rpc_header():
+    """include/gs_rpc.h (host-side RPC fragmentation) is product-only."""
+    if not os.path.exists(PRODUCT_LIB):
+        pytest.skip("product library not built")
+    src = open(os.path.join(REPO, "include", "gs_rpc.h")).read()
+    names = set(re.findall(r"^[a-z_0-9 \*]+?\b(gs_[a-z_0-9]+)\(", src, re.M))
+    assert {"gs_rpc_size", "gs_fragment_rpc"} <= names
+    lib = C.CDLL(PRODUCT_LIB)
+    for name in names:
+        assert hasattr(lib, name), f"product library does not export {name}"
+
+
 def test_product_params_match_oracle(oracle_path):
     if not os.path.exists(PRODUCT_LIB):
         pytest.skip("product library not built")
