@@ -222,3 +222,19 @@ def test_empty_rpc_and_bad_arguments():
         fragment_rpc(RpcShape(), 0)
     with pytest.raises(GossipEngineError):  # control entries without a control message
         fragment_rpc(RpcShape(graft_size=[6]), LIMIT)
+
+
+def test_product_matches_golden_fixture():
+    """tests/golden/rpc_fragment.json (tests/golden/make_rpc_golden.py): the oracle's
+    fragment sizes on the reference test's RPCs and on seeded random RPCs."""
+    import json
+    from pubsub_amd.rpc import RpcShape, fragment_rpc
+    cases = json.load(open(os.path.join(REPO, "tests", "golden", "rpc_fragment.json")))
+    assert len(cases) == 36
+    for c in cases:
+        shape = RpcShape(**c["shape"])
+        if "error" in c:
+            with pytest.raises(GossipEngineError, match=c["error"]):
+                fragment_rpc(shape, c["limit"])
+        else:
+            assert list(fragment_rpc(shape, c["limit"]).frag_size) == c["frag_size"], c["name"]
