@@ -161,6 +161,14 @@ def check_against_oracle(rpc, limit):
         exp = ([(k, GS_RPC_IWANT, w.ids) for k, r in enumerate(want) for w in ctl_of(r).iwant]
                + [(k, GS_RPC_IHAVE, h.ids) for k, r in enumerate(want) for h in ctl_of(r).ihave])
     assert got_buckets == exp
+    # every bucket's ids come from the entry bucket_src names
+    n_ih = sum(len(h.ids) for h in c.ihave)
+    owner = ([(GS_RPC_IHAVE, j) for j, h in enumerate(c.ihave) for _ in h.ids]
+             + [(GS_RPC_IWANT, j) for j, w in enumerate(c.iwant) for _ in w.ids])
+    assert len(owner) == len(all_ids) >= n_ih
+    for i, b in enumerate(got.id_bucket):
+        if b >= 0:
+            assert owner[i] == (int(got.bucket_kind[b]), int(got.bucket_src[b]))
     kept = {id(m) for _, _, ids in exp for m in ids}
     for i, m in enumerate(all_ids):
         assert (got.id_bucket[i] >= 0) == (id(m) in kept)
