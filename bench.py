@@ -112,28 +112,51 @@ def algorithmic_bytes(kernel, eng, wl, per_hop):
     return None, {}
 
 
-def cpu_baseline(wl):
-    """The CPU oracle (a faithful single-threaded C++ restatement of the
-    reference's routers + peerScore) on a bounded sample of the workload."""
+def cpu_info():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return model
+
+
+def cpu_baseline(wl, seconds=20.0):
+    """The CPU oracle (a faithful C++ restatement of the reference's routers +
+    peerScore, OpenMP over nodes in every per-node phase) on a bounded sample
+    of the SAME workload: same degree, topic count, scoring and per-peer
+    message rate (every peer receives all 1000 msgs/round), fewer peers."""
+    import ctypes
     lib = os.path.join(REPO, "oracle", "_build", "libgossip_oracle.so")
     if not os.path.exists(lib):
         return None
+    threads = ctypes.CDLL(lib).gs_oracle_threads()
     n = 2000
-    T = min(wl["topics"], 8)
-    swl = dict(wl, n=n, topics=T, slots=max(256, wl["slots"] if T == 1 else 256))
-    rounds = 3
-    eng, _ = build_engine(swl, rounds + 1, 11, 0, lib=lib, n=n, msgs_per_round=100)
-    eng.step(HOPS_PER_ROUND + 1)
+    swl = dict(wl, n=n)
+    rounds = 8
+    eng, _ = build_engine(swl, rounds + 2, 11, 0, lib=lib, n=n)
+    eng.step(HOPS_PER_ROUND + 1)  # Join + one warm-up round
     c0 = eng.counters()
     t0 = time.perf_counter()
-    eng.step(rounds * HOPS_PER_ROUND - 1)
+    hops = 0
+    while hops < rounds * HOPS_PER_ROUND and (time.perf_counter() - t0 < seconds or hops < HOPS_PER_ROUND):
+        eng.step(1)
+        hops += 1
     dt = time.perf_counter() - t0
     c1 = eng.counters()
     dlv = c1["deliveries"] - c0["deliveries"]
-    return {"value": dlv / dt, "unit": "deliveries/s", "cores": 1, "kind": "port",
-            "rounds_per_sec": (rounds * HOPS_PER_ROUND - 1) / HOPS_PER_ROUND / dt,
-            "sample": f"oracle/ (C++ restatement), {n} peers k=32, {T} topics, Eth2 scoring, "
-                      f"100 msgs/round, {rounds} rounds after warm-up, 1 thread, {dt:.1f} s"}
+    rps = hops / HOPS_PER_ROUND / dt
+    return {"value": dlv / dt, "unit": "deliveries/s", "cores": threads, "kind": "port",
+            "rounds_per_sec_sample": rps,
+            "rounds_per_sec_extrapolated_1M": rps * n / wl["n"],
+            "extrapolation": f"per-peer linear: rounds/s x {n}/{wl['n']} (labelled estimate, not measured)",
+            "cpu_model": cpu_info(), "nproc": os.cpu_count(),
+            "sample": f"oracle/ (C++ restatement, OpenMP {threads} threads), {n} peers k={wl['k']}, "
+                      f"{wl['topics']} topics, Eth2 scoring, {MSGS_PER_ROUND} msgs/round, {hops} hops "
+                      f"after 1 warm-up round, {dt:.1f} s"}
 
 
 def main():
@@ -148,6 +171,19 @@ def main():
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # not launched by torch.distributed.run: start the N ranks ourselves (a
+        # child process, before anything here touches the GPU) and exit with its code
+        import socket
+        import subprocess
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; refusing to report a different GPU count")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None

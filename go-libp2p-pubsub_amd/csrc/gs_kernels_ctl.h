@@ -555,6 +555,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     GS_STAMPB(7);
   }
   cIwantSent = (long long)wave_sum_ll(cIwantSent);
+  cGray = (long long)wave_sum_ll(cGray);  // per-lane (sender) counts
 
   // ---- gossipTracer.AddPromise (gossip_tracer.go:48-75) for every sender we
   // sent an IWANT, senders ascending; table lane q = entry q

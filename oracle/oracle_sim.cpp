@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <memory>
+#include <omp.h>
 #include <unordered_map>
 
 #include "oracle_core.hpp"
@@ -68,6 +69,8 @@ struct Node {
   std::map<int, double> memo;            // S0: hop-start score snapshot
   std::map<int, std::vector<RPC>> out;   // RPCs sent during this hop, per destination
   std::map<int, int> acceptStatus;       // AcceptFrom result per sender this hop
+  gs_counters ctr{};                     // this node's event counters (summed by gs_read_counters)
+  std::vector<gs_trace_event> ev;        // this node's trace events (it is the tracing host)
 
   double Score(int p);                   // gs.score.Score (0 when scoring is off)
   void sendRPC(int p, RPC rpc);
@@ -120,15 +123,13 @@ struct Sim {
   int64_t now() const { return hop * cfg.hop_ns; }
   // EventTracer (trace.go:61-499) of the hosts with traced[u] != 0
   std::vector<uint8_t> traced;
-  std::vector<gs_trace_event> events;
+  std::vector<gs_trace_event> events;  // drained from the nodes' buffers by gs_trace_read
   size_t traceRead = 0;
-  void emit(int type, int node, int peer, int topic, int64_t msg, int phase) {
-    if (traced.empty() || !traced[node]) return;
-    gs_trace_event e;
-    e.hop = hop; e.msg = msg; e.type = type; e.node = node; e.peer = peer;
-    e.topic = (int16_t)topic; e.phase = (int16_t)phase;
-    events.push_back(e);
-  }
+  // Events go to the tracing host's own buffer, so nodes run in parallel
+  // (OpenMP over nodes in every per-node phase; the canonical event order
+  // of gs_trace.h is keyed by host, so the merge order does not matter).
+  void emit(int type, int node, int peer, int topic, int64_t msg, int phase);
+  gs_counters total() const;
 
   int edgeIndex(int u, int v) const {
     auto b = col.begin() + rowptr[u], e = col.begin() + rowptr[u + 1];
@@ -146,6 +147,26 @@ struct Sim {
   void step();
 };
 
+void Sim::emit(int type, int node, int peer, int topic, int64_t msg, int phase) {
+  if (traced.empty() || !traced[node]) return;
+  gs_trace_event e;
+  e.hop = hop; e.msg = msg; e.type = type; e.node = node; e.peer = peer;
+  e.topic = (int16_t)topic; e.phase = (int16_t)phase;
+  if (nodes.empty()) events.push_back(e); else nodes[node].ev.push_back(e);
+}
+
+gs_counters Sim::total() const {
+  gs_counters c = ctr;
+  for (const Node& nd : nodes) {
+    c.published += nd.ctr.published; c.deliveries += nd.ctr.deliveries; c.duplicates += nd.ctr.duplicates;
+    c.transmissions += nd.ctr.transmissions; c.grafts_sent += nd.ctr.grafts_sent;
+    c.prunes_sent += nd.ctr.prunes_sent; c.ihave_sent += nd.ctr.ihave_sent; c.iwant_sent += nd.ctr.iwant_sent;
+    c.iwant_served += nd.ctr.iwant_served; c.promises_broken += nd.ctr.promises_broken;
+    c.graylisted += nd.ctr.graylisted;
+  }
+  return c;
+}
+
 double Node::Score(int p) { return sim->scoring ? score.score(p) : 0.0; }
 
 // sendRPC / doSendRPC — gossipsub.go:1092-1156 (queues never drop in the
@@ -157,10 +178,10 @@ void Node::sendRPC(int p, RPC rpc) {
     rpc.ctl.ihave = g->second;
     gossip.erase(g);
   }
-  sim->ctr.grafts_sent += (int64_t)rpc.ctl.graft.size();
-  sim->ctr.prunes_sent += (int64_t)rpc.ctl.prune.size();
-  sim->ctr.ihave_sent += (int64_t)rpc.ctl.ihave.size();
-  sim->ctr.iwant_sent += (int64_t)rpc.ctl.iwant.size();
+  ctr.grafts_sent += (int64_t)rpc.ctl.graft.size();
+  ctr.prunes_sent += (int64_t)rpc.ctl.prune.size();
+  ctr.ihave_sent += (int64_t)rpc.ctl.ihave.size();
+  ctr.iwant_sent += (int64_t)rpc.ctl.iwant.size();
   out[p].push_back(std::move(rpc));
 }
 
@@ -220,7 +241,7 @@ void Node::localPublish(const Msg& m) {
   sim->emit(GS_TRACE_PUBLISH_MESSAGE, id, -1, m.topic, m.id, 1);  // validation.go:217
   sim->emit(GS_TRACE_DELIVER_MESSAGE, id, id, m.topic, m.id, 1);  // pubsub.go:1057
   seen.insert(m.id);
-  sim->ctr.published++;
+  ctr.published++;
   if (sim->record) sim->deliv[id][m.id] = {(int32_t)sim->hop, -1};
   routerPublish(m, id);
 }
@@ -235,13 +256,13 @@ void Node::handleMessage(int from, const Msg& m) {
   }
   if (seen.count(m.id)) {                   // duplicate (pubsub.go:1010-1013)
     sim->emit(GS_TRACE_DUPLICATE_MESSAGE, id, from, m.topic, m.id, 2);
-    sim->ctr.duplicates++;
+    ctr.duplicates++;
     if (sim->scoring) score.DuplicateMessage(m, from, sim->now());
     return;
   }
   seen.insert(m.id);                        // markSeen
   sim->emit(GS_TRACE_DELIVER_MESSAGE, id, from, m.topic, m.id, 2);
-  sim->ctr.deliveries++;
+  ctr.deliveries++;
   if (sim->record) sim->deliv[id][m.id] = {(int32_t)sim->hop, from};
   if (sim->scoring) {                       // tracer.DeliverMessage -> raw tracers
     score.DeliverMessage(m, from, sim->now());
@@ -347,7 +368,7 @@ void Node::handleRPC(int from, const Control& ctl) {
   r.publish = ihave;
   if (!iwant.empty()) r.ctl.iwant = iwant;
   r.ctl.prune = prune;
-  sim->ctr.iwant_served += (int64_t)ihave.size();
+  ctr.iwant_served += (int64_t)ihave.size();
   sendRPC(from, std::move(r));
 }
 
@@ -484,7 +505,7 @@ void Node::applyIwantPenalties() {  // gossipsub.go:1566-1571
   auto broken = gtracer.GetBrokenPromises(sim->now());
   for (auto& kv : broken) {
     score.AddPenalty(kv.first, kv.second);
-    sim->ctr.promises_broken += kv.second;
+    ctr.promises_broken += kv.second;
   }
 }
 
@@ -743,7 +764,11 @@ void Sim::step() {
     for (auto& kv : nd.out) inbox[kv.first][nd.id] = std::move(kv.second);
     nd.out.clear();
   }
+  // Every per-node phase below touches only the node's own state (its router
+  // maps, peerScore, mcache, outbox, counters and trace buffer) and reads
+  // shared immutable data, so nodes run in parallel; the phase order is kept.
   if (hop == 0) {  // Join: the GRAFTs it sends arrive in hop 1
+#pragma omp parallel for schedule(dynamic, 64)
     for (int u = 0; u < N; ++u)
       for (int tp = 0; tp < T; ++tp)
         if ((nodes[u].mySubs >> tp) & 1) {
@@ -752,11 +777,14 @@ void Sim::step() {
         }
   }
   // S0 memo
-  if (scoring)
-    for (Node& nd : nodes) {
+  if (scoring) {
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int u = 0; u < N; ++u) {
+      Node& nd = nodes[u];
       nd.memo.clear();
       for (int v : nd.nbrs) nd.memo[v] = nd.score.score(v);
     }
+  }
   // local publishes of this hop
   while (nextPub < msgs.size() && msgHop[nextPub] == hop) {
     const Msg& m = msgs[nextPub];
@@ -764,7 +792,9 @@ void Sim::step() {
     nextPub++;
   }
   // phase A: payload messages, senders ascending
-  for (Node& nd : nodes) {
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int u = 0; u < N; ++u) {
+    Node& nd = nodes[u];
     nd.acceptStatus.clear();
     for (auto& kv : inbox[nd.id]) {
       int s = kv.first;
@@ -774,15 +804,17 @@ void Sim::step() {
         else if (scoring && nd.memo[s] < thr.GraylistThreshold) st = PeerGater::AcceptNone;
       }
       nd.acceptStatus[s] = st;
-      for (const RPC& r : kv.second) ctr.transmissions += (int64_t)r.publish.size();  // copies on the wire
-      if (st == PeerGater::AcceptNone) { ctr.graylisted += (int64_t)kv.second.size(); continue; }
+      for (const RPC& r : kv.second) nd.ctr.transmissions += (int64_t)r.publish.size();  // copies on the wire
+      if (st == PeerGater::AcceptNone) { nd.ctr.graylisted += (int64_t)kv.second.size(); continue; }
       for (const RPC& r : kv.second)
         for (int64_t mid : r.publish) nd.handleMessage(s, msgs[mid]);
     }
   }
   // phase B: control, per RPC, senders ascending
   if (cfg.router == GS_ROUTER_GOSSIPSUB) {
-    for (Node& nd : nodes) {
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int u = 0; u < N; ++u) {
+      Node& nd = nodes[u];
       for (auto& kv : inbox[nd.id]) {
         int s = kv.first;
         if (nd.acceptStatus[s] == PeerGater::AcceptNone) continue;
@@ -791,12 +823,17 @@ void Sim::step() {
       }
     }
   }
-  if (refreshDue(t))
-    for (Node& nd : nodes) nd.score.refreshScores(t);
-  if (scoring && t > 0 && t % (60 * kSecond) == 0)
-    for (Node& nd : nodes) nd.score.gc(t);
+  if (refreshDue(t)) {
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int u = 0; u < N; ++u) nodes[u].score.refreshScores(t);
+  }
+  if (scoring && t > 0 && t % (60 * kSecond) == 0) {
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int u = 0; u < N; ++u) nodes[u].score.gc(t);
+  }
   if (heartbeatDue(t)) {
-    for (Node& nd : nodes) nd.heartbeat();
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int u = 0; u < N; ++u) nodes[u].heartbeat();
     ctr.heartbeats++;
   }
   ctr.hops++;
@@ -965,7 +1002,7 @@ int gs_set_topic_score_params(gs_engine* eng, int32_t topic, const gs_topic_scor
 
 int64_t gs_num_edges(const gs_engine* eng) { return eng->sim.E; }
 int64_t gs_current_hop(const gs_engine* eng) { return eng->sim.hop; }
-int gs_read_counters(gs_engine* eng, gs_counters* out) { *out = eng->sim.ctr; return GS_OK; }
+int gs_read_counters(gs_engine* eng, gs_counters* out) { *out = eng->sim.total(); return GS_OK; }
 
 int gs_read_scores(gs_engine* eng, double* score) {
   Sim& s = eng->sim;
@@ -1079,7 +1116,13 @@ int gs_set_trace(gs_engine* g, const uint8_t* node_mask, int64_t capacity) {
 }
 int gs_trace_read(gs_engine* g, gs_trace_event* out, int64_t cap, int64_t* n) {
   Sim& s = g->sim;
-  if (s.traceRead == 0) std::stable_sort(s.events.begin(), s.events.end(), gs_trace_less);
+  if (s.traceRead == 0) {
+    for (Node& nd : s.nodes) {
+      s.events.insert(s.events.end(), nd.ev.begin(), nd.ev.end());
+      nd.ev.clear();
+    }
+    std::stable_sort(s.events.begin(), s.events.end(), gs_trace_less);
+  }
   const int64_t k = std::min<int64_t>(cap, (int64_t)(s.events.size() - s.traceRead));
   for (int64_t i = 0; i < k; ++i) out[i] = s.events[s.traceRead + i];
   s.traceRead += (size_t)k;
@@ -1093,6 +1136,17 @@ int gs_trace_encode(const gs_trace_event*, int64_t, int32_t, int64_t, const char
   set_error("gs_trace_encode is in the product library");
   return GS_EUNSUPPORTED;
 }
+// Oracle-only: OpenMP threads the per-node phases use (bench.py's cpu_baseline).
+int gs_oracle_threads(void) {
+  int n = 1;
+#pragma omp parallel
+  {
+#pragma omp single
+    n = omp_get_num_threads();
+  }
+  return n;
+}
+
 int gs_read_exchange_stats(gs_engine*, double* host_ms, int64_t* bytes_in) {
   *host_ms = 0;
   *bytes_in = 0;

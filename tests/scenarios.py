@@ -5,7 +5,7 @@ bit-exactly (float64 compared on their bit patterns)."""
 import numpy as np
 
 from pubsub_amd import (NewFloodSub, NewGossipSub, NewRandomSub, PeerScoreParams, Second,
-                        TopicScoreParams, WithFloodPublish, WithGossipSubParams, WithHop,
+                        TopicScoreParams, WithDirectPeers, WithFloodPublish, WithGossipSubParams, WithHop,
                         WithMessageWindow, WithPeerScore, WithRecordDeliveries, WithSeed,
                         eth2_peer_score_params, eth2_thresholds, eth2_topic_score_params)
 from pubsub_amd import graphs
@@ -55,10 +55,26 @@ def gossipsub_dense(lib, seed=1, msgs=100, extra=()):
 
 
 def gossipsub_scored(lib, n=300, k=20, topics=1, seed=3, msgs=300, hb=12, flood=False, sub_frac=1.0,
-                     app_neg_frac=0.0, ip_groups=0, params=None, window=1024, extra=()):
-    """gossipsub v1.1 with Eth2-derived scoring over a random regular graph."""
+                     app_neg_frac=0.0, ip_groups=0, params=None, window=1024, extra=(), app_neg=-150.0,
+                     direct_frac=0.0, topic0_frac=0.0):
+    """gossipsub v1.1 with Eth2-derived scoring over a random regular graph.
+    window = slots_per_topic; direct_frac: fraction of the undirected edges
+    made direct peers on both ends (WithDirectPeers); topic0_frac: fraction of
+    the messages forced onto topic 0."""
     rng = np.random.default_rng(seed)
     g = graphs.random_regular(n, k, seed)
+    if direct_frac:
+        rowptr, col, _ = g
+        src = np.repeat(np.arange(n), np.diff(rowptr))
+        pick = np.random.default_rng(seed + 55).random(len(col)) < direct_frac
+        und = set()
+        for u, v in zip(src[pick], col[pick]):
+            und.add((min(u, v), max(u, v)))
+        direct = np.zeros(len(col), dtype=np.uint8)
+        for e in range(len(col)):
+            if (min(src[e], col[e]), max(src[e], col[e])) in und:
+                direct[e] = 1
+        extra = tuple(extra) + (WithDirectPeers(direct),)
     if sub_frac >= 1.0:
         subs = graphs.all_subscribed(n, topics)
     else:
@@ -69,7 +85,7 @@ def gossipsub_scored(lib, n=300, k=20, topics=1, seed=3, msgs=300, hb=12, flood=
     thr = eth2_thresholds()
     app = np.zeros(n)
     if app_neg_frac:
-        app[rng.random(n) < app_neg_frac] = -150.0
+        app[rng.random(n) < app_neg_frac] = app_neg
     ipv4 = None
     if ip_groups:
         ipv4 = (rng.integers(0, ip_groups, n) + (10 << 24)).astype(np.uint32)
@@ -83,9 +99,11 @@ def gossipsub_scored(lib, n=300, k=20, topics=1, seed=3, msgs=300, hb=12, flood=
     rng2 = np.random.default_rng(seed + 100)
     src = rng2.integers(0, n, msgs).astype(np.int32)
     top = rng2.integers(0, topics, msgs).astype(np.int32)
+    if topic0_frac:
+        top[rng2.random(msgs) < topic0_frac] = 0
     hops = (5 + (np.arange(msgs) * (hb * 10 - 20)) // msgs).astype(np.int64)
     e.publish(src, top, hops)
-    st = window // topics
+    st = window
     if msgs > st:
         # the engine reads back only messages whose slot is not recycled yet:
         # each topic's last `st` messages (slots are a ring per topic)
@@ -112,8 +130,28 @@ SCENARIOS = {
     "gossipsub_slot_reuse": lambda lib, x=(): gossipsub_scored(lib, n=200, seed=13, msgs=400, hb=16, window=320,
                                                                extra=x),
     "gossipsub_slot_reuse_4t": lambda lib, x=(): gossipsub_scored(lib, n=200, topics=4, seed=17, msgs=600, hb=16,
-                                                                  window=512, extra=x),
+                                                                  window=128, extra=x),
+    # graylisting (score < GraylistThreshold -> AcceptNone, gossipsub.go:584) and
+    # direct peers (AcceptAll, always forwarded, GRAFT answered with PRUNE)
+    "gossipsub_graylist_direct": lambda lib, x=(): gossipsub_scored(lib, n=300, k=20, seed=23, app_neg_frac=0.15,
+                                                                    app_neg=-400.0, direct_frac=0.03, extra=x),
 }
+
+# The benchmarked shapes (bench.py), at a size the oracle finishes in seconds:
+# the same kernel instantiations as the 1M-peer runs.
+HEAVY = {
+    # config4: 64 topics x 256 slots -> W = 256 words (4 per lane), degree 32 ->
+    # 2048 (edge, topic) pairs per node (batches of 32), 8-bit phase-A counters
+    "c4shape": lambda lib, x=(): gossipsub_scored(lib, n=1000, k=32, topics=64, window=256, msgs=1200, hb=8,
+                                                  seed=21, extra=x),
+    # W = 256 with more than 255 live messages in topic 0: 32-bit counters
+    "c4shape_wide": lambda lib, x=(): gossipsub_scored(lib, n=1000, k=32, topics=16, window=1024, msgs=1200, hb=8,
+                                                       seed=22, topic0_frac=0.4, extra=x),
+    # config3: 1 topic x 10048 slots -> W = 157 words (3 per lane)
+    "c3shape": lambda lib, x=(): gossipsub_scored(lib, n=2000, k=32, topics=1, window=10048, msgs=2000, hb=8,
+                                                  seed=23, extra=x),
+}
+SCENARIOS.update(HEAVY)
 
 
 def snapshot(e, msg_ids):
