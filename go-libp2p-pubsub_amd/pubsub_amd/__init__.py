@@ -4,7 +4,9 @@ Mirrors the router-selection / parameter API of go-libp2p-pubsub over the
 C-ABI in include/gossip_engine.h; the compute runs in the HIP library
 build/libgossip_engine.so (gfx950).
 """
-from ._abi import (GS_ROUTER_FLOODSUB, GS_ROUTER_GOSSIPSUB, GS_ROUTER_RANDOMSUB)  # noqa: F401
+from ._abi import (GS_BEHAVE_GRAFT_SPAM, GS_BEHAVE_IHAVE_SPAM, GS_BEHAVE_IWANT_SPAM, GS_BEHAVE_NO_FORWARD, GS_MSG_IGNORE,  # noqa: F401
+                   GS_MSG_PHANTOM, GS_MSG_REJECT, GS_MSG_VALID, GS_ROUTER_FLOODSUB, GS_ROUTER_GOSSIPSUB,
+                   GS_ROUTER_RANDOMSUB)
 from .params import (DefaultGossipSubParams, DefaultPeerGaterParams, GossipSubParams,  # noqa: F401
                      Hour, Microsecond, Millisecond, Minute, NewPeerGaterParams, PeerGaterParams,
                      PeerScoreParams, PeerScoreThresholds, ScoreParameterDecay,
@@ -13,4 +15,4 @@ from .params import (DefaultGossipSubParams, DefaultPeerGaterParams, GossipSubPa
 from .engine import (PRODUCT_LIB, Engine, GossipEngineError, NewFloodSub, NewGossipSub,  # noqa: F401
                      NewRandomSub, PROTOCOLS, WithDevice, WithEventTracer, encode_trace, WithDirectPeers, WithFloodPublish, WithGossipSubParams,
                      WithHop, WithMessageWindow, WithPartition, WithPeerScore, WithRecordDeliveries, WithSeed,
-                     load)
+                     WithBehaviour, WithPeerGater, WithValidation, load)

@@ -25,6 +25,12 @@ GS_FLAG_SCORING = 1 << 0
 GS_FLAG_FLOOD_PUBLISH = 1 << 1
 GS_FLAG_RECORD_DELIVERIES = 1 << 2
 
+GS_MSG_VALID, GS_MSG_REJECT, GS_MSG_IGNORE, GS_MSG_PHANTOM = 0, 1, 2, 3
+GS_BEHAVE_NO_FORWARD, GS_BEHAVE_IWANT_SPAM, GS_BEHAVE_GRAFT_SPAM, GS_BEHAVE_IHAVE_SPAM = 1, 2, 4, 8
+REJECT_REASONS = ["blacklisted peer", "blacklisted source", "missing signature", "unexpected signature",
+                  "unexpected auth info", "invalid signature", "validation queue full", "validation throttled",
+                  "validation failed", "validation ignored", "self originated message"]  # tracer.go:27-38
+
 i32, i64, u32, u64, f64, u8 = C.c_int32, C.c_int64, C.c_uint32, C.c_uint64, C.c_double, C.c_uint8
 
 
@@ -90,7 +96,7 @@ class ConfigC(C.Structure):
 
 # gs_trace_event (gossip_engine.h): 32 bytes
 TRACE_EVENT_DTYPE = np.dtype([("hop", "<i8"), ("msg", "<i8"), ("type", "<i4"), ("node", "<i4"),
-                              ("peer", "<i4"), ("topic", "<i2"), ("phase", "<i2")])
+                              ("peer", "<i4"), ("topic", "<i2"), ("phase", "u1"), ("reason", "u1")])
 TRACE_TYPES = ["PUBLISH_MESSAGE", "REJECT_MESSAGE", "DUPLICATE_MESSAGE", "DELIVER_MESSAGE", "ADD_PEER",
                "REMOVE_PEER", "RECV_RPC", "SEND_RPC", "DROP_RPC", "JOIN", "LEAVE", "GRAFT", "PRUNE"]
 GS_TRACE_FORMAT_PB, GS_TRACE_FORMAT_JSON = 0, 1
@@ -101,11 +107,12 @@ class CountersC(C.Structure):
         ("hops", i64), ("heartbeats", i64), ("published", i64), ("deliveries", i64),
         ("duplicates", i64), ("transmissions", i64), ("grafts_sent", i64), ("prunes_sent", i64),
         ("ihave_sent", i64), ("iwant_sent", i64), ("iwant_served", i64),
-        ("promises_broken", i64), ("graylisted", i64), ("reserved", i64 * 3),
+        ("promises_broken", i64), ("graylisted", i64), ("rejected", i64), ("throttled", i64),
+        ("gated", i64),
     ]
 
     def as_dict(self):
-        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+        return {f: getattr(self, f) for f, _ in self._fields_}
 
 
 P = C.c_void_p
@@ -144,6 +151,10 @@ ABI_FUNCTIONS = [
     ("gs_set_peer_attrs", C.c_int, [P, C.POINTER(f64), C.POINTER(u32)]),
     ("gs_set_ip_whitelist", C.c_int, [P, i32, C.POINTER(u32), C.POINTER(u32)]),
     ("gs_publish", C.c_int, [P, i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i64), C.POINTER(i64)]),
+    ("gs_publish_ex", C.c_int, [P, i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i64), C.POINTER(u8),
+                                C.POINTER(i64)]),
+    ("gs_set_validation", C.c_int, [P, C.POINTER(u8), i32]),
+    ("gs_set_behaviour", C.c_int, [P, C.POINTER(u8)]),
     ("gs_step", C.c_int, [P, i64]),
     ("gs_sync", C.c_int, [P]),
     ("gs_set_topic_score_params", C.c_int, [P, i32, C.POINTER(TopicScoreParamsC)]),

@@ -95,6 +95,25 @@ def WithEventTracer(nodes, capacity=1 << 22):
     return ("trace", (nodes, int(capacity)))
 
 
+def WithPeerGater(params):
+    """WithPeerGater (peer_gater.go:164-191): random early drop of payload from
+    peers with poor goodput while the validation queue is throttling."""
+    return ("gater", params)
+
+
+def WithValidation(topic_validators, queue_per_hop=0):
+    """RegisterTopicValidator for the topics with topic_validators[t] true (the
+    verdict is each message's `kind`, see Engine.publish), and the validation
+    queue: at most queue_per_hop received messages enter validation per node
+    per hop (0 = unlimited; WithValidateQueueSize, validation.go:236-241)."""
+    return ("validation", (topic_validators, int(queue_per_hop)))
+
+
+def WithBehaviour(bits):
+    """Per-node attacker behaviours (uint8[N] of GS_BEHAVE_* bits)."""
+    return ("behaviour", bits)
+
+
 def WithPartition(rank, world, transport):
     """Simulate only this rank's node range; exchange RPCs with the other
     ranks through `transport` (a pubsub_amd.transport.TorchTransport) once per
@@ -141,7 +160,8 @@ class Engine:
             C.byref(cfg), C.byref(gsp_c),
             C.byref(psp_c) if psp_c is not None else None,
             topics_c, scored_c,
-            C.byref(thr_c) if thr_c is not None else None, None, C.byref(h)))
+            C.byref(thr_c) if thr_c is not None else None,
+            C.byref(opts["gater"].to_c()) if opts.get("gater") is not None else None, C.byref(h)))
         self.h = h
         rowptr, col, outbound = graph
         self.rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
@@ -171,6 +191,15 @@ class Engine:
         self.edge_range = (int(self.rowptr[b.value]), int(self.rowptr[e.value]))
         subs = np.ascontiguousarray(subscriptions, dtype=np.uint64)
         _check(self.lib, self.lib.gs_set_subscriptions(h, _ptr(subs, C.c_uint64)))
+        val = opts.get("validation")
+        if val is not None:
+            tv = np.zeros(num_topics, dtype=np.uint8)
+            tv[:] = np.asarray(val[0], dtype=bool)[:num_topics] if np.ndim(val[0]) else bool(val[0])
+            _check(self.lib, self.lib.gs_set_validation(h, _ptr(tv, C.c_uint8), val[1]))
+        beh = opts.get("behaviour")
+        if beh is not None:
+            beh = np.ascontiguousarray(beh, dtype=np.uint8)
+            _check(self.lib, self.lib.gs_set_behaviour(h, _ptr(beh, C.c_uint8)))
         app = np.ascontiguousarray(app_score, dtype=np.float64) if app_score is not None else None
         ips = np.ascontiguousarray(ipv4, dtype=np.uint32) if ipv4 is not None else None
         if app is not None or ips is not None:
@@ -188,13 +217,16 @@ class Engine:
             pass
 
     # ---------------------------------------------------------------- driving
-    def publish(self, src, topic, hop):
+    def publish(self, src, topic, hop, kind=None):
+        """Topic.Publish at node src[i] at hop hop[i]; kind[i] (GS_MSG_*) is the
+        verdict of the receivers' topic validator, or PHANTOM (advertised only)."""
         src = np.ascontiguousarray(src, dtype=np.int32)
         topic = np.ascontiguousarray(topic, dtype=np.int32)
         hop = np.ascontiguousarray(hop, dtype=np.int64)
         ids = np.empty(len(src), dtype=np.int64)
-        _check(self.lib, self.lib.gs_publish(self.h, len(src), _ptr(src, C.c_int32), _ptr(topic, C.c_int32),
-                                             _ptr(hop, C.c_int64), _ptr(ids, C.c_int64)))
+        kd = np.ascontiguousarray(kind, dtype=np.uint8) if kind is not None else None
+        _check(self.lib, self.lib.gs_publish_ex(self.h, len(src), _ptr(src, C.c_int32), _ptr(topic, C.c_int32),
+                                                _ptr(hop, C.c_int64), _ptr(kd, C.c_uint8), _ptr(ids, C.c_int64)))
         self.n_published += len(src)
         return ids
 

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 1
+#define GS_ABI_VERSION 2
 
 /* ---- error codes ------------------------------------------------------- */
 #define GS_OK 0
@@ -176,7 +176,12 @@ typedef struct gs_counters {
   int64_t iwant_served;    /* messages served in response to IWANT           */
   int64_t promises_broken; /* broken IWANT promises turned into P7 penalties */
   int64_t graylisted;      /* RPCs dropped by AcceptFrom == AcceptNone       */
-  int64_t reserved[3];
+  int64_t rejected;        /* messages rejected by validation (ValidationReject
+                              / ValidationIgnore, validation.go:331-336)      */
+  int64_t throttled;       /* copies dropped by a full validation queue
+                              (RejectValidationQueueFull, validation.go:236-241) */
+  int64_t gated;           /* payload RPCs dropped by the peer gater
+                              (AcceptControl, pubsub.go:951-955)              */
 } gs_counters;
 
 /* ---- defaults / helpers ------------------------------------------------ */
@@ -199,7 +204,8 @@ int gs_validate_peer_gater_params(const gs_peer_gater_params* p);
 typedef struct gs_engine gs_engine;
 
 /* Creates the engine.  gossipsub/score/threshold/gater params may be NULL
- * when unused by the router.  topics[T] and topic_scored[T] give the
+ * when unused by the router.  gater != NULL enables the peer gater
+ * (WithPeerGater, peer_gater.go:164-191; gossipsub only).  topics[T] and topic_scored[T] give the
  * PeerScoreParams.Topics map (topic_scored[t] != 0 <=> key present). */
 int gs_engine_create(const gs_config* cfg, const gs_gossipsub_params* gsp,
                      const gs_peer_score_params* psp,
@@ -228,6 +234,39 @@ int gs_set_ip_whitelist(gs_engine* eng, int32_t n, const uint32_t* net, const ui
  * are assigned in call order and written to ids_out (may be NULL). */
 int gs_publish(gs_engine* eng, int32_t n, const int32_t* src, const int32_t* topic,
                const int64_t* hop, int64_t* ids_out);
+
+/* ---- adversarial model ---------------------- */
+/* Message kinds (gs_publish_ex).  REJECT / IGNORE are the verdict every
+ * receiver's topic validator returns (RegisterTopicValidator, validation.go;
+ * they apply on topics with a validator, gs_set_validation, else the message
+ * is valid); the author forwards it without validating (an attacker).
+ * PHANTOM: an id the author advertises in IHAVE (it sits in the author's
+ * mcache) but never sends or serves — IHAVE spam of unpublished ids
+ * (gossipsub_spam_test.go:135-270), whose IWANT promises break (P7). */
+#define GS_MSG_VALID 0
+#define GS_MSG_REJECT 1
+#define GS_MSG_IGNORE 2
+#define GS_MSG_PHANTOM 3
+/* gs_publish with a kind per message (kind == NULL: all valid). */
+int gs_publish_ex(gs_engine* eng, int32_t n, const int32_t* src, const int32_t* topic,
+                  const int64_t* hop, const uint8_t* kind, int64_t* ids_out);
+/* Topic validators (topic_validator[t] != 0: RegisterTopicValidator(t)) and
+ * the validation queue: at most queue_per_hop received messages enter
+ * validation per node per hop (0 = unlimited); later fresh copies are
+ * dropped with RejectValidationQueueFull (validation.go:236-241), which is
+ * what drives the peer gater (peer_gater.go:413-420).  Before the first step. */
+int gs_set_validation(gs_engine* eng, const uint8_t* topic_validator, int32_t queue_per_hop);
+/* Per-node behaviour bits (simulated attackers, restating the reference's
+ * attack mocks).  Before the first step; NULL = all honest. */
+#define GS_BEHAVE_NO_FORWARD 1u /* sybilSquatter (gossipsub_test.go:1781-1815): relays
+                                   nothing, serves no IWANT, emits no IHAVE */
+#define GS_BEHAVE_IWANT_SPAM 2u /* re-requests every message it receives from its
+                                   sender (gossipsub_spam_test.go:24-132)      */
+#define GS_BEHAVE_GRAFT_SPAM 4u /* every heartbeat re-GRAFTs the topic peers it is
+                                   in backoff with (gossipsub_spam_test.go:349-548) */
+#define GS_BEHAVE_IHAVE_SPAM 8u /* emitGossip to every topic peer, mesh peers included
+                                   (IHAVE spam, gossipsub_spam_test.go:196-222) */
+int gs_set_behaviour(gs_engine* eng, const uint8_t* behaviour /*[N]*/);
 
 /* Advances the simulation by `hops` lock-step hops. */
 int gs_step(gs_engine* eng, int64_t hops);
@@ -320,14 +359,28 @@ int gs_read_deliveries(gs_engine* eng, int64_t id, int32_t* hop /*[N]*/,
  * Join, 1 local publish, 2 received messages, 3 received control, 4 heartbeat;
  * gs_trace_read returns events in the canonical order of include/gs_trace.h. */
 typedef struct gs_trace_event {
-  int64_t hop;   /* virtual time: timestamp = hop * hop_ns */
-  int64_t msg;   /* message id, -1 = none */
-  int32_t type;  /* GS_TRACE_* */
-  int32_t node;  /* the tracing host */
-  int32_t peer;  /* peer / receivedFrom, -1 = none */
-  int16_t topic; /* -1 = none */
-  int16_t phase;
+  int64_t hop;    /* virtual time: timestamp = hop * hop_ns */
+  int64_t msg;    /* message id, -1 = none */
+  int32_t type;   /* GS_TRACE_* */
+  int32_t node;   /* the tracing host */
+  int32_t peer;   /* peer / receivedFrom, -1 = none */
+  int16_t topic;  /* -1 = none */
+  uint8_t phase;
+  uint8_t reason; /* REJECT_MESSAGE: GS_REJECT_* */
 } gs_trace_event;
+/* RejectMessage reasons, in the order of tracer.go:27-38 (their strings are
+ * what the encoders write). */
+#define GS_REJECT_BLACKLISTED_PEER 0
+#define GS_REJECT_BLACKLISTED_SOURCE 1
+#define GS_REJECT_MISSING_SIGNATURE 2
+#define GS_REJECT_UNEXPECTED_SIGNATURE 3
+#define GS_REJECT_UNEXPECTED_AUTH_INFO 4
+#define GS_REJECT_INVALID_SIGNATURE 5
+#define GS_REJECT_QUEUE_FULL 6
+#define GS_REJECT_VALIDATION_THROTTLED 7
+#define GS_REJECT_VALIDATION_FAILED 8
+#define GS_REJECT_VALIDATION_IGNORED 9
+#define GS_REJECT_SELF_ORIGIN 10
 /* Before the first step: trace the hosts with node_mask[u] != 0 (NULL: off),
  * keeping up to `capacity` events between two gs_trace_read calls (more is a
  * GS_ECAPACITY error of gs_step). */

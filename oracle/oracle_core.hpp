@@ -692,6 +692,15 @@ class PeerGater {
       ++it;
     }
   }
+  // The per-peer part of AcceptFrom (:340-357): (1 + deliver) / (1 + total),
+  // or -1 when total == 0 (AcceptAll).
+  double acceptThreshold(int p) {
+    Stats& st = getPeerStats(p);
+    double total = st.deliver + params.DuplicateWeight * st.duplicate + params.IgnoreWeight * st.ignore +
+                   params.RejectWeight * st.reject;
+    if (total == 0) return -1;
+    return (1 + st.deliver) / (1 + total);
+  }
   // AcceptFrom — :320-363.  `u` is the uniform draw replacing rand.Float64().
   int AcceptFrom(int p, int64_t now, double u) {
     if (lastThrottle == kTimeZero || now - lastThrottle > params.Quiet) return AcceptAll;

@@ -45,6 +45,14 @@ struct RPC {
   Control ctl;
 };
 
+// Peer-gater view of one node at hop start (AcceptFrom, peer_gater.go:320-363):
+// every AcceptFrom of the hop decides on this snapshot, as the score filters
+// decide on the S0 memo.
+struct GateSnap {
+  bool active = false;          // quiet period, throttle and ratio checks passed
+  std::map<int, double> thr;    // (1 + deliver) / (1 + total) per peer; absent = AcceptAll
+};
+
 struct Sim;
 
 struct Node {
@@ -70,6 +78,11 @@ struct Node {
   std::map<int, std::vector<RPC>> out;   // RPCs sent during this hop, per destination
   std::map<int, int> acceptStatus;       // AcceptFrom result per sender this hop
   gs_counters ctr{};                     // this node's event counters (summed by gs_read_counters)
+  PeerGater gater;                       // gs.gate (WithPeerGater), when sim->gaterOn
+  GateSnap gsnap;
+  int valUsed = 0;                       // validation-queue entries used this hop
+  uint8_t behave = 0;                    // GS_BEHAVE_* bits
+  int acceptFrom(int s, uint32_t draw);  // AcceptFrom incl. the gater, per RPC
   std::vector<gs_trace_event> ev;        // this node's trace events (it is the tracing host)
 
   double Score(int p);                   // gs.score.Score (0 when scoring is off)
@@ -102,6 +115,12 @@ struct Sim {
   std::vector<uint8_t> tscored;
   gs_peer_score_thresholds thr{};
   bool scoring = false, floodPublish = false, record = false;
+  bool gaterOn = false;
+  gs_peer_gater_params gaterParams{};
+  std::vector<uint8_t> topicVal;   // RegisterTopicValidator per topic
+  int32_t valQueue = 0;            // validation queue entries per node per hop (0 = unlimited)
+  std::vector<uint8_t> behave;     // GS_BEHAVE_* per node
+  std::vector<uint8_t> msgKind;    // GS_MSG_* per message id
   int N = 0, T = 0;
   int64_t E = 0;
   std::vector<int64_t> rowptr;
@@ -128,7 +147,7 @@ struct Sim {
   // Events go to the tracing host's own buffer, so nodes run in parallel
   // (OpenMP over nodes in every per-node phase; the canonical event order
   // of gs_trace.h is keyed by host, so the merge order does not matter).
-  void emit(int type, int node, int peer, int topic, int64_t msg, int phase);
+  void emit(int type, int node, int peer, int topic, int64_t msg, int phase, int reason = 0);
   gs_counters total() const;
 
   int edgeIndex(int u, int v) const {
@@ -143,15 +162,21 @@ struct Sim {
     return (t - gp.HeartbeatInitialDelay) % gp.HeartbeatInterval == 0;
   }
   bool refreshDue(int64_t t) const { return scoring && t > 0 && t % sp.DecayInterval == 0; }
+  bool gaterDecayDue(int64_t t) const { return gaterOn && t > 0 && t % gaterParams.DecayInterval == 0; }
+  int kindOf(const Msg& m) const {  // verdict of m's topic validator (GS_MSG_VALID without one)
+    const int k = msgKind[m.id];
+    if (k == GS_MSG_PHANTOM) return k;
+    return topicVal[m.topic] ? k : GS_MSG_VALID;
+  }
   void start();
   void step();
 };
 
-void Sim::emit(int type, int node, int peer, int topic, int64_t msg, int phase) {
+void Sim::emit(int type, int node, int peer, int topic, int64_t msg, int phase, int reason) {
   if (traced.empty() || !traced[node]) return;
   gs_trace_event e;
   e.hop = hop; e.msg = msg; e.type = type; e.node = node; e.peer = peer;
-  e.topic = (int16_t)topic; e.phase = (int16_t)phase;
+  e.topic = (int16_t)topic; e.phase = (uint8_t)phase; e.reason = (uint8_t)reason;
   if (nodes.empty()) events.push_back(e); else nodes[node].ev.push_back(e);
 }
 
@@ -162,7 +187,8 @@ gs_counters Sim::total() const {
     c.transmissions += nd.ctr.transmissions; c.grafts_sent += nd.ctr.grafts_sent;
     c.prunes_sent += nd.ctr.prunes_sent; c.ihave_sent += nd.ctr.ihave_sent; c.iwant_sent += nd.ctr.iwant_sent;
     c.iwant_served += nd.ctr.iwant_served; c.promises_broken += nd.ctr.promises_broken;
-    c.graylisted += nd.ctr.graylisted;
+    c.graylisted += nd.ctr.graylisted; c.rejected += nd.ctr.rejected; c.throttled += nd.ctr.throttled;
+    c.gated += nd.ctr.gated;
   }
   return c;
 }
@@ -172,6 +198,7 @@ double Node::Score(int p) { return sim->scoring ? score.score(p) : 0.0; }
 // sendRPC / doSendRPC — gossipsub.go:1092-1156 (queues never drop in the
 // simulator; pending gossip is piggybacked exactly as sendRPC does).
 void Node::sendRPC(int p, RPC rpc) {
+  if ((behave & GS_BEHAVE_NO_FORWARD) && rpc.hasCtl) return;  // a squatter sends no control at all
   auto g = gossip.find(p);
   if (g != gossip.end()) {  // piggybackGossip gossipsub.go:1736-1744
     rpc.hasCtl = true;
@@ -238,6 +265,13 @@ void Node::join(int topic) {
 // (topic.go:207-245, validation.go:216-226, pubsub.go:1056-1060).  Raw tracers
 // skip self-originated messages (trace.go:89,101,132,162).
 void Node::localPublish(const Msg& m) {
+  if (sim->msgKind[m.id] == GS_MSG_PHANTOM) {
+    // an advertised-only id: in the author's mcache (so emitGossip lists it)
+    // and seen set, never sent (IHAVE spam, gossipsub_spam_test.go:196-203)
+    seen.insert(m.id);
+    if (sim->cfg.router == GS_ROUTER_GOSSIPSUB) mcache.Put(m);
+    return;
+  }
   sim->emit(GS_TRACE_PUBLISH_MESSAGE, id, -1, m.topic, m.id, 1);  // validation.go:217
   sim->emit(GS_TRACE_DELIVER_MESSAGE, id, id, m.topic, m.id, 1);  // pubsub.go:1057
   seen.insert(m.id);
@@ -246,29 +280,76 @@ void Node::localPublish(const Msg& m) {
   routerPublish(m, id);
 }
 
-// pushMsg — pubsub.go:978-1022 with instantaneous accept (no validators, no
-// signature: validation.go:230-243 returns true), then publishMessage.
+// pushMsg — pubsub.go:978-1022, then the validation pipeline (validation.go:
+// 230-351) with instantaneous validators: Push queues a message of a topic with
+// a validator (dropped with RejectValidationQueueFull when this hop's queue
+// entries are used up), validate() marks it seen, traces ValidateMessage and
+// applies the verdict; an accepted message is published (publishMessage).
 void Node::handleMessage(int from, const Msg& m) {
   if (!((mySubs >> m.topic) & 1)) return;  // subscribedToMsg / canRelayMsg (pubsub.go:959)
+  const int64_t now = sim->now();
   if (m.from == id && from != id) {         // self-origin rejection (pubsub.go:1001-1006)
-    if (sim->scoring) score.RejectMessage(m, from, RejectSelfOrigin, sim->now());
+    if (sim->scoring) score.RejectMessage(m, from, RejectSelfOrigin, now);
+    if (sim->gaterOn) gater.RejectMessage(from, RejectSelfOrigin, now);
     return;
   }
   if (seen.count(m.id)) {                   // duplicate (pubsub.go:1010-1013)
     sim->emit(GS_TRACE_DUPLICATE_MESSAGE, id, from, m.topic, m.id, 2);
     ctr.duplicates++;
-    if (sim->scoring) score.DuplicateMessage(m, from, sim->now());
+    if (sim->scoring) score.DuplicateMessage(m, from, now);
+    if (sim->gaterOn) gater.DuplicateMessage(from);
     return;
   }
-  seen.insert(m.id);                        // markSeen
+  if (sim->topicVal[m.topic]) {             // val.Push: a validator applies (validation.go:230-243)
+    if (sim->valQueue > 0 && valUsed >= sim->valQueue) {
+      // RejectValidationQueueFull: not marked seen, a later copy may validate
+      sim->emit(GS_TRACE_REJECT_MESSAGE, id, from, m.topic, m.id, 2, GS_REJECT_QUEUE_FULL);
+      ctr.throttled++;
+      if (sim->scoring) gtracer.RejectMessage(m.id, RejectValidationQueueFull);  // peerScore ignores it
+      if (sim->gaterOn) gater.RejectMessage(from, RejectValidationQueueFull, now);
+      return;
+    }
+    valUsed++;
+    seen.insert(m.id);                      // validate(): markSeen, then ValidateMessage
+    if (sim->scoring) { score.ValidateMessage(m, now); gtracer.ValidateMessage(m.id); }
+    if (sim->gaterOn) gater.ValidateMessage();
+    const int kind = sim->kindOf(m);
+    if (kind == GS_MSG_REJECT || kind == GS_MSG_IGNORE) {  // validation.go:331-336, 349-352
+      const int reason = kind == GS_MSG_REJECT ? RejectValidationFailed : RejectValidationIgnored;
+      sim->emit(GS_TRACE_REJECT_MESSAGE, id, from, m.topic, m.id, 2,
+                kind == GS_MSG_REJECT ? GS_REJECT_VALIDATION_FAILED : GS_REJECT_VALIDATION_IGNORED);
+      ctr.rejected++;
+      if (sim->scoring) { score.RejectMessage(m, from, reason, now); gtracer.RejectMessage(m.id, reason); }
+      if (sim->gaterOn) gater.RejectMessage(from, reason, now);
+      return;
+    }
+  } else {
+    seen.insert(m.id);                      // markSeen
+  }
   sim->emit(GS_TRACE_DELIVER_MESSAGE, id, from, m.topic, m.id, 2);
   ctr.deliveries++;
   if (sim->record) sim->deliv[id][m.id] = {(int32_t)sim->hop, from};
   if (sim->scoring) {                       // tracer.DeliverMessage -> raw tracers
-    score.DeliverMessage(m, from, sim->now());
+    score.DeliverMessage(m, from, now);
     gtracer.DeliverMessage(m.id);
   }
+  if (sim->gaterOn) gater.DeliverMessage(from);
+  if (behave & GS_BEHAVE_NO_FORWARD) return;  // a squatter relays nothing
   routerPublish(m, from);
+}
+
+// AcceptFrom — gossipsub.go:578-589, then peerGater.AcceptFrom (peer_gater.go:
+// 320-363) on the hop-start snapshot; `draw` names the RPC (the message id of a
+// payload RPC, 0xFFFFFFFF for the sender's control RPCs of this hop).
+int Node::acceptFrom(int s, uint32_t draw) {
+  if (sim->cfg.router != GS_ROUTER_GOSSIPSUB) return PeerGater::AcceptAll;
+  if (direct.count(s)) return PeerGater::AcceptAll;
+  if (sim->scoring && memo[s] < sim->thr.GraylistThreshold) return PeerGater::AcceptNone;
+  if (!sim->gaterOn || !gsnap.active) return PeerGater::AcceptAll;
+  auto it = gsnap.thr.find(s);
+  if (it == gsnap.thr.end()) return PeerGater::AcceptAll;  // total == 0
+  const double u = gs_key_to_unit(gs_key64(sim->cfg.seed, GS_SITE_GATER, id, s, (uint32_t)sim->hop, draw));
+  return u < it->second ? PeerGater::AcceptAll : PeerGater::AcceptControl;
 }
 
 void Node::routerPublish(const Msg& m, int from) {
@@ -407,8 +488,10 @@ std::vector<int64_t> Node::handleIHave(int p, const Control& ctl) {
 std::vector<int64_t> Node::handleIWant(int p, const Control& ctl) {
   double sc = Score(p);
   if (sc < sim->thr.GossipThreshold) return {};
+  if (behave & GS_BEHAVE_NO_FORWARD) return {};  // a squatter serves nothing
   std::set<int64_t> ihave;
   for (int64_t mid : ctl.iwant) {
+    if (sim->msgKind[mid] == GS_MSG_PHANTOM) continue;  // advertised, never served
     int count = 0;
     if (!mcache.GetForPeer(mid, p, nullptr, &count)) continue;
     if (count > sim->gp.GossipRetransmission) continue;
@@ -511,17 +594,19 @@ void Node::applyIwantPenalties() {  // gossipsub.go:1566-1571
 
 // emitGossip — gossipsub.go:1658-1712
 void Node::emitGossip(int topic, const std::set<int>& exclude) {
+  if (behave & GS_BEHAVE_NO_FORWARD) return;  // a squatter emits no gossip
   std::vector<int64_t> mids = mcache.GetGossipIDs(topic);
   if (mids.empty()) return;
+  const bool spam = (behave & GS_BEHAVE_IHAVE_SPAM) != 0;  // IHAVE to every topic peer
   std::vector<int> peers;
   auto tm = topics.find(topic);
   if (tm != topics.end())
     for (int p : tm->second)
-      if (!exclude.count(p) && !direct.count(p) && Score(p) >= sim->thr.GossipThreshold) peers.push_back(p);
+      if (spam || (!exclude.count(p) && !direct.count(p) && Score(p) >= sim->thr.GossipThreshold)) peers.push_back(p);
   int target = sim->gp.Dlazy;
   int factor = (int)(sim->gp.GossipFactor * (double)peers.size());
   if (factor > target) target = factor;
-  if (target > (int)peers.size()) {
+  if (spam || target > (int)peers.size()) {
     target = (int)peers.size();
   } else {
     std::vector<std::pair<uint64_t, int>> keyed;
@@ -589,6 +674,12 @@ void Node::heartbeat() {
     std::vector<int> cur(peers.begin(), peers.end());
     for (int p : cur)
       if (score(p) < 0) { prunePeer(p); noPX[p] = true; }
+    // a GRAFT spammer first leaves the mesh (PRUNE with backoff), then re-GRAFTs
+    // during the backoff (gossipsub_spam_test.go:428-446)
+    if ((behave & GS_BEHAVE_GRAFT_SPAM) && heartbeatTicks == 1) {
+      std::vector<int> all(peers.begin(), peers.end());
+      for (int p : all) prunePeer(p);
+    }
     // do we have enough peers?
     if ((int)peers.size() < gp.Dlo) {
       auto& bo = backoff[topic];
@@ -667,6 +758,16 @@ void Node::heartbeat() {
         if (bo.empty()) backoff.erase(topic);
       }
     }
+    if ((behave & GS_BEHAVE_GRAFT_SPAM) && heartbeatTicks > 1) {
+      // GRAFT during backoff (gossipsub_spam_test.go:428-500): every topic peer we
+      // are in backoff with gets a GRAFT; our own mesh is left as it is
+      auto bt = backoff.find(topic);
+      auto tm = topics.find(topic);
+      if (bt != backoff.end() && tm != topics.end())
+        for (auto& be : bt->second)
+          if (be.second > now && !peers.count(be.first) && tm->second.count(be.first))
+            tograft[be.first].push_back(topic);
+    }
     emitGossip(topic, peers);
   }
   // expire fanout for topics we haven't published to in a while
@@ -740,6 +841,11 @@ void Sim::start() {
     nd.score.appSpecificScore = [this](int p) { return appScore.empty() ? 0.0 : appScore[p]; };
     nd.score.whitelist = whitelist;
     nd.gtracer.followUpTime = gp.IWantFollowupTime;
+    nd.behave = behave.empty() ? 0 : behave[u];
+    if (gaterOn) {
+      nd.gater.params = gaterParams;
+      nd.gater.getIP = [this](int p) { return ipv4.empty() ? 0u : ipv4[p]; };  // 0 = "<unknown>"
+    }
     for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) {
       int v = col[e];
       emit(GS_TRACE_ADD_PEER, u, v, -1, -1, 0);  // AddPeer gossipsub.go:507, floodsub.go:45
@@ -749,6 +855,7 @@ void Sim::start() {
       std::vector<uint32_t> ips;
       if (!ipv4.empty() && ipv4[v] != 0) ips.push_back(ipv4[v]);
       if (scoring) nd.score.AddPeer(v, ips);
+      if (gaterOn) nd.gater.AddPeer(v);  // tracer.AddPeer -> peerGater.AddPeer (peer_gater.go:366-372)
       for (int t = 0; t < T; ++t)
         if (!subs.empty() && ((subs[v] >> t) & 1)) nd.topics[t].insert(v);
     }
@@ -776,13 +883,25 @@ void Sim::step() {
           nodes[u].join(tp);
         }
   }
-  // S0 memo
-  if (scoring) {
+  // S0 memo and the gater snapshot
+  if (scoring || gaterOn) {
 #pragma omp parallel for schedule(dynamic, 64)
     for (int u = 0; u < N; ++u) {
       Node& nd = nodes[u];
       nd.memo.clear();
-      for (int v : nd.nbrs) nd.memo[v] = nd.score.score(v);
+      if (scoring)
+        for (int v : nd.nbrs) nd.memo[v] = nd.score.score(v);
+      if (gaterOn) {
+        PeerGater& g = nd.gater;
+        nd.gsnap.thr.clear();
+        nd.gsnap.active = !(g.lastThrottle == kTimeZero || t - g.lastThrottle > g.params.Quiet) &&
+                          g.throttle != 0 && !(g.validate != 0 && g.throttle / g.validate < g.params.Threshold);
+        if (nd.gsnap.active)
+          for (int v : nd.nbrs) {
+            const double th = g.acceptThreshold(v);
+            if (th >= 0) nd.gsnap.thr[v] = th;
+          }
+      }
     }
   }
   // local publishes of this hop
@@ -791,23 +910,47 @@ void Sim::step() {
     nodes[m.from].localPublish(m);
     nextPub++;
   }
-  // phase A: payload messages, senders ascending
+  // phase A: payload messages, senders ascending; a sender's messages in
+  // ascending id (their order only matters for the validation queue)
 #pragma omp parallel for schedule(dynamic, 64)
   for (int u = 0; u < N; ++u) {
     Node& nd = nodes[u];
     nd.acceptStatus.clear();
+    nd.valUsed = 0;
     for (auto& kv : inbox[nd.id]) {
       int s = kv.first;
-      int st = PeerGater::AcceptAll;
-      if (cfg.router == GS_ROUTER_GOSSIPSUB) {  // AcceptFrom gossipsub.go:578-589
-        if (nd.direct.count(s)) st = PeerGater::AcceptAll;
-        else if (scoring && nd.memo[s] < thr.GraylistThreshold) st = PeerGater::AcceptNone;
-      }
-      nd.acceptStatus[s] = st;
+      bool anyCtl = false;
+      for (const RPC& r : kv.second) anyCtl |= r.hasCtl;
+      // one AcceptFrom per RPC; a sender's control RPCs of one hop share one draw
+      const int ctlSt = anyCtl ? nd.acceptFrom(s, 0xFFFFFFFFu) : PeerGater::AcceptAll;
+      nd.acceptStatus[s] = ctlSt;
       for (const RPC& r : kv.second) nd.ctr.transmissions += (int64_t)r.publish.size();  // copies on the wire
-      if (st == PeerGater::AcceptNone) { nd.ctr.graylisted += (int64_t)kv.second.size(); continue; }
-      for (const RPC& r : kv.second)
-        for (int64_t mid : r.publish) nd.handleMessage(s, msgs[mid]);
+      bool throttledPeer = anyCtl && ctlSt == PeerGater::AcceptControl;
+      std::vector<int64_t> mids;
+      int64_t gray = 0;
+      for (const RPC& r : kv.second) {
+        const int st = r.hasCtl ? ctlSt : nd.acceptFrom(s, (uint32_t)r.publish[0]);
+        if (st == PeerGater::AcceptNone) { gray++; continue; }          // pubsub.go:947-949
+        if (st == PeerGater::AcceptControl) {                            // pubsub.go:951-955
+          throttledPeer = true;
+          if (!r.publish.empty()) nd.ctr.gated++;
+          continue;
+        }
+        mids.insert(mids.end(), r.publish.begin(), r.publish.end());
+      }
+      nd.ctr.graylisted += gray;
+      if (gray) continue;  // AcceptNone is per sender and hop (the S0 memo)
+      // tracer.ThrottlePeer -> gossipTracer.ThrottlePeer (gossip_tracer.go:163-181)
+      if (throttledPeer && scoring) nd.gtracer.ThrottlePeer(s);
+      std::sort(mids.begin(), mids.end());
+      for (int64_t mid : mids) nd.handleMessage(s, msgs[mid]);
+      if ((nd.behave & GS_BEHAVE_IWANT_SPAM) && !mids.empty() && cfg.router == GS_ROUTER_GOSSIPSUB) {
+        // re-request every message received from s (gossipsub_spam_test.go:113-128)
+        RPC r;
+        r.hasCtl = true;
+        r.ctl.iwant = mids;
+        nd.sendRPC(s, std::move(r));
+      }
     }
   }
   // phase B: control, per RPC, senders ascending
@@ -826,6 +969,10 @@ void Sim::step() {
   if (refreshDue(t)) {
 #pragma omp parallel for schedule(dynamic, 64)
     for (int u = 0; u < N; ++u) nodes[u].score.refreshScores(t);
+  }
+  if (gaterDecayDue(t)) {  // peerGater.background ticker (peer_gater.go:204-217)
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int u = 0; u < N; ++u) nodes[u].gater.decayStats(t);
   }
   if (scoring && t > 0 && t % (60 * kSecond) == 0) {
 #pragma omp parallel for schedule(dynamic, 64)
@@ -869,7 +1016,6 @@ int gs_validate_peer_gater_params(const gs_peer_gater_params* p) { return valida
 int gs_engine_create(const gs_config* cfg, const gs_gossipsub_params* gsp, const gs_peer_score_params* psp,
                      const gs_topic_score_params* topics, const uint8_t* topic_scored,
                      const gs_peer_score_thresholds* thr, const gs_peer_gater_params* gater, gs_engine** out) {
-  (void)gater;
   if (!cfg || !out) { set_error("null argument"); return GS_EINVAL; }
   if (cfg->num_nodes <= 0 || cfg->num_topics <= 0 || cfg->num_topics > 64 || cfg->hop_ns <= 0) {
     set_error("invalid config: num_nodes > 0, 1 <= num_topics <= 64, hop_ns > 0 required");
@@ -887,6 +1033,15 @@ int gs_engine_create(const gs_config* cfg, const gs_gossipsub_params* gsp, const
   s.record = (cfg->flags & GS_FLAG_RECORD_DELIVERIES) != 0;
   s.tparams.assign(s.T, gs_topic_score_params{});
   s.tscored.assign(s.T, 0);
+  s.topicVal.assign(s.T, 0);
+  if (gater) {
+    if (cfg->router != GS_ROUTER_GOSSIPSUB) { set_error("pubsub router is not gossipsub"); return GS_EINVAL; }
+    int rc = validateGaterParams(gater);
+    if (rc) return rc;
+    if (gater->DecayInterval % cfg->hop_ns != 0) { set_error("gater DecayInterval must be a multiple of hop_ns"); return GS_EUNSUPPORTED; }
+    s.gaterOn = true;
+    s.gaterParams = *gater;
+  }
   if (cfg->router == GS_ROUTER_GOSSIPSUB) {
     if (s.gp.HistoryGossip > s.gp.HistoryLength) {
       set_error("invalid parameters for message cache; gossip slots cannot be larger than history slots");
@@ -962,21 +1117,46 @@ int gs_set_ip_whitelist(gs_engine* eng, int32_t n, const uint32_t* net, const ui
   return GS_OK;
 }
 
-int gs_publish(gs_engine* eng, int32_t n, const int32_t* src, const int32_t* topic, const int64_t* hop,
-               int64_t* ids_out) {
+int gs_publish_ex(gs_engine* eng, int32_t n, const int32_t* src, const int32_t* topic, const int64_t* hop,
+                  const uint8_t* kind, int64_t* ids_out) {
   Sim& s = eng->sim;
   int64_t last = s.msgHop.empty() ? s.hop : std::max(s.hop, s.msgHop.back());
   for (int i = 0; i < n; ++i) {
-    if (src[i] < 0 || src[i] >= s.N || topic[i] < 0 || topic[i] >= s.T || hop[i] < last) {
-      set_error("publish: bad src/topic or hop not non-decreasing from the current hop"); return GS_EINVAL; }
+    if (src[i] < 0 || src[i] >= s.N || topic[i] < 0 || topic[i] >= s.T || hop[i] < last ||
+        (kind && kind[i] > GS_MSG_PHANTOM)) {
+      set_error("publish: bad src/topic/kind or hop not non-decreasing from the current hop"); return GS_EINVAL; }
     last = hop[i];
   }
   for (int i = 0; i < n; ++i) {
     int64_t id = (int64_t)s.msgs.size();
     s.msgs.push_back(Msg{id, topic[i], src[i]});
     s.msgHop.push_back(hop[i]);
+    s.msgKind.push_back(kind ? kind[i] : (uint8_t)GS_MSG_VALID);
     if (ids_out) ids_out[i] = id;
   }
+  return GS_OK;
+}
+
+int gs_publish(gs_engine* eng, int32_t n, const int32_t* src, const int32_t* topic, const int64_t* hop,
+               int64_t* ids_out) {
+  return gs_publish_ex(eng, n, src, topic, hop, nullptr, ids_out);
+}
+
+int gs_set_validation(gs_engine* eng, const uint8_t* topic_validator, int32_t queue_per_hop) {
+  Sim& s = eng->sim;
+  if (s.started) { set_error("validation must be set before the first step"); return GS_ESTATE; }
+  if (queue_per_hop < 0) { set_error("queue_per_hop must be >= 0"); return GS_EINVAL; }
+  s.topicVal.assign(s.T, 0);
+  if (topic_validator) s.topicVal.assign(topic_validator, topic_validator + s.T);
+  s.valQueue = queue_per_hop;
+  return GS_OK;
+}
+
+int gs_set_behaviour(gs_engine* eng, const uint8_t* behaviour) {
+  Sim& s = eng->sim;
+  if (s.started) { set_error("behaviours must be set before the first step"); return GS_ESTATE; }
+  s.behave.clear();
+  if (behaviour) s.behave.assign(behaviour, behaviour + s.N);
   return GS_OK;
 }
 

@@ -9,7 +9,7 @@ from pubsub_amd import (NewFloodSub, NewGossipSub, NewRandomSub, PeerScoreParams
                         WithMessageWindow, WithPeerScore, WithRecordDeliveries, WithSeed,
                         eth2_peer_score_params, eth2_thresholds, eth2_topic_score_params)
 from pubsub_amd import graphs
-from pubsub_amd.params import GossipSubParams, Millisecond, PeerScoreThresholds
+from pubsub_amd.params import GossipSubParams, Millisecond, PeerScoreThresholds  # noqa: F401
 
 HOP = 100 * Millisecond
 
@@ -213,3 +213,181 @@ def compare(a, b):
                 idx = np.argwhere(x != y)[:5]
                 bad.append(f"{k}: {int((x != y).sum())} mismatches, first at {idx.tolist()}")
     return bad
+
+
+# ---------------------------------------------------------------- adversarial
+# The reference's attack tests restated on the simulator (gossipsub_spam_test.go,
+# gossipsub_test.go:1388-1469, 1665-1815) and a config-5-like mix.  Each builder
+# returns (engine, hops); tests/test_oracle_spam.py checks the reference's own
+# assertions on the oracle, the GPU parity tests compare the engine with it.
+from pubsub_amd import (GS_BEHAVE_GRAFT_SPAM, GS_BEHAVE_IHAVE_SPAM, GS_BEHAVE_IWANT_SPAM, GS_BEHAVE_NO_FORWARD,  # noqa: E402
+                        GS_MSG_PHANTOM, GS_MSG_REJECT, DefaultPeerGaterParams, ScoreParameterDecay,
+                        WithBehaviour, WithPeerGater, WithValidation)
+from pubsub_amd.params import Minute  # noqa: E402
+
+
+def _pair():
+    """Two connected hosts (connect(t, hosts[0], hosts[1])): host 0 dialed."""
+    return (np.array([0, 1, 2], dtype=np.int64), np.array([1, 0], dtype=np.int32),
+            np.array([1, 0], dtype=np.uint8))
+
+
+def _spam_score(bpw=-1.0):
+    """The legit host's score params in gossipsub_spam_test.go:151-166 / 365-380."""
+    return (PeerScoreParams(AppSpecificScore=True, BehaviourPenaltyWeight=bpw,
+                            BehaviourPenaltyDecay=ScoreParameterDecay(Minute), DecayInterval=Second,
+                            DecayToZero=0.01),
+            PeerScoreThresholds(GossipThreshold=-100, PublishThreshold=-500, GraylistThreshold=-1000))
+
+
+def spam_iwant(lib, extra=()):
+    """TestGossipsubAttackSpamIWANT (gossipsub_spam_test.go:24-132): host 1
+    re-requests every message it gets; host 0 publishes one message."""
+    e = NewGossipSub(2, 1, _pair(), graphs.all_subscribed(2, 1), WithRecordDeliveries(), WithHop(HOP),
+                     WithMessageWindow(64), WithBehaviour(np.array([0, GS_BEHAVE_IWANT_SPAM], np.uint8)),
+                     *extra, lib=lib)
+    e.publish([0], [0], [5])
+    return e, 80
+
+
+def spam_ihave(lib, topics=1, per_topic=3 * 5000, extra=()):
+    """TestGossipsubAttackSpamIHAVE (gossipsub_spam_test.go:135-270): host 1
+    advertises ids it never sends (3 x MaxIHaveLength of them)."""
+    sp, thr = _spam_score()
+    n_ph = topics * per_topic
+    e = NewGossipSub(2, topics, _pair(), graphs.all_subscribed(2, topics), WithPeerScore(sp, thr),
+                     WithHop(HOP), WithMessageWindow(((per_topic + 63) // 64) * 64),
+                     WithBehaviour(np.array([0, GS_BEHAVE_IHAVE_SPAM], np.uint8)), *extra, lib=lib)
+    e.publish(np.ones(n_ph, np.int32), np.repeat(np.arange(topics), per_topic).astype(np.int32),
+              np.full(n_ph, 2, np.int64), kind=np.full(n_ph, GS_MSG_PHANTOM, np.uint8))
+    return e, 70
+
+
+def spam_graft(lib, extra=()):
+    """TestGossipsubAttackGRAFTDuringBackoff (gossipsub_spam_test.go:349-548):
+    host 1 leaves host 0's mesh with a PRUNE, then GRAFTs during the backoff."""
+    sp, thr = _spam_score(-100.0)
+    e = NewGossipSub(2, 1, _pair(), graphs.all_subscribed(2, 1), WithPeerScore(sp, thr), WithHop(HOP),
+                     WithMessageWindow(64), WithBehaviour(np.array([0, GS_BEHAVE_GRAFT_SPAM], np.uint8)),
+                     *extra, lib=lib)
+    return e, 80
+
+
+def spam_invalid(lib, extra=()):
+    """TestGossipsubAttackInvalidMessageSpam (gossipsub_spam_test.go:563-703):
+    host 1 sends 100 messages host 0's validator rejects (Eth2 scoring)."""
+    sp = eth2_peer_score_params(1)
+    thr = eth2_thresholds()
+    e = NewGossipSub(2, 1, _pair(), graphs.all_subscribed(2, 1), WithPeerScore(sp, thr), WithHop(HOP),
+                     WithMessageWindow(128), WithValidation([1]), WithRecordDeliveries(), *extra, lib=lib)
+    e.publish(np.ones(100, np.int32), np.zeros(100, np.int32), 5 + np.arange(100, dtype=np.int64) // 10,
+              kind=np.full(100, GS_MSG_REJECT, np.uint8))
+    return e, 40
+
+
+def squatters(lib, extra=()):
+    """TestGossipsubOpportunisticGrafting (gossipsub_test.go:1665-1779): 10
+    honest hosts (connectSome degree 5) and 40 sybilSquatters connected to every
+    honest host; 1000 messages from the honest hosts."""
+    n, honest = 50, 10
+    r, c, o = graphs.connect_some(honest, 5, 31)
+    pairs = [(int(u), int(v)) for u in range(honest) for v in c[r[u]:r[u + 1]] if o[r[u] + list(c[r[u]:r[u + 1]]).index(v)] and u < n]
+    und = {(min(a, b), max(a, b)): a for a, b in pairs}
+    for s in range(honest, n):
+        for h in range(honest):
+            und[(h, s)] = s  # connect(t, squatter, real): the squatter dials
+    g = graphs._to_csr(n, np.array([[d, b if d == a else a] for (a, b), d in und.items()], dtype=np.int64))
+    tp = TopicScoreParams(TopicWeight=1, TimeInMeshWeight=0.0002777, TimeInMeshQuantum=Second,
+                          TimeInMeshCap=3600, FirstMessageDeliveriesWeight=1,
+                          FirstMessageDeliveriesDecay=0.9997, FirstMessageDeliveriesCap=100,
+                          InvalidMessageDeliveriesDecay=0.99997)
+    sp = PeerScoreParams(Topics={0: tp}, AppSpecificScore=True, AppSpecificWeight=0, DecayInterval=Second,
+                         DecayToZero=0.01)
+    thr = PeerScoreThresholds(GossipThreshold=-10, PublishThreshold=-100, GraylistThreshold=-10000,
+                              OpportunisticGraftThreshold=1)
+    gp = GossipSubParams(PruneBackoff=500 * Millisecond, GraftFloodThreshold=100 * Millisecond,
+                         OpportunisticGraftTicks=2)
+    beh = np.zeros(n, np.uint8)
+    beh[honest:] = GS_BEHAVE_NO_FORWARD
+    e = NewGossipSub(n, 1, g, graphs.all_subscribed(n, 1), WithPeerScore(sp, thr), WithGossipSubParams(gp),
+                     WithFloodPublish(True), WithHop(HOP), WithMessageWindow(1024), WithBehaviour(beh),
+                     *extra, lib=lib)
+    # 1000 messages 20 ms apart = 5 per 100 ms hop, from hosts i % 10, after 1 s
+    e.publish((np.arange(1000) % honest).astype(np.int32), np.zeros(1000, np.int32),
+              10 + np.arange(1000, dtype=np.int64) // 5)
+    e.honest = honest
+    return e, 10 + 200 + 70
+
+
+def sinkhole(lib, extra=()):
+    """TestGossipsubNegativeScore (gossipsub_test.go:1388-1469): host 0 has app
+    score -1000; 20 messages, one from every host."""
+    n = 20
+    sp = PeerScoreParams(AppSpecificScore=True, AppSpecificWeight=1, DecayInterval=Second, DecayToZero=0.01)
+    thr = PeerScoreThresholds(GossipThreshold=-10, PublishThreshold=-100, GraylistThreshold=-10000)
+    app = np.zeros(n)
+    app[0] = -1000
+    e = NewGossipSub(n, 1, graphs.dense_connect(n, 41), graphs.all_subscribed(n, 1), WithPeerScore(sp, thr),
+                     WithRecordDeliveries(), WithHop(HOP), WithMessageWindow(64), *extra, app_score=app,
+                     lib=lib)
+    e.publish(np.arange(n, dtype=np.int32), np.zeros(n, np.int32), 30 + np.arange(n, dtype=np.int64) // 5)
+    return e, 30 + 4 + 20
+
+
+def adversarial_mix(lib, n=400, k=16, seed=51, sybil_frac=0.2, queue=6, msgs=600, hb=10, gater=True,
+                    extra=()):
+    """A config-5-like mix: 20% Sybils split over IWANT spam,
+    GRAFT spam, phantom-IHAVE spam and invalid-message publishing, 20 Sybils
+    per shared IP (P6), the peer gater, topic validator with a bounded queue,
+    Eth2 scoring."""
+    rng = np.random.default_rng(seed)
+    g = graphs.random_regular(n, k, seed)
+    sybil = rng.random(n) < sybil_frac
+    ids = np.flatnonzero(sybil)
+    beh = np.zeros(n, np.uint8)
+    kind_of = rng.integers(0, 4, len(ids))        # 0 IWANT spam, 1 GRAFT spam, 2 phantom IHAVE, 3 invalid
+    beh[ids[kind_of == 0]] = GS_BEHAVE_IWANT_SPAM
+    beh[ids[kind_of == 1]] = GS_BEHAVE_GRAFT_SPAM
+    beh[ids[kind_of == 2]] = GS_BEHAVE_IHAVE_SPAM
+    ipv4 = (np.arange(n) + (10 << 24)).astype(np.uint32)
+    ipv4[ids] = (192 << 24) + (np.arange(len(ids)) // 20).astype(np.uint32)
+    sp = eth2_peer_score_params(1)
+    thr = eth2_thresholds()
+    opts = [WithPeerScore(sp, thr), WithHop(HOP), WithMessageWindow(2048), WithSeed(seed), WithBehaviour(beh),
+            WithValidation([1], queue), WithRecordDeliveries()]
+    if gater:
+        opts.append(WithPeerGater(DefaultPeerGaterParams()))
+    e = NewGossipSub(n, 1, g, graphs.all_subscribed(n, 1), *opts, *extra, ipv4=ipv4, lib=lib)
+    honest_ids = np.flatnonzero(~sybil)
+    hops = (5 + (np.arange(msgs) * (hb * 10 - 20)) // msgs).astype(np.int64)
+    src = rng.choice(honest_ids, msgs).astype(np.int32)
+    kind = np.zeros(msgs, np.uint8)
+    inv = ids[kind_of == 3]
+    ph = ids[kind_of == 2]
+    # a third of the slots go to invalid messages, a sixth to phantom ids
+    r = rng.random(msgs)
+    if len(inv):
+        sel = r < 1 / 3
+        src[sel] = rng.choice(inv, int(sel.sum()))
+        kind[sel] = GS_MSG_REJECT
+    if len(ph):
+        sel = (r >= 1 / 3) & (r < 0.5)
+        src[sel] = rng.choice(ph, int(sel.sum()))
+        kind[sel] = GS_MSG_PHANTOM
+    e.publish(src, np.zeros(msgs, np.int32), hops, kind=kind)
+    e.sybil = sybil
+    return e, hb * 10 + 5
+
+
+ADVERSARIAL = {
+    "spam_iwant": spam_iwant,
+    "spam_ihave": spam_ihave,
+    "spam_ihave_2t": lambda lib, x=(): spam_ihave(lib, topics=2, per_topic=4000, extra=x),
+    "spam_graft": spam_graft,
+    "spam_invalid": spam_invalid,
+    "squatters": squatters,
+    "sinkhole": sinkhole,
+    "adversarial_mix": adversarial_mix,
+    "adversarial_mix_nogater": lambda lib, x=(): adversarial_mix(lib, gater=False, queue=0, seed=52, extra=x),
+}
+SCENARIOS.update(ADVERSARIAL)
