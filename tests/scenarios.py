@@ -380,14 +380,14 @@ def adversarial_mix(lib, n=400, k=16, seed=51, sybil_frac=0.2, queue=6, msgs=600
 
 
 ADVERSARIAL = {
-    "spam_iwant": spam_iwant,
-    "spam_ihave": spam_ihave,
+    "spam_iwant": lambda lib, x=(): spam_iwant(lib, extra=x),
+    "spam_ihave": lambda lib, x=(): spam_ihave(lib, extra=x),
     "spam_ihave_2t": lambda lib, x=(): spam_ihave(lib, topics=2, per_topic=4000, extra=x),
-    "spam_graft": spam_graft,
-    "spam_invalid": spam_invalid,
-    "squatters": squatters,
-    "sinkhole": sinkhole,
-    "adversarial_mix": adversarial_mix,
+    "spam_graft": lambda lib, x=(): spam_graft(lib, extra=x),
+    "spam_invalid": lambda lib, x=(): spam_invalid(lib, extra=x),
+    "squatters": lambda lib, x=(): squatters(lib, extra=x),
+    "sinkhole": lambda lib, x=(): sinkhole(lib, extra=x),
+    "adversarial_mix": lambda lib, x=(): adversarial_mix(lib, extra=x),
     "adversarial_mix_nogater": lambda lib, x=(): adversarial_mix(lib, gater=False, queue=0, seed=52, extra=x),
 }
 SCENARIOS.update(ADVERSARIAL)
