@@ -260,6 +260,7 @@ def spam_ihave(lib, topics=1, per_topic=3 * 5000, extra=()):
                      WithBehaviour(np.array([0, GS_BEHAVE_IHAVE_SPAM], np.uint8)), *extra, lib=lib)
     e.publish(np.ones(n_ph, np.int32), np.repeat(np.arange(topics), per_topic).astype(np.int32),
               np.full(n_ph, 2, np.int64), kind=np.full(n_ph, GS_MSG_PHANTOM, np.uint8))
+    e.snapshot_ids = []  # phantom ids are never delivered
     return e, 70
 
 
@@ -270,6 +271,7 @@ def spam_graft(lib, extra=()):
     e = NewGossipSub(2, 1, _pair(), graphs.all_subscribed(2, 1), WithPeerScore(sp, thr), WithHop(HOP),
                      WithMessageWindow(64), WithBehaviour(np.array([0, GS_BEHAVE_GRAFT_SPAM], np.uint8)),
                      *extra, lib=lib)
+    e.snapshot_ids = []
     return e, 80
 
 
@@ -311,7 +313,7 @@ def squatters(lib, extra=()):
     beh[honest:] = GS_BEHAVE_NO_FORWARD
     e = NewGossipSub(n, 1, g, graphs.all_subscribed(n, 1), WithPeerScore(sp, thr), WithGossipSubParams(gp),
                      WithFloodPublish(True), WithHop(HOP), WithMessageWindow(1024), WithBehaviour(beh),
-                     *extra, lib=lib)
+                     WithRecordDeliveries(), *extra, lib=lib)
     # 1000 messages 20 ms apart = 5 per 100 ms hop, from hosts i % 10, after 1 s
     e.publish((np.arange(1000) % honest).astype(np.int32), np.zeros(1000, np.int32),
               10 + np.arange(1000, dtype=np.int64) // 5)
