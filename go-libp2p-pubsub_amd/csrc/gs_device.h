@@ -20,11 +20,13 @@
 #define GS_QCAP 320    // phase A delivery queue (>= 63 pending + 256 appended per sub-round)
 #define GS_TABLE 64    // promise table entries per node (one per lane)
 #define GS_PTX 512     // IWANT-retransmission (mcache peertx) entries per node
+#define GS_CUTS 64     // IHAVE entries above MaxIHaveLength one node can cut per hop
 
 // device counter slots (same order as gs_counters)
 enum {
   C_HOPS = 0, C_HEARTBEATS, C_PUBLISHED, C_DELIVERIES, C_DUPLICATES, C_TRANSMISSIONS, C_GRAFTS,
-  C_PRUNES, C_IHAVE, C_IWANT_SENT, C_IWANT_SERVED, C_PROMISES_BROKEN, C_GRAYLISTED, C_NCOUNTERS = 16
+  C_PRUNES, C_IHAVE, C_IWANT_SENT, C_IWANT_SERVED, C_PROMISES_BROKEN, C_GRAYLISTED, C_REJECTED,
+  C_THROTTLED, C_GATED, C_NCOUNTERS = 16
 };
 // device error codes (first one wins)
 enum {
@@ -101,6 +103,24 @@ struct Dev {
   int32_t* nAuth;  // [N] live message slots authored by the node
   int32_t needAge, record;
   uint64_t* sel;   // [N][S] randomsub target mask (randomsub only)
+  // ---- adversarial model (gs_publish_ex / gs_set_validation / gs_set_behaviour / gater)
+  uint8_t* slotKind;     // [S] GS_MSG_* of the slot's message
+  uint64_t topicVal;     // topics with a validator (RegisterTopicValidator)
+  int32_t valQueue;      // validation-queue entries per node per hop, 0 = unlimited
+  int32_t anyBehave;     // some node has a GS_BEHAVE_* bit
+  const uint8_t* behave; // [N] GS_BEHAVE_* bits (nullptr: all honest)
+  int64_t* cSpam[2];     // [E] IWANT-spam request list (arena record), -1 = none
+  uint8_t* cNSrv[2];     // [E] reply RPCs carrying served messages (0..2)
+  // peer gater (peer_gater.go), one per node; stats per (observer, IP) kept on
+  // the observer's first edge to a peer of that IP (gGrp = its in-row index)
+  int32_t gater;
+  double gThreshold, gGlobalDecay, gSourceDecay, gDecayToZero, gDupW, gIgnW, gRejW;
+  int64_t gQuiet;
+  double* gValidate;     // [N]
+  double* gThrottle;     // [N]
+  int64_t* gLast;        // [N] lastThrottle, INT64_MIN = never
+  double* gSt;           // [4][E] deliver, duplicate, ignore, reject (at group edges)
+  uint8_t* gGrp;         // [E] in-row index of the edge holding this peer's IP stats
   int64_t* lastpub;        // [N][T], INT64_MIN = none
   uint64_t* fanoutPresent; // [N]
   int64_t* promMid;  // [N][64]
@@ -150,6 +170,7 @@ struct Dev {
   const int32_t* mTopic;
   const int32_t* mSlot;
   const int64_t* mId;
+  const uint8_t* mKind;
   // counters / error
   unsigned long long* stamps;  // debug builds only (GS_STAMPS)
   double* pad;                 // [256][64][2] scratch targets of branch-free predicated accesses
@@ -158,6 +179,9 @@ struct Dev {
 };
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ bool behaves(const Dev& d, int v, unsigned bit) {
+  return d.behave != nullptr && (d.behave[v] & bit) != 0;
+}
 
 // ---- trace events (gossip_engine.h gs_trace_event) -----------------------
 #define GS_TRACE_COPY 100  // internal: one delivered copy; the host turns every
@@ -165,7 +189,7 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ bool is_traced(const Dev& d, int v) { return d.traced != nullptr && d.traced[v] != 0; }
 __device__ __forceinline__ void set_err(const Dev& d, int code);
 __device__ __forceinline__ void trace_emit(const Dev& d, int64_t hop, int type, int node, int peer, int topic,
-                                           int64_t msg, int phase) {
+                                           int64_t msg, int phase, int reason = 0) {
   const unsigned long long k = atomicAdd(d.traceN, 1ull);
   if ((int64_t)k >= d.traceCap) {
     set_err(d, E_TRACE);
@@ -178,7 +202,8 @@ __device__ __forceinline__ void trace_emit(const Dev& d, int64_t hop, int type, 
   e.node = node;
   e.peer = peer;
   e.topic = (int16_t)topic;
-  e.phase = (int16_t)phase;
+  e.phase = (uint8_t)phase;
+  e.reason = (uint8_t)reason;
   d.trace[k] = e;
 }
 
@@ -486,4 +511,69 @@ __device__ __forceinline__ void arena_read(const Dev& d, int buf, int64_t rec, u
     atomicOr(&lds[slot >> 6], 1ull << (slot & 63));
   }
   __syncthreads();
+}
+
+// The k-th smallest (key, id) of a candidate set spread over the wave: radix
+// select on the 64-bit key (8 passes of 8-bit digits, a 256-bin LDS
+// histogram), then the id among equal keys.  `each(fn)` calls fn(key, id) for
+// this lane's share of the candidates (re-run every pass); k in [1, count].
+// Taking every candidate with (key, id) <= (K, M) takes exactly k of them:
+// the keyed "shuffle, then truncate" of gs_rng.h.  Wave-uniform call.
+template <class F>
+__device__ __forceinline__ void select_kth(F&& each, int k, uint32_t* hist, unsigned long long& K, long long& M) {
+  const int lane = lane_id();
+  unsigned long long prefix = 0;
+  int kk = k;
+  for (int pass = 7; pass >= 0; --pass) {
+    const int sh = 8 * pass;
+    for (int q = lane; q < 256; q += 64) hist[q] = 0u;
+    __syncthreads();
+    const unsigned long long hiMask = pass == 7 ? 0ull : (~0ull << (sh + 8));
+    each([&](unsigned long long key, long long) {
+      if ((key & hiMask) == (prefix & hiMask)) atomicAdd(&hist[(key >> sh) & 255], 1u);
+    });
+    __syncthreads();
+    const uint32_t c0 = hist[4 * lane], c1 = hist[4 * lane + 1], c2 = hist[4 * lane + 2], c3 = hist[4 * lane + 3];
+    const int sum = (int)(c0 + c1 + c2 + c3);
+    const int incl = wave_incl_sum(sum);
+    const int excl = incl - sum;
+    const bool mine = excl < kk && kk <= incl;
+    int digit = 0, below = 0;
+    if (mine) {
+      const uint32_t cs[4] = {c0, c1, c2, c3};
+      int acc = excl, dd = 0;
+      for (; dd < 3; ++dd) {
+        if (acc + (int)cs[dd] >= kk) break;
+        acc += (int)cs[dd];
+      }
+      digit = 4 * lane + dd;
+      below = acc;
+    }
+    const unsigned long long m = __ballot(mine);
+    __syncthreads();
+    if (!m) {  // k above the candidate count: take everything
+      K = ~0ull;
+      M = INT64_MAX;
+      return;
+    }
+    const int src = __ffsll((long long)m) - 1;
+    digit = lane_get(digit, src);
+    below = lane_get(below, src);
+    prefix |= (unsigned long long)digit << sh;
+    kk -= below;
+  }
+  K = prefix;
+  long long prev = INT64_MIN;  // the kk-th smallest id among the keys equal to K
+  for (int q = 0; q < kk; ++q) {
+    long long best = INT64_MAX;
+    each([&](unsigned long long key, long long id) {
+      if (key == prefix && id > prev && id < best) best = id;
+    });
+    for (int o = 32; o > 0; o >>= 1) {
+      const long long y = __shfl_xor(best, o);
+      best = y < best ? y : best;
+    }
+    prev = best;
+  }
+  M = prev;
 }

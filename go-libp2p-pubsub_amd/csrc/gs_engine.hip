@@ -71,6 +71,15 @@ struct gs_engine {
   int64_t heartbeats = 0;
   std::vector<int32_t> mSrc, mTopic, mSlot;
   std::vector<int64_t> mId, mHop;
+  std::vector<uint8_t> mKind;          // GS_MSG_* per message
+  // adversarial model (gs_set_validation / gs_set_behaviour / WithPeerGater)
+  uint64_t topicVal = 0;
+  int32_t valQueue = 0;
+  std::vector<uint8_t> behaveH;
+  uint8_t behaveAll = 0;               // OR of every node's bits
+  bool gaterOn = false;
+  gs_peer_gater_params gaterP{};
+  bool gaterDecayDue(int64_t t) const { return gaterOn && t > 0 && t % gaterP.DecayInterval == 0; }
   size_t uploaded = 0, msgCap = 0, nextMsg = 0;
   std::vector<int64_t> topicCounter, slotOwnerHop, slotOwnerId;
   // device
@@ -251,6 +260,10 @@ int gs_engine::start() {
   n1 = part[rank + 1];
   e0 = rowptr[n0];
   e1 = rowptr[n1];
+  if (world > 1 && (behaveAll & GS_BEHAVE_IWANT_SPAM)) {
+    gs_set_error("IWANT spammers need an unpartitioned engine (their request lists are not exchanged)");
+    return GS_EUNSUPPORTED;
+  }
   if (world > 1 && cfg.router == GS_ROUTER_RANDOMSUB) {
     gs_set_error("a partitioned engine supports floodsub and gossipsub (randomsub target masks are not exchanged)");
     return GS_EUNSUPPORTED;
@@ -420,6 +433,53 @@ int gs_engine::start() {
   x.poolCnt = dalloc<unsigned long long>(2); chk(x.poolCnt);
   x.slotSrc = dalloc<int32_t>(S, 0xFF); x.slotPubHop = dalloc<int64_t>(S); x.slotMid = dalloc<int64_t>(S, 0xFF);
   chk(x.slotSrc); chk(x.slotPubHop); chk(x.slotMid);
+  // adversarial model
+  x.slotKind = dalloc<uint8_t>(S); chk(x.slotKind);
+  x.topicVal = topicVal;
+  x.valQueue = valQueue;
+  x.anyImd = topicVal != 0 ? 1 : 0;  // P4 can only come from a validator's rejection
+  x.anyBehave = behaveAll != 0;
+  x.behave = nullptr;
+  x.cSpam[0] = x.cSpam[1] = nullptr;
+  x.cNSrv[0] = x.cNSrv[1] = nullptr;
+  if (behaveAll) {
+    uint8_t* b = dalloc<uint8_t>(N); chk(b);
+    if (b) HIPCHECK(hipMemcpyAsync(b, behaveH.data(), N, hipMemcpyHostToDevice, stream));
+    x.behave = b;
+    if (behaveAll & GS_BEHAVE_IWANT_SPAM)
+      for (int k = 0; k < 2; ++k) {
+        x.cSpam[k] = dalloc<int64_t>(E, 0xFF); chk(x.cSpam[k]);
+        x.cNSrv[k] = dalloc<uint8_t>(E); chk(x.cNSrv[k]);
+      }
+  }
+  x.gater = gaterOn ? 1 : 0;
+  x.gValidate = x.gThrottle = nullptr;
+  x.gLast = nullptr;
+  x.gSt = nullptr;
+  x.gGrp = nullptr;
+  if (gaterOn) {
+    x.gThreshold = gaterP.Threshold; x.gGlobalDecay = gaterP.GlobalDecay; x.gSourceDecay = gaterP.SourceDecay;
+    x.gDecayToZero = gaterP.DecayToZero; x.gDupW = gaterP.DuplicateWeight; x.gIgnW = gaterP.IgnoreWeight;
+    x.gRejW = gaterP.RejectWeight; x.gQuiet = gaterP.Quiet;
+    x.gValidate = dalloc<double>(N); x.gThrottle = dalloc<double>(N); x.gLast = dalloc<int64_t>(N);
+    x.gSt = dalloc<double>(4 * (size_t)E); x.gGrp = dalloc<uint8_t>(E);
+    chk(x.gValidate); chk(x.gThrottle); chk(x.gLast); chk(x.gSt); chk(x.gGrp);
+    if (ok) {
+      // peers of one IP share a stats object (peer_gater.go:262-280); getIP = ipv4, 0 = "<unknown>"
+      std::vector<uint8_t> grp(E);
+      for (int u = 0; u < N; ++u)
+        for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) {
+          const uint32_t ip = ipv4.empty() ? 0u : ipv4[col[e]];
+          int64_t f = rowptr[u];
+          while ((ipv4.empty() ? 0u : ipv4[col[f]]) != ip) ++f;
+          grp[e] = (uint8_t)(f - rowptr[u]);
+        }
+      std::vector<int64_t> never(N, INT64_MIN);
+      HIPCHECK(hipMemcpyAsync(x.gGrp, grp.data(), E, hipMemcpyHostToDevice, stream));
+      HIPCHECK(hipMemcpyAsync(x.gLast, never.data(), (size_t)N * 8, hipMemcpyHostToDevice, stream));
+      HIPCHECK(hipStreamSynchronize(stream));
+    }
+  }
 #ifdef GS_STAMPS
   x.stamps = dalloc<unsigned long long>((size_t)(N / 1024 + 1) * 16);  // phase A | phase B
 #endif
@@ -449,9 +509,9 @@ int gs_engine::start() {
     for (int u = n0; u < n1; ++u) {
       if (!traceMask[u]) continue;
       for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e)
-        tracePending.push_back(gs_trace_event{0, -1, GS_TRACE_ADD_PEER, u, col[e], -1, 0});
+        tracePending.push_back(gs_trace_event{0, -1, GS_TRACE_ADD_PEER, u, col[e], -1, 0, 0});
       for (int t = 0; t < T; ++t)
-        if ((sub[u] >> t) & 1) tracePending.push_back(gs_trace_event{0, -1, GS_TRACE_JOIN, u, -1, (int16_t)t, 0});
+        if ((sub[u] >> t) & 1) tracePending.push_back(gs_trace_event{0, -1, GS_TRACE_JOIN, u, -1, (int16_t)t, 0, 0});
     }
   }
   if (world > 1) {
@@ -490,6 +550,10 @@ int gs_engine::uploadMessages() {
     size_t cap = std::max<size_t>(1024, n * 2);
     int32_t *s = nullptr, *t = nullptr, *sl = nullptr;
     int64_t* id = nullptr;
+    uint8_t* kd = nullptr;
+    HIPCHECK(hipMalloc(&kd, cap));
+    allocs.push_back(kd);
+    d.mKind = kd;
     HIPCHECK(hipMalloc(&s, cap * 4));
     HIPCHECK(hipMalloc(&t, cap * 4));
     HIPCHECK(hipMalloc(&sl, cap * 4));
@@ -504,6 +568,7 @@ int gs_engine::uploadMessages() {
   HIPCHECK(hipMemcpyAsync((void*)(d.mTopic + uploaded), mTopic.data() + uploaded, k * 4, hipMemcpyHostToDevice, stream));
   HIPCHECK(hipMemcpyAsync((void*)(d.mSlot + uploaded), mSlot.data() + uploaded, k * 4, hipMemcpyHostToDevice, stream));
   HIPCHECK(hipMemcpyAsync((void*)(d.mId + uploaded), mId.data() + uploaded, k * 8, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipMemcpyAsync((void*)(d.mKind + uploaded), mKind.data() + uploaded, k, hipMemcpyHostToDevice, stream));
   HIPCHECK(hipStreamSynchronize(stream));
   uploaded = n;
   return GS_OK;
@@ -622,13 +687,24 @@ int gs_engine::stepOne() {
     }
     const size_t nCnt = ((size_t)T * d.maxDeg + 7) & ~(size_t)7;
     const int nYp = (nY + 15) & ~15;
-    const size_t lds = (narrow ? 2 : 4) * nCnt + 16 * (size_t)nR + (size_t)nYp + (d.needAge ? 4 * nCnt : 0);
+    // the adversarial model (validators, gater, attackers) has its own
+    // instantiation: the honest path keeps its LDS budget and code
+    const bool adv = topicVal != 0 || gaterOn || behaveAll != 0;
+    size_t lds = (narrow ? 2 : 4) * nCnt + 16 * (size_t)nR + (size_t)nYp + (d.needAge ? 4 * nCnt : 0);
+    if (adv) lds += 4 * nCnt + 4 * 64 * 4 + 8 * 64 + 8 * (size_t)nR + (valQueue > 0 ? 8 * (size_t)nYp : 0);
     TIMED(this, GS_K_PHASE_A, launch_wpl(W, [&](auto w) {
             if (!nOwn) return;
-            if (narrow)
-              k_phase_a<decltype(w)::value, true><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR, nYp);
-            else
-              k_phase_a<decltype(w)::value, false><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR, nYp);
+            constexpr int WV = decltype(w)::value;
+            if (adv) {
+              if (narrow)
+                k_phase_a<WV, true, true><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR, nYp);
+              else
+                k_phase_a<WV, false, true><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR, nYp);
+            } else if (narrow) {
+              k_phase_a<WV, true, false><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR, nYp);
+            } else {
+              k_phase_a<WV, false, false><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR, nYp);
+            }
           }));
   }
   if (!retireWords.empty()) {
@@ -651,9 +727,20 @@ int gs_engine::stepOne() {
   }
   if (gossip) {
     if (scoring) TIMED(this, GS_K_SCORE, (k_score_rows<2><<<sgb, 64, 0, stream>>>(d, nullptr)));
+    // MaxIHaveLength cuts are possible only if the messages (phantom ids
+    // included) that can sit in one gossip window outnumber MaxIHaveLength:
+    // published within HistoryGossip + 1 heartbeats plus the delivery age bound
+    int cutMode = 0;
+    {
+      const int64_t lo = h - (int64_t)(gp.HistoryGossip + 1) * H - maxAge - 2;
+      const auto a = std::lower_bound(mHop.begin(), mHop.end(), lo);
+      const auto b2 = std::upper_bound(mHop.begin(), mHop.end(), h);
+      cutMode = (int64_t)(b2 - a) > (int64_t)gp.MaxIHaveLength ? 1 : 0;
+    }
+    const size_t ldsB = cutMode ? (256 * 4 + GS_CUTS * 4 + GS_CUTS * 16 + 64 * 16 + 128 * 4 + 16) : 0;
     TIMED(this, GS_K_PHASE_B,
           launch_wpl(W, [&](auto wpl) {
-            if (nOwn) k_phase_b<decltype(wpl)::value><<<nOwn, 64, 0, stream>>>(d, h, now, cur, head);
+            if (nOwn) k_phase_b<decltype(wpl)::value><<<nOwn, 64, ldsB, stream>>>(d, h, now, cur, head, cutMode);
           }));
   }
   if (refreshDue(now)) {
@@ -664,6 +751,10 @@ int gs_engine::stepOne() {
     // pending delivery counts are 16-bit: fold them before they can overflow
     k_fold_all<<<pb, 256, 0, stream>>>(d);
     hopsSinceFold = 0;
+  }
+  if (gaterDecayDue(now)) {  // peerGater.background ticker (peer_gater.go:204-217)
+    const int64_t nth = std::max<int64_t>(nOwn, eOwn);
+    if (nth) k_gater_decay<<<nblk(nth, 256), 256, 0, stream>>>(d);
   }
   if (heartbeatDue(now)) {
     ticks++;
@@ -711,8 +802,8 @@ int gs_engine::checkDeviceError() {
       gs_set_error("a message was first delivered later than the message window allows; raise slots_per_topic");
       return GS_ECAPACITY;
     case E_TRUNCATE:
-      gs_set_error("IHAVE/IWANT truncation at MaxIHaveLength is not built in this version");
-      return GS_EUNSUPPORTED;
+      gs_set_error("more than 64 IHAVE entries above MaxIHaveLength reached one node in one hop");
+      return GS_ECAPACITY;
     case E_FCAP:
       gs_set_error("more first deliveries (plus own publishes) at one node in one hop than its "
                    "frontier list holds (min(slots + 64, 2^31 / num_nodes) entries)");
@@ -897,9 +988,12 @@ int gs_engine::drainTrace() {
       return std::tie(hop, msg, node, peer) < std::tie(o.hop, o.msg, o.node, o.peer);
     }
   };
+  // a copy is the delivering one (DeliverMessage), a rejected first copy or a
+  // copy dropped by a full validation queue (RejectMessage), or else a duplicate
   std::vector<Key> delivered;
   for (const auto& e : ev)
-    if (e.type == GS_TRACE_DELIVER_MESSAGE && e.phase == 2) delivered.push_back(Key{e.hop, e.msg, e.node, e.peer});
+    if ((e.type == GS_TRACE_DELIVER_MESSAGE || e.type == GS_TRACE_REJECT_MESSAGE) && e.phase == 2)
+      delivered.push_back(Key{e.hop, e.msg, e.node, e.peer});
   std::sort(delivered.begin(), delivered.end());
   std::vector<gs_trace_event> keep(tracePending.begin() + traceOut, tracePending.end());
   for (auto e : ev) {
@@ -941,7 +1035,6 @@ const char* gs_last_error(void) { return g_err.c_str(); }
 int gs_engine_create(const gs_config* cfg, const gs_gossipsub_params* gsp, const gs_peer_score_params* psp,
                      const gs_topic_score_params* topics, const uint8_t* topic_scored,
                      const gs_peer_score_thresholds* thr, const gs_peer_gater_params* gater, gs_engine** out) {
-  (void)gater;
   if (!cfg || !out) { gs_set_error("null argument"); return GS_EINVAL; }
   if (cfg->num_nodes <= 0 || cfg->num_topics <= 0 || cfg->num_topics > 64 || cfg->hop_ns <= 0) {
     gs_set_error("invalid config: num_nodes > 0, 1 <= num_topics <= 64, hop_ns > 0 required");
@@ -952,6 +1045,15 @@ int gs_engine_create(const gs_config* cfg, const gs_gossipsub_params* gsp, const
     gs_set_error("slots_per_topic must be a positive multiple of 64");
     return GS_EINVAL;
   }
+  if (gater) {
+    if (cfg->router != GS_ROUTER_GOSSIPSUB) { gs_set_error("pubsub router is not gossipsub"); return GS_EINVAL; }
+    int rc = gs_validate_peer_gater_params(gater);
+    if (rc) return rc;
+    if (gater->DecayInterval % cfg->hop_ns != 0) {
+      gs_set_error("gater DecayInterval must be a multiple of hop_ns");
+      return GS_EUNSUPPORTED;
+    }
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
     gs_set_error("no HIP device available: the gossip engine needs an MI355X (gfx950)");
@@ -960,6 +1062,10 @@ int gs_engine_create(const gs_config* cfg, const gs_gossipsub_params* gsp, const
   if (cfg->device < 0 || cfg->device >= ndev) { gs_set_error("bad device ordinal"); return GS_EINVAL; }
   std::unique_ptr<gs_engine> g(new gs_engine());
   g->cfg = *cfg;
+  if (gater) {
+    g->gaterOn = true;
+    g->gaterP = *gater;
+  }
   g->N = cfg->num_nodes;
   g->T = cfg->num_topics;
   g->St = cfg->slots_per_topic;
@@ -1078,10 +1184,16 @@ int gs_set_ip_whitelist(gs_engine* g, int32_t n, const uint32_t* net, const uint
 
 int gs_publish(gs_engine* g, int32_t n, const int32_t* src, const int32_t* topic, const int64_t* hop,
                int64_t* ids_out) {
+  return gs_publish_ex(g, n, src, topic, hop, nullptr, ids_out);
+}
+
+int gs_publish_ex(gs_engine* g, int32_t n, const int32_t* src, const int32_t* topic, const int64_t* hop,
+                  const uint8_t* kind, int64_t* ids_out) {
   int64_t last = g->mHop.empty() ? g->hop : std::max(g->hop, g->mHop.back());
   for (int i = 0; i < n; ++i) {
-    if (src[i] < 0 || src[i] >= g->N || topic[i] < 0 || topic[i] >= g->T || hop[i] < last) {
-      gs_set_error("publish: bad src/topic or hop not non-decreasing from the current hop");
+    if (src[i] < 0 || src[i] >= g->N || topic[i] < 0 || topic[i] >= g->T || hop[i] < last ||
+        (kind && kind[i] > GS_MSG_PHANTOM)) {
+      gs_set_error("publish: bad src/topic/kind or hop not non-decreasing from the current hop");
       return GS_EINVAL;
     }
     last = hop[i];
@@ -1110,10 +1222,38 @@ int gs_publish(gs_engine* g, int32_t n, const int32_t* src, const int32_t* topic
     g->mSlot.push_back(slots[i]);
     g->mId.push_back(id);
     g->mHop.push_back(hop[i]);
+    g->mKind.push_back(kind ? kind[i] : (uint8_t)GS_MSG_VALID);
     g->slotOwnerId[slots[i]] = id;
     if (ids_out) ids_out[i] = id;
   }
   return g->uploadMessages();
+}
+
+int gs_set_validation(gs_engine* g, const uint8_t* topic_validator, int32_t queue_per_hop) {
+  if (g->started) { gs_set_error("validation must be set before the first step"); return GS_ESTATE; }
+  if (queue_per_hop < 0) { gs_set_error("queue_per_hop must be >= 0"); return GS_EINVAL; }
+  g->topicVal = 0;
+  if (topic_validator)
+    for (int t = 0; t < g->T; ++t)
+      if (topic_validator[t]) g->topicVal |= 1ull << t;
+  g->valQueue = queue_per_hop;
+  return GS_OK;
+}
+
+int gs_set_behaviour(gs_engine* g, const uint8_t* behaviour) {
+  if (g->started) { gs_set_error("behaviours must be set before the first step"); return GS_ESTATE; }
+  g->behaveH.clear();
+  g->behaveAll = 0;
+  if (behaviour) {
+    g->behaveH.assign(behaviour, behaviour + g->N);
+    for (uint8_t b : g->behaveH) g->behaveAll |= b;
+    if (g->behaveAll & ~(uint8_t)(GS_BEHAVE_NO_FORWARD | GS_BEHAVE_IWANT_SPAM | GS_BEHAVE_GRAFT_SPAM |
+                                  GS_BEHAVE_IHAVE_SPAM)) {
+      gs_set_error("unknown behaviour bit");
+      return GS_EINVAL;
+    }
+  }
+  return GS_OK;
 }
 
 int gs_step(gs_engine* g, int64_t hops) {
@@ -1243,6 +1383,9 @@ int gs_read_counters(gs_engine* g, gs_counters* out) {
     out->iwant_served = (int64_t)c[C_IWANT_SERVED];
     out->promises_broken = (int64_t)c[C_PROMISES_BROKEN];
     out->graylisted = (int64_t)c[C_GRAYLISTED];
+    out->rejected = (int64_t)c[C_REJECTED];
+    out->throttled = (int64_t)c[C_THROTTLED];
+    out->gated = (int64_t)c[C_GATED];
   }
   out->hops = g->hop;
   out->heartbeats = g->heartbeats;

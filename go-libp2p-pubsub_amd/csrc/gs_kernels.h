@@ -271,6 +271,8 @@ __global__ __launch_bounds__(64) void k_join(Dev d, int64_t hop, int64_t now, in
       if (is_traced(d, u)) trace_emit(d, hop, GS_TRACE_GRAFT, u, v, t, -1, 0);  // gossipsub.go:1057
     }
   }
+  const bool silent = behaves(d, u, GS_BEHAVE_NO_FORWARD);  // a squatter sends no control
+  if (silent) gj = 0;
   if (valid) {
     d.mesh[e] = meshl;
     d.cGraftJoin[cur][e] = gj;
@@ -329,6 +331,7 @@ __global__ void k_fwd(Dev d, int cur) {
     const uint64_t m = d.mesh[e];
     const bool dir = d.direct[e];
     relay = joined & (m | (dir ? sv : 0));
+    if (behaves(d, u, GS_BEHAVE_NO_FORWARD)) relay = 0;  // a squatter relays nothing
     if (d.floodPublish) {
       pub = (dir || d.score0[e] >= d.publishThr) ? sv : 0;
     } else {
@@ -465,7 +468,20 @@ __device__ __forceinline__ int wave_min_int(int x) {
 // one topic in this hop (every topic has <= 255 live message slots), so the
 // (sender, topic) counters are 8-bit copies | 8-bit first deliveries, two per
 // LDS word: half the counter table, more waves per CU.
-template <int WPL, bool NARROW>
+// ADV (the adversarial model: topic validators, the peer gater, attacker
+// behaviours; host-selected, so the honest path compiles without it):
+//   * every payload RPC passes AcceptFrom's peer gater (peer_gater.go:320-363)
+//     on the hop-start gater state: payload RPCs carry one draw each
+//     (GS_SITE_GATER, key = message id), a sender's control RPCs share one;
+//     AcceptControl drops the payload and throttles the peer's promises;
+//   * a fresh message of a topic with a validator is validated (validation.go:
+//     274-351): REJECT / IGNORE verdicts mark it seen without delivering it
+//     (P4 for every copy of a rejected message); with a bounded validation
+//     queue only the first valQueue fresh messages in arrival order (first
+//     deliverer, then message id) are validated, the copies of the rest are
+//     RejectValidationQueueFull (not seen; the gater's throttle counter);
+//   * an IWANT spammer re-requests every message it received, per sender.
+template <int WPL, bool NARROW, bool ADV>
 __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int head, WMask amR, WMask amW,
                                                 int nR, int nY) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
@@ -476,6 +492,13 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   uint64_t* sYm = sD + nR;                                // [nR] young-slot mask of each amR word
   uint8_t* sFirst = (uint8_t*)(sYm + nR);                 // [nY] lowest deliverer per young slot
   uint32_t* sUnc = (uint32_t*)(sFirst + nY);              // [MD][T] uncredited duplicates (needAge)
+  // ADV tables after sUnc (present only in the ADV launch)
+  uint32_t* sInv = sUnc + (d.needAge ? nCnt : 0);         // [MD][T] copies of rejected messages
+  uint32_t* sPer = sInv + nCnt;                           // [4][64] per sender: accepted copies, valid /
+                                                          // rejected / ignored first deliveries
+  double* sGThr = (double*)(sPer + 4 * 64);               // [64] gater threshold per sender, < 0 = accept
+  uint64_t* sDrop = (uint64_t*)(sGThr + 64);              // [nR] fresh messages dropped by a full queue
+  uint64_t* sKey = sDrop + nR;                            // [nY] queue order keys (ff << 56 | mid)
   __shared__ int sBlk[64];        // first list block of each sender
   __shared__ uint64_t sRelay[64], sPub[64];
   __shared__ int sSnd[64];        // sender node | jr << 24 | graylisted << 31
@@ -499,10 +522,11 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   uint64_t relay = 0, pub = 0;
   bool gray = false;
   int irOff = 0, irN = 0;
+  int64_t r = 0;
   if (valid) {
     const int64_t e = base + lane;
     u = d.col[e];
-    const int64_t r = d.rev[e];
+    r = d.rev[e];
     jr = (int)(r - d.rowptr[u]);
     relay = d.fwdRelay[prv][r] & sv;
     pub = d.fwdPub[prv][r] & sv;
@@ -535,6 +559,35 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     }
   }
   for (int k = lane; k < nY / 16; k += 64) ((uint4*)sFirst)[k] = make_uint4(~0u, ~0u, ~0u, ~0u);
+  // ---- ADV: the hop-start peer-gater decision inputs (lane = in-edge)
+  bool ctlGated = false;  // the sender's control RPCs of this hop got AcceptControl
+  int nSrvRpc = 0;        // reply RPCs of the sender carrying served messages
+  if constexpr (ADV) {
+    for (int k = lane; k < nCnt / 4; k += 64) ((uint4*)sInv)[k] = make_uint4(0, 0, 0, 0);
+    for (int k = lane; k < 4 * 64; k += 64) sPer[k] = 0;
+    for (int k = lane; k < nR; k += 64) sDrop[k] = 0;
+    double thr = -1.0;
+    if (d.gater && valid && !gray && !d.direct[base + lane]) {
+      // AcceptFrom's circuit breaker on this node's hop-start counters (:329-342)
+      const int64_t last = d.gLast[v];
+      const double gv = d.gValidate[v], gt = d.gThrottle[v];
+      const bool active = !(last == INT64_MIN || h * d.hop_ns - last > d.gQuiet) && gt != 0 &&
+                          !(gv != 0 && gt / gv < d.gThreshold);
+      if (active) {
+        const int64_t ge = base + d.gGrp[base + lane];
+        const double de = d.gSt[ge], du = d.gSt[d.E + ge], ig = d.gSt[2 * d.E + ge], rj = d.gSt[3 * d.E + ge];
+        const double total = de + d.gDupW * du + d.gIgnW * ig + d.gRejW * rj;
+        if (total != 0) thr = (1 + de) / (1 + total);
+      }
+    }
+    sGThr[lane] = thr;
+    if (valid && thr >= 0 && (d.cPre[prv][r] != 0 || d.cHb[prv][r] != 0)) {
+      const double uu = gs_key_to_unit(gs_key64(d.seed, GS_SITE_GATER, v, u, (uint32_t)h, 0xFFFFFFFFu));
+      ctlGated = !(uu < thr);
+    }
+    if (valid && d.cNSrv[prv] != nullptr) nSrvRpc = d.cNSrv[prv][r];
+    else if (irN) nSrvRpc = 1;
+  }
   // per-sender view for the block-parallel walk
   const int nb = (Ln + 3) >> 2;  // 16-byte blocks of the sender's list
   const int bincl = wave_incl_sum(nb);
@@ -550,19 +603,47 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
 
   int nSent = 0, nGray = 0;
   long long nCopies = 0;  // delivered copies (non-graylisted)
+  int nGatedCopies = 0;   // ADV: payload RPCs dropped by the gater
+  uint64_t throttled = 0; // ADV: senders throttled this hop (ThrottlePeer), lane-uniform after the ballot
+  // ADV: the verdict of slot's message: its kind on a topic with a validator
+  auto kindOf = [&](int slot, int t) -> int {
+    if constexpr (!ADV) return GS_MSG_VALID;
+    return ((d.topicVal >> t) & 1) ? (int)d.slotKind[slot] : GS_MSG_VALID;
+  };
+  // ADV: the gater's AcceptFrom for the payload RPC carrying slot from sender i
+  auto gated = [&](int i, int slot) -> bool {
+    if constexpr (!ADV) return false;
+    const double thr = sGThr[i];
+    if (thr < 0) return false;
+    const uint32_t mid = (uint32_t)d.slotMid[slot];
+    const double uu = gs_key_to_unit(gs_key64(d.seed, GS_SITE_GATER, v, d.col[base + i], (uint32_t)h, mid));
+    return !(uu < thr);
+  };
   // One delivered copy of `slot` from sender i (sent, not graylisted).
   const bool trv = is_traced(d, v);
-  auto deliver = [&](int i, int slot) {
+  auto deliver = [&](int i, int slot, bool payloadRpc) {
+    if (payloadRpc && gated(i, slot)) {  // AcceptControl: payload ignored (pubsub.go:951-955)
+      ++nGatedCopies;
+      throttled |= 1ull << i;
+      return;
+    }
     const int w = slot >> 6;
     const int t = (int)__umulhi((unsigned)slot, d.stMagic);
     if (trv) trace_emit(d, h, GS_TRACE_COPY, v, d.col[base + i], t, d.slotMid[slot], 2);
+    const int kind = kindOf(slot, t);
+    if constexpr (ADV) {
+      atomicAdd(&sPer[i], 1u);
+      if (kind == GS_MSG_REJECT) atomicAdd(&sInv[i * T + t], 1u);
+    }
 #ifndef GS_EXP_NOADD
-    if (NARROW) {
-      // no-return add: the host proved the 8-bit count cannot overflow
-      const int pl = i * T + t;
-      atomicAdd(&scnt[pl >> 1], 1u << (16 * (pl & 1)));
-    } else {
-      atomicAdd(&scnt[i * T + t], 1u);
+    if (kind == GS_MSG_VALID) {
+      if (NARROW) {
+        // no-return add: the host proved the 8-bit count cannot overflow
+        const int pl = i * T + t;
+        atomicAdd(&scnt[pl >> 1], 1u << (16 * (pl & 1)));
+      } else {
+        atomicAdd(&scnt[i * T + t], 1u);
+      }
     }
     ++nCopies;
 #endif
@@ -573,7 +654,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
       const bool had = (d.seen[(int64_t)v * W + w] >> (slot & 63)) & 1;
       // markDuplicateMessageDelivery window (score.go:955): a copy of a message
       // first delivered before this hop is credited only within the window
-      if (had && d.needAge) {
+      if (had && d.needAge && kind == GS_MSG_VALID) {
         const int64_t firstHop = d.slotPubHop[slot] + d.age[(int64_t)v * d.S + slot];
         if ((h - firstHop) * d.hop_ns > d.tp[t].MmdWindow) atomicAdd(&sUnc[i * T + t], 1u);
       }
@@ -604,109 +685,110 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   // ---- pass 1a: every 16-byte block of every sender's list is one work item;
   // lane l takes items l, l+64, ...  (PB loads in flight per lane).  The
   // entries actually sent (about a quarter: the sender's per-edge topic masks)
-  // are compacted into an LDS queue and delivered 64 at a time by all lanes.
-  int qh = 0, qt = 0;  // queue head / tail (wave-uniform)
-#ifdef GS_STAMPS
-  long long accDel = 0;  // cycles in the delivery drains
-  long long accLd = 0;   // cycles from a round's start to its list blocks' arrival
-#endif
-  constexpr int PB = 8;
-  for (int b0 = 0; b0 < totalBlk; b0 += 64 * PB) {
-#ifdef GS_STAMPS
-    const long long tl0 = clock64();
-#endif
-    int si[PB], kb[PB];
-    uint4 q[PB];
+  // are compacted into an LDS queue and handed to fn 64 at a time by all lanes.
+  // fn(i, slot) sees every sent, non-graylisted copy; walk() also counts
+  // nSent / nGray when `count` (the first walk).
+  auto walk = [&](auto&& fn, bool count) {
+    int qh = 0, qt = 0;  // queue head / tail (wave-uniform)
+    constexpr int PB = 8;
+    for (int b0 = 0; b0 < totalBlk; b0 += 64 * PB) {
+      int si[PB], kb[PB];
+      uint4 q[PB];
 #pragma unroll
-    for (int r = 0; r < PB; ++r) {
-      const int bidx = b0 + r * 64 + lane;
-      si[r] = -1;
-      kb[r] = 0;
-      q[r] = make_uint4(0, 0, 0, 0);
-      if (bidx < totalBlk) {
-        int lo = 0, hi = 63;  // last sender whose first block is <= bidx
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (sBlk[mid] <= bidx) lo = mid; else hi = mid - 1;
+      for (int rr = 0; rr < PB; ++rr) {
+        const int bidx = b0 + rr * 64 + lane;
+        si[rr] = -1;
+        kb[rr] = 0;
+        q[rr] = make_uint4(0, 0, 0, 0);
+        if (bidx < totalBlk) {
+          int lo = 0, hi = 63;  // last sender whose first block is <= bidx
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (sBlk[mid] <= bidx) lo = mid; else hi = mid - 1;
+          }
+          si[rr] = lo;
+          kb[rr] = bidx - sBlk[lo];
+          const int uu = sSnd[lo] & 0xFFFFFF;
+          q[rr] = *(const uint4*)(d.fl[prv] + (int64_t)uu * FC + 4 * kb[rr]);
         }
-        si[r] = lo;
-        kb[r] = bidx - sBlk[lo];
-        const int uu = sSnd[lo] & 0xFFFFFF;
-        q[r] = *(const uint4*)(d.fl[prv] + (int64_t)uu * FC + 4 * kb[r]);
       }
-    }
-#ifdef GS_STAMPS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    accLd += clock64() - tl0;
-#endif
 #pragma unroll
-    for (int r = 0; r < PB; ++r) {
-      uint32_t en[4];
-      bool sn[4];
-      {
-        const int i = si[r] < 0 ? 0 : si[r];
-        const int snd = sSnd[i];
-        const int uu = snd & 0xFFFFFF;
-        const int jri = (snd >> 24) & 0x7F;
-        const bool isGray = snd < 0;
-        const uint64_t rl = sRelay[i], pb = sPub[i];
-        const int n = si[r] < 0 ? 0 : min(4, sLn[i] - 4 * kb[r]);
+      for (int rr = 0; rr < PB; ++rr) {
+        uint32_t en[4];
+        bool sn[4];
+        {
+          const int i = si[rr] < 0 ? 0 : si[rr];
+          const int snd = sSnd[i];
+          const int uu = snd & 0xFFFFFF;
+          const int jri = (snd >> 24) & 0x7F;
+          const bool isGray = snd < 0;
+          const uint64_t rl = sRelay[i], pb = sPub[i];
+          const int n = si[rr] < 0 ? 0 : min(4, sLn[i] - 4 * kb[rr]);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const uint32_t ent = c == 0 ? q[rr].x : (c == 1 ? q[rr].y : (c == 2 ? q[rr].z : q[rr].w));
+            const int slot = (int)(ent & 0xFFFF);
+            const int tag = (int)(ent >> 16);
+            const int t = (int)__umulhi((unsigned)slot, d.stMagic);
+            bool sent = c < n && (tag == 255 ? ((pb >> t) & 1) : ((rl >> t) & 1));
+            sent = sent && tag != jri;  // ReceivedFrom exclusion (gossipsub.go:1003)
+            if (sent && d.router == 1) sent = (d.sel[(int64_t)uu * d.S + slot] >> jri) & 1;
+            if (sent && authV && d.slotSrc[slot] == v) sent = false;  // never to the author
+            if (count) {
+              nSent += sent;
+              if (sent && isGray) ++nGray;  // one RPC per relayed message, all dropped
+            }
+            sn[c] = sent && !isGray;
+            en[c] = (uint32_t)slot | ((uint32_t)i << 16);
+          }
+        }
+        // c-major positions (delivery order does not matter: every update is
+        // a commutative LDS atomic)
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const uint32_t ent = c == 0 ? q[r].x : (c == 1 ? q[r].y : (c == 2 ? q[r].z : q[r].w));
-          const int slot = (int)(ent & 0xFFFF);
-          const int tag = (int)(ent >> 16);
-          const int t = (int)__umulhi((unsigned)slot, d.stMagic);
-          bool sent = c < n && (tag == 255 ? ((pb >> t) & 1) : ((rl >> t) & 1));
-          sent = sent && tag != jri;  // ReceivedFrom exclusion (gossipsub.go:1003)
-          if (sent && d.router == 1) sent = (d.sel[(int64_t)uu * d.S + slot] >> jri) & 1;
-          if (sent && authV && d.slotSrc[slot] == v) sent = false;  // never to the author
-          nSent += sent;
-          if (sent && isGray) ++nGray;  // one RPC per relayed message, all dropped
-          sn[c] = sent && !isGray;
-          en[c] = (uint32_t)slot | ((uint32_t)i << 16);
+          const uint64_t m = __ballot(sn[c]);
+          if (sn[c]) sQ[qt + lane_rank(m)] = en[c];
+          qt += __popcll(m);
         }
-      }
-      // c-major positions (delivery order does not matter: every update is
-      // a commutative LDS atomic)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const uint64_t m = __ballot(sn[c]);
-        if (sn[c]) sQ[qt + lane_rank(m)] = en[c];
-        qt += __popcll(m);
-      }
-      __syncthreads();
-      if (qt >= 64) {
-#ifdef GS_STAMPS
-        const long long tq0 = clock64();
-#endif
-        while (qt - qh >= 64) {
-          const uint32_t ent = sQ[qh + lane];
-          deliver((int)(ent >> 16), (int)(ent & 0xFFFF));
-          qh += 64;
+        __syncthreads();
+        if (qt >= 64) {
+          while (qt - qh >= 64) {
+            const uint32_t ent = sQ[qh + lane];
+            fn((int)(ent >> 16), (int)(ent & 0xFFFF));
+            qh += 64;
+          }
+          // move the (< 64) pending copies to the front
+          const uint32_t rest = lane < qt - qh ? sQ[qh + lane] : 0u;
+          __syncthreads();
+          if (lane < qt - qh) sQ[lane] = rest;
+          qt -= qh;
+          qh = 0;
+          __syncthreads();
         }
-        // move the (< 64) pending copies to the front
-        const uint32_t rest = lane < qt - qh ? sQ[qh + lane] : 0u;
-        __syncthreads();
-        if (lane < qt - qh) sQ[lane] = rest;
-        qt -= qh;
-        qh = 0;
-        __syncthreads();
-#ifdef GS_STAMPS
-        accDel += clock64() - tq0;
-#endif
       }
     }
+    if (lane < qt - qh) {
+      const uint32_t ent = sQ[qh + lane];
+      fn((int)(ent >> 16), (int)(ent & 0xFFFF));
+    }
+    __syncthreads();
+  };
+  walk([&](int i, int slot) { deliver(i, slot, true); }, true);
+  // ---- pass 1b: IWANT responses (in the sender's reply RPCs, rare)
+  nSent += irN;
+  if (!gray) {
+    if (ADV && ctlGated) {
+      nGatedCopies += nSrvRpc;  // the served replies' payload is ignored
+    } else {
+      for (int k = 0; k < irN; ++k) deliver(lane, d.pool[prv][irOff + k], false);
+    }
   }
-  if (lane < qt - qh) {
-    const uint32_t ent = sQ[qh + lane];
-    deliver((int)(ent >> 16), (int)(ent & 0xFFFF));
-  }
-  // ---- pass 1b: IWANT responses (one list per sender, rare)
-  for (int k = 0; k < irN; ++k) {
-    const int slot = d.pool[prv][irOff + k];
-    ++nSent;
-    if (!gray) deliver(lane, slot);
+  if constexpr (ADV) {
+    if (ctlGated) throttled |= 1ull << lane;
+    // lane-uniform set of throttled senders
+    uint64_t all = 0;
+    for (int o = 0; o < 64; ++o) all |= lane_get64(throttled, o);
+    throttled = all;
   }
   __syncthreads();
 
@@ -718,13 +800,14 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   if (scoring) sRelay[lane] = valid ? d.mesh[base + lane] : 0ull;  // pass 3: in-edge mesh words
   long long nDeliv = 0;
   uint64_t Uw[WPL], Sw[WPL], Hw[WPL], Ow[WPL];
+  uint64_t Xw[WPL];  // ADV: fresh messages validated as REJECT / IGNORE (seen, not delivered)
   int rkw[WPL];  // rank of the lane's word in amR
   // index of young slot b of the amR word of rank rk in sFirst
   auto fidx = [&](int rk, int b) -> int { return sYp[rk] + __popcll(sYm[rk] & ((1ull << b) - 1)); };
 #pragma unroll
   for (int j = 0; j < WPL; ++j) {
     const int w = lane + 64 * j;
-    Uw[j] = Sw[j] = Hw[j] = Ow[j] = 0;
+    Uw[j] = Sw[j] = Hw[j] = Ow[j] = Xw[j] = 0;
     rkw[j] = 0;
     if (w < W && wm_has(amR, w)) {
       rkw[j] = wm_rank(amR, w);
@@ -735,10 +818,80 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
       }
     }
   }
+  long long nValidated = 0, nRejected = 0, nThrottledCopies = 0;
+  bool anyDrop = false;
+  if constexpr (ADV) {
+    // ---- the validation queue: the first valQueue fresh messages of topics
+    // with a validator, in arrival order (first deliverer, then message id),
+    // are validated; the rest are dropped (RejectValidationQueueFull)
+    int nCand = 0;
+#pragma unroll
+    for (int j = 0; j < WPL; ++j) {
+      const int w = lane + 64 * j;
+      const int t = (int)__umulhi((unsigned)(w * 64), d.stMagic);
+      if (!((d.topicVal >> t) & 1)) continue;
+      nCand += __popcll(Uw[j] & ~Sw[j]);
+    }
+    const int candIncl = wave_incl_sum(nCand);
+    const int nAll = wave_last(candIncl);
+    if (d.valQueue > 0 && nAll > d.valQueue) {
+      // keys ff << 56 | mid, ranked by counting (nAll is at most the young slots)
+      int pos = candIncl - nCand;
+#pragma unroll
+      for (int j = 0; j < WPL; ++j) {
+        const int w = lane + 64 * j;
+        const int t = (int)__umulhi((unsigned)(w * 64), d.stMagic);
+        if (!((d.topicVal >> t) & 1)) continue;
+        uint64_t y = Uw[j] & ~Sw[j];
+        while (y) {
+          const int b = __ffsll((long long)y) - 1;
+          y &= y - 1;
+          const int slot = w * 64 + b;
+          sKey[pos++] = ((uint64_t)sFirst[fidx(rkw[j], b)] << 56) | (uint64_t)d.slotMid[slot];
+        }
+      }
+      __syncthreads();
+      pos = candIncl - nCand;
+#pragma unroll
+      for (int j = 0; j < WPL; ++j) {
+        const int w = lane + 64 * j;
+        const int t = (int)__umulhi((unsigned)(w * 64), d.stMagic);
+        if (!((d.topicVal >> t) & 1)) continue;
+        uint64_t y = Uw[j] & ~Sw[j];
+        while (y) {
+          const int b = __ffsll((long long)y) - 1;
+          y &= y - 1;
+          const uint64_t key = sKey[pos++];
+          int rank = 0;
+          for (int q = 0; q < nAll; ++q) rank += sKey[q] < key ? 1 : 0;
+          if (rank >= d.valQueue) atomicOr((unsigned long long*)&sDrop[rkw[j]], 1ull << b);
+        }
+      }
+      anyDrop = true;
+      __syncthreads();
+    }
+    nValidated = nAll < d.valQueue || d.valQueue == 0 ? nAll : d.valQueue;
+  }
 #pragma unroll
   for (int j = 0; j < WPL; ++j) {
     const int w = lane + 64 * j;
     Uw[j] &= ~Sw[j];
+    if constexpr (ADV) {
+      if (Uw[j]) {
+        if (anyDrop) Uw[j] &= ~sDrop[rkw[j]];
+        const int t = (int)__umulhi((unsigned)(w * 64), d.stMagic);
+        if ((d.topicVal >> t) & 1) {
+          // verdicts: REJECT / IGNORE are seen but not delivered
+          uint64_t y = Uw[j];
+          while (y) {
+            const int b = __ffsll((long long)y) - 1;
+            y &= y - 1;
+            const int k = d.slotKind[w * 64 + b];
+            if (k == GS_MSG_REJECT || k == GS_MSG_IGNORE) Xw[j] |= 1ull << b;
+          }
+        }
+      }
+    }
     if (Uw[j]) {
       Ow[j] = d.oldm[w];
       if (d.router == 2) Hw[j] = d.hist[((int64_t)head * d.N + v) * W + w];
@@ -748,7 +901,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   if (scoring) {
 #pragma unroll
     for (int j = 0; j < WPL; ++j) {
-      uint64_t y = Uw[j];
+      uint64_t y = Uw[j] & ~Xw[j];
       const int t = (int)__umulhi((unsigned)((lane + 64 * j) * 64), d.stMagic);
       while (y) {
         const int b = __ffsll((long long)y) - 1;
@@ -759,6 +912,91 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
       }
     }
   }
+  if constexpr (ADV) {
+    // per first deliverer: valid / rejected / ignored first deliveries (gater
+    // DeliverMessage / RejectMessage, peer_gater.go:397-432), REJECT traces
+#pragma unroll
+    for (int j = 0; j < WPL; ++j) {
+      uint64_t y = Uw[j];
+      const int w = lane + 64 * j;
+      while (y) {
+        const int b = __ffsll((long long)y) - 1;
+        y &= y - 1;
+        const int ff = sFirst[fidx(rkw[j], b)];
+        const bool x = (Xw[j] >> b) & 1;
+        const int slot = w * 64 + b;
+        const int k = x ? d.slotKind[slot] : GS_MSG_VALID;
+        atomicAdd(&sPer[(k == GS_MSG_VALID ? 1 : k == GS_MSG_REJECT ? 2 : 3) * 64 + ff], 1u);
+        if (x) {
+          ++nRejected;
+          if (trv)  // validation.go:333 / :351
+            trace_emit(d, h, GS_TRACE_REJECT_MESSAGE, v, d.col[base + ff], (int)__umulhi((unsigned)slot, d.stMagic),
+                       d.slotMid[slot], 2, k == GS_MSG_REJECT ? GS_REJECT_VALIDATION_FAILED : GS_REJECT_VALIDATION_IGNORED);
+        }
+      }
+    }
+    if (anyDrop) {
+      // ---- second walk: every copy of a dropped message is RejectValidation-
+      // QueueFull: neither a delivery nor a duplicate (its counts leave the
+      // tables), the gater's throttle, and it fulfils promises (gossip_tracer.go:133)
+      auto drop = [&](int i, int slot, bool payloadRpc) {
+        const int rk = sRk[slot >> 6];
+        if (rk == 0xFFFF || !((sDrop[rk] >> (slot & 63)) & 1)) return;
+        if (payloadRpc && gated(i, slot)) return;
+        const int t = (int)__umulhi((unsigned)slot, d.stMagic);
+        const int kind = kindOf(slot, t);
+        atomicSub(&sPer[i], 1u);
+        if (kind == GS_MSG_REJECT) atomicSub(&sInv[i * T + t], 1u);
+        if (kind == GS_MSG_VALID) {
+          if (NARROW) {
+            const int pl = i * T + t;
+            atomicSub(&scnt[pl >> 1], 1u << (16 * (pl & 1)));
+          } else {
+            atomicSub(&scnt[i * T + t], 1u);
+          }
+        }
+        ++nThrottledCopies;
+        --nCopies;
+        if (trv)  // validation.go:240
+          trace_emit(d, h, GS_TRACE_REJECT_MESSAGE, v, d.col[base + i], t, d.slotMid[slot], 2, GS_REJECT_QUEUE_FULL);
+      };
+      walk([&](int i, int slot) { drop(i, slot, true); }, false);
+      if (!gray && !ctlGated)
+        for (int k = 0; k < irN; ++k) drop(lane, d.pool[prv][irOff + k], false);
+      __syncthreads();
+    }
+    if (scoring && (anyDrop || throttled)) {
+      // promises: a dropped message fulfils its promises, a throttled peer
+      // loses its own (gossip_tracer.go:119-126, 163-181); lane = table entry
+      const int n = d.promN[v];
+      if (n > 0) {
+        const int64_t ti = (int64_t)v * GS_TABLE + lane;
+        int64_t pm = -1, pe = 0;
+        int ps = 0, pg = 0;
+        bool live = lane < n;
+        if (live) {
+          pm = d.promMid[ti];
+          pe = d.promExp[ti];
+          ps = d.promSlot[ti];
+          pg = d.promEdge[ti];
+          if ((throttled >> pg) & 1) live = false;
+          const int rk = sRk[ps >> 6];
+          if (anyDrop && rk != 0xFFFF && ((sDrop[rk] >> (ps & 63)) & 1)) live = false;
+        }
+        const unsigned long long lm = __ballot(live);
+        const int pos = __popcll(lm & ((1ull << lane) - 1));
+        __syncthreads();
+        if (live) {
+          const int64_t to = (int64_t)v * GS_TABLE + pos;
+          d.promMid[to] = pm;
+          d.promExp[to] = pe;
+          d.promSlot[to] = ps;
+          d.promEdge[to] = (uint8_t)pg;
+        }
+        if (lane == 0) d.promN[v] = __popcll(lm);
+      }
+    }
+  }
   __syncthreads();
   GS_STAMP(3);
   // ---- pass 3 (lane = in-edge): fmd += fresh, mmd += fresh + creditable
@@ -766,17 +1004,6 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   // scored topic is the edge's mesh bit (tracer.Graft / tracer.Prune accompany
   // every mesh change).  Batches of 8 topics, the next batch's loads issued
   // before this batch's stores.
-#ifdef GS_STAMPS
-  {
-    const long long tc = (long long)wave_sum_ll(nCopies);
-    const long long mc = accDel;  // delivery-drain cycles
-    if ((blockIdx.x & 1023) == 0 && lane == 0) {
-      d.stamps[(blockIdx.x >> 10) * 8 + 5] = tc;
-      d.stamps[(blockIdx.x >> 10) * 8 + 6] = accLd;
-      d.stamps[(blockIdx.x >> 10) * 8 + 7] = mc;
-    }
-  }
-#endif
   if (scoring) {
     // The counts go to the pending-delivery words dlt (eff_counters).  v's
     // in-edges own the contiguous pairs [base*T, (base+deg)*T), pair index
@@ -825,6 +1052,97 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     };
     if (nP > 16 * 64) rmw(std::integral_constant<int, 32>{});
     else rmw(std::integral_constant<int, 16>{});
+    if constexpr (ADV) {
+      // P4: every non-dropped copy of a rejected message is an invalid delivery
+      // of its sender (RejectMessage, then DuplicateMessage on the invalid
+      // record: score.go:766-783, 808-810), +1 steps, uncapped
+      for (int pl = lane; pl < nP; pl += 64) {
+        const int t = pl % T;
+        const uint32_t n = ((scoredT >> t) & 1) ? sInv[pl] : 0u;
+        if (!n) continue;
+        double x = d.imd[base * T + pl];
+        for (uint32_t k = 0; k < n; ++k) x += 1.0;
+        d.imd[base * T + pl] = x;
+        d.sdirty[base + pl / T] = 1;  // a score-lowering change
+      }
+    }
+  }
+  if constexpr (ADV) {
+    __syncthreads();
+    if (d.gater) {
+      // peerGater counters (peer_gater.go:390-440): per IP group (+1 steps)
+      // and per node; lane = in-edge, its group's stats edge gets the sums
+      const int cp = valid ? (int)sPer[lane] : 0;
+      const int fv = valid ? (int)sPer[64 + lane] : 0, fr = valid ? (int)sPer[128 + lane] : 0,
+                fi = valid ? (int)sPer[192 + lane] : 0;
+      const int dup = cp - fv - fr - fi;
+      const int g = valid ? d.gGrp[base + lane] : 0;
+      __syncthreads();
+      for (int k = lane; k < 4 * 64; k += 64) sPer[k] = 0;
+      __syncthreads();
+      if (valid) {
+        if (fv) atomicAdd(&sPer[g], (uint32_t)fv);
+        if (dup) atomicAdd(&sPer[64 + g], (uint32_t)dup);
+        if (fi) atomicAdd(&sPer[128 + g], (uint32_t)fi);
+        if (fr) atomicAdd(&sPer[192 + g], (uint32_t)fr);
+      }
+      __syncthreads();
+      if (valid && g == lane) {
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t n = sPer[k * 64 + lane];
+          if (!n) continue;
+          double x = d.gSt[k * d.E + base + lane];
+          for (uint32_t c = 0; c < n; ++c) x += 1.0;
+          d.gSt[k * d.E + base + lane] = x;
+        }
+      }
+      const long long thc = (long long)wave_sum_ll(nThrottledCopies);
+      if (lane == 0) {
+        if (nValidated) {
+          double x = d.gValidate[v];
+          for (long long c = 0; c < nValidated; ++c) x += 1.0;
+          d.gValidate[v] = x;
+        }
+        if (thc) {
+          double x = d.gThrottle[v];
+          for (long long c = 0; c < thc; ++c) x += 1.0;
+          d.gThrottle[v] = x;
+          d.gLast[v] = h * d.hop_ns;
+        }
+      }
+    }
+    if (d.cSpam[cur] != nullptr && valid && !gray && behaves(d, v, GS_BEHAVE_IWANT_SPAM)) {
+      // IWANT spam (gossipsub_spam_test.go:113-128): one request per message
+      // received from this sender (its accepted copies), in an extra RPC
+      auto each = [&](auto&& fn) {
+        const uint32_t* L = d.fl[prv] + (int64_t)u * FC;
+        for (int k = 0; k < Ln; ++k) {
+          const uint32_t ent = L[k];
+          const int slot = (int)(ent & 0xFFFF), tag = (int)(ent >> 16);
+          const int t = (int)__umulhi((unsigned)slot, d.stMagic);
+          bool sent = tag == 255 ? ((pub >> t) & 1) : ((relay >> t) & 1);
+          sent = sent && tag != jr;
+          if (sent && authV && d.slotSrc[slot] == v) sent = false;
+          if (sent && !gated(lane, slot)) fn(slot);
+        }
+        if (!ctlGated)
+          for (int k = 0; k < irN; ++k) fn(d.pool[prv][irOff + k]);
+      };
+      int n = 0;
+      each([&](int) { ++n; });
+      if (n) {
+        const unsigned long long off = atomicAdd(&d.poolCnt[cur], (unsigned long long)n);
+        if ((int64_t)(off + n) > d.poolCap) {
+          set_err(d, E_POOL);
+        } else {
+          int p = (int)off;
+          each([&](int slot) { d.pool[cur][p++] = slot; });
+          d.cSpam[cur][base + lane] = ((int64_t)off << 24) | (int64_t)n;
+          d.cPre[cur][base + lane] = (uint8_t)(d.cPre[cur][base + lane] + 1);
+          ctr_add(d, C_IWANT_SENT, (unsigned long long)n);
+        }
+      }
+    }
   }
   // ---- pass 2b: the stores of the first deliveries (after pass 3's loads,
   // which would otherwise wait for them)
@@ -833,16 +1151,17 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   for (int j = 0; j < WPL; ++j) {
     const int w = lane + 64 * j;
     const uint64_t U = Uw[j];
-    const int k = __popcll(U);
+    const uint64_t Ud = U & ~Xw[j];  // delivered (valid) fresh messages
+    const int k = __popcll(Ud);
     const int incl = wave_incl_sum(k);
     int rank = running + incl - k;
     running += wave_last(incl);
     if (U) {
       if ((U & Ow[j]) || !wm_has(amW, w)) set_err(d, E_LATE);
       d.seen[(int64_t)v * W + w] = Sw[j] | U;
-      if (d.router == 2) d.hist[((int64_t)head * d.N + v) * W + w] = Hw[j] | U;
+      if (d.router == 2 && Ud) d.hist[((int64_t)head * d.N + v) * W + w] = Hw[j] | Ud;
       nDeliv += k;
-      uint64_t y = U;
+      uint64_t y = Ud;
       while (y) {
         const int b = __ffsll((long long)y) - 1;
         y &= y - 1;
@@ -851,8 +1170,10 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
         if (trv)  // pubsub.go:1057, ReceivedFrom = the first deliverer
           trace_emit(d, h, GS_TRACE_DELIVER_MESSAGE, v, d.col[base + ff], (int)__umulhi((unsigned)slot, d.stMagic),
                      d.slotMid[slot], 2);
-        if (rank < FC) Lv[rank] = (uint32_t)slot | ((uint32_t)ff << 16);
-        else set_err(d, E_FCAP);
+        if (!behaves(d, v, GS_BEHAVE_NO_FORWARD)) {  // a squatter relays nothing
+          if (rank < FC) Lv[rank] = (uint32_t)slot | ((uint32_t)ff << 16);
+          else set_err(d, E_FCAP);
+        }
         ++rank;
         if (d.needAge || d.record) {
           const int64_t a = h - d.slotPubHop[slot];
@@ -862,11 +1183,11 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
       }
     }
     if (d.router == 1) {  // randomsub: targets of every message first delivered here
-      unsigned long long lanesWith = __ballot(U != 0);
+      unsigned long long lanesWith = __ballot(Ud != 0);
       while (lanesWith) {
         const int src = __ffsll((long long)lanesWith) - 1;
         lanesWith &= lanesWith - 1;
-        uint64_t y = lane_get64(U, src);
+        uint64_t y = lane_get64(Ud, src);
         const int wsrc = src + 64 * j;
         const int rks = lane_get(rkw[j], src);
         while (y) {
@@ -878,14 +1199,26 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     }
   }
   GS_STAMP(4);
-  if (lane == 0) d.fln[cur][v] = running < FC ? running : FC;
+  if (lane == 0) d.fln[cur][v] = behaves(d, v, GS_BEHAVE_NO_FORWARD) ? 0 : (running < FC ? running : FC);
   const long long deliv = (long long)wave_sum_ll(nDeliv);
   const unsigned long long copies = wave_sum_ll(nCopies), s2 = wave_sum_ll(nSent), s3 = wave_sum_ll(nGray);
   if (lane == 0) {
     if (deliv) ctr_add(d, C_DELIVERIES, (unsigned long long)deliv);
-    if (copies - deliv) ctr_add(d, C_DUPLICATES, copies - deliv);
     if (s2) ctr_add(d, C_TRANSMISSIONS, s2);
     if (s3) ctr_add(d, C_GRAYLISTED, s3);
+  }
+  if constexpr (ADV) {
+    const unsigned long long rej = wave_sum_ll(nRejected), thc = wave_sum_ll(nThrottledCopies);
+    const unsigned long long gc = wave_sum_ll(nGatedCopies);
+    if (lane == 0) {
+      const unsigned long long dups = copies - (unsigned long long)deliv - rej;
+      if (dups) ctr_add(d, C_DUPLICATES, dups);
+      if (rej) ctr_add(d, C_REJECTED, rej);
+      if (thc) ctr_add(d, C_THROTTLED, thc);
+      if (gc) ctr_add(d, C_GATED, gc);
+    }
+  } else {
+    if (lane == 0 && copies - deliv) ctr_add(d, C_DUPLICATES, copies - deliv);
   }
 }
 
@@ -923,8 +1256,21 @@ __global__ void k_publish(Dev d, int b, int n, int64_t h, int cur, int head) {
   d.slotSrc[slot] = src;
   d.slotPubHop[slot] = h;
   d.slotMid[slot] = d.mId[b + i];
+  const uint8_t kind = d.mKind[b + i];
+  d.slotKind[slot] = kind;
   if (src < d.n0 || src >= d.n1) return;
   atomicAdd(&d.nAuth[src], 1);
+  if (kind == GS_MSG_PHANTOM) {
+    // an advertised-only id: in the author's seen set and mcache (emitGossip
+    // lists it), never sent or traced (IHAVE spam, gossipsub_spam_test.go:196-203)
+    const int w = slot >> 6;
+    const unsigned long long bit = 1ull << (slot & 63);
+    atomicOr((unsigned long long*)&d.seen[(int64_t)src * d.W + w], bit);
+    if (d.router == 2) atomicOr((unsigned long long*)&d.hist[((int64_t)head * d.N + src) * d.W + w], bit);
+    if (d.needAge) d.age[(int64_t)src * d.S + slot] = 0;
+    if (d.record) d.ffrom[(int64_t)src * d.S + slot] = 255;
+    return;
+  }
   if (is_traced(d, src)) {  // validation.go:217, then pubsub.go:1057 with ReceivedFrom = self
     trace_emit(d, h, GS_TRACE_PUBLISH_MESSAGE, src, -1, d.mTopic[b + i], d.mId[b + i], 1);
     trace_emit(d, h, GS_TRACE_DELIVER_MESSAGE, src, src, d.mTopic[b + i], d.mId[b + i], 1);
@@ -952,7 +1298,7 @@ __global__ void k_publist(Dev d, int b, int n, int cur) {
   uint32_t* L = d.fl[cur] + (int64_t)src * d.FC;
   int len = d.fln[cur][src];
   for (int j = i; j < n; ++j) {
-    if (d.mSrc[b + j] != src) continue;
+    if (d.mSrc[b + j] != src || d.mKind[b + j] == GS_MSG_PHANTOM) continue;  // phantoms are never sent
     const uint32_t slot = (uint32_t)d.mSlot[b + j];
     if (len >= d.FC) {
       set_err(d, E_FCAP);
@@ -980,4 +1326,26 @@ __global__ __launch_bounds__(64) void k_publish_rs(Dev d, int b) {
   const int p = lane < deg ? d.col[base + lane] : -1;
   const uint64_t subp = p >= 0 ? d.sub[p] : 0;
   rs_select(d, u, deg, p, subp, slot, 255);
+}
+
+// ---------------------------------------------------------------- peer gater decay
+// peerGater.decayStats (peer_gater.go:219-259) every gater DecayInterval: the
+// node counters (thread per node) and the per-IP stats held on group edges
+// (thread per edge).  Every peer stays connected (static graph), so no stats
+// object expires.
+__device__ __forceinline__ double gdecay(double x, double f, double z) {
+  x *= f;
+  return x < z ? 0.0 : x;
+}
+__global__ void k_gater_decay(Dev d) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < d.n1 - d.n0) {
+    const int v = d.n0 + (int)i;
+    d.gValidate[v] = gdecay(d.gValidate[v], d.gGlobalDecay, d.gDecayToZero);
+    d.gThrottle[v] = gdecay(d.gThrottle[v], d.gGlobalDecay, d.gDecayToZero);
+  }
+  const int64_t e = d.e0 + i;
+  if (e >= d.e1) return;
+  if (d.rowptr[d.esrc[e]] + d.gGrp[e] != e) return;  // not a group's stats edge
+  for (int k = 0; k < 4; ++k) d.gSt[k * d.E + e] = gdecay(d.gSt[k * d.E + e], d.gSourceDecay, d.gDecayToZero);
 }

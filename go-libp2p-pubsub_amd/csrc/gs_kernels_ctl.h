@@ -160,7 +160,7 @@ __device__ __forceinline__ int lane_prefix(int x, int* total) {
 // Id lists (IWANT requests / responses) are sets: their order in the arena is
 // irrelevant to every reader.
 template <int WPL>
-__global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, int cur, int head) {
+__global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, int cur, int head, int cutMode) {
   __shared__ uint64_t scache[64 * WPL];  // v's mcache windows (handleIWant, step 2)
   uint64_t* const sseen = scache;        // then v's seen row (handleIHave, step 3)
   // step 2's peertx hash; the step-3 arrays below live in the same LDS once
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
   const unsigned long long cmask = __ballot(ctl);
   if (!cmask) return;
   uint64_t gJoin = 0, gHb = 0, pRep = 0, pHb = 0, ihaveT = 0, meshE = 0;
-  int64_t iwRec = -1;
+  int64_t iwRec = -1, spRec = -1;
   int ph = 0, ia = 0, u = 0;
   double sc = 0.0;
   bool gl = false;
@@ -213,6 +213,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     pHb = d.cPruneHb[prv][r];
     ihaveT = d.cIhave[prv][r];
     iwRec = d.cIwant[prv][r];
+    if (d.cSpam[prv] != nullptr) spRec = d.cSpam[prv][r];  // IWANT spam RPC (an extra reply-group RPC)
     ph = d.peerhave[e];
     ia = d.iasked[e];
     u = d.col[e];
@@ -231,7 +232,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
   // ---- step 1: order-dependent control, senders ascending.  Only GRAFTs and
   // PRUNEs depend on the order (the running mesh size, backoff, the live
   // score); a sender whose RPCs carry neither is handled in its own lane.
-  bool gateIWant = false, gateIHave = false, prunesHb = false;
+  bool gateIWant = false, gateIHave = false, prunesHb = false, gateSpam = false;
   uint64_t pruneOut = 0;
   int nRep1 = 0;
   long long cPrunes = 0, cGray = 0;
@@ -243,6 +244,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
       const bool gossipOK = sc >= d.gossipThr;
       if (gossipOK) ph += npre;
       gateIWant = gossipOK && iwRec >= 0;  // handleIWant (gossipsub.go:674-711): step 2
+      gateSpam = gossipOK && spRec >= 0;
     }
     if (hb && sc >= d.gossipThr) {
       ph++;
@@ -260,6 +262,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
       const uint64_t gJoin_i = lane_get64(gJoin, i), gHb_i = lane_get64(gHb, i);
       const uint64_t pRep_i = lane_get64(pRep, i), pHb_i = lane_get64(pHb, i), ihaveT_i = lane_get64(ihaveT, i);
       const int64_t iwRec_i = (int64_t)lane_get64((uint64_t)iwRec, i);
+      const int64_t spRec_i = (int64_t)lane_get64((uint64_t)spRec, i);
       int ph_i = lane_get(ph, i);
       const int ia_i = lane_get(ia, i);
       double sc_i = lane_getf(sc, i);
@@ -289,13 +292,14 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
         }
       }
       // (2) reply RPCs: IWANT requests and PRUNEs answering our own control
-      bool gIW = false;
+      bool gIW = false, gSP = false;
       const int nRep = npre_i - __popcll(gJoin_i);
       if (nRep > 0) {
         fresh();
         const bool gossipOK = sc_i >= d.gossipThr;
         if (gossipOK) ph_i += nRep;
         gIW = gossipOK && iwRec_i >= 0;  // handleIWant (gossipsub.go:674-711): step 2
+        gSP = gossipOK && spRec_i >= 0;
         prune_topics(d, ei, v, pRep_i, now, meshcnt, mE, dirty);
       }
       // (3) heartbeat RPC: IHAVE (step 3), GRAFT, PRUNE
@@ -325,6 +329,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
         pruneOut = pOut;
         nRep1 = nR;
         gateIWant = gIW;
+        gateSpam = gSP;
         gateIHave = gIH;
         prunesHb = prunes != 0;
       }
@@ -333,22 +338,34 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
   }
 
   GS_STAMPB(1);
-  // ---- step 2: handleIWant — serve cached messages at most GossipRetransmission times per peer
+  const bool silent = behaves(d, v, GS_BEHAVE_NO_FORWARD);  // a squatter serves nothing, sends nothing
+  if (silent) gateIWant = gateSpam = false;
+  // ---- step 2: handleIWant — serve cached messages at most GossipRetransmission
+  // times per peer; the IHAVE-reply list and the IWANT-spam list of a sender
+  // are two RPCs (two replies), served from one peertx table
   int64_t respRec = -1;
   long long cServed = 0;
-  if (__ballot(gateIWant)) {
+  int nSrv = 0;  // reply RPCs carrying served messages to this sender
+  if (__ballot(gateIWant || gateSpam)) {
+    __shared__ int sSpOff[64], sSpN[64], sItI[64], sCntS[64];
     for (int w = lane; w < W; w += 64) {
       uint64_t x = 0;
       for (int k = 0; k < d.HL; ++k) x |= d.hist[((int64_t)((head + k) % d.R) * d.N + v) * W + w];
       scache[w] = x;
     }
     for (int k = lane; k < GS_PTXH; k += 64) sH[k] = 0u;
-    const int n = gateIWant ? (int)(iwRec & 0xFFFFFF) : 0;
+    const int nI = gateIWant ? (int)(iwRec & 0xFFFFFF) : 0;
+    const int nS = gateSpam ? (int)(spRec & 0xFFFFFF) : 0;
+    const int itI = (nI + 15) >> 4, itS = (nS + 15) >> 4;
     int totalItems;
-    sIt[lane] = lane_prefix((n + 15) >> 4, &totalItems);
+    sIt[lane] = lane_prefix(itI + itS, &totalItems);
     sReqOff[lane] = gateIWant ? (int)(iwRec >> 24) : 0;
-    sReqN[lane] = n;
+    sReqN[lane] = nI;
+    sSpOff[lane] = gateSpam ? (int)(spRec >> 24) : 0;
+    sSpN[lane] = nS;
+    sItI[lane] = itI;
     sCnt[lane] = 0;
+    sCntS[lane] = 0;
     sCur[lane] = 0;
     __syncthreads();
     const int ptxN = d.ptxN[v];
@@ -359,24 +376,43 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
       while (atomicCAS(&sH[hsl], 0u, e32) != 0u) hsl = (hsl + 1) & (GS_PTXH - 1);
     }
     __syncthreads();
+    // item b: 16 ids of the IHAVE-reply list (k < itI) or of the spam list
+    auto item = [&](int b, int& i, int& off, int& cnt, bool& sp) {
+      int k;
+      i = item_sender(sIt, b, k);
+      sp = k >= sItI[i];
+      if (sp) {
+        k -= sItI[i];
+        off = sSpOff[i] + 16 * k;
+        cnt = min(16, sSpN[i] - 16 * k);
+      } else {
+        off = sReqOff[i] + 16 * k;
+        cnt = min(16, sReqN[i] - 16 * k);
+      }
+    };
+    // mcache.GetForPeer finds the id (mcache.go:66-80); a phantom id is never served
+    auto cached = [&](int slot) {
+      return ((scache[slot >> 6] >> (slot & 63)) & 1) && d.slotKind[slot] != GS_MSG_PHANTOM;
+    };
     // pass a: increments and per-sender served counts
     for (int b = lane; b < totalItems; b += 64) {
-      int k;
-      const int i = item_sender(sIt, b, k);
-      const int off = sReqOff[i] + 16 * k, cnt = min(16, sReqN[i] - 16 * k);
+      int i, off, cnt;
+      bool sp;
+      item(b, i, off, cnt, sp);
       int c = 0;
       for (int q = 0; q < cnt; ++q) {
         const int slot = d.pool[prv][off + q];
-        if (!((scache[slot >> 6] >> (slot & 63)) & 1)) continue;  // not in the cache
+        if (!cached(slot)) continue;
         const uint64_t key = ((uint64_t)(uint32_t)slot << 32) | ((uint64_t)i << 8);
         const int count = ptx_incr(d, sH, key);
         if (count >= 1 && count <= d.GR) ++c;
       }
-      if (c) atomicAdd(&sCnt[i], c);
+      if (c) atomicAdd(sp ? &sCntS[i] : &sCnt[i], c);
     }
     __syncthreads();
     int totalServed;
-    const int myServed = sCnt[lane];
+    const int myServed = sCnt[lane] + sCntS[lane];
+    nSrv = (sCnt[lane] > 0 ? 1 : 0) + (sCntS[lane] > 0 ? 1 : 0);
     const int myOff = lane_prefix(myServed, &totalServed);
     if (lane == 0 && totalServed) sBase = atomicAdd(&d.poolCnt[cur], (unsigned long long)totalServed);
     __syncthreads();
@@ -384,19 +420,21 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
       const unsigned long long poolBase = sBase;
       if (poolBase + totalServed > (unsigned long long)d.poolCap) {
         if (lane == 0) set_err(d, E_POOL);
+        nSrv = 0;
       } else {
         sOut[lane] = (int)poolBase + myOff;
         if (myServed) respRec = ((int64_t)(poolBase + myOff) << 24) | (int64_t)myServed;
         cServed = totalServed;
         __syncthreads();
-        // pass b: write the served ids (the counts are final now)
+        // pass b: write the served ids (the counts are final now; an id is in
+        // at most one of a sender's two lists)
         for (int b = lane; b < totalItems; b += 64) {
-          int k;
-          const int i = item_sender(sIt, b, k);
-          const int off = sReqOff[i] + 16 * k, cnt = min(16, sReqN[i] - 16 * k);
+          int i, off, cnt;
+          bool sp;
+          item(b, i, off, cnt, sp);
           for (int q = 0; q < cnt; ++q) {
             const int slot = d.pool[prv][off + q];
-            if (!((scache[slot >> 6] >> (slot & 63)) & 1)) continue;
+            if (!cached(slot)) continue;
             const uint64_t key = ((uint64_t)(uint32_t)slot << 32) | ((uint64_t)i << 8);
             const int count = ptx_count(sH, key);
             if (count >= 1 && count <= d.GR) d.pool[cur][sOut[i] + atomicAdd(&sCur[i], 1)] = slot;
@@ -444,8 +482,80 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     // the sender minus v's seen row, four words loaded at once.
     const int nHas = (totalItems + 31) >> 5;
     for (int k = lane; k < nHas; k += 64) sHas[k] = 0u;
-    __syncthreads();
-    auto wants = [&](int uu, int t, auto&& fn) {
+    // ---- MaxIHaveLength cuts (cutMode: the host saw that a topic may hold
+    // more gossip ids than that).  Item cut: a sender with more than
+    // MaxIHaveLength ids of a topic advertised its own keyed subset to v
+    // (emitGossip, gossipsub.go:1702-1709: the MaxIHaveLength smallest
+    // (GS_SITE_EMIT_MIDS key, id) of its heartbeat hop h - 1).  Sender cut:
+    // more wants than MaxIHaveLength - iasked are cut to the smallest
+    // (GS_SITE_IWANT key, id) (handleIHave, :650-653).
+    extern __shared__ __attribute__((aligned(16))) uint32_t smemB[];
+    uint32_t* const cHist = smemB;                                  // [256] radix histogram
+    int* const cItem = (int*)(smemB + 256);                         // [GS_CUTS] cut items
+    unsigned long long* const cK = (unsigned long long*)(smemB + 256 + GS_CUTS);  // [GS_CUTS] threshold key
+    long long* const cM = (long long*)(cK + GS_CUTS);               // [GS_CUTS] threshold id
+    unsigned long long* const iK = (unsigned long long*)(cM + GS_CUTS);  // [64] sender cut key
+    long long* const iM = (long long*)(iK + 64);                   // [64] sender cut id
+    uint32_t* const cBits = (uint32_t*)(iM + 64);                   // [128] item is cut
+    int* const cN = (int*)(cBits + 128);
+    int nCut = 0;
+    if (cutMode) {
+      for (int k = lane; k < 128; k += 64) cBits[k] = 0u;
+      if (lane == 0) *cN = 0;
+      __syncthreads();
+      for (int b = lane; b < totalItems; b += 64) {
+        int k;
+        const int i = item_sender(sIt, b, k);
+        const int t = kth_bit(sTm[i], k);
+        const int uu = sNode[i];
+        int nm = 0;
+        for (int w = t * Wt; w < (t + 1) * Wt; ++w) nm += __popcll(d.gw[(int64_t)uu * W + w]);
+        if (nm > d.MaxIHaveLength) {
+          const int pos = atomicAdd(cN, 1);
+          if (pos < GS_CUTS) {
+            cItem[pos] = b;
+            atomicOr(&cBits[b >> 5], 1u << (b & 31));
+          } else {
+            set_err(d, E_TRUNCATE);
+          }
+        }
+      }
+      __syncthreads();
+      nCut = min(*cN, GS_CUTS);
+      for (int c = 0; c < nCut; ++c) {
+        const int b = cItem[c];
+        int k;
+        const int i = item_sender(sIt, b, k);
+        const int t = kth_bit(sTm[i], k);
+        const int uu = sNode[i];
+        // every gossip id of the sender's topic t, lane-strided over words
+        auto each = [&](auto&& fn) {
+          for (int w = t * Wt + lane; w < (t + 1) * Wt; w += 64) {
+            uint64_t y = d.gw[(int64_t)uu * W + w];
+            while (y) {
+              const int bb = __ffsll((long long)y) - 1;
+              y &= y - 1;
+              const int64_t mid = d.slotMid[(int64_t)w * 64 + bb];
+              fn(gs_key64(d.seed, GS_SITE_EMIT_MIDS, uu, v, (uint32_t)mid, (uint32_t)(h - 1)), mid);
+            }
+          }
+        };
+        unsigned long long K;
+        long long M;
+        select_kth(each, d.MaxIHaveLength, cHist, K, M);
+        if (lane == 0) {
+          cK[c] = K;
+          cM[c] = M;
+        }
+        __syncthreads();
+      }
+    }
+    // the advertised wants of item b: fn(w, want) per word with a want
+    auto wants = [&](int b, int uu, int t, auto&& fn) {
+      int ci = -1;
+      if (nCut && ((cBits[b >> 5] >> (b & 31)) & 1))
+        for (int c = 0; c < nCut; ++c)
+          if (cItem[c] == b) ci = c;
       const int wEnd = (t + 1) * Wt;
       for (int w0 = t * Wt; w0 < wEnd; w0 += 4) {
         uint64_t g[4];
@@ -453,11 +563,25 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
         for (int q = 0; q < 4; ++q) g[q] = d.gw[(int64_t)uu * W + min(w0 + q, wEnd - 1)];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const uint64_t want = w0 + q < wEnd ? g[q] & ~sseen[w0 + q] : 0ull;
+          uint64_t want = w0 + q < wEnd ? g[q] & ~sseen[w0 + q] : 0ull;
+          if (want && ci >= 0) {
+            // keep the ids of the sender's subset for v
+            const unsigned long long K = cK[ci];
+            const long long M = cM[ci];
+            uint64_t y = want;
+            while (y) {
+              const int bb = __ffsll((long long)y) - 1;
+              y &= y - 1;
+              const int64_t mid = d.slotMid[(int64_t)(w0 + q) * 64 + bb];
+              const unsigned long long key = gs_key64(d.seed, GS_SITE_EMIT_MIDS, uu, v, (uint32_t)mid, (uint32_t)(h - 1));
+              if (key > K || (key == K && mid > M)) want &= ~(1ull << bb);
+            }
+          }
           if (want) fn(w0 + q, want);
         }
       }
     };
+    __syncthreads();
     // pass a: want counts and the per-sender smallest promise key; items with
     // a want are flagged for passes a2 / b
     for (int b = lane; b < totalItems; b += 64) {
@@ -467,7 +591,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
       const int uu = sNode[i];
       int c = 0;
       uint64_t bestKey = ~0ull;
-      wants(uu, t, [&](int w, uint64_t want) {
+      wants(b, uu, t, [&](int w, uint64_t want) {
         c += __popcll(want);
         uint64_t y = want;
         while (y) {
@@ -494,7 +618,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
       const int t = kth_bit(sTm[i], k);
       const int uu = sNode[i];
       const uint64_t best = sKey[i];
-      wants(uu, t, [&](int w, uint64_t want) {
+      wants(b, uu, t, [&](int w, uint64_t want) {
         uint64_t y = want;
         while (y) {
           const int bb = __ffsll((long long)y) - 1;
@@ -507,8 +631,57 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     }
     __syncthreads();
     GS_STAMPB(6);
+    // the sender cut: iask = MaxIHaveLength - iasked of the smallest keys
+    const int myWantAll = sCnt[lane];
+    const bool iaCut = gateIHave && myWantAll > 0 && myWantAll + ia > d.MaxIHaveLength;
+    const int myWant = iaCut ? d.MaxIHaveLength - ia : myWantAll;
+    if (cutMode) {
+      unsigned long long cm = __ballot(iaCut);
+      while (cm) {
+        const int i = __ffsll((long long)cm) - 1;
+        cm &= cm - 1;
+        const int uu = sNode[i];
+        const int kk = lane_get(myWant, i);
+        const int b0 = sIt[i];
+        const int nItems = __popcll(sTm[i]);
+        // every want of sender i over its items, lane-strided over words
+        auto each = [&](auto&& fn) {
+          for (int k = 0; k < nItems; ++k) {
+            const int t = kth_bit(sTm[i], k);
+            const int b = b0 + k;
+            int ci = -1;
+            if (nCut && ((cBits[b >> 5] >> (b & 31)) & 1))
+              for (int c = 0; c < nCut; ++c)
+                if (cItem[c] == b) ci = c;
+            for (int w = t * Wt + lane; w < (t + 1) * Wt; w += 64) {
+              uint64_t y = d.gw[(int64_t)uu * W + w] & ~sseen[w];
+              while (y) {
+                const int bb = __ffsll((long long)y) - 1;
+                y &= y - 1;
+                const int64_t mid = d.slotMid[(int64_t)w * 64 + bb];
+                if (ci >= 0) {
+                  const unsigned long long ke = gs_key64(d.seed, GS_SITE_EMIT_MIDS, uu, v, (uint32_t)mid, (uint32_t)(h - 1));
+                  if (ke > cK[ci] || (ke == cK[ci] && mid > cM[ci])) continue;
+                }
+                fn(gs_key64(d.seed, GS_SITE_IWANT, v, uu, (uint32_t)mid, (uint32_t)h), mid);
+              }
+            }
+          }
+        };
+        unsigned long long K;
+        long long M;
+        select_kth(each, kk, cHist, K, M);
+        if (lane == 0) {
+          iK[i] = K;
+          iM[i] = M;
+        }
+        __syncthreads();
+      }
+    } else if (__ballot(iaCut)) {
+      if (lane == 0) set_err(d, E_TRUNCATE);  // the host ruled the cut out
+    }
+    const uint64_t cutSenders = __ballot(iaCut);
     int totalWant;
-    const int myWant = sCnt[lane];
     const int myOff = lane_prefix(myWant, &totalWant);
     if (lane == 0 && totalWant) sBase = atomicAdd(&d.poolCnt[cur], (unsigned long long)totalWant);
     __syncthreads();
@@ -527,26 +700,27 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
           const int t = kth_bit(sTm[i], k);
           const int uu = sNode[i];
           const long long bestMid = sMid[i];
-          wants(uu, t, [&](int w, uint64_t want) {
+          const bool cutI = (cutSenders >> i) & 1;
+          wants(b, uu, t, [&](int w, uint64_t want) {
             uint64_t y = want;
             while (y) {
               const int bb = __ffsll((long long)y) - 1;
               y &= y - 1;
               const int slot = w * 64 + bb;
+              const int64_t mid = d.slotMid[slot];
+              if (cutI) {
+                const unsigned long long key = gs_key64(d.seed, GS_SITE_IWANT, v, uu, (uint32_t)mid, (uint32_t)h);
+                if (key > iK[i] || (key == iK[i] && mid > iM[i])) continue;
+              }
               d.pool[cur][sOut[i] + atomicAdd(&sCur[i], 1)] = slot;
-              if (d.slotMid[slot] == bestMid) sSlot[i] = slot;
+              if (mid == bestMid) sSlot[i] = slot;
             }
           });
         }
         if (myWant) {
-          int iask = myWant;
-          if (iask + ia > d.MaxIHaveLength) {
-            iask = d.MaxIHaveLength - ia;
-            set_err(d, E_TRUNCATE);  // per-peer IWANT truncation is not built
-          }
           iwantRec = ((int64_t)(poolBase + myOff) << 24) | (int64_t)myWant;
-          ia += iask;
-          cIwantSent = iask;
+          ia += myWant;
+          cIwantSent = silent ? 0 : myWant;
           iwantAny = true;
         }
       }
@@ -609,19 +783,26 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     d.cIhave[prv][r] = 0;
     d.cIwant[prv][r] = -1;
     d.cIresp[prv][r] = -1;
+    if (d.cSpam[prv] != nullptr) {
+      d.cSpam[prv][r] = -1;
+      d.cNSrv[prv][r] = 0;
+    }
     if (!gl) {
       d.mesh[e] = meshE;
       d.peerhave[e] = ph;
       d.iasked[e] = ia;
-      const int nReplies = nRep1 + (respRec >= 0 ? 1 : 0) + ((iwantAny || prunesHb) ? 1 : 0);
-      if (nReplies) {
+      // one reply per control RPC that produced one (HandleRPC, gossipsub.go:602-607)
+      const int nReplies = nRep1 + nSrv + ((iwantAny || prunesHb) ? 1 : 0);
+      if (nReplies && !silent) {
         d.cPre[cur][e] = (uint8_t)(d.cPre[cur][e] + nReplies);
         d.cPruneReply[cur][e] |= pruneOut;
         if (iwantRec >= 0) d.cIwant[cur][e] = iwantRec;
         if (respRec >= 0) d.cIresp[cur][e] = respRec;
+        if (nSrv && d.cNSrv[cur] != nullptr) d.cNSrv[cur][e] = (uint8_t)nSrv;
       }
     }
   }
+  if (silent) cPrunes = 0;  // the PRUNE replies of a squatter are never sent
   if (lane == 0) {
     if (cPrunes) ctr_add(d, C_PRUNES, (unsigned long long)cPrunes);
     if (cIwantSent) ctr_add(d, C_IWANT_SENT, (unsigned long long)cIwantSent);
@@ -711,7 +892,11 @@ __device__ __forceinline__ uint64_t emit_gossip(const Dev& d, int v, int t, int6
                                                 int nm) {
   const int lane = lane_id();
   if (nm == 0) return 0;  // nm: message ids of topic t in the gossip windows
-  if (nm > d.MaxIHaveLength && lane == 0) set_err(d, E_TRUNCATE);
+  if (behaves(d, v, GS_BEHAVE_NO_FORWARD)) return 0;  // a squatter emits no gossip
+  // an IHAVE spammer advertises to every topic peer (mesh, direct, any score)
+  if (behaves(d, v, GS_BEHAVE_IHAVE_SPAM)) return valid && inTopic ? (1ull << t) : 0;
+  // more than MaxIHaveLength ids: each receiver's own keyed subset
+  // (gossipsub.go:1702-1709) is cut by the receiver in k_phase_b
   const bool base = valid && inTopic && !excl && !dir;
   // A graft never lowers a score (P1 is 0 at meshTime 0, the P3 deficit term
   // is switched off; weights validated w1 >= 0, w3 <= 0), so a cached score
@@ -804,13 +989,16 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
   bool dirtyUp = false;  // a GRAFT (never lowers it) changed it since Slive
   uint64_t tograft = 0, toprune = 0, ihave = 0;
   const uint32_t hw = (uint32_t)hop;
+  const bool graftSpam = behaves(d, v, GS_BEHAVE_GRAFT_SPAM);
+  uint64_t spamGraft = 0;  // GRAFTs without a mesh change (not traced as Graft)
   for (int t = 0; t < d.T; ++t) {
     if (!((joined >> t) & 1)) continue;
     const uint64_t bit = 1ull << t;
     const bool inTopic = valid && ((subv >> t) & 1);
     bool m = valid && (meshl & bit);
-    // drop all peers with negative score, without PX
-    if (m && S < 0) {
+    // drop all peers with negative score, without PX; a GRAFT spammer first
+    // leaves its whole mesh (gossipsub_spam_test.go:428-446)
+    if (m && (S < 0 || (graftSpam && ticks == 1))) {
       stats_prune(d, e, t);
       meshl &= ~bit;
       add_backoff(d, e, t, now, d.PruneBackoff);
@@ -941,6 +1129,12 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
         }
       }
     }
+    // a GRAFT spammer re-GRAFTs the topic peers it is in backoff with, leaving
+    // its own mesh as it is (gossipsub_spam_test.go:449-500)
+    if (graftSpam && ticks > 1 && inTopic && !m) {
+      const int64_t be = d.backoff[tix(d, t, e)];
+      if (be != 0 && be > now) spamGraft |= bit;
+    }
     ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, m, dir, Slive, dirty, dirtyUp, base, sterm,
                          lane_get(nmT, t));
   }
@@ -981,6 +1175,8 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
     for (uint64_t m = toprune; m; m &= m - 1) trace_emit(d, hop, GS_TRACE_PRUNE, v, vcol, __ffsll((long long)m) - 1, -1, 4);
     for (uint64_t m = tograft; m; m &= m - 1) trace_emit(d, hop, GS_TRACE_GRAFT, v, vcol, __ffsll((long long)m) - 1, -1, 4);
   }
+  tograft |= spamGraft;
+  if (behaves(d, v, GS_BEHAVE_NO_FORWARD)) tograft = toprune = ihave = 0;  // a squatter sends nothing
   if (valid) {
     d.mesh[e] = meshl;
     d.fanout[e] = fanl;
@@ -1034,7 +1230,13 @@ __global__ void k_read_deliv(Dev d, int slot, int64_t pubhop, int32_t* hop, int3
   const int v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= d.N) return;
   if (v < d.n0 || v >= d.n1) { hop[v] = -1; from[v] = -1; return; }  // another rank's node
-  const bool s = (d.seen[(int64_t)v * d.W + (slot >> 6)] >> (slot & 63)) & 1;
+  bool s = (d.seen[(int64_t)v * d.W + (slot >> 6)] >> (slot & 63)) & 1;
+  // a rejected / ignored message is seen but never delivered (the author's own
+  // publish is), a phantom id is never delivered at all
+  const int kind = d.slotKind[slot];
+  const int t = slot / d.St;
+  if (kind == GS_MSG_PHANTOM) s = false;
+  if ((kind == GS_MSG_REJECT || kind == GS_MSG_IGNORE) && ((d.topicVal >> t) & 1) && d.slotSrc[slot] != v) s = false;
   if (!s) { hop[v] = -1; from[v] = -1; return; }
   hop[v] = (int32_t)(pubhop + d.age[(int64_t)v * d.S + slot]);
   const uint8_t f = d.ffrom[(int64_t)v * d.S + slot];

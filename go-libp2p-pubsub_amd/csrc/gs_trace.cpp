@@ -78,6 +78,13 @@ struct Field {  // one field of a sub-message: bytes (base64 in JSON) or string
   bool isBytes;
 };
 
+// rejection reasons, tracer.go:27-38 (GS_REJECT_* order)
+const char* kReason[] = {"blacklisted peer", "blacklisted source", "missing signature", "unexpected signature",
+                         "unexpected auth info", "invalid signature", "validation queue full",
+                         "validation throttled", "validation failed", "validation ignored",
+                         "self originated message"};
+const int kNumReasons = 11;
+
 // pb.TraceEvent field number / JSON name of the sub-message of each type
 const int kSubField[13] = {4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
 const char* kSubName[13] = {"publishMessage", "rejectMessage", "duplicateMessage", "deliverMessage", "addPeer",
@@ -87,6 +94,13 @@ std::vector<Field> sub_fields(const gs_trace_event& e, const std::string& topic,
   switch (e.type) {
     case GS_TRACE_PUBLISH_MESSAGE:  // trace.proto PublishMessage {messageID=1, topic=2}
       return {{1, "messageID", msg_bytes(e.msg), true}, {2, "topic", topic, false}};
+    case GS_TRACE_REJECT_MESSAGE:  // {messageID=1, receivedFrom=2, reason=3, topic=4}
+      return {{1, "messageID", msg_bytes(e.msg), true}, {2, "receivedFrom", peer_bytes(e.peer), true},
+              {3, "reason", e.reason < kNumReasons ? kReason[e.reason] : "", false}, {4, "topic", topic, false}};
+    case GS_TRACE_REMOVE_PEER:  // {peerID=1}
+      return {{1, "peerID", peer_bytes(e.peer), true}};
+    case GS_TRACE_LEAVE:  // {topic=2} (pb/trace.proto:99-101)
+      return {{2, "topic", topic, false}};
     case GS_TRACE_DUPLICATE_MESSAGE:  // {messageID=1, receivedFrom=2, topic=3}
       return {{1, "messageID", msg_bytes(e.msg), true}, {2, "receivedFrom", peer_bytes(e.peer), true},
               {3, "topic", topic, false}};

@@ -606,7 +606,8 @@ void Node::emitGossip(int topic, const std::set<int>& exclude) {
   int target = sim->gp.Dlazy;
   int factor = (int)(sim->gp.GossipFactor * (double)peers.size());
   if (factor > target) target = factor;
-  if (spam || target > (int)peers.size()) {
+  if (spam) target = (int)peers.size();
+  if (target >= (int)peers.size()) {
     target = (int)peers.size();
   } else {
     std::vector<std::pair<uint64_t, int>> keyed;

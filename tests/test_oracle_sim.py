@@ -13,7 +13,9 @@ def test_scenario_runs_and_is_deterministic(oracle_path, name):
     b = scenarios.run(oracle_path, name)
     assert scenarios.compare(a, b) == []
     c = a["counters"]
-    assert c["published"] > 0 and c["deliveries"] > 0
+    assert c["hops"] > 0
+    if name not in ("spam_graft", "spam_ihave", "spam_ihave_2t", "spam_invalid"):  # no valid publishes there
+        assert c["published"] > 0 and c["deliveries"] > 0
 
 
 def test_dense_gossipsub_delivers_everything(oracle_path):
