@@ -168,6 +168,19 @@ struct gs_engine {
     return (t - gp.HeartbeatInitialDelay) % gp.HeartbeatInterval == 0;
   }
   bool refreshDue(int64_t t) const { return scoring && t > 0 && t % sp.DecayInterval == 0; }
+  // Message-window policy: a message must be first delivered within maxAge
+  // hops of its publish (phase A tracks first deliverers for those "young"
+  // slots only), and its slot is recycled only after retireHops.  Honest
+  // runs deliver everything within a few hops (3 heartbeats is ample); with
+  // the adversarial model (validation drops, the gater, spam) messages can
+  // arrive much later through gossip, so the window then spans the gossip
+  // history twice over.
+  void setWindow() {
+    const bool adv = topicVal != 0 || gaterOn || behaveAll != 0;
+    maxAge = (adv ? gp.HistoryLength + gp.HistoryGossip + 3 : 3) * H;
+    retireHops = maxAge + (int64_t)(gp.HistoryLength + 2) * H;
+    if (cfg.router != GS_ROUTER_GOSSIPSUB) retireHops = maxAge + 2;
+  }
   int start();
   int stepOne();
   int uploadMessages();
@@ -691,7 +704,7 @@ int gs_engine::stepOne() {
     // instantiation: the honest path keeps its LDS budget and code
     const bool adv = topicVal != 0 || gaterOn || behaveAll != 0;
     size_t lds = (narrow ? 2 : 4) * nCnt + 16 * (size_t)nR + (size_t)nYp + (d.needAge ? 4 * nCnt : 0);
-    if (adv) lds += 4 * nCnt + 4 * 64 * 4 + 8 * 64 + 8 * (size_t)nR + (valQueue > 0 ? 8 * (size_t)nYp : 0);
+    if (adv) lds += 4 * nCnt + 4 * 64 * 4 + 8 * 64 + 8 * (size_t)nR;
     TIMED(this, GS_K_PHASE_A, launch_wpl(W, [&](auto w) {
             if (!nOwn) return;
             constexpr int WV = decltype(w)::value;
@@ -1104,11 +1117,7 @@ int gs_engine_create(const gs_config* cfg, const gs_gossipsub_params* gsp, const
   } else {
     g->R = 1;
   }
-  // message-window policy: a message must be first delivered within maxAge
-  // hops of its publish, and its slot is recycled only after retireHops
-  g->maxAge = 3 * g->H;
-  g->retireHops = g->maxAge + (int64_t)(g->gp.HistoryLength + 2) * g->H;
-  if (cfg->router != GS_ROUTER_GOSSIPSUB) g->retireHops = g->maxAge + 2;
+  g->setWindow();
   if (g->maxAge > 30000) { gs_set_error("heartbeat interval too long in hops"); return GS_EUNSUPPORTED; }
   if (g->scoring) {
     if (!psp || !topics || !topic_scored || !thr) {
@@ -1230,18 +1239,25 @@ int gs_publish_ex(gs_engine* g, int32_t n, const int32_t* src, const int32_t* to
 }
 
 int gs_set_validation(gs_engine* g, const uint8_t* topic_validator, int32_t queue_per_hop) {
-  if (g->started) { gs_set_error("validation must be set before the first step"); return GS_ESTATE; }
+  if (g->started || !g->mId.empty()) {
+    gs_set_error("validation must be set before the first publish");
+    return GS_ESTATE;
+  }
   if (queue_per_hop < 0) { gs_set_error("queue_per_hop must be >= 0"); return GS_EINVAL; }
   g->topicVal = 0;
   if (topic_validator)
     for (int t = 0; t < g->T; ++t)
       if (topic_validator[t]) g->topicVal |= 1ull << t;
   g->valQueue = queue_per_hop;
+  g->setWindow();
   return GS_OK;
 }
 
 int gs_set_behaviour(gs_engine* g, const uint8_t* behaviour) {
-  if (g->started) { gs_set_error("behaviours must be set before the first step"); return GS_ESTATE; }
+  if (g->started || !g->mId.empty()) {
+    gs_set_error("behaviours must be set before the first publish");
+    return GS_ESTATE;
+  }
   g->behaveH.clear();
   g->behaveAll = 0;
   if (behaviour) {
@@ -1253,6 +1269,7 @@ int gs_set_behaviour(gs_engine* g, const uint8_t* behaviour) {
       return GS_EINVAL;
     }
   }
+  g->setWindow();
   return GS_OK;
 }
 

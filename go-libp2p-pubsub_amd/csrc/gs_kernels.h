@@ -498,7 +498,6 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
                                                           // rejected / ignored first deliveries
   double* sGThr = (double*)(sPer + 4 * 64);               // [64] gater threshold per sender, < 0 = accept
   uint64_t* sDrop = (uint64_t*)(sGThr + 64);              // [nR] fresh messages dropped by a full queue
-  uint64_t* sKey = sDrop + nR;                            // [nY] queue order keys (ff << 56 | mid)
   __shared__ int sBlk[64];        // first list block of each sender
   __shared__ uint64_t sRelay[64], sPub[64];
   __shared__ int sSnd[64];        // sender node | jr << 24 | graylisted << 31
@@ -835,23 +834,26 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     const int candIncl = wave_incl_sum(nCand);
     const int nAll = wave_last(candIncl);
     if (d.valQueue > 0 && nAll > d.valQueue) {
-      // keys ff << 56 | mid, ranked by counting (nAll is at most the young slots)
-      int pos = candIncl - nCand;
+      // the valQueue-th smallest key ff << 56 | mid (radix select over the
+      // lanes' own fresh words; the walk queue's LDS is free now)
+      auto each = [&](auto&& fn) {
 #pragma unroll
-      for (int j = 0; j < WPL; ++j) {
-        const int w = lane + 64 * j;
-        const int t = (int)__umulhi((unsigned)(w * 64), d.stMagic);
-        if (!((d.topicVal >> t) & 1)) continue;
-        uint64_t y = Uw[j] & ~Sw[j];
-        while (y) {
-          const int b = __ffsll((long long)y) - 1;
-          y &= y - 1;
-          const int slot = w * 64 + b;
-          sKey[pos++] = ((uint64_t)sFirst[fidx(rkw[j], b)] << 56) | (uint64_t)d.slotMid[slot];
+        for (int j = 0; j < WPL; ++j) {
+          const int w = lane + 64 * j;
+          const int t = (int)__umulhi((unsigned)(w * 64), d.stMagic);
+          if (!((d.topicVal >> t) & 1)) continue;
+          uint64_t y = Uw[j] & ~Sw[j];
+          while (y) {
+            const int b = __ffsll((long long)y) - 1;
+            y &= y - 1;
+            const long long mid = d.slotMid[w * 64 + b];
+            fn(((unsigned long long)sFirst[fidx(rkw[j], b)] << 56) | (unsigned long long)mid, mid);
+          }
         }
-      }
-      __syncthreads();
-      pos = candIncl - nCand;
+      };
+      unsigned long long K;
+      long long M;
+      select_kth(each, d.valQueue, sQ, K, M);
 #pragma unroll
       for (int j = 0; j < WPL; ++j) {
         const int w = lane + 64 * j;
@@ -861,10 +863,9 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
         while (y) {
           const int b = __ffsll((long long)y) - 1;
           y &= y - 1;
-          const uint64_t key = sKey[pos++];
-          int rank = 0;
-          for (int q = 0; q < nAll; ++q) rank += sKey[q] < key ? 1 : 0;
-          if (rank >= d.valQueue) atomicOr((unsigned long long*)&sDrop[rkw[j]], 1ull << b);
+          const unsigned long long key =
+              ((unsigned long long)sFirst[fidx(rkw[j], b)] << 56) | (unsigned long long)d.slotMid[w * 64 + b];
+          if (key > K) atomicOr((unsigned long long*)&sDrop[rkw[j]], 1ull << b);
         }
       }
       anyDrop = true;
@@ -1021,7 +1022,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
       const int copies = NARROW ? (int)(c & 0xFF) : (int)(c & 0xFFFF);
       const int nf = NARROW ? (int)(c >> 8) : (int)(c >> 16);
       int credited = copies - nf;
-      if (d.needAge) credited -= (int)sUnc[pl];
+      if (d.needAge && ((scoredT >> t) & 1)) credited -= (int)sUnc[pl];  // unscored: no counts at all
       const uint32_t addM = ((sRelay[i] >> t) & 1) ? (uint32_t)(nf + credited) : 0u;
       if ((q & 0xFFFF) + nf > 0xFFFF || (q >> 16) + addM > 0xFFFF) set_err(d, E_DELTA);
       return q + (uint32_t)nf + (addM << 16);
