@@ -21,6 +21,9 @@
 #define GS_TABLE 64    // promise table entries per node (one per lane)
 #define GS_PTX 512     // IWANT-retransmission (mcache peertx) entries per node
 #define GS_CUTS 64     // IHAVE entries above MaxIHaveLength one node can cut per hop
+// phase B dynamic LDS: the MaxIHaveLength-cut tables (cut mode), then the big
+// peertx hash (IWANT-spam runs)
+#define GS_CUTLDS (256 * 4 + GS_CUTS * 4 + GS_CUTS * 16 + 64 * 16 + 128 * 4 + 16)
 
 // device counter slots (same order as gs_counters)
 enum {
@@ -128,7 +131,9 @@ struct Dev {
   int32_t* promSlot;
   uint8_t* promEdge;
   int32_t* promN;
-  uint64_t* ptx;     // [N][GS_PTX] packed (slot << 32 | edge << 8 | count)
+  uint64_t* ptx;     // [N][ptxCap] packed (slot << 32 | edge << 8 | count)
+  int32_t ptxCap;    // entries per node: GS_PTX, more when IWANT spammers run
+  int32_t ptxHBits;  // log2 of the dynamic LDS hash of a larger table
   int32_t* ptxN;
   // per-edge state
   uint64_t* mesh;

@@ -407,7 +407,11 @@ int gs_engine::start() {
   const size_t NQ = (size_t)N * GS_TABLE;
   x.promMid = dalloc<int64_t>(NQ); x.promExp = dalloc<int64_t>(NQ); x.promSlot = dalloc<int32_t>(NQ);
   x.promEdge = dalloc<uint8_t>(NQ); x.promN = dalloc<int32_t>(N);
-  x.ptx = dalloc<uint64_t>((size_t)N * GS_PTX); x.ptxN = dalloc<int32_t>(N);
+  // mcache.peertx: 512 entries per node; an IWANT spammer's requests add one
+  // per (message, spammer) to every neighbour's table, so spam runs get 4096
+  x.ptxCap = (behaveAll & GS_BEHAVE_IWANT_SPAM) ? 4096 : GS_PTX;
+  x.ptxHBits = 13;  // the dynamic hash of the 4096-entry table: 8192 slots (32 KiB)
+  x.ptx = dalloc<uint64_t>((size_t)N * x.ptxCap); x.ptxN = dalloc<int32_t>(N);
   chk(x.promMid); chk(x.promExp); chk(x.promSlot); chk(x.promEdge); chk(x.promN);
   chk(x.ptx); chk(x.ptxN);
   x.mesh = dalloc<uint64_t>(E); x.fanout = dalloc<uint64_t>(E);
@@ -750,7 +754,7 @@ int gs_engine::stepOne() {
       const auto b2 = std::upper_bound(mHop.begin(), mHop.end(), h);
       cutMode = (int64_t)(b2 - a) > (int64_t)gp.MaxIHaveLength ? 1 : 0;
     }
-    const size_t ldsB = cutMode ? (256 * 4 + GS_CUTS * 4 + GS_CUTS * 16 + 64 * 16 + 128 * 4 + 16) : 0;
+    const size_t ldsB = d.ptxCap > GS_PTX ? GS_CUTLDS + 4 * ((size_t)1 << d.ptxHBits) : (cutMode ? GS_CUTLDS : 0);
     TIMED(this, GS_K_PHASE_B,
           launch_wpl(W, [&](auto wpl) {
             if (nOwn) k_phase_b<decltype(wpl)::value><<<nOwn, 64, ldsB, stream>>>(d, h, now, cur, head, cutMode);
@@ -810,7 +814,9 @@ int gs_engine::checkDeviceError() {
     case E_NONE: return GS_OK;
     case E_POOL: gs_set_error("IWANT payload arena overflow (4 ids per edge per hop)"); return GS_ECAPACITY;
     case E_PROMISES: gs_set_error("per-node promise table overflow (64 entries)"); return GS_ECAPACITY;
-    case E_PEERTX: gs_set_error("per-node IWANT retransmission table overflow (512 entries)"); return GS_ECAPACITY;
+    case E_PEERTX:
+      gs_set_error("per-node IWANT retransmission table overflow (512 entries; 4096 with IWANT spammers)");
+      return GS_ECAPACITY;
     case E_LATE:
       gs_set_error("a message was first delivered later than the message window allows; raise slots_per_topic");
       return GS_ECAPACITY;

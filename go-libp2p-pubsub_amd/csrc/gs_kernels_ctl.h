@@ -75,8 +75,10 @@ __device__ __forceinline__ uint32_t ptx_to32(uint64_t ent) { return ptx_key32(en
 __device__ __forceinline__ uint64_t ptx_to64(uint32_t e) {
   return ((uint64_t)(e >> 14) << 32) | ((uint64_t)((e >> 8) & 0x3F) << 8) | (uint64_t)(e & 0xFF);
 }
-__device__ __forceinline__ int ptx_hash(uint32_t key) {
-  return (int)((key * 0x9E3779B1u) >> 22);  // 10 bits
+// hbits: log2 of the hash size (GS_PTXH, or the larger dynamic table of an
+// IWANT-spam run)
+__device__ __forceinline__ int ptx_hash(uint32_t key, int hbits) {
+  return (int)((key * 0x9E3779B1u) >> (32 - hbits));
 }
 
 // k-th set bit (0-based) of m
@@ -87,10 +89,11 @@ __device__ __forceinline__ int kth_bit(uint64_t m, int k) {
 
 // ++peertx[slot][edge] (mcache.GetForPeer, mcache.go:66-80) in the LDS hash;
 // returns the new count, or 0 when the table is full (E_PEERTX raised).
-__device__ __forceinline__ int ptx_incr(const Dev& d, unsigned int* sH, uint64_t key64) {
+__device__ __forceinline__ int ptx_incr(const Dev& d, unsigned int* sH, int hbits, uint64_t key64) {
   const uint32_t key = ptx_key32(key64);
-  int hsl = ptx_hash(key);
-  for (int probe = 0; probe < GS_PTXH; ++probe) {
+  const int hmask = (1 << hbits) - 1;
+  int hsl = ptx_hash(key, hbits);
+  for (int probe = 0; probe <= hmask; ++probe) {
     unsigned int cur = sH[hsl];
     while (true) {
       if (cur == 0) {
@@ -105,20 +108,21 @@ __device__ __forceinline__ int ptx_incr(const Dev& d, unsigned int* sH, uint64_t
       if (prev == cur) return (int)(nw & 0xFF);
       cur = prev;
     }
-    hsl = (hsl + 1) & (GS_PTXH - 1);
+    hsl = (hsl + 1) & hmask;
   }
   set_err(d, E_PEERTX);
   return 0;
 }
 
-__device__ __forceinline__ int ptx_count(const unsigned int* sH, uint64_t key64) {
+__device__ __forceinline__ int ptx_count(const unsigned int* sH, int hbits, uint64_t key64) {
   const uint32_t key = ptx_key32(key64);
-  int hsl = ptx_hash(key);
-  for (int probe = 0; probe < GS_PTXH; ++probe) {
+  const int hmask = (1 << hbits) - 1;
+  int hsl = ptx_hash(key, hbits);
+  for (int probe = 0; probe <= hmask; ++probe) {
     const unsigned int cur = sH[hsl];
     if (cur == 0) return 0;
     if ((cur & ~0xFFu) == key) return (int)(cur & 0xFF);
-    hsl = (hsl + 1) & (GS_PTXH - 1);
+    hsl = (hsl + 1) & hmask;
   }
   return 0;
 }
@@ -348,12 +352,18 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
   int nSrv = 0;  // reply RPCs carrying served messages to this sender
   if (__ballot(gateIWant || gateSpam)) {
     __shared__ int sSpOff[64], sSpN[64], sItI[64], sCntS[64];
+    // the peertx hash: static, or a larger dynamic table (IWANT-spam runs)
+    extern __shared__ __attribute__((aligned(16))) uint32_t smemH[];
+    const bool big = d.ptxCap > GS_PTX;
+    unsigned int* const hT = big ? (unsigned int*)(smemH + GS_CUTLDS / 4) : sH;
+    const int hbits = big ? d.ptxHBits : 10;
+    const int hN = 1 << hbits;
     for (int w = lane; w < W; w += 64) {
       uint64_t x = 0;
       for (int k = 0; k < d.HL; ++k) x |= d.hist[((int64_t)((head + k) % d.R) * d.N + v) * W + w];
       scache[w] = x;
     }
-    for (int k = lane; k < GS_PTXH; k += 64) sH[k] = 0u;
+    for (int k = lane; k < hN; k += 64) hT[k] = 0u;
     const int nI = gateIWant ? (int)(iwRec & 0xFFFFFF) : 0;
     const int nS = gateSpam ? (int)(spRec & 0xFFFFFF) : 0;
     const int itI = (nI + 15) >> 4, itS = (nS + 15) >> 4;
@@ -370,10 +380,10 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     __syncthreads();
     const int ptxN = d.ptxN[v];
     for (int q = lane; q < ptxN; q += 64) {
-      const unsigned long long ent = d.ptx[(int64_t)v * GS_PTX + q];
+      const unsigned long long ent = d.ptx[(int64_t)v * d.ptxCap + q];
       const unsigned int e32 = ptx_to32(ent);
-      int hsl = ptx_hash(e32 & ~0xFFu);
-      while (atomicCAS(&sH[hsl], 0u, e32) != 0u) hsl = (hsl + 1) & (GS_PTXH - 1);
+      int hsl = ptx_hash(e32 & ~0xFFu, hbits);
+      while (atomicCAS(&hT[hsl], 0u, e32) != 0u) hsl = (hsl + 1) & (hN - 1);
     }
     __syncthreads();
     // item b: 16 ids of the IHAVE-reply list (k < itI) or of the spam list
@@ -404,7 +414,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
         const int slot = d.pool[prv][off + q];
         if (!cached(slot)) continue;
         const uint64_t key = ((uint64_t)(uint32_t)slot << 32) | ((uint64_t)i << 8);
-        const int count = ptx_incr(d, sH, key);
+        const int count = ptx_incr(d, hT, hbits, key);
         if (count >= 1 && count <= d.GR) ++c;
       }
       if (c) atomicAdd(sp ? &sCntS[i] : &sCnt[i], c);
@@ -436,7 +446,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
             const int slot = d.pool[prv][off + q];
             if (!cached(slot)) continue;
             const uint64_t key = ((uint64_t)(uint32_t)slot << 32) | ((uint64_t)i << 8);
-            const int count = ptx_count(sH, key);
+            const int count = ptx_count(hT, hbits, key);
             if (count >= 1 && count <= d.GR) d.pool[cur][sOut[i] + atomicAdd(&sCur[i], 1)] = slot;
           }
         }
@@ -446,15 +456,15 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     {  // peertx table back to its list form
       __syncthreads();
       int kept = 0;
-      for (int q0 = 0; q0 < GS_PTXH; q0 += 64) {
-        const unsigned int e32 = sH[q0 + lane];
+      for (int q0 = 0; q0 < hN; q0 += 64) {
+        const unsigned int e32 = hT[q0 + lane];
         int tot;
         const int pos = kept + lane_prefix(e32 != 0u ? 1 : 0, &tot);
-        if (e32 && pos < GS_PTX) d.ptx[(int64_t)v * GS_PTX + pos] = ptx_to64(e32);
+        if (e32 && pos < d.ptxCap) d.ptx[(int64_t)v * d.ptxCap + pos] = ptx_to64(e32);
         kept += tot;
       }
-      if (kept > GS_PTX && lane == 0) set_err(d, E_PEERTX);
-      if (lane == 0) d.ptxN[v] = kept < GS_PTX ? kept : GS_PTX;
+      if (kept > d.ptxCap && lane == 0) set_err(d, E_PEERTX);
+      if (lane == 0) d.ptxN[v] = kept < d.ptxCap ? kept : d.ptxCap;
     }
     __syncthreads();  // sH is reused by step 3
   }
@@ -1210,13 +1220,13 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
       uint64_t ent = 0;
       bool live = q < n;
       if (live) {
-        ent = d.ptx[(int64_t)v * GS_PTX + q];
+        ent = d.ptx[(int64_t)v * d.ptxCap + q];
         const int slot = (int)(ent >> 32);
         if ((lastw[slot >> 6] >> (slot & 63)) & 1) live = false;
       }
       const unsigned long long lm = __ballot(live);
       const int pos = kept + __popcll(lm & ((1ull << lane) - 1));
-      if (live) d.ptx[(int64_t)v * GS_PTX + pos] = ent;  // pos <= q: in-place compaction is safe
+      if (live) d.ptx[(int64_t)v * d.ptxCap + pos] = ent;  // pos <= q: in-place compaction is safe
       kept += __popcll(lm);
     }
     if (lane == 0) d.ptxN[v] = kept;
