@@ -113,6 +113,8 @@ struct Dev {
   int32_t anyBehave;     // some node has a GS_BEHAVE_* bit
   const uint8_t* behave; // [N] GS_BEHAVE_* bits (nullptr: all honest)
   int64_t* cSpam[2];     // [E] IWANT-spam request list (arena record), -1 = none
+  int32_t* pmaskRow;     // [N] row of an IWANT spammer in pmask, -1 = none (nullptr: no spammers)
+  uint64_t* pmask;       // [spammers][S] drec.peers: in-edges whose duplicate was counted
   uint8_t* cNSrv[2];     // [E] reply RPCs carrying served messages (0..2)
   // peer gater (peer_gater.go), one per node; stats per (observer, IP) kept on
   // the observer's first edge to a peer of that IP (gGrp = its in-row index)

@@ -458,16 +458,26 @@ int gs_engine::start() {
   x.anyBehave = behaveAll != 0;
   x.behave = nullptr;
   x.cSpam[0] = x.cSpam[1] = nullptr;
+  x.pmaskRow = nullptr;
+  x.pmask = nullptr;
   x.cNSrv[0] = x.cNSrv[1] = nullptr;
   if (behaveAll) {
     uint8_t* b = dalloc<uint8_t>(N); chk(b);
     if (b) HIPCHECK(hipMemcpyAsync(b, behaveH.data(), N, hipMemcpyHostToDevice, stream));
     x.behave = b;
-    if (behaveAll & GS_BEHAVE_IWANT_SPAM)
+    if (behaveAll & GS_BEHAVE_IWANT_SPAM) {
       for (int k = 0; k < 2; ++k) {
         x.cSpam[k] = dalloc<int64_t>(E, 0xFF); chk(x.cSpam[k]);
         x.cNSrv[k] = dalloc<uint8_t>(E); chk(x.cNSrv[k]);
       }
+      std::vector<int32_t> row(N, -1);
+      int nsp = 0;
+      for (int v = 0; v < N; ++v)
+        if (behaveH[v] & GS_BEHAVE_IWANT_SPAM) row[v] = nsp++;
+      x.pmaskRow = dalloc<int32_t>(N); chk(x.pmaskRow);
+      x.pmask = dalloc<uint64_t>((size_t)nsp * S); chk(x.pmask);
+      if (ok) HIPCHECK(hipMemcpyAsync(x.pmaskRow, row.data(), (size_t)N * 4, hipMemcpyHostToDevice, stream));
+    }
   }
   x.gater = gaterOn ? 1 : 0;
   x.gValidate = x.gThrottle = nullptr;
@@ -707,7 +717,8 @@ int gs_engine::stepOne() {
     // the adversarial model (validators, gater, attackers) has its own
     // instantiation: the honest path keeps its LDS budget and code
     const bool adv = topicVal != 0 || gaterOn || behaveAll != 0;
-    size_t lds = (narrow ? 2 : 4) * nCnt + 16 * (size_t)nR + (size_t)nYp + (d.needAge ? 4 * nCnt : 0);
+    const bool hasUnc = d.needAge || (adv && d.pmaskRow != nullptr);
+    size_t lds = (narrow ? 2 : 4) * nCnt + 16 * (size_t)nR + (size_t)nYp + (hasUnc ? 4 * nCnt : 0);
     if (adv) lds += 4 * nCnt + 4 * 64 * 4 + 8 * 64 + 8 * (size_t)nR;
     TIMED(this, GS_K_PHASE_A, launch_wpl(W, [&](auto w) {
             if (!nOwn) return;

@@ -491,9 +491,14 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   uint64_t* sD = (uint64_t*)(smem32 + nCntW);             // [nR] delivered young slots (non-graylisted)
   uint64_t* sYm = sD + nR;                                // [nR] young-slot mask of each amR word
   uint8_t* sFirst = (uint8_t*)(sYm + nR);                 // [nY] lowest deliverer per young slot
-  uint32_t* sUnc = (uint32_t*)(sFirst + nY);              // [MD][T] uncredited duplicates (needAge)
+  uint32_t* sUnc = (uint32_t*)(sFirst + nY);              // [MD][T] uncredited duplicates (needAge / pmask)
+  // drec.peers of this node (score.go:786-818): the senders whose duplicate
+  // of a message was already counted — tracked only for nodes that re-request
+  // messages they have (IWANT spammers), the only receivers of repeats
+  const int prow = (ADV && d.pmaskRow != nullptr) ? d.pmaskRow[d.n0 + blockIdx.x] : -1;
+  const bool hasUnc = d.needAge || (ADV && d.pmaskRow != nullptr);
   // ADV tables after sUnc (present only in the ADV launch)
-  uint32_t* sInv = sUnc + (d.needAge ? nCnt : 0);         // [MD][T] copies of rejected messages
+  uint32_t* sInv = sUnc + (hasUnc ? nCnt : 0);            // [MD][T] copies of rejected messages
   uint32_t* sPer = sInv + nCnt;                           // [4][64] per sender: accepted copies, valid /
                                                           // rejected / ignored first deliveries
   double* sGThr = (double*)(sPer + 4 * 64);               // [64] gater threshold per sender, < 0 = accept
@@ -540,7 +545,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   GS_STAMP(0);
   const bool authV = d.nAuth[v] > 0;  // v authored a live message: author exclusion possible
   for (int k = lane; k < nCntW / 4; k += 64) ((uint4*)scnt)[k] = make_uint4(0, 0, 0, 0);
-  if (d.needAge)
+  if (hasUnc)
     for (int k = lane; k < nCnt / 4; k += 64) ((uint4*)sUnc)[k] = make_uint4(0, 0, 0, 0);
   for (int k = lane; k < nR; k += 64) {
     sD[k] = 0;
@@ -649,13 +654,21 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     const int rk = sRk[w];
     const uint64_t ym = rk == 0xFFFF ? 0ull : sYm[rk];
     const bool young = (ym >> (slot & 63)) & 1;
-    if (d.needAge || !young) {
+    unsigned long long pold = 0;  // this node's drec.peers of the message before the copy
+    if (prow >= 0 && kind == GS_MSG_VALID)
+      pold = atomicOr((unsigned long long*)&d.pmask[(int64_t)prow * d.S + slot], 1ull << i);
+    if (d.needAge || !young || prow >= 0) {
       const bool had = (d.seen[(int64_t)v * W + w] >> (slot & 63)) & 1;
       // markDuplicateMessageDelivery window (score.go:955): a copy of a message
-      // first delivered before this hop is credited only within the window
-      if (had && d.needAge && kind == GS_MSG_VALID) {
-        const int64_t firstHop = d.slotPubHop[slot] + d.age[(int64_t)v * d.S + slot];
-        if ((h - firstHop) * d.hop_ns > d.tp[t].MmdWindow) atomicAdd(&sUnc[i * T + t], 1u);
+      // first delivered before this hop is credited only within the window;
+      // a second duplicate from the same peer is not counted (score.go:801-805)
+      if (had && kind == GS_MSG_VALID) {
+        bool unc = (pold >> i) & 1;
+        if (d.needAge && !unc) {
+          const int64_t firstHop = d.slotPubHop[slot] + d.age[(int64_t)v * d.S + slot];
+          unc = (h - firstHop) * d.hop_ns > d.tp[t].MmdWindow;
+        }
+        if (unc) atomicAdd(&sUnc[i * T + t], 1u);
       }
       if (!young) {
         // outside the young slots only an old duplicate is possible; a first
@@ -865,7 +878,10 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
           y &= y - 1;
           const unsigned long long key =
               ((unsigned long long)sFirst[fidx(rkw[j], b)] << 56) | (unsigned long long)d.slotMid[w * 64 + b];
-          if (key > K) atomicOr((unsigned long long*)&sDrop[rkw[j]], 1ull << b);
+          if (key > K) {
+            atomicOr((unsigned long long*)&sDrop[rkw[j]], 1ull << b);
+            if (prow >= 0) d.pmask[(int64_t)prow * d.S + w * 64 + b] = 0;  // never seen: no record
+          }
         }
       }
       anyDrop = true;
@@ -1022,7 +1038,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
       const int copies = NARROW ? (int)(c & 0xFF) : (int)(c & 0xFFFF);
       const int nf = NARROW ? (int)(c >> 8) : (int)(c >> 16);
       int credited = copies - nf;
-      if (d.needAge && ((scoredT >> t) & 1)) credited -= (int)sUnc[pl];  // unscored: no counts at all
+      if (hasUnc && ((scoredT >> t) & 1)) credited -= (int)sUnc[pl];  // unscored: no counts at all
       const uint32_t addM = ((sRelay[i] >> t) & 1) ? (uint32_t)(nf + credited) : 0u;
       if ((q & 0xFFFF) + nf > 0xFFFF || (q >> 16) + addM > 0xFFFF) set_err(d, E_DELTA);
       return q + (uint32_t)nf + (addM << 16);
@@ -1171,6 +1187,8 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
         if (trv)  // pubsub.go:1057, ReceivedFrom = the first deliverer
           trace_emit(d, h, GS_TRACE_DELIVER_MESSAGE, v, d.col[base + ff], (int)__umulhi((unsigned)slot, d.stMagic),
                      d.slotMid[slot], 2);
+        if (prow >= 0)  // DeliverMessage does not add the deliverer to drec.peers
+          atomicAnd((unsigned long long*)&d.pmask[(int64_t)prow * d.S + slot], ~(1ull << ff));
         if (!behaves(d, v, GS_BEHAVE_NO_FORWARD)) {  // a squatter relays nothing
           if (rank < FC) Lv[rank] = (uint32_t)slot | ((uint32_t)ff << 16);
           else set_err(d, E_FCAP);
@@ -1241,6 +1259,14 @@ __global__ void k_retire(Dev d, int cur, const int32_t* __restrict__ words, int 
   const int v = d.n0 + (int)(k / nwords);
   const int w = words[k % nwords];
   d.seen[(int64_t)v * d.W + w] &= ~d.pubmask[cur][w];
+  if (d.pmaskRow != nullptr && d.pmaskRow[v] >= 0) {  // a recycled slot starts a fresh record
+    uint64_t y = d.pubmask[cur][w];
+    while (y) {
+      const int b = __ffsll((long long)y) - 1;
+      y &= y - 1;
+      d.pmask[(int64_t)d.pmaskRow[v] * d.S + w * 64 + b] = 0;
+    }
+  }
 }
 
 // ---------------------------------------------------------------- local publish
