@@ -809,7 +809,9 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   // loads of the pass are issued before its first store (on gfx9 a load's
   // wait also waits for every older store).
   uint32_t* Lv = d.fl[cur] + (int64_t)v * FC;
-  if (scoring) sRelay[lane] = valid ? d.mesh[base + lane] : 0ull;  // pass 3: in-edge mesh words
+  // pass 3's in-edge mesh words replace the relay masks in sRelay; the ADV
+  // launch still walks the lists again (queue drops) and loads them later
+  if (!ADV && scoring) sRelay[lane] = valid ? d.mesh[base + lane] : 0ull;
   long long nDeliv = 0;
   uint64_t Uw[WPL], Sw[WPL], Hw[WPL], Ow[WPL];
   uint64_t Xw[WPL];  // ADV: fresh messages validated as REJECT / IGNORE (seen, not delivered)
@@ -1013,6 +1015,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
         if (lane == 0) d.promN[v] = __popcll(lm);
       }
     }
+    if (scoring) sRelay[lane] = valid ? d.mesh[base + lane] : 0ull;
   }
   __syncthreads();
   GS_STAMP(3);
