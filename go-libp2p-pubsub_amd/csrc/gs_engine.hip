@@ -145,6 +145,7 @@ struct gs_engine {
     for (hipEvent_t ev : evPool) (void)hipEventDestroy(ev);
     for (uint8_t* p : {xSend, xRecv, xSendE, xRecvE}) if (p) (void)hipFree(p);
     if (xHost) (void)hipHostFree(xHost);
+    if (errRing) (void)hipHostFree(errRing);
     for (void* p : allocs) (void)hipFree(p);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -185,6 +186,16 @@ struct gs_engine {
   int stepOne();
   int uploadMessages();
   int checkDeviceError();
+  // Device error flags, copied to pinned memory after every hop so the first
+  // failing hop is named; an error is sticky (the state after it is not the
+  // reference's), every later gs_step returns it again.
+  static constexpr int kErrRing = 64;
+  int32_t* errRing = nullptr;
+  int stickyRc = GS_OK;
+  std::string stickyMsg;
+  int drainErrors(int64_t firstHop, int n);
+  int deviceErrorCode(int32_t err);
+  int deviceErrorText(int32_t err, int64_t atHop);
 };
 
 // Contiguous node ranges balanced by edges: rank r owns the nodes whose CSR
@@ -821,6 +832,30 @@ int gs_engine::checkDeviceError() {
   resolveTimings();
   int32_t err = 0;
   HIPCHECK(hipMemcpy(&err, d.err, 4, hipMemcpyDeviceToHost));
+  return deviceErrorText(err, -1);
+}
+
+// Waits for the last n hops (first one = firstHop) and reports the first whose
+// device error flag is set.
+int gs_engine::drainErrors(int64_t firstHop, int n) {
+  HIPCHECK(hipStreamSynchronize(stream));
+  resolveTimings();
+  for (int i = 0; i < n; ++i)
+    if (errRing[i]) return deviceErrorText(errRing[i], firstHop + i);
+  return GS_OK;
+}
+
+int gs_engine::deviceErrorText(int32_t err, int64_t atHop) {
+  const int rc = deviceErrorCode(err);
+  if (rc != GS_OK && atHop >= 0) {
+    g_err = "hop " + std::to_string(atHop) + ": " + g_err;
+    stickyRc = rc;
+    stickyMsg = g_err;
+  }
+  return rc;
+}
+
+int gs_engine::deviceErrorCode(int32_t err) {
   switch (err) {
     case E_NONE: return GS_OK;
     case E_POOL: gs_set_error("IWANT payload arena overflow (4 ids per edge per hop)"); return GS_ECAPACITY;
@@ -1296,15 +1331,26 @@ int gs_step(gs_engine* g, int64_t hops) {
     int rc = g->start();
     if (rc) return rc;
   }
+  if (g->stickyRc) {
+    gs_set_error(g->stickyMsg);
+    return g->stickyRc;
+  }
+  if (!g->errRing)
+    HIPCHECK(hipHostMalloc((void**)&g->errRing, gs_engine::kErrRing * sizeof(int32_t), hipHostMallocDefault));
+  int64_t first = g->hop;
+  int n = 0;
   for (int64_t i = 0; i < hops; ++i) {
     int rc = g->stepOne();
     if (rc) return rc;
-    if (g->pendKid.size() > 4096) {
-      HIPCHECK(hipStreamSynchronize(g->stream));
-      g->resolveTimings();
+    HIPCHECK(hipMemcpyAsync(g->errRing + n, g->d.err, 4, hipMemcpyDeviceToHost, g->stream));
+    if (++n == gs_engine::kErrRing || g->pendKid.size() > 4096) {
+      rc = g->drainErrors(first, n);
+      if (rc) return rc;
+      first = g->hop;
+      n = 0;
     }
   }
-  return g->checkDeviceError();
+  return g->drainErrors(first, n);
 }
 
 int gs_sync(gs_engine* g) {

@@ -97,6 +97,18 @@ bool check_shape(const gs_rpc_shape* r) {
     ids += r->iwant_nids[i];
   }
   if (ids && !r->id_len) return false;
+  // sizes are byte counts: never negative (a TopicID length may be -1 = nil)
+  auto nonneg = [](const int64_t* a, int64_t n) {
+    for (int64_t i = 0; i < n; ++i)
+      if (a[i] < 0) return false;
+    return true;
+  };
+  if (!nonneg(r->sub_size, r->n_sub) || !nonneg(r->pub_size, r->n_pub) || !nonneg(r->graft_size, r->n_graft) ||
+      !nonneg(r->prune_size, r->n_prune) || !nonneg(r->id_len, ids))
+    return false;
+  if (r->ihave_topic_len)
+    for (int32_t i = 0; i < r->n_ihave; ++i)
+      if (r->ihave_topic_len[i] < -1) return false;
   if (!r->has_control && (r->n_ihave || r->n_iwant || r->n_graft || r->n_prune)) return false;
   return true;
 }
@@ -114,7 +126,9 @@ extern "C" int64_t gs_rpc_size(const gs_rpc_shape* rpc) {
 extern "C" int gs_fragment_rpc(const gs_rpc_shape* rpc, int64_t limit, gs_rpc_fragments* out) {
   if (!check_shape(rpc) || !out || limit <= 0 || (rpc->n_sub && !out->sub_frag) ||
       (rpc->n_pub && !out->pub_frag) || (rpc->n_graft && !out->graft_frag) ||
-      (rpc->n_prune && !out->prune_frag) || out->frag_cap < 0 || out->bucket_cap < 0) {
+      (rpc->n_prune && !out->prune_frag) || out->frag_cap < 0 || out->bucket_cap < 0 ||
+      (out->frag_cap > 0 && !out->frag_size) ||
+      (out->bucket_cap > 0 && (!out->bucket_frag || !out->bucket_kind || !out->bucket_src))) {
     gs_set_error("gs_fragment_rpc: bad arguments");
     return GS_EINVAL;
   }

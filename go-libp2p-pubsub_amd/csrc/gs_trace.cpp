@@ -58,15 +58,52 @@ std::string b64(const std::string& s) {
   }
   return o;
 }
-std::string jstr(const std::string& s) {  // encoding/json string escaping (HTML-safe)
+// encoding/json's string encoder as of the reference's Go (1.13-1.15,
+// encode.go encodeState.string with escapeHTML): \" \\ \n \r \t short
+// escapes, other control bytes and < > & as \u00XX, U+2028 / U+2029 escaped,
+// invalid UTF-8 replaced by \ufffd (one per bad byte, utf8.DecodeRuneInString).
+std::string jstr(const std::string& s) {
   std::string o = "\"";
-  for (unsigned char c : s) {
-    if (c == '"' || c == '\\') { o += '\\'; o += (char)c; }
-    else if (c < 0x20 || c == '<' || c == '>' || c == '&') {
-      char buf[8];
-      std::snprintf(buf, sizeof buf, "\\u%04x", c);
-      o += buf;
-    } else o += (char)c;
+  const size_t n = s.size();
+  for (size_t i = 0; i < n;) {
+    const unsigned char c = (unsigned char)s[i];
+    if (c < 0x80) {
+      if (c == '"' || c == '\\') { o += '\\'; o += (char)c; }
+      else if (c == '\n') o += "\\n";
+      else if (c == '\r') o += "\\r";
+      else if (c == '\t') o += "\\t";
+      else if (c < 0x20 || c == '<' || c == '>' || c == '&') {
+        char buf[8];
+        std::snprintf(buf, sizeof buf, "\\u%04x", c);
+        o += buf;
+      } else o += (char)c;
+      ++i;
+      continue;
+    }
+    // decode one rune; width 0 = invalid
+    uint32_t r = 0;
+    size_t w = 0;
+    auto cont = [&](size_t k) { return i + k < n && ((unsigned char)s[i + k] & 0xC0) == 0x80; };
+    if (c >= 0xC2 && c <= 0xDF && cont(1)) {
+      r = ((c & 0x1F) << 6) | (s[i + 1] & 0x3F);
+      w = 2;
+    } else if (c >= 0xE0 && c <= 0xEF && cont(1) && cont(2)) {
+      r = ((c & 0x0F) << 12) | ((s[i + 1] & 0x3F) << 6) | (s[i + 2] & 0x3F);
+      if (r >= 0x800 && !(r >= 0xD800 && r <= 0xDFFF)) w = 3;
+    } else if (c >= 0xF0 && c <= 0xF4 && cont(1) && cont(2) && cont(3)) {
+      r = ((c & 0x07) << 18) | ((s[i + 1] & 0x3F) << 12) | ((s[i + 2] & 0x3F) << 6) | (s[i + 3] & 0x3F);
+      if (r >= 0x10000 && r <= 0x10FFFF) w = 4;
+    }
+    if (w == 0) {
+      o += "\\ufffd";
+      ++i;
+    } else if (r == 0x2028 || r == 0x2029) {
+      o += r == 0x2028 ? "\\u2028" : "\\u2029";
+      i += w;
+    } else {
+      o.append(s, i, w);
+      i += w;
+    }
   }
   return o + "\"";
 }

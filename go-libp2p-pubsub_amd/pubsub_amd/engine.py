@@ -336,7 +336,7 @@ def encode_trace(events, fmt=_abi.GS_TRACE_FORMAT_PB, hop_ns=100 * Millisecond, 
     ev = np.ascontiguousarray(events, dtype=_abi.TRACE_EVENT_DTYPE)
     names = None
     if topic_names is not None:
-        names = (C.c_char_p * len(topic_names))(*[t.encode() for t in topic_names])
+        names = (C.c_char_p * len(topic_names))(*[t if isinstance(t, bytes) else t.encode() for t in topic_names])
     need = C.c_int64()
     rc = lib.gs_trace_encode(ev.ctypes.data, len(ev), fmt, hop_ns, names, proto.encode(), None, 0, C.byref(need))
     if rc not in (_abi.GS_OK, _abi.GS_ECAPACITY):

@@ -116,6 +116,13 @@ struct Sim {
   gs_peer_score_thresholds thr{};
   bool scoring = false, floodPublish = false, record = false;
   bool gaterOn = false;
+  // Reference order (gs_oracle_reference_order): each RPC is
+  // handled whole, in arrival order — AcceptFrom on the live score and gater,
+  // its messages, then its control (pubsub.go:946-969) — and the Publish
+  // filters read the live score.  Off: the engine's canonical schedule
+  // (hop-start memo S0, every payload of the hop before any control).
+  bool refOrder = false;
+  bool liveScore = false;  // AcceptFrom / Publish filters on the live score (refOrder implies it)
   gs_peer_gater_params gaterParams{};
   std::vector<uint8_t> topicVal;   // RegisterTopicValidator per topic
   int32_t valQueue = 0;            // validation queue entries per node per hop (0 = unlimited)
@@ -344,6 +351,12 @@ void Node::handleMessage(int from, const Msg& m) {
 int Node::acceptFrom(int s, uint32_t draw) {
   if (sim->cfg.router != GS_ROUTER_GOSSIPSUB) return PeerGater::AcceptAll;
   if (direct.count(s)) return PeerGater::AcceptAll;
+  if (sim->liveScore) {  // gossipsub.go:578-589 on the live score, then peer_gater.go:320-363 live
+    if (sim->scoring && Score(s) < sim->thr.GraylistThreshold) return PeerGater::AcceptNone;
+    if (!sim->gaterOn) return PeerGater::AcceptAll;
+    const double u = gs_key_to_unit(gs_key64(sim->cfg.seed, GS_SITE_GATER, id, s, (uint32_t)sim->hop, draw));
+    return gater.AcceptFrom(s, sim->now(), u);
+  }
   if (sim->scoring && memo[s] < sim->thr.GraylistThreshold) return PeerGater::AcceptNone;
   if (!sim->gaterOn || !gsnap.active) return PeerGater::AcceptAll;
   auto it = gsnap.thr.find(s);
@@ -404,7 +417,7 @@ void Node::gsPublish(const Msg& m, int from) {
   std::set<int> tosend;
   auto tm = topics.find(topic);
   if (tm == topics.end()) return;
-  auto s0 = [&](int p) { return sim->scoring ? memo[p] : 0.0; };
+  auto s0 = [&](int p) { return sim->scoring ? (sim->liveScore ? Score(p) : memo[p]) : 0.0; };
   if (sim->floodPublish && from == id) {
     for (int p : tm->second)
       if (direct.count(p) || s0(p) >= sim->thr.PublishThreshold) tosend.insert(p);
@@ -911,10 +924,41 @@ void Sim::step() {
     nodes[m.from].localPublish(m);
     nextPub++;
   }
+  if (refOrder) {  // handleIncomingRPC per RPC, senders ascending, RPCs in send order
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int u = 0; u < N; ++u) {
+      Node& nd = nodes[u];
+      nd.valUsed = 0;
+      for (auto& kv : inbox[nd.id]) {
+        const int s = kv.first;
+        std::vector<int64_t> got;  // accepted payload (the IWANT spammer re-requests it)
+        for (const RPC& r : kv.second) {
+          nd.ctr.transmissions += (int64_t)r.publish.size();
+          const int st = nd.acceptFrom(s, r.hasCtl ? 0xFFFFFFFFu : (uint32_t)r.publish[0]);
+          if (st == PeerGater::AcceptNone) { nd.ctr.graylisted++; continue; }  // pubsub.go:947-949
+          if (st == PeerGater::AcceptControl) {                                // pubsub.go:951-955
+            if (!r.publish.empty()) nd.ctr.gated++;
+            if (scoring) nd.gtracer.ThrottlePeer(s);
+          } else {
+            for (int64_t mid : r.publish) nd.handleMessage(s, msgs[mid]);
+            got.insert(got.end(), r.publish.begin(), r.publish.end());
+          }
+          if (r.hasCtl && cfg.router == GS_ROUTER_GOSSIPSUB) nd.handleRPC(s, r.ctl);  // pubsub.go:969
+        }
+        if ((nd.behave & GS_BEHAVE_IWANT_SPAM) && !got.empty() && cfg.router == GS_ROUTER_GOSSIPSUB) {
+          std::sort(got.begin(), got.end());
+          RPC r;
+          r.hasCtl = true;
+          r.ctl.iwant = got;
+          nd.sendRPC(s, std::move(r));
+        }
+      }
+    }
+  }
   // phase A: payload messages, senders ascending; a sender's messages in
   // ascending id (their order only matters for the validation queue)
 #pragma omp parallel for schedule(dynamic, 64)
-  for (int u = 0; u < N; ++u) {
+  for (int u = 0; u < (refOrder ? 0 : N); ++u) {
     Node& nd = nodes[u];
     nd.acceptStatus.clear();
     nd.valUsed = 0;
@@ -955,7 +999,7 @@ void Sim::step() {
     }
   }
   // phase B: control, per RPC, senders ascending
-  if (cfg.router == GS_ROUTER_GOSSIPSUB) {
+  if (cfg.router == GS_ROUTER_GOSSIPSUB && !refOrder) {
 #pragma omp parallel for schedule(dynamic, 64)
     for (int u = 0; u < N; ++u) {
       Node& nd = nodes[u];
@@ -1070,6 +1114,15 @@ int gs_engine_create(const gs_config* cfg, const gs_gossipsub_params* gsp, const
 }
 
 int gs_engine_destroy(gs_engine* eng) { delete eng; return GS_OK; }
+// Oracle-only switch (tests/test_oracle_schedule.py): the reference's per-RPC
+// order with live scores instead of the engine's canonical schedule.
+int gs_oracle_reference_order(gs_engine* eng, int32_t on) {
+  if (eng->sim.hop != 0) { set_error("gs_oracle_reference_order: set before the first step"); return GS_EINVAL; }
+  // 1: per-RPC order + live scores; 2: the canonical phase split with live scores
+  eng->sim.refOrder = on == 1;
+  eng->sim.liveScore = on != 0;
+  return GS_OK;
+}
 
 int gs_set_graph(gs_engine* eng, const int64_t* rowptr, const int32_t* col, const uint8_t* outbound,
                  const uint8_t* direct) {

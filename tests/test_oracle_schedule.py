@@ -1,0 +1,74 @@
+"""The engine's canonical schedule against the reference's own order, on the
+oracle (DESIGN.md §3 "Schedule").  gs_oracle_reference_order switches the
+oracle (test infrastructure only) to
+  1: handleIncomingRPC per RPC — AcceptFrom on the live score and gater, the
+     RPC's messages, then its control (pubsub.go:946-969), senders ascending,
+     RPCs in send order, Publish filters on the live score
+     (gossipsub.go:584, 956-999);
+  2: the canonical phase split, but every score read live.
+Mode 2 pins the hop-start memo S0: it decides exactly as the live score on
+every parity scenario; only the peer gater's hop-start snapshot differs
+(adversarial_mix).  Mode 1 measures the schedule itself: meshes and delivery
+counts agree; the IHAVE / payload race (an IHAVE handled before a later
+sender's copy of the same message asks for it) changes IWANT and duplicate
+counts."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import scenarios
+
+FAST = [n for n in scenarios.SCENARIOS if n not in scenarios.HEAVY]
+
+
+def _run(oracle_path, name, mode):
+    e, hops = scenarios.SCENARIOS[name](oracle_path)
+    if mode:
+        assert e.lib.gs_oracle_reference_order(e.h, C.c_int32(mode)) == 0
+    e.step(hops)
+    return scenarios.snapshot(e, getattr(e, "snapshot_ids", range(e.n_published)))
+
+
+def test_mode_only_before_first_step(oracle_path):
+    e, _ = scenarios.SCENARIOS["gossipsub_dense"](oracle_path)
+    e.step(1)
+    assert e.lib.gs_oracle_reference_order(e.h, C.c_int32(1)) != 0
+
+
+@pytest.mark.parametrize("name", FAST)
+def test_live_scores_equal_hop_start_memo(oracle_path, name):
+    a = _run(oracle_path, name, 0)
+    b = _run(oracle_path, name, 2)
+    bad = scenarios.compare(a, b)
+    if name == "adversarial_mix":
+        # the gater's hop-start snapshot vs its live counters: a few percent of
+        # the throttled copies, never the mesh
+        assert np.array_equal(a["mesh"], b["mesh"])
+        ca, cb = a["counters"], b["counters"]
+        assert abs(ca["deliveries"] - cb["deliveries"]) <= 1e-3 * ca["deliveries"]
+        assert abs(ca["throttled"] - cb["throttled"]) <= 0.1 * ca["throttled"]
+    else:
+        assert bad == [], "\n".join(bad)
+
+
+@pytest.mark.parametrize("name", FAST)
+def test_reference_order_distance(oracle_path, name):
+    a = _run(oracle_path, name, 0)
+    b = _run(oracle_path, name, 1)
+    ca, cb = a["counters"], b["counters"]
+    assert np.array_equal(a["mesh"], b["mesh"]), "meshes differ"
+    if not any(k in name for k in ("gossipsub", "sinkhole", "squatters", "adversarial", "spam_invalid")):
+        # floodsub / randomsub carry no control; the spam pairs handle one RPC kind per hop
+        assert scenarios.compare(a, b) == []
+        return
+    if "adversarial" not in name and name != "spam_invalid":
+        assert ca["deliveries"] == cb["deliveries"]
+        # the race only ever adds IWANTs: a message still unseen when the
+        # IHAVE is handled, delivered later in the same hop
+        assert cb["iwant_sent"] >= ca["iwant_sent"]
+        hop_diff = sum(int(((h1 != h2) & ((h1 >= 0) | (h2 >= 0))).sum()) for (h1, _), (h2, _) in
+                       zip(a["deliv"], b["deliv"]))
+        assert hop_diff <= 1e-3 * ca["deliveries"]
+    else:
+        assert abs(ca["deliveries"] - cb["deliveries"]) <= 1e-3 * ca["deliveries"] + 1

@@ -98,6 +98,17 @@ def test_oracle_encoder_sizes():
     assert O.size(O.Message(data=b"x" * 196)) == 199
     assert O.size(O.SubOpts(subscribe=True, topicid="test")) == 8
     assert O.size(O.Prune("t", peers=[b"p1"], backoff=300)) == 3 + 6 + 3
+    # hand-derived from the gogo Size() methods of pb/rpc.pb.go (tag 1 byte,
+    # uvarint length, body): ControlPrune with two PX peers and a backoff ...
+    #   topicID "topic" 1+1+5; peers PeerInfo{peerID "peer-a"} 1+1+(1+1+6),
+    #   PeerInfo{peerID "p"} 1+1+(1+1+1); backoff 60: 1+1
+    assert O.size(O.Prune("topic", peers=[b"peer-a", b"p"], backoff=60)) == 7 + 10 + 5 + 2
+    # ... inside ControlMessage (field 4) inside RPC (field 3)
+    assert O.size(O.RPC(control=O.Control(prune=[O.Prune("topic", peers=[b"peer-a", b"p"], backoff=60)]))) == \
+        1 + 1 + (1 + 1 + 24)
+    # ControlIHave with a TopicID: topicID "blocks" 1+1+6; ids "m1", "msg22": 1+1+2, 1+1+5
+    assert O.size(O.IHave("blocks", [b"m1", b"msg22"])) == 8 + 4 + 7
+    assert O.size(O.IHave(None, [b"m1"])) == 4   # a nil TopicID is not written
 
 
 # ---- product against the oracle --------------------------------------------
@@ -230,6 +241,49 @@ def test_empty_rpc_and_bad_arguments():
         fragment_rpc(RpcShape(), 0)
     with pytest.raises(GossipEngineError):  # control entries without a control message
         fragment_rpc(RpcShape(graft_size=[6]), LIMIT)
+
+
+def _raw_call(pub=(10,), sub=(), topic_len=None, frag_cap=4, bucket_cap=4, null=()):
+    """gs_fragment_rpc through ctypes with hand-built arguments."""
+    import ctypes as C
+    from pubsub_amd import rpc as R
+    lib = R._library()
+    keep = []
+
+    def arr(vals, ct):
+        a = (ct * max(1, len(vals)))(*vals)
+        keep.append(a)
+        return C.cast(a, C.POINTER(ct))
+
+    sh = R._Shape()
+    sh.n_pub, sh.pub_size = len(pub), arr(pub, C.c_int64)
+    sh.n_sub, sh.sub_size = len(sub), arr(sub, C.c_int64)
+    if topic_len is not None:
+        sh.has_control, sh.n_ihave = 1, 1
+        sh.ihave_topic_len, sh.ihave_nids = arr([topic_len], C.c_int64), arr([0], C.c_int32)
+    fr = R._Frags()
+    fr.sub_frag, fr.pub_frag = arr([0] * 4, C.c_int32), arr([0] * 4, C.c_int32)
+    fr.frag_cap, fr.bucket_cap = frag_cap, bucket_cap
+    for name, ct in (("frag_size", C.c_int64), ("bucket_frag", C.c_int32), ("bucket_kind", C.c_int32),
+                     ("bucket_src", C.c_int32)):
+        if name not in null:
+            setattr(fr, name, arr([0] * 4, ct))
+    return lib.gs_fragment_rpc(C.byref(sh), 1 << 20, C.byref(fr))
+
+
+@pytest.mark.parametrize("case", [dict(pub=(-1,)), dict(sub=(-3,)), dict(topic_len=-2),
+                                  dict(null=("frag_size",)), dict(null=("bucket_frag",)),
+                                  dict(null=("bucket_kind",)), dict(null=("bucket_src",))])
+def test_fragment_rpc_rejects_bad_arguments(case):
+    """Negative part sizes, a TopicID length below -1 (nil) and NULL output
+    arrays with a non-zero capacity are GS_EINVAL, not a silently wrong split."""
+    assert _raw_call(**case) == -1  # GS_EINVAL
+
+
+def test_fragment_rpc_accepts_null_outputs_without_capacity():
+    assert _raw_call(topic_len=-1) == 0
+    assert _raw_call(frag_cap=0, bucket_cap=0, null=("frag_size", "bucket_frag", "bucket_kind", "bucket_src")) \
+        == -5  # GS_ECAPACITY: one fragment needed, none room for
 
 
 def test_product_matches_golden_fixture():

@@ -182,6 +182,19 @@ def test_encode_json_lines():
     assert list(d[6]["prune"]) == ["peerID", "topic"]
 
 
+def test_encode_json_string_escapes():
+    """encoding/json's string encoder (Go 1.13-1.15 encodeState.string, HTML-safe):
+    short escapes for \\n \\r \\t, \\u00XX for other control bytes and < > &,
+    U+2028 / U+2029 escaped, one \\ufffd per invalid UTF-8 byte."""
+    _need_product()
+    name = b'x\n\r\t"\\<>&\x01\xe2\x80\xa8\xe2\x80\xa9\xff\xc3(z\xc3\xa9'
+    out = encode_trace(_events(SAMPLE)[1:2], _abi.GS_TRACE_FORMAT_JSON, topic_names=[b"a", b"b", name])
+    want = (b'"topic":"x\\n\\r\\t\\"\\\\\\u003c\\u003e\\u0026\\u0001\\u2028\\u2029'
+            b'\\ufffd\\ufffd(z\xc3\xa9"')
+    assert want in out, out
+    assert json.loads(out)["join"]["topic"] == 'x\n\r\t"\\<>&\x01\u2028\u2029\ufffd\ufffd(z\u00e9'
+
+
 def test_encode_round_trip_sizes(oracle_path):
     """A real event stream encodes to one record per event in both formats."""
     _need_product()
