@@ -50,7 +50,7 @@ def build_engine(wl, rounds, seed, device, lib=None, n=None, msgs_per_round=MSGS
     subs = graphs.all_subscribed(n, T)
     opts = [WithPeerScore(eth2_peer_score_params(T), eth2_thresholds()), WithHop(100 * Millisecond),
             WithMessageWindow(wl["slots"]), WithSeed(seed)]
-    if lib is None:
+    if lib is None or "libgossip_engine" in os.path.basename(lib):
         opts.append(WithDevice(device))
     eng = NewGossipSub(n, T, g, subs, *opts, *extra, lib=lib)
     per_hop = msgs_per_round // HOPS_PER_ROUND
@@ -94,7 +94,10 @@ def algorithmic_bytes(kernel, eng, wl, per_hop):
         items = per_hop["deliveries"] + per_hop["published"]   # frontier-list entries written per hop
         list_reads = 4.0 * items * fwd_edges / N     # each list is read by the neighbours it forwards to
         list_writes = 4.0 * items
-        pending = 8.0 * T * E                        # pending-delivery counts, read + write per (edge, topic)
+        # pending-delivery counts per (edge, topic): written to the hop's ring
+        # slot (2 B, no read) when the engine keeps a ring, else a 4 B read +
+        # write of dlt
+        pending = (2.0 if per_hop.get("ring") else 8.0) * T * E
         seen = 16.0 * N * per_hop["active_words"]    # seen words of the active window, read + write
         meta = 49.0 * E                              # rev, col, fwd masks, IWANT ref, S0 memo, direct, mesh
         b = list_reads + list_writes + pending + seen + meta
@@ -102,9 +105,18 @@ def algorithmic_bytes(kernel, eng, wl, per_hop):
                        bytes_lists=int(list_reads + list_writes), bytes_pending=int(pending),
                        bytes_seen=int(seen), bytes_meta=int(meta))
     if kernel == "refresh":
-        # per (edge, topic): fmd/mmd/mfp/imd r+w 64, pending counts r 4, flags r 1,
-        # graftTime r 8 + meshTime w 8 (mesh edges); per edge: bp r+w 16, dirty w 1
-        return E * (77.0 * T + 17), dict(E=E, T=T)
+        # What the kernel must move (it skips unchanged writes; imd exists only
+        # once a validator rejected something, never in this workload):
+        # reads per (edge, topic) dlt 4, fmd / mmd / mfp 24, graftTime 8,
+        # flags 1; writes per (edge, topic) in the mesh: meshTime 8 and the
+        # decayed fmd / mmd 16 (pairs outside the mesh hold zeros or decay
+        # without fresh credit; counted as unwritten); per edge: bp r+w 16,
+        # score0 w 8, sdirty w 1
+        mesh_pairs = per_hop.get("mesh_pairs", 0)
+        return E * (37.0 * T + 25) + 24.0 * mesh_pairs, dict(E=E, T=T, mesh_pairs=mesh_pairs)
+    if kernel == "ring_fold":
+        # per (edge, topic): the used ring slots (2 B each) read, dlt read + written
+        return E * T * (2.0 * per_hop.get("ring_slots", 0) + 8.0), dict(E=E, T=T)
     if kernel == "score":
         # full pass: per (edge, topic) flags 1 + fmd/mfp/imd 24 + pending 4 (+ mmd, meshTime when
         # active); per edge col 4 + app 8 + p6 8 + bp 8 + out 8
@@ -168,6 +180,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="partition", choices=["partition", "replicas"])
     ap.add_argument("--peers", type=int, default=0, help="override the workload's peer count (rehearsals)")
+    ap.add_argument("--lib", default=None, help="timing experiments only: another build of the product library "
+                    "(results are labelled with it)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -211,7 +225,7 @@ def main():
     rounds = args.warmup + args.steps + 1
     t_setup = time.perf_counter()
     # partitioned ranks simulate ONE graph and schedule (same seed); replicas differ
-    eng, g = build_engine(wl, rounds, 3 if partitioned else 3 + rank, local, extra=extra)
+    eng, g = build_engine(wl, rounds, 3 if partitioned else 3 + rank, local, extra=extra, lib=args.lib)
     # hop 0 (Join) + warm-up rounds: meshes form, the message window fills
     eng.step(1 + args.warmup * HOPS_PER_ROUND)
     setup_s = time.perf_counter() - t_setup
@@ -259,7 +273,11 @@ def main():
     nh = args.steps * HOPS_PER_ROUND
     per_hop = {"deliveries": (c1["deliveries"] - c0["deliveries"]) / nh,
                "published": (c1["published"] - c0["published"]) / nh,
-               "active_words": float(np.mean([active_words(eng, wl, hop0 + i) for i in range(nh)]))}
+               "active_words": float(np.mean([active_words(eng, wl, hop0 + i) for i in range(nh)])),
+               # the pending-count ring is in use when its fold kernel ran (once per refresh)
+               "ring": kstats.get("ring_fold", (0, 0))[1] > 0,
+               "ring_slots": nh / max(1, kstats.get("ring_fold", (0, 1))[1]),
+               "mesh_pairs": int(np.bitwise_count(eng.mesh()[eng.edge_range[0]:eng.edge_range[1]]).sum(dtype=np.int64))}
     bytes_per_launch, bytes_info = algorithmic_bytes(dom, eng, wl, per_hop)
     roofline = None
     pmc = os.path.join(REPO, "profiles", f"pmc_traffic_{args.workload}.json")
@@ -286,7 +304,7 @@ def main():
     # the score kernels' rooflines too (north-star target: >= 50% of HBM on
     # score / propagation): refreshScores streams every (edge, topic) record
     rooflines = {}
-    for k in ("refresh",):
+    for k in ("refresh", "ring_fold"):
         if k in kstats and kstats[k][1]:
             b_k, _ = algorithmic_bytes(k, eng, wl, per_hop)
             ms_k = kstats[k][0] / kstats[k][1]
@@ -323,6 +341,8 @@ def main():
         "rooflines_other": rooflines,
         "setup_s": round(setup_s, 1),
     }
+    if args.lib:
+        out["experiment_lib"] = os.path.basename(args.lib)
     if partitioned:
         out["exchange"] = {"rank0_host_ms_per_step": round((x1[0] - x0[0]) / args.steps, 3),
                            "rank0_bytes_in_per_step": (x1[1] - x0[1]) // args.steps,

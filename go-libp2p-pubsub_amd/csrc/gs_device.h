@@ -18,6 +18,8 @@
 #define GS_WAVE 64
 #define GS_MAX_WPL 4   // words per lane in the node-wave kernels: W <= 256
 #define GS_QCAP 320    // phase A delivery queue (>= 63 pending + 256 appended per sub-round)
+#define GS_BMAP 32     // phase A: list blocks mapped to senders without a search (64 per entry)
+#define GS_RING_MAX 16 // pending-count ring slots (a slot adds <= 255 per field: 16 * 255 < 2^16 - 2^15)
 #define GS_TABLE 64    // promise table entries per node (one per lane)
 #define GS_PTX 512     // IWANT-retransmission (mcache peertx) entries per node
 #define GS_CUTS 64     // IHAVE entries above MaxIHaveLength one node can cut per hop
@@ -148,8 +150,16 @@ struct Dev {
   int64_t* backoff;  // [T][E], 0 = none
   double *fmd, *mmd, *mfp, *imd;  // per-(edge, topic) rows (tix)
   int32_t anyImd;                 // 0: no invalid delivery ever recorded, imd is all 0 (P4 = 0)
-  uint32_t* dlt;                  // tiled: deliveries not yet folded into fmd / mmd,
-                                  // (+1s to fmd) | (+1s to mmd) << 16 (see eff_counters)
+  uint32_t* dlt;                  // [E][T]: deliveries not yet folded into fmd / mmd,
+                                  // (+1s to fmd) | (+1s to mmd) << 16 (see eff_fmd)
+  // Per-hop pending counts of NARROW hops: phase A writes ring slot ringSlot
+  // ((+1s to fmd) | (+1s to mmd) << 8 per pair, every pair of the node, so no
+  // slot needs clearing) instead of a read-modify-write of dlt; slots
+  // [0, nRing) hold counts not yet folded into dlt (k_ring_fold, refresh)
+  uint16_t* ring;                 // [slot][E][T]
+  int64_t ringStride;             // pairs per slot
+  int32_t nRing;                  // slots readers must add to dlt
+  int32_t ringSlot;               // the slot phase A writes this hop, -1: dlt read-modify-write
   int64_t *graftTime, *meshTime;  // [T][E]
   uint8_t* flags;                 // [T][E] bit0 inMesh, bit1 P3 active
   double* bp;                     // [E] behaviourPenalty
@@ -296,6 +306,22 @@ __device__ __forceinline__ double eff_fmd(const TopicP& tp, double fmd, uint32_t
 __device__ __forceinline__ double eff_mmd(const TopicP& tp, double mmd, uint32_t q) {
   return (q >> 16) ? add_ones_capped(mmd, (int)(q >> 16), tp.MmdCap) : mmd;
 }
+// dlt's pending counts plus those of the unfolded ring slots, as (+1s to fmd)
+// | (+1s to mmd) << 16; the sum stays below 2^16 per field (E_DELTA bounds dlt,
+// a slot adds at most 255 per field, at most GS_RING_MAX slots)
+__device__ __forceinline__ uint32_t pend_q(const Dev& d, int64_t i) {
+  uint32_t q = d.dlt[i];
+  for (int r = 0; r < d.nRing; ++r) {
+    const uint32_t x = d.ring[(int64_t)r * d.ringStride + i];
+    q += (x & 0xFFu) | ((x >> 8) << 16);
+  }
+  return q;
+}
+// Clears the pending counts of pair i (they were folded by the caller).
+__device__ __forceinline__ void pend_clear(const Dev& d, int64_t i) {
+  d.dlt[i] = 0;
+  for (int r = 0; r < d.nRing; ++r) d.ring[(int64_t)r * d.ringStride + i] = 0;
+}
 
 // One topic's contribution topicScore * TopicWeight (score.go:265-311) of
 // pair i, split into its loads (all issued at once) and its arithmetic.
@@ -308,7 +334,7 @@ struct TermIn {
 __device__ __forceinline__ TermIn term_load(const Dev& d, int64_t i) {
   TermIn x;
   x.fl = d.flags[i];
-  x.q = d.dlt[i];
+  x.q = pend_q(d, i);
   x.mt = d.meshTime[i];
   x.mm = d.mmd[i];
   x.fmd = d.fmd[i];
@@ -405,12 +431,13 @@ __device__ __forceinline__ void stats_prune(const Dev& d, int64_t e, int t) {
   d.sdirty[e] = 1;
   const uint8_t fl = d.flags[i];
   const TopicP& tp = d.tp[t];
-  const uint32_t q = d.dlt[i];
+  const uint32_t q = pend_q(d, i);
   double mm = d.mmd[i];
-  if (q >> 16) {  // fold the pending mesh deliveries: the deficit reads the counter
+  if (q >> 16) {  // fold the pending deliveries: the deficit reads the mesh counter
     mm = eff_mmd(tp, mm, q);
     d.mmd[i] = mm;
-    d.dlt[i] = q & 0xFFFF;
+    if (q & 0xFFFF) d.fmd[i] = eff_fmd(tp, d.fmd[i], q);
+    pend_clear(d, i);
   }
   const double thr = tp.MmdThreshold;
   if ((fl & 2) && mm < thr) {

@@ -206,11 +206,11 @@ __global__ __launch_bounds__(64) void k_refresh_rows(Dev d, int64_t now) {
   }
 }
 
-// Folds the pending deliveries of every pair into fmd / mmd.
+// Folds the pending deliveries of every pair (dlt and the ring) into fmd / mmd.
 __global__ void k_fold_all(Dev d) {
   const int64_t p = d.e0 * d.T + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= d.e1 * d.T) return;
-  const uint32_t q = d.dlt[p];
+  const uint32_t q = pend_q(d, p);
   if (!q) return;
   int64_t e;
   int t;
@@ -218,7 +218,39 @@ __global__ void k_fold_all(Dev d) {
   const TopicP& tp = d.tp[t];
   d.fmd[p] = eff_fmd(tp, d.fmd[p], q);
   d.mmd[p] = eff_mmd(tp, d.mmd[p], q);
-  d.dlt[p] = 0;
+  d.dlt[p] = 0;  // the host forgets the ring slots (nRing = 0)
+}
+
+// Folds the ring's slots [0, nRing) into dlt: 8 pairs per thread, one 16-byte
+// load per slot; the host then sets nRing = 0.
+__global__ void k_ring_fold(Dev d) {
+  const int64_t p0 = d.e0 * d.T + 8 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  const int64_t pe = d.e1 * d.T;
+  if (p0 >= pe) return;
+  uint32_t f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (p0 + 8 <= pe && (p0 & 7) == 0) {
+    for (int r = 0; r < d.nRing; ++r) {
+      const uint4 x = *(const uint4*)(d.ring + (int64_t)r * d.ringStride + p0);
+      const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        f[2 * k] += (w[k] & 0xFFu) | (((w[k] >> 8) & 0xFFu) << 16);
+        f[2 * k + 1] += ((w[k] >> 16) & 0xFFu) | ((w[k] >> 24) << 16);
+      }
+    }
+  } else {
+    for (int r = 0; r < d.nRing; ++r)
+      for (int k = 0; k < 8 && p0 + k < pe; ++k) {
+        const uint32_t x = d.ring[(int64_t)r * d.ringStride + p0 + k];
+        f[k] += (x & 0xFFu) | ((x >> 8) << 16);
+      }
+  }
+  for (int k = 0; k < 8 && p0 + k < pe; ++k) {
+    if (!f[k]) continue;
+    const uint32_t q = d.dlt[p0 + k];
+    if ((q & 0xFFFF) + (f[k] & 0xFFFF) > 0xFFFF || (q >> 16) + (f[k] >> 16) > 0xFFFF) set_err(d, E_DELTA);
+    d.dlt[p0 + k] = q + f[k];
+  }
 }
 
 // Folds the pending deliveries of topic t into fmd / mmd.
@@ -504,6 +536,11 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   double* sGThr = (double*)(sPer + 4 * 64);               // [64] gater threshold per sender, < 0 = accept
   uint64_t* sDrop = (uint64_t*)(sGThr + 64);              // [nR] fresh messages dropped by a full queue
   __shared__ int sBlk[64];        // first list block of each sender
+  // block -> sender without a search: a bit per list block where a non-empty
+  // sender's list starts (the first GS_BMAP * 64 blocks), and the non-empty
+  // senders in ascending order as node | first block << 24 | sender << 48
+  __shared__ uint64_t sStart[GS_BMAP];
+  __shared__ uint64_t sComp[64];
   __shared__ uint64_t sRelay[64], sPub[64];
   __shared__ int sSnd[64];        // sender node | jr << 24 | graylisted << 31
   __shared__ int sLn[64];
@@ -597,6 +634,17 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   const int bincl = wave_incl_sum(nb);
   const int totalBlk = wave_last(bincl);
   sBlk[lane] = bincl - nb;
+  {
+    const uint64_t ne = __ballot(nb > 0);
+    for (int k = lane; k < GS_BMAP; k += 64) sStart[k] = 0ull;
+    __syncthreads();
+    const int fb = bincl - nb;
+    if (nb > 0) {
+      sComp[__popcll(ne & ((1ull << lane) - 1))] =
+          (uint64_t)(unsigned)u | ((uint64_t)(unsigned)fb << 24) | ((uint64_t)lane << 48);
+      if (fb < 64 * GS_BMAP) atomicOr((unsigned long long*)&sStart[fb >> 6], 1ull << (fb & 63));
+    }
+  }
   sRelay[lane] = relay;
   sPub[lane] = pub;
   sSnd[lane] = valid ? (u | (jr << 24) | (gray ? (1 << 31) : 0)) : 0;
@@ -702,17 +750,31 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   // nSent / nGray when `count` (the first walk).
   auto walk = [&](auto&& fn, bool count) {
     int qh = 0, qt = 0;  // queue head / tail (wave-uniform)
+    int rankPrev = -1;   // rank (among non-empty senders) of the sender of the block before the window
     constexpr int PB = 8;
     for (int b0 = 0; b0 < totalBlk; b0 += 64 * PB) {
       int si[PB], kb[PB];
       uint4 q[PB];
 #pragma unroll
       for (int rr = 0; rr < PB; ++rr) {
-        const int bidx = b0 + rr * 64 + lane;
+        const int B = b0 + rr * 64;  // the window's first block (wave-uniform, a multiple of 64)
+        const int bidx = B + lane;
         si[rr] = -1;
         kb[rr] = 0;
         q[rr] = make_uint4(0, 0, 0, 0);
-        if (bidx < totalBlk) {
+        if (B < 64 * GS_BMAP) {
+          // sender of block B + lane: the non-empty sender whose rank is the
+          // window's starting rank plus the list starts at offsets <= lane
+          const uint64_t mb = sStart[B >> 6];
+          const int rank = rankPrev + __popcll(mb & ((2ull << lane) - 1));
+          rankPrev += __popcll(mb);
+          if (bidx < totalBlk) {
+            const uint64_t ce = sComp[rank];
+            si[rr] = (int)(ce >> 48);
+            kb[rr] = bidx - (int)((ce >> 24) & 0xFFFFFF);
+            q[rr] = *(const uint4*)(d.fl[prv] + (int64_t)(ce & 0xFFFFFF) * FC + 4 * kb[rr]);
+          }
+        } else if (bidx < totalBlk) {
           int lo = 0, hi = 63;  // last sender whose first block is <= bidx
           while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
@@ -827,8 +889,12 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
       rkw[j] = wm_rank(amR, w);
       const uint64_t D = sD[rkw[j]];
       if (D) {
+        // the pass's loads in one round trip: seen, and (for the first
+        // deliveries it may hold) the old-slot mask and the mcache window
         Sw[j] = d.seen[(int64_t)v * W + w];
         Uw[j] = D;  // & ~seen below
+        Ow[j] = d.oldm[w];
+        if (d.router == 2) Hw[j] = d.hist[((int64_t)head * d.N + v) * W + w];
       }
     }
   }
@@ -910,10 +976,6 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
           }
         }
       }
-    }
-    if (Uw[j]) {
-      Ow[j] = d.oldm[w];
-      if (d.router == 2) Hw[j] = d.hist[((int64_t)head * d.N + v) * W + w];
     }
   }
   // first deliveries per (topic, first deliverer) for the counters of pass 3
@@ -1070,8 +1132,46 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
         }
       }
     };
-    if (nP > 16 * 64) rmw(std::integral_constant<int, 32>{});
-    else rmw(std::integral_constant<int, 16>{});
+#ifndef GS_EXP_NOPASS3
+    // a batch no larger than the node's pairs need: a batch slot past nP is a
+    // scratch store (config3: 32 pairs, one slot)
+    if (NARROW && d.ringSlot >= 0) {
+      // the hop's counts go to ring slot ringSlot: stores only, every pair of
+      // the node (zeros included), 8 pairs per 16-byte store when aligned
+      uint16_t* const rv = d.ring + (int64_t)d.ringSlot * d.ringStride + base * T;
+      auto val = [&](int pl, int i, int t) -> uint32_t {
+        const uint32_t q = upd(pl, i, t, 0u);  // nf | addM << 16, each <= 255 (NARROW)
+        return (q & 0xFFu) | ((q >> 16) << 8);
+      };
+      if (((base * T) & 7) == 0) {
+        for (int p0 = 8 * lane; p0 < nP; p0 += 8 * 64) {
+          int i = p0 / T, t = p0 - (p0 / T) * T;
+          uint32_t h[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            h[k] = p0 + k < nP ? val(p0 + k, i, t) : 0u;
+            if (++t == T) { t = 0; ++i; }
+          }
+          if (p0 + 8 <= nP) {
+            *(uint4*)(rv + p0) = make_uint4(h[0] | h[1] << 16, h[2] | h[3] << 16, h[4] | h[5] << 16, h[6] | h[7] << 16);
+          } else {
+            for (int k = 0; p0 + k < nP; ++k) rv[p0 + k] = (uint16_t)h[k];
+          }
+        }
+      } else {
+        for (int pl = lane; pl < nP; pl += 64) rv[pl] = (uint16_t)val(pl, pl / T, pl % T);
+      }
+    } else if (nP > 16 * 64) {
+      rmw(std::integral_constant<int, 32>{});
+    } else if (nP > 4 * 64) {
+      rmw(std::integral_constant<int, 16>{});
+    } else if (nP > 64) {
+      rmw(std::integral_constant<int, 4>{});
+    } else {
+      rmw(std::integral_constant<int, 1>{});
+    }
+#endif
+    GS_STAMP(5);
     if constexpr (ADV) {
       // P4: every non-dropped copy of a rejected message is an invalid delivery
       // of its sender (RejectMessage, then DuplicateMessage on the invalid

@@ -163,8 +163,13 @@ __device__ __forceinline__ int lane_prefix(int x, int* total) {
 //   step 4: per-edge results and reply RPCs written once.
 // Id lists (IWANT requests / responses) are sets: their order in the arena is
 // irrelevant to every reader.
-template <int WPL>
-__global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, int cur, int head, int cutMode) {
+// ADV (host-selected: attacker behaviours, validators / gater, phantom ids, or
+// a possible MaxIHaveLength cut) compiles in the IWANT-spam replies, silent
+// squatters, the dynamic peertx hash, phantom ids and the cuts; the honest
+// instantiation carries none of them.
+template <int WPL, bool ADV>
+__global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, int cur, int head, int cutModeArg) {
+  const int cutMode = ADV ? cutModeArg : 0;
   __shared__ uint64_t scache[64 * WPL];  // v's mcache windows (handleIWant, step 2)
   uint64_t* const sseen = scache;        // then v's seen row (handleIHave, step 3)
   // step 2's peertx hash; the step-3 arrays below live in the same LDS once
@@ -217,7 +222,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     pHb = d.cPruneHb[prv][r];
     ihaveT = d.cIhave[prv][r];
     iwRec = d.cIwant[prv][r];
-    if (d.cSpam[prv] != nullptr) spRec = d.cSpam[prv][r];  // IWANT spam RPC (an extra reply-group RPC)
+    if (ADV && d.cSpam[prv] != nullptr) spRec = d.cSpam[prv][r];  // IWANT spam RPC (an extra reply-group RPC)
     ph = d.peerhave[e];
     ia = d.iasked[e];
     u = d.col[e];
@@ -342,7 +347,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
   }
 
   GS_STAMPB(1);
-  const bool silent = behaves(d, v, GS_BEHAVE_NO_FORWARD);  // a squatter serves nothing, sends nothing
+  const bool silent = ADV && behaves(d, v, GS_BEHAVE_NO_FORWARD);  // a squatter serves nothing, sends nothing
   if (silent) gateIWant = gateSpam = false;
   // ---- step 2: handleIWant — serve cached messages at most GossipRetransmission
   // times per peer; the IHAVE-reply list and the IWANT-spam list of a sender
@@ -354,9 +359,10 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     __shared__ int sSpOff[64], sSpN[64], sItI[64], sCntS[64];
     // the peertx hash: static, or a larger dynamic table (IWANT-spam runs)
     extern __shared__ __attribute__((aligned(16))) uint32_t smemH[];
-    const bool big = d.ptxCap > GS_PTX;
+    const bool big = ADV && d.ptxCap > GS_PTX;
     unsigned int* const hT = big ? (unsigned int*)(smemH + GS_CUTLDS / 4) : sH;
     const int hbits = big ? d.ptxHBits : 10;
+    const int ptxCap = ADV ? d.ptxCap : GS_PTX;  // the honest instantiation always has GS_PTX
     const int hN = 1 << hbits;
     for (int w = lane; w < W; w += 64) {
       uint64_t x = 0;
@@ -380,7 +386,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     __syncthreads();
     const int ptxN = d.ptxN[v];
     for (int q = lane; q < ptxN; q += 64) {
-      const unsigned long long ent = d.ptx[(int64_t)v * d.ptxCap + q];
+      const unsigned long long ent = d.ptx[(int64_t)v * ptxCap + q];
       const unsigned int e32 = ptx_to32(ent);
       int hsl = ptx_hash(e32 & ~0xFFu, hbits);
       while (atomicCAS(&hT[hsl], 0u, e32) != 0u) hsl = (hsl + 1) & (hN - 1);
@@ -402,7 +408,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     };
     // mcache.GetForPeer finds the id (mcache.go:66-80); a phantom id is never served
     auto cached = [&](int slot) {
-      return ((scache[slot >> 6] >> (slot & 63)) & 1) && d.slotKind[slot] != GS_MSG_PHANTOM;
+      return ((scache[slot >> 6] >> (slot & 63)) & 1) && !(ADV && d.slotKind[slot] == GS_MSG_PHANTOM);
     };
     // pass a: increments and per-sender served counts
     for (int b = lane; b < totalItems; b += 64) {
@@ -460,11 +466,11 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
         const unsigned int e32 = hT[q0 + lane];
         int tot;
         const int pos = kept + lane_prefix(e32 != 0u ? 1 : 0, &tot);
-        if (e32 && pos < d.ptxCap) d.ptx[(int64_t)v * d.ptxCap + pos] = ptx_to64(e32);
+        if (e32 && pos < ptxCap) d.ptx[(int64_t)v * ptxCap + pos] = ptx_to64(e32);
         kept += tot;
       }
-      if (kept > d.ptxCap && lane == 0) set_err(d, E_PEERTX);
-      if (lane == 0) d.ptxN[v] = kept < d.ptxCap ? kept : d.ptxCap;
+      if (kept > ptxCap && lane == 0) set_err(d, E_PEERTX);
+      if (lane == 0) d.ptxN[v] = kept < ptxCap ? kept : ptxCap;
     }
     __syncthreads();  // sH is reused by step 3
   }
@@ -793,7 +799,7 @@ __global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, i
     d.cIhave[prv][r] = 0;
     d.cIwant[prv][r] = -1;
     d.cIresp[prv][r] = -1;
-    if (d.cSpam[prv] != nullptr) {
+    if (ADV && d.cSpam[prv] != nullptr) {
       d.cSpam[prv][r] = -1;
       d.cNSrv[prv][r] = 0;
     }

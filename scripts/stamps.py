@@ -31,6 +31,10 @@ def main():
     for i, nm in enumerate(names):
         print(f"{nm}: mean {d[:, i].mean():.0f} cycles  p50 {np.median(d[:, i]):.0f}  p99 {np.percentile(d[:, i], 99):.0f}")
     print("total mean", d.sum(1).mean())
+    s5 = buf.reshape(-1, 8)[: len(buf) // 16, :6].astype(np.int64)
+    s5 = s5[(s5[:, 0] > 0) & (s5[:, 4] > 0) & (s5[:, 5] > 0)]
+    if len(s5):
+        print(f"  pass3 rmw only: mean {(s5[:, 5] - s5[:, 3]).mean():.0f}, pass2b stores: mean {(s5[:, 4] - s5[:, 5]).mean():.0f}")
     c = buf.reshape(-1, 8)[: len(buf) // 16, 5:8].astype(np.int64)
     print("copies/node mean", c[:, 0].mean(), "pass-1 list-load cycles mean", c[:, 1].mean(), "pass-1 delivery-drain cycles mean",
           c[:, 2].mean())
