@@ -94,10 +94,7 @@ def algorithmic_bytes(kernel, eng, wl, per_hop):
         items = per_hop["deliveries"] + per_hop["published"]   # frontier-list entries written per hop
         list_reads = 4.0 * items * fwd_edges / N     # each list is read by the neighbours it forwards to
         list_writes = 4.0 * items
-        # pending-delivery counts per (edge, topic): written to the hop's ring
-        # slot (2 B, no read) when the engine keeps a ring, else a 4 B read +
-        # write of dlt
-        pending = (2.0 if per_hop.get("ring") else 8.0) * T * E
+        pending = 8.0 * T * E                        # pending-delivery counts, read + write per (edge, topic)
         seen = 16.0 * N * per_hop["active_words"]    # seen words of the active window, read + write
         meta = 49.0 * E                              # rev, col, fwd masks, IWANT ref, S0 memo, direct, mesh
         b = list_reads + list_writes + pending + seen + meta
@@ -114,9 +111,6 @@ def algorithmic_bytes(kernel, eng, wl, per_hop):
         # score0 w 8, sdirty w 1
         mesh_pairs = per_hop.get("mesh_pairs", 0)
         return E * (37.0 * T + 25) + 24.0 * mesh_pairs, dict(E=E, T=T, mesh_pairs=mesh_pairs)
-    if kernel == "ring_fold":
-        # per (edge, topic): the used ring slots (2 B each) read, dlt read + written
-        return E * T * (2.0 * per_hop.get("ring_slots", 0) + 8.0), dict(E=E, T=T)
     if kernel == "score":
         # full pass: per (edge, topic) flags 1 + fmd/mfp/imd 24 + pending 4 (+ mmd, meshTime when
         # active); per edge col 4 + app 8 + p6 8 + bp 8 + out 8
@@ -274,9 +268,6 @@ def main():
     per_hop = {"deliveries": (c1["deliveries"] - c0["deliveries"]) / nh,
                "published": (c1["published"] - c0["published"]) / nh,
                "active_words": float(np.mean([active_words(eng, wl, hop0 + i) for i in range(nh)])),
-               # the pending-count ring is in use when its fold kernel ran (once per refresh)
-               "ring": kstats.get("ring_fold", (0, 0))[1] > 0,
-               "ring_slots": nh / max(1, kstats.get("ring_fold", (0, 1))[1]),
                "mesh_pairs": int(np.bitwise_count(eng.mesh()[eng.edge_range[0]:eng.edge_range[1]]).sum(dtype=np.int64))}
     bytes_per_launch, bytes_info = algorithmic_bytes(dom, eng, wl, per_hop)
     roofline = None
@@ -304,7 +295,7 @@ def main():
     # the score kernels' rooflines too (north-star target: >= 50% of HBM on
     # score / propagation): refreshScores streams every (edge, topic) record
     rooflines = {}
-    for k in ("refresh", "ring_fold"):
+    for k in ("refresh",):
         if k in kstats and kstats[k][1]:
             b_k, _ = algorithmic_bytes(k, eng, wl, per_hop)
             ms_k = kstats[k][0] / kstats[k][1]

@@ -19,7 +19,6 @@
 #define GS_MAX_WPL 4   // words per lane in the node-wave kernels: W <= 256
 #define GS_QCAP 320    // phase A delivery queue (>= 63 pending + 256 appended per sub-round)
 #define GS_BMAP 32     // phase A: list blocks mapped to senders without a search (64 per entry)
-#define GS_RING_MAX 16 // pending-count ring slots (a slot adds <= 255 per field: 16 * 255 < 2^16 - 2^15)
 #define GS_TABLE 64    // promise table entries per node (one per lane)
 #define GS_PTX 512     // IWANT-retransmission (mcache peertx) entries per node
 #define GS_CUTS 64     // IHAVE entries above MaxIHaveLength one node can cut per hop
@@ -152,14 +151,6 @@ struct Dev {
   int32_t anyImd;                 // 0: no invalid delivery ever recorded, imd is all 0 (P4 = 0)
   uint32_t* dlt;                  // [E][T]: deliveries not yet folded into fmd / mmd,
                                   // (+1s to fmd) | (+1s to mmd) << 16 (see eff_fmd)
-  // Per-hop pending counts of NARROW hops: phase A writes ring slot ringSlot
-  // ((+1s to fmd) | (+1s to mmd) << 8 per pair, every pair of the node, so no
-  // slot needs clearing) instead of a read-modify-write of dlt; slots
-  // [0, nRing) hold counts not yet folded into dlt (k_ring_fold, refresh)
-  uint16_t* ring;                 // [slot][E][T]
-  int64_t ringStride;             // pairs per slot
-  int32_t nRing;                  // slots readers must add to dlt
-  int32_t ringSlot;               // the slot phase A writes this hop, -1: dlt read-modify-write
   int64_t *graftTime, *meshTime;  // [T][E]
   uint8_t* flags;                 // [T][E] bit0 inMesh, bit1 P3 active
   double* bp;                     // [E] behaviourPenalty
@@ -265,18 +256,43 @@ __device__ __forceinline__ int wave_sum_int(int v) {
 
 // k smallest (key, lane) among candidate lanes: the keyed "shuffle then take
 // k" of gs_rng.h.  k <= 0 selects every candidate (getPeers count semantics).
+// Radix selection from the key's top bit down, one ballot per bit: the
+// candidates whose key has a 0 at the bit are all smaller than those with a
+// 1, so either all of them are taken (and the search continues among the
+// ones) or the search narrows to them.  Random keys separate n candidates
+// after about log2(n) bits; equal keys fall back to the lowest lanes.
 __device__ __forceinline__ bool select_k(bool cand, uint64_t key, int k) {
   const int lane = lane_id();
-  unsigned long long m = __ballot(cand);
-  if (k <= 0 || __popcll(m) <= k) return cand;
-  int rank = 0;
-  while (m) {
-    int j = __ffsll((long long)m) - 1;
-    m &= m - 1;
-    uint64_t kj = lane_get64(key, j);
-    if (kj < key || (kj == key && j < lane)) rank++;
+  unsigned long long act = __ballot(cand);
+  int n = __popcll(act);
+  if (k <= 0 || n <= k) return cand;
+  unsigned long long sel = 0;
+  int need = k;
+  for (int b = 63; b >= 0; --b) {
+    const unsigned long long z = __ballot(((act >> lane) & 1) && !((key >> b) & 1));
+    const int nz = __popcll(z);
+    if (nz <= need) {
+      sel |= z;
+      need -= nz;
+      act &= ~z;
+      n -= nz;
+    } else {
+      act = z;
+      n = nz;
+    }
+    if (need == 0) break;
+    if (n == need) {  // every remaining candidate is needed
+      sel |= act;
+      need = 0;
+      break;
+    }
   }
-  return cand && rank < k;
+  while (need > 0 && act) {  // identical keys: lowest lanes first
+    sel |= act & (~act + 1);
+    act &= act - 1;
+    need--;
+  }
+  return (sel >> lane) & 1;
 }
 
 // "+1, cap" applied n times — markFirstMessageDelivery / markDuplicate-
@@ -306,22 +322,6 @@ __device__ __forceinline__ double eff_fmd(const TopicP& tp, double fmd, uint32_t
 __device__ __forceinline__ double eff_mmd(const TopicP& tp, double mmd, uint32_t q) {
   return (q >> 16) ? add_ones_capped(mmd, (int)(q >> 16), tp.MmdCap) : mmd;
 }
-// dlt's pending counts plus those of the unfolded ring slots, as (+1s to fmd)
-// | (+1s to mmd) << 16; the sum stays below 2^16 per field (E_DELTA bounds dlt,
-// a slot adds at most 255 per field, at most GS_RING_MAX slots)
-__device__ __forceinline__ uint32_t pend_q(const Dev& d, int64_t i) {
-  uint32_t q = d.dlt[i];
-  for (int r = 0; r < d.nRing; ++r) {
-    const uint32_t x = d.ring[(int64_t)r * d.ringStride + i];
-    q += (x & 0xFFu) | ((x >> 8) << 16);
-  }
-  return q;
-}
-// Clears the pending counts of pair i (they were folded by the caller).
-__device__ __forceinline__ void pend_clear(const Dev& d, int64_t i) {
-  d.dlt[i] = 0;
-  for (int r = 0; r < d.nRing; ++r) d.ring[(int64_t)r * d.ringStride + i] = 0;
-}
 
 // One topic's contribution topicScore * TopicWeight (score.go:265-311) of
 // pair i, split into its loads (all issued at once) and its arithmetic.
@@ -334,7 +334,7 @@ struct TermIn {
 __device__ __forceinline__ TermIn term_load(const Dev& d, int64_t i) {
   TermIn x;
   x.fl = d.flags[i];
-  x.q = pend_q(d, i);
+  x.q = d.dlt[i];
   x.mt = d.meshTime[i];
   x.mm = d.mmd[i];
   x.fmd = d.fmd[i];
@@ -431,13 +431,12 @@ __device__ __forceinline__ void stats_prune(const Dev& d, int64_t e, int t) {
   d.sdirty[e] = 1;
   const uint8_t fl = d.flags[i];
   const TopicP& tp = d.tp[t];
-  const uint32_t q = pend_q(d, i);
+  const uint32_t q = d.dlt[i];
   double mm = d.mmd[i];
-  if (q >> 16) {  // fold the pending deliveries: the deficit reads the mesh counter
+  if (q >> 16) {  // fold the pending mesh deliveries: the deficit reads the counter
     mm = eff_mmd(tp, mm, q);
     d.mmd[i] = mm;
-    if (q & 0xFFFF) d.fmd[i] = eff_fmd(tp, d.fmd[i], q);
-    pend_clear(d, i);
+    d.dlt[i] = q & 0xFFFF;
   }
   const double thr = tp.MmdThreshold;
   if ((fl & 2) && mm < thr) {
@@ -474,24 +473,10 @@ __device__ __forceinline__ int wave_incl_sum(int x) {
 __device__ __forceinline__ int lane_rank(uint64_t m) {
   return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
-// select_k for wave-uniform call sites that can spare 64 u64 of LDS (skey):
-// the candidates' keys are compacted in lane order, and every lane counts the
-// smaller ones in one broadcast-read loop (no per-candidate scalar work).
-// Same result as select_k: ties by lane, since compaction keeps lane order.
+// Former LDS rank-loop variant (kept for its call sites): now select_k.
 __device__ __forceinline__ bool select_k_lds(bool cand, uint64_t key, int k, uint64_t* skey) {
-  const unsigned long long m = __ballot(cand);
-  const int n = __popcll(m);
-  if (k <= 0 || n <= k) return cand;
-  const int pos = lane_rank(m);
-  __syncthreads();  // previous users of skey are done
-  if (cand) skey[pos] = key;
-  __syncthreads();
-  int rank = 0;
-  for (int q = 0; q < n; ++q) {
-    const uint64_t kq = skey[q];
-    rank += (kq < key || (kq == key && q < pos)) ? 1 : 0;
-  }
-  return cand && rank < k;
+  (void)skey;  // the radix selection needs no LDS
+  return select_k(cand, key, k);
 }
 
 // Value of lane 63 (wave-uniform).

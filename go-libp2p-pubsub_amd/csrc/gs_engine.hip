@@ -52,15 +52,6 @@ struct gs_engine {
   int64_t retireHops = 0;
   std::vector<int32_t> topicLive;  // per-topic live message count (phase-A counter width)
   int64_t hopsSinceFold = 0, foldEvery = 1;  // pending-delivery fold cadence (dlt)
-  int ringR = 0, nRing = 0;                   // pending-count ring: slots, slots in use
-  // folds the ring's used slots into dlt (readers of dlt alone may follow)
-  void ringFold() {
-    if (!nRing) return;
-    const int64_t pairs = (e1 - e0) * (int64_t)T;
-    if (pairs) k_ring_fold<<<(unsigned)(((pairs + 7) / 8 + 255) / 256), 256, 0, stream>>>(d);
-    nRing = 0;
-    d.nRing = 0;
-  }
   std::vector<uint64_t> yWord, yTabH;          // phase A young-slot tables (per hop)
   int64_t refreshedHop = -1;                 // hop of the last refreshScores (S0 exact after it)
   int maxAge = 0;
@@ -459,21 +450,6 @@ int gs_engine::start() {
   if (!ok) { gs_set_error("device allocation failed (per-(edge, topic) state)"); return GS_ENOMEM; }
   x.backoff -= shift; x.fmd -= shift; x.mmd -= shift; x.mfp -= shift; x.imd -= shift;
   x.dlt -= shift; x.graftTime -= shift; x.meshTime -= shift; x.flags -= shift;
-  // pending-count ring: one slot per hop between two refreshes (<= GS_RING_MAX),
-  // at most 48 GB; fewer than 2 slots: phase A keeps its dlt read-modify-write
-  x.ring = nullptr; x.ringStride = (int64_t)TE; x.nRing = 0; x.ringSlot = -1;
-  ringR = 0;
-  if (scoring) {
-    int64_t R = std::min<int64_t>(GS_RING_MAX, sp.DecayInterval / cfg.hop_ns);
-    R = std::min<int64_t>(R, (int64_t)((48ull << 30) / (2 * TE)));
-    if (R >= 2) {
-      uint16_t* rb = dalloc<uint16_t>((size_t)R * TE);
-      if (rb) {
-        x.ring = rb - shift;
-        ringR = (int)R;
-      }
-    }
-  }
   x.bp = dalloc<double>(E); x.peerhave = dalloc<int32_t>(E); x.iasked = dalloc<int32_t>(E);
   chk(x.score0); chk(x.score1); chk(x.backoff); chk(x.fmd); chk(x.mmd); chk(x.mfp); chk(x.imd);
   chk(x.graftTime); chk(x.meshTime); chk(x.flags); chk(x.bp); chk(x.peerhave); chk(x.iasked);
@@ -756,13 +732,6 @@ int gs_engine::stepOne() {
     const bool hasUnc = d.needAge || (adv && d.pmaskRow != nullptr);
     size_t lds = (narrow ? 2 : 4) * nCnt + 16 * (size_t)nR + (size_t)nYp + (hasUnc ? 4 * nCnt : 0);
     if (adv) lds += 4 * nCnt + 4 * 64 * 4 + 8 * 64 + 8 * (size_t)nR;
-    // NARROW hops write their counts to the next ring slot (folding a full ring first)
-    if (narrow && ringR > 0 && scoring) {
-      if (nRing == ringR) ringFold();
-      d.ringSlot = nRing;
-    } else {
-      d.ringSlot = -1;
-    }
     TIMED(this, GS_K_PHASE_A, launch_wpl(W, [&](auto w) {
             if (!nOwn) return;
             constexpr int WV = decltype(w)::value;
@@ -777,11 +746,6 @@ int gs_engine::stepOne() {
               k_phase_a<WV, false, false><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR, nYp);
             }
           }));
-    if (d.ringSlot >= 0) {
-      nRing++;
-      d.nRing = nRing;
-      d.ringSlot = -1;
-    }
   }
   if (!retireWords.empty()) {
     if ((int)retireWords.size() > retireCap) {
@@ -825,15 +789,12 @@ int gs_engine::stepOne() {
           }));
   }
   if (refreshDue(now)) {
-    if (nRing) TIMED(this, GS_K_RING_FOLD, ringFold());
     TIMED(this, GS_K_REFRESH, (k_refresh_rows<<<nblk(eOwn, GS_RG), 64, 0, stream>>>(d, now)));
     refreshedHop = h;
     hopsSinceFold = 0;
   } else if (scoring && ++hopsSinceFold >= foldEvery) {
     // pending delivery counts are 16-bit: fold them before they can overflow
     k_fold_all<<<pb, 256, 0, stream>>>(d);
-    nRing = 0;
-    d.nRing = 0;
     hopsSinceFold = 0;
   }
   if (gaterDecayDue(now)) {  // peerGater.background ticker (peer_gater.go:204-217)
@@ -1421,10 +1382,7 @@ int gs_set_topic_score_params(gs_engine* g, int32_t topic, const gs_topic_score_
   g->tscored[topic] = 1;
   if (!g->started) return GS_OK;
   TopicP tp = to_dev(*p, g->scoring);
-  if (g->scoring) {
-    g->ringFold();
-    k_fold<<<nblk(g->E, 256), 256, 0, g->stream>>>(g->d, topic);  // with the old caps
-  }
+  if (g->scoring) k_fold<<<nblk(g->E, 256), 256, 0, g->stream>>>(g->d, topic);  // with the old caps
   HIPCHECK(hipMemcpyAsync(g->dTp + topic, &tp, sizeof(TopicP), hipMemcpyHostToDevice, g->stream));
   HIPCHECK(hipMemsetAsync(g->d.sdirty, 1, (size_t)g->E, g->stream));  // every score may have changed
   if (existed && g->scoring &&
@@ -1554,11 +1512,7 @@ int gs_read_backoff(gs_engine* g, int64_t* expire) { return copy_back_pairs(g, e
 int gs_read_topic_stats(gs_engine* g, double* fmd, double* mmd, double* mfp, double* imd, int64_t* mesh_time,
                         int64_t* graft_time, uint8_t* flags) {
   int rc;
-  if (g->started && g->scoring) {
-    k_fold_all<<<nblk((int64_t)g->E * g->T, 256), 256, 0, g->stream>>>(g->d);
-    g->nRing = 0;
-    g->d.nRing = 0;
-  }
+  if (g->started && g->scoring) k_fold_all<<<nblk((int64_t)g->E * g->T, 256), 256, 0, g->stream>>>(g->d);
   if ((rc = copy_back_pairs(g, fmd, g->d.fmd))) return rc;
   if ((rc = copy_back_pairs(g, mmd, g->d.mmd))) return rc;
   if ((rc = copy_back_pairs(g, mfp, g->d.mfp))) return rc;

@@ -206,11 +206,11 @@ __global__ __launch_bounds__(64) void k_refresh_rows(Dev d, int64_t now) {
   }
 }
 
-// Folds the pending deliveries of every pair (dlt and the ring) into fmd / mmd.
+// Folds the pending deliveries of every pair into fmd / mmd.
 __global__ void k_fold_all(Dev d) {
   const int64_t p = d.e0 * d.T + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= d.e1 * d.T) return;
-  const uint32_t q = pend_q(d, p);
+  const uint32_t q = d.dlt[p];
   if (!q) return;
   int64_t e;
   int t;
@@ -218,39 +218,7 @@ __global__ void k_fold_all(Dev d) {
   const TopicP& tp = d.tp[t];
   d.fmd[p] = eff_fmd(tp, d.fmd[p], q);
   d.mmd[p] = eff_mmd(tp, d.mmd[p], q);
-  d.dlt[p] = 0;  // the host forgets the ring slots (nRing = 0)
-}
-
-// Folds the ring's slots [0, nRing) into dlt: 8 pairs per thread, one 16-byte
-// load per slot; the host then sets nRing = 0.
-__global__ void k_ring_fold(Dev d) {
-  const int64_t p0 = d.e0 * d.T + 8 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
-  const int64_t pe = d.e1 * d.T;
-  if (p0 >= pe) return;
-  uint32_t f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (p0 + 8 <= pe && (p0 & 7) == 0) {
-    for (int r = 0; r < d.nRing; ++r) {
-      const uint4 x = *(const uint4*)(d.ring + (int64_t)r * d.ringStride + p0);
-      const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        f[2 * k] += (w[k] & 0xFFu) | (((w[k] >> 8) & 0xFFu) << 16);
-        f[2 * k + 1] += ((w[k] >> 16) & 0xFFu) | ((w[k] >> 24) << 16);
-      }
-    }
-  } else {
-    for (int r = 0; r < d.nRing; ++r)
-      for (int k = 0; k < 8 && p0 + k < pe; ++k) {
-        const uint32_t x = d.ring[(int64_t)r * d.ringStride + p0 + k];
-        f[k] += (x & 0xFFu) | ((x >> 8) << 16);
-      }
-  }
-  for (int k = 0; k < 8 && p0 + k < pe; ++k) {
-    if (!f[k]) continue;
-    const uint32_t q = d.dlt[p0 + k];
-    if ((q & 0xFFFF) + (f[k] & 0xFFFF) > 0xFFFF || (q >> 16) + (f[k] >> 16) > 0xFFFF) set_err(d, E_DELTA);
-    d.dlt[p0 + k] = q + f[k];
-  }
+  d.dlt[p] = 0;
 }
 
 // Folds the pending deliveries of topic t into fmd / mmd.
@@ -1135,33 +1103,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
 #ifndef GS_EXP_NOPASS3
     // a batch no larger than the node's pairs need: a batch slot past nP is a
     // scratch store (config3: 32 pairs, one slot)
-    if (NARROW && d.ringSlot >= 0) {
-      // the hop's counts go to ring slot ringSlot: stores only, every pair of
-      // the node (zeros included), 8 pairs per 16-byte store when aligned
-      uint16_t* const rv = d.ring + (int64_t)d.ringSlot * d.ringStride + base * T;
-      auto val = [&](int pl, int i, int t) -> uint32_t {
-        const uint32_t q = upd(pl, i, t, 0u);  // nf | addM << 16, each <= 255 (NARROW)
-        return (q & 0xFFu) | ((q >> 16) << 8);
-      };
-      if (((base * T) & 7) == 0) {
-        for (int p0 = 8 * lane; p0 < nP; p0 += 8 * 64) {
-          int i = p0 / T, t = p0 - (p0 / T) * T;
-          uint32_t h[8];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            h[k] = p0 + k < nP ? val(p0 + k, i, t) : 0u;
-            if (++t == T) { t = 0; ++i; }
-          }
-          if (p0 + 8 <= nP) {
-            *(uint4*)(rv + p0) = make_uint4(h[0] | h[1] << 16, h[2] | h[3] << 16, h[4] | h[5] << 16, h[6] | h[7] << 16);
-          } else {
-            for (int k = 0; p0 + k < nP; ++k) rv[p0 + k] = (uint16_t)h[k];
-          }
-        }
-      } else {
-        for (int pl = lane; pl < nP; pl += 64) rv[pl] = (uint16_t)val(pl, pl / T, pl % T);
-      }
-    } else if (nP > 16 * 64) {
+    if (nP > 16 * 64) {
       rmw(std::integral_constant<int, 32>{});
     } else if (nP > 4 * 64) {
       rmw(std::integral_constant<int, 16>{});

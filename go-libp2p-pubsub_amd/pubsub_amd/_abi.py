@@ -181,7 +181,7 @@ ABI_FUNCTIONS = [
 ]
 
 KERNEL_NAMES = ["score", "refresh", "join", "fanout", "fwd", "phase_a", "publish", "phase_b",
-                "hb_pre", "heartbeat", "ring_fold"]
+                "hb_pre", "heartbeat"]
 
 
 def bind(path):
