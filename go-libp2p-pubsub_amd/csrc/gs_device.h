@@ -77,7 +77,17 @@ struct Dev {
   const int32_t* rev;
   const uint8_t* outbound;
   const uint8_t* direct;
-  const uint64_t* sub;
+  const uint64_t* sub;      // [N] the node's own subscriptions (p.mySubs)
+  const uint64_t* subA;     // [N] its announced subscriptions: what its peers' topic maps hold
+  // connection churn (gs_schedule_events); nullptr: every connection up, every
+  // peer's score record present and connected
+  uint8_t* alive;           // [E] the connection of the edge is up
+  uint8_t* rstate;          // [E] peerScore record of the edge's peer: 0 none, 1 connected, 2 retained
+  int64_t* rexpire;         // [E] retained record expiry (score.go:634)
+  const uint32_t* ipv4;     // [N] (P6 recount)
+  const uint8_t* ipWL;      // [N] the node's IP is whitelisted for P6
+  int64_t RetainScore;
+  int32_t IPThr;
   // score params
   const TopicP* tp;
   const double* app;
@@ -195,6 +205,9 @@ __device__ __forceinline__ bool behaves(const Dev& d, int v, unsigned bit) {
 #define GS_TRACE_COPY 100  // internal: one delivered copy; the host turns every
                            // copy but the delivering one into DUPLICATE_MESSAGE
 __device__ __forceinline__ bool is_traced(const Dev& d, int v) { return d.traced != nullptr && d.traced[v] != 0; }
+__device__ __forceinline__ bool edge_up(const Dev& d, int64_t e) { return d.alive == nullptr || d.alive[e] != 0; }
+// Score(p) of an observer without a record of p is 0 (score.go:246-249)
+__device__ __forceinline__ bool has_record(const Dev& d, int64_t e) { return d.rstate == nullptr || d.rstate[e] != 0; }
 __device__ __forceinline__ void set_err(const Dev& d, int code);
 __device__ __forceinline__ void trace_emit(const Dev& d, int64_t hop, int type, int node, int peer, int topic,
                                            int64_t msg, int phase, int reason = 0) {
@@ -411,7 +424,7 @@ __device__ __forceinline__ double edge_score_wave(const Dev& d, int64_t e, doubl
   double score = 0.0;
   for (int t = 0; t < d.T; ++t)
     if ((scoredT >> t) & 1) score += lds[t];
-  return score_tail_v(d, score, app, p6, b);
+  return has_record(d, e) ? score_tail_v(d, score, app, p6, b) : 0.0;
 }
 
 // peerScore.Graft — score.go:640-658 (scored topics only)

@@ -63,6 +63,25 @@ struct gs_engine {
   std::vector<double> app;
   std::vector<uint32_t> ipv4;
   std::vector<std::pair<uint32_t, uint32_t>> whitelist;
+  // connection churn and subscription changes (gs_schedule_events)
+  struct Event { int64_t hop; int32_t kind, a, b; };
+  std::vector<Event> events;
+  size_t nextEv = 0;
+  struct Ann { int node, topic; bool sub; };
+  std::vector<Ann> pendAnn;            // announcements arriving next hop
+  std::vector<uint64_t> subA;          // announced subscriptions (host copy of d.subA)
+  std::vector<uint8_t> aliveH;         // [E] host copy of d.alive
+  bool churnOn = false;
+  bool churnWindow = false;            // events scheduled before the first publish: wide window
+  uint64_t* dSubA = nullptr;
+  uint64_t* dSubOwn = nullptr;
+  double* dP6w = nullptr;              // writable view of d.p6 (k_p6)
+  int32_t* dEv = nullptr;
+  int64_t evCap = 0;
+  bool p6Live() const { return scoring && sp.IPColocationFactorWeight != 0 && !ipv4.empty(); }
+  int enableChurn();
+  int applyEvents(int64_t h);
+  int uploadList(const std::vector<int32_t>& v);
   bool graphSet = false, started = false;
   // schedule
   int64_t hop = 0;
@@ -178,7 +197,8 @@ struct gs_engine {
   // arrive much later through gossip, so the window then spans the gossip
   // history twice over.
   void setWindow() {
-    const bool adv = topicVal != 0 || gaterOn || behaveAll != 0;
+    // (churn too: a peer that joins or reconnects late catches up through gossip)
+    const bool adv = topicVal != 0 || gaterOn || behaveAll != 0 || churnWindow;
     maxAge = (adv ? gp.HistoryLength + gp.HistoryGossip + 3 : 3) * H;
     retireHops = maxAge + (int64_t)(gp.HistoryLength + 2) * H;
     if (cfg.router != GS_ROUTER_GOSSIPSUB) retireHops = maxAge + 2;
@@ -361,6 +381,7 @@ int gs_engine::start() {
   uint8_t* dOut = dalloc<uint8_t>(E); chk(dOut);
   uint8_t* dDir = dalloc<uint8_t>(E); chk(dDir);
   uint64_t* dSub = dalloc<uint64_t>(N); chk(dSub);
+  dSubA = dalloc<uint64_t>(N); chk(dSubA);
   double* dApp = dalloc<double>(N); chk(dApp);
   double* dP6 = dalloc<double>(E); chk(dP6);
   dTp = dalloc<TopicP>(T); chk(dTp);
@@ -372,13 +393,19 @@ int gs_engine::start() {
   HIPCHECK(hipMemcpyAsync(dOut, outbound.data(), E, hipMemcpyHostToDevice, stream));
   HIPCHECK(hipMemcpyAsync(dDir, direct.data(), E, hipMemcpyHostToDevice, stream));
   HIPCHECK(hipMemcpyAsync(dSub, sub.data(), N * 8, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipMemcpyAsync(dSubA, sub.data(), N * 8, hipMemcpyHostToDevice, stream));
+  subA = sub;
+  dSubOwn = dSub;
+  dP6w = dP6;
   HIPCHECK(hipMemcpyAsync(dApp, app.data(), N * 8, hipMemcpyHostToDevice, stream));
   HIPCHECK(hipMemcpyAsync(dP6, p6.data(), E * 8, hipMemcpyHostToDevice, stream));
   std::vector<TopicP> htp(T);
   for (int t = 0; t < T; ++t) htp[t] = to_dev(tps[t], scoring && tscored[t]);
   HIPCHECK(hipMemcpyAsync(dTp, htp.data(), T * sizeof(TopicP), hipMemcpyHostToDevice, stream));
   x.rowptr = dRowptr; x.col = dCol; x.esrc = dEsrc; x.rev = dRev; x.outbound = dOut; x.direct = dDir;
-  x.sub = dSub; x.app = dApp; x.p6 = dP6; x.tp = dTp;
+  x.sub = dSub; x.subA = dSubA; x.app = dApp; x.p6 = dP6; x.tp = dTp;
+  x.alive = nullptr; x.rstate = nullptr; x.rexpire = nullptr; x.ipv4 = nullptr; x.ipWL = nullptr;
+  x.RetainScore = sp.RetainScore; x.IPThr = sp.IPColocationFactorThreshold;
 
   x.seen = dalloc<uint64_t>(NW); chk(x.seen);
   x.hist = dalloc<uint64_t>((size_t)R * NW); chk(x.hist);
@@ -577,6 +604,10 @@ int gs_engine::start() {
     HIPCHECK(hipMemcpyAsync(x.lastpub, lp.data(), lp.size() * 8, hipMemcpyHostToDevice, stream));
     HIPCHECK(hipStreamSynchronize(stream));
   }
+  if (!events.empty()) {
+    const int rc = enableChurn();
+    if (rc) return rc;
+  }
   started = true;
   return uploadMessages();
 }
@@ -624,10 +655,132 @@ static void launch_wpl(int W, F f) {
   }
 }
 
+// Connection churn state (gs_schedule_events): connection flags, score-record
+// states and the P6 inputs, allocated on the first scheduled event.
+int gs_engine::enableChurn() {
+  if (churnOn) return GS_OK;
+  auto* al = dalloc<uint8_t>(E);
+  auto* rs = scoring ? dalloc<uint8_t>(E) : nullptr;
+  auto* rx = scoring ? dalloc<int64_t>(E) : nullptr;
+  auto* ip = dalloc<uint32_t>(N);
+  auto* wl = dalloc<uint8_t>(N);
+  if (!al || (scoring && (!rs || !rx)) || !ip || !wl) { gs_set_error("device allocation failed (churn state)"); return GS_ENOMEM; }
+  HIPCHECK(hipMemsetAsync(al, 1, (size_t)E, stream));
+  if (rs) HIPCHECK(hipMemsetAsync(rs, 1, (size_t)E, stream));
+  std::vector<uint32_t> iph(N, 0);
+  std::vector<uint8_t> wlh(N, 0);
+  for (int v = 0; v < N; ++v) {
+    iph[v] = ipv4.empty() ? 0u : ipv4[v];
+    for (auto& nm : whitelist)
+      if ((iph[v] & nm.second) == (nm.first & nm.second)) { wlh[v] = 1; break; }
+  }
+  HIPCHECK(hipMemcpyAsync(ip, iph.data(), (size_t)N * 4, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipMemcpyAsync(wl, wlh.data(), (size_t)N, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipStreamSynchronize(stream));  // iph / wlh are pageable
+  d.alive = al; d.rstate = rs; d.rexpire = rx; d.ipv4 = ip; d.ipWL = wl;
+  aliveH.assign((size_t)E, 1);
+  churnOn = true;
+  return GS_OK;
+}
+
+int gs_engine::uploadList(const std::vector<int32_t>& v) {
+  if ((int64_t)v.size() > evCap) {
+    int32_t* p = nullptr;
+    const int64_t cap = std::max<int64_t>(1024, 2 * (int64_t)v.size());
+    HIPCHECK(hipMalloc(&p, (size_t)cap * 4));
+    allocs.push_back(p);
+    dEv = p;
+    evCap = cap;
+  }
+  HIPCHECK(hipMemcpyAsync(dEv, v.data(), v.size() * 4, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipStreamSynchronize(stream));  // v is pageable
+  return GS_OK;
+}
+
+// The events of hop h, at its start (the oracle's Sim::applyEvents): the
+// announcements of hop h - 1 reach the peers, then every disconnect, connect,
+// leave and join of hop h in that order.
+int gs_engine::applyEvents(int64_t h) {
+  const int64_t now = h * cfg.hop_ns;
+  const int cur = (int)(h & 1), prv = cur ^ 1;
+  bool subAChanged = false, subChanged = false, recChanged = false;
+  for (const Ann& an : pendAnn) {
+    const uint64_t bit = 1ull << an.topic;
+    subA[an.node] = an.sub ? (subA[an.node] | bit) : (subA[an.node] & ~bit);
+    subAChanged = true;
+  }
+  pendAnn.clear();
+  size_t end = nextEv;
+  while (end < events.size() && events[end].hop == h) end++;
+  std::vector<int32_t> down, up, leave, join;
+  auto edgeOf = [&](int a, int b) -> int64_t {
+    auto bgn = col.begin() + rowptr[a], fin = col.begin() + rowptr[a + 1];
+    auto it = std::lower_bound(bgn, fin, b);
+    return (int64_t)(it - col.begin());
+  };
+  for (int pass = GS_EV_DISCONNECT; pass <= GS_EV_JOIN; ++pass)
+    for (size_t k = nextEv; k < end; ++k) {
+      const Event& ev = events[k];
+      if (ev.kind != pass) continue;
+      if (pass <= GS_EV_CONNECT) {
+        const int64_t ab = edgeOf(ev.a, ev.b), ba = edgeOf(ev.b, ev.a);
+        const uint8_t want = pass == GS_EV_CONNECT ? 1 : 0;
+        if (aliveH[ab] == want) continue;
+        aliveH[ab] = aliveH[ba] = want;
+        auto& lst = pass == GS_EV_CONNECT ? up : down;
+        lst.push_back((int32_t)ab);
+        lst.push_back((int32_t)ba);
+      } else {
+        const uint64_t bit = 1ull << ev.b;
+        const bool joinEv = pass == GS_EV_JOIN;
+        if (((sub[ev.a] & bit) != 0) == joinEv) continue;
+        sub[ev.a] = joinEv ? (sub[ev.a] | bit) : (sub[ev.a] & ~bit);
+        subChanged = true;
+        pendAnn.push_back({ev.a, ev.b, joinEv});
+        auto& lst = joinEv ? join : leave;
+        lst.push_back(ev.a);
+        lst.push_back(ev.b);
+      }
+    }
+  nextEv = end;
+  if (subAChanged) HIPCHECK(hipMemcpyAsync(dSubA, subA.data(), (size_t)N * 8, hipMemcpyHostToDevice, stream));
+  if (subChanged) HIPCHECK(hipMemcpyAsync(dSubOwn, sub.data(), (size_t)N * 8, hipMemcpyHostToDevice, stream));
+  if (subAChanged || subChanged) HIPCHECK(hipStreamSynchronize(stream));  // pageable sources
+  if (!down.empty()) {
+    int rc = uploadList(down);
+    if (rc) return rc;
+    k_edge_down<<<(unsigned)down.size(), 64, 0, stream>>>(d, dEv, h, now, prv);
+    recChanged = true;
+  }
+  if (!up.empty()) {
+    int rc = uploadList(up);
+    if (rc) return rc;
+    k_edge_up<<<nblk((int64_t)up.size(), 256), 256, 0, stream>>>(d, dEv, (int)up.size(), h);
+    recChanged = true;
+  }
+  if (recChanged && p6Live() && n1 > n0) k_p6<<<n1 - n0, 64, 0, stream>>>(d, dP6w);
+  if (!leave.empty()) {
+    int rc = uploadList(leave);
+    if (rc) return rc;
+    k_leave<<<(unsigned)(leave.size() / 2), 64, 0, stream>>>(d, dEv, h, cur);
+  }
+  if (!join.empty()) {
+    int rc = uploadList(join);
+    if (rc) return rc;
+    k_join_pairs<<<(unsigned)(join.size() / 2), 64, 0, stream>>>(d, dEv, h, now, cur);
+  }
+  HIPCHECK(hipGetLastError());
+  return GS_OK;
+}
+
 int gs_engine::stepOne() {
   const int64_t h = hop;
   const int64_t now = h * cfg.hop_ns;
   const int cur = (int)(h & 1);
+  if (churnOn) {
+    const int rc = applyEvents(h);
+    if (rc) return rc;
+  }
   const bool gossip = cfg.router == GS_ROUTER_GOSSIPSUB;
   // this hop's local publishes [b, e)
   size_t b = nextMsg, e = b;
@@ -790,6 +943,7 @@ int gs_engine::stepOne() {
   }
   if (refreshDue(now)) {
     TIMED(this, GS_K_REFRESH, (k_refresh_rows<<<nblk(eOwn, GS_RG), 64, 0, stream>>>(d, now)));
+    if (churnOn && p6Live() && nOwn) k_p6<<<nOwn, 64, 0, stream>>>(d, dP6w);  // expired records
     refreshedHop = h;
     hopsSinceFold = 0;
   } else if (scoring && ++hopsSinceFold >= foldEvery) {
@@ -1309,6 +1463,35 @@ int gs_set_validation(gs_engine* g, const uint8_t* topic_validator, int32_t queu
       if (topic_validator[t]) g->topicVal |= 1ull << t;
   g->valQueue = queue_per_hop;
   g->setWindow();
+  return GS_OK;
+}
+
+int gs_schedule_events(gs_engine* g, int32_t n, const int32_t* kind, const int32_t* a, const int32_t* b,
+                       const int64_t* hop) {
+  if (n < 0 || (n > 0 && (!kind || !a || !b || !hop))) { gs_set_error("gs_schedule_events: bad arguments"); return GS_EINVAL; }
+  if (!g->graphSet) { gs_set_error("graph not set"); return GS_ESTATE; }
+  if (g->gaterOn) { gs_set_error("connection churn with the peer gater is not supported"); return GS_EUNSUPPORTED; }
+  if (g->world > 1) { gs_set_error("connection churn needs an unpartitioned engine"); return GS_EUNSUPPORTED; }
+  int64_t last = g->events.empty() ? std::max<int64_t>(1, g->hop) : std::max(g->hop, g->events.back().hop);
+  auto isEdge = [&](int x, int y) {
+    auto bgn = g->col.begin() + g->rowptr[x], fin = g->col.begin() + g->rowptr[x + 1];
+    auto it = std::lower_bound(bgn, fin, y);
+    return it != fin && *it == y;
+  };
+  for (int32_t i = 0; i < n; ++i) {
+    bool ok = hop[i] >= last && hop[i] >= 1 && kind[i] >= GS_EV_DISCONNECT && kind[i] <= GS_EV_JOIN &&
+              a[i] >= 0 && a[i] < g->N;
+    if (ok && kind[i] <= GS_EV_CONNECT) ok = b[i] >= 0 && b[i] < g->N && isEdge(a[i], b[i]);
+    if (ok && kind[i] >= GS_EV_LEAVE) ok = b[i] >= 0 && b[i] < g->T;
+    if (!ok) { gs_set_error("gs_schedule_events: bad event (kind, nodes, topic or hop order)"); return GS_EINVAL; }
+    last = hop[i];
+  }
+  for (int32_t i = 0; i < n; ++i) g->events.push_back({hop[i], kind[i], a[i], b[i]});
+  if (n > 0 && !g->started && g->mId.empty()) {
+    g->churnWindow = true;  // late joiners catch up through gossip: the wide message window
+    g->setWindow();
+  }
+  if (g->started && n > 0) return g->enableChurn();
   return GS_OK;
 }
 

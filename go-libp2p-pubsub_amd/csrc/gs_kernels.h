@@ -110,7 +110,7 @@ __global__ __launch_bounds__(64) void k_score_rows(Dev d, double* __restrict__ o
     double score = 0.0;
     for (int t = 0; t < T; ++t)
       if ((scoredT >> t) & 1) score += sT[lane * 65 + t];
-    score = score_tail(d, e, score);
+    score = has_record(d, e) ? score_tail(d, e, score) : 0.0;
     if (MODE == 0) out[e] = score;
     if (MODE == 1 || MODE == 3) { d.score0[e] = score; d.sdirty[e] = 0; }
     if (MODE >= 2) d.score1[e] = score;
@@ -132,6 +132,29 @@ __global__ __launch_bounds__(64) void k_refresh_rows(Dev d, int64_t now) {
   const TopicP& tp = d.tp[tl];
   const bool act = lane < T && tp.scored;
   const uint64_t scoredT = __ballot(act);
+  // churn: a retained record is not decayed; past its expiry it is dropped
+  // (score.go:500-509); the host then recounts P6 (removeIPs)
+  uint64_t frozen = 0;
+  if (d.rstate != nullptr) {
+    for (int j = 0; j < ng; ++j) {
+      const int64_t ej = e0 + j;
+      const uint8_t st = d.rstate[ej];
+      if (st == 1) continue;
+      frozen |= 1ull << j;
+      if (st == 2 && now > d.rexpire[ej]) {
+        for (int t = lane; t < T; t += 64) {
+          const int64_t i = ej * T + t;
+          d.fmd[i] = 0; d.mmd[i] = 0; d.mfp[i] = 0; d.imd[i] = 0; d.dlt[i] = 0;
+          d.meshTime[i] = 0; d.graftTime[i] = 0; d.flags[i] = 0;
+        }
+        if (lane == 0) {
+          d.bp[ej] = 0;
+          d.rstate[ej] = 0;
+        }
+      }
+    }
+    __syncthreads();  // the dropped records' zeros before the loads below
+  }
   for (int j0 = 0; j0 < ng; j0 += GS_SB) {
     uint32_t q[GS_SB];
     double fmd[GS_SB], mmd[GS_SB], mfp[GS_SB], imd[GS_SB];
@@ -153,7 +176,9 @@ __global__ __launch_bounds__(64) void k_refresh_rows(Dev d, int64_t now) {
       if (j0 + k >= ng) break;
       const int64_t i = (e0 + j0 + k) * T + tl;
       double term = 0.0;
-      if (act) {
+      if (act && ((frozen >> (j0 + k)) & 1)) {
+        term = topic_term(d, tp, i);  // not decayed: the stored record as it is
+      } else if (act) {
         TermIn x;
         x.q = 0;
         double v = eff_fmd(tp, fmd[k], q[k]) * tp.FmdDecay;
@@ -192,11 +217,14 @@ __global__ __launch_bounds__(64) void k_refresh_rows(Dev d, int64_t now) {
   __syncthreads();
   if (lane < ng) {
     const int64_t e = e0 + lane;
-    double b = d.bp[e] * d.BPDecay;
-    if (b < d.DecayToZero) b = 0;
-    d.bp[e] = b;
+    double b = d.bp[e];
+    if (!((frozen >> lane) & 1)) {
+      b *= d.BPDecay;
+      if (b < d.DecayToZero) b = 0;
+      d.bp[e] = b;
+    }
     double score = 0.0;
-    if (d.scoring) {
+    if (d.scoring && has_record(d, e)) {
       for (int t = 0; t < T; ++t)
         if ((scoredT >> t) & 1) score += sT[lane * 65 + t];
       score = score_tail(d, e, score);
@@ -254,7 +282,7 @@ __global__ __launch_bounds__(64) void k_join(Dev d, int64_t hop, int64_t now, in
   const bool valid = lane < deg;
   const int64_t e = base + lane;
   const int v = valid ? d.col[e] : 0;
-  const uint64_t subv = valid ? d.sub[v] : 0;
+  const uint64_t subv = valid ? d.subA[v] : 0;
   const bool dir = valid && d.direct[e];
   const double s = valid ? d.score0[e] : 0.0;
   uint64_t meshl = 0, gj = 0;
@@ -302,7 +330,7 @@ __global__ __launch_bounds__(64) void k_fanout_pub(Dev d, const int32_t* __restr
   const bool present = (d.fanoutPresent[u] >> t) & 1;
   const int have = __popcll(__ballot((fo >> t) & 1));
   if (!present || have == 0) {
-    const bool cand = valid && ((d.sub[v] >> t) & 1) && !d.direct[e] && d.score0[e] >= d.publishThr;
+    const bool cand = valid && edge_up(d, e) && ((d.subA[v] >> t) & 1) && !d.direct[e] && d.score0[e] >= d.publishThr;
     const uint64_t key = gs_key64(d.seed, GS_SITE_GP_FANOUT_PUB, u, (uint32_t)hop, v, t);
     const bool sel = select_k(cand, key, d.D);
     const unsigned long long any = __ballot(sel);
@@ -321,7 +349,7 @@ __global__ void k_fwd(Dev d, int cur) {
   const int64_t e = d.e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= d.e1) return;
   const int u = d.esrc[e];
-  const uint64_t sv = d.sub[d.col[e]];
+  const uint64_t sv = d.subA[d.col[e]];  // the peer's subscriptions as u knows them
   uint64_t relay, pub;
   if (d.router != 2) {  // floodsub.go:85-99 / randomsub.go:115-150: every topic peer
     relay = sv;
@@ -338,6 +366,7 @@ __global__ void k_fwd(Dev d, int cur) {
       pub = (dir ? sv : 0) | (m & joined) | (d.fanout[e] & ~joined);
     }
   }
+  if (!edge_up(d, e)) relay = pub = 0;  // no connection: nothing is sent
   // partitioned engine: a forwarding set that changed since this parity was
   // last exchanged must reach the receiver's rank (gs_exchange.h)
   if (d.xmark && (d.fwdRelay[cur][e] != relay || d.fwdPub[cur][e] != pub)) d.xmark[e] = 1;
@@ -537,8 +566,11 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     u = d.col[e];
     r = d.rev[e];
     jr = (int)(r - d.rowptr[u]);
-    relay = d.fwdRelay[prv][r] & sv;
-    pub = d.fwdPub[prv][r] & sv;
+    // what the sender sent (counted as transmissions even when v is not
+    // subscribed: a peer that left is still in the sender's mesh until its
+    // PRUNE arrives); only copies of v's own topics are handled (pubsub.go:959)
+    relay = d.fwdRelay[prv][r];
+    pub = d.fwdPub[prv][r];
     const int64_t ir = d.cIresp[prv][r];
     if (ir >= 0) {
       irOff = (int)(ir >> 24);
@@ -780,7 +812,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
               nSent += sent;
               if (sent && isGray) ++nGray;  // one RPC per relayed message, all dropped
             }
-            sn[c] = sent && !isGray;
+            sn[c] = sent && !isGray && ((sv >> t) & 1);
             en[c] = (uint32_t)slot | ((uint32_t)i << 16);
           }
         }
@@ -822,7 +854,10 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     if (ADV && ctlGated) {
       nGatedCopies += nSrvRpc;  // the served replies' payload is ignored
     } else {
-      for (int k = 0; k < irN; ++k) deliver(lane, d.pool[prv][irOff + k], false);
+      for (int k = 0; k < irN; ++k) {
+        const int slot = d.pool[prv][irOff + k];
+        if ((sv >> (int)__umulhi((unsigned)slot, d.stMagic)) & 1) deliver(lane, slot, false);
+      }
     }
   }
   if constexpr (ADV) {
@@ -1257,7 +1292,8 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
         while (y) {
           const int b = __ffsll((long long)y) - 1;
           y &= y - 1;
-          rs_select(d, v, deg, valid ? u : -1, valid ? d.sub[u] : 0, wsrc * 64 + b, sFirst[fidx(rks, b)]);
+          rs_select(d, v, deg, valid ? u : -1, valid && edge_up(d, base + lane) ? d.subA[u] : 0, wsrc * 64 + b,
+                    sFirst[fidx(rks, b)]);
         }
       }
     }
@@ -1396,7 +1432,7 @@ __global__ __launch_bounds__(64) void k_publish_rs(Dev d, int b) {
   const int64_t base = d.rowptr[u];
   const int deg = (int)(d.rowptr[u + 1] - base);
   const int p = lane < deg ? d.col[base + lane] : -1;
-  const uint64_t subp = p >= 0 ? d.sub[p] : 0;
+  const uint64_t subp = p >= 0 && edge_up(d, base + lane) ? d.subA[p] : 0;
   rs_select(d, u, deg, p, subp, slot, 255);
 }
 

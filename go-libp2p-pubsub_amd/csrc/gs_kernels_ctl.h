@@ -877,7 +877,7 @@ __global__ __launch_bounds__(64) void k_hb_pre(Dev d, int64_t now, uint64_t tick
     const int pe = lane_get(edge, q);
     const unsigned long long same = __ballot(broken && edge == pe);
     bm &= ~same;
-    if (lane == 0) {
+    if (lane == 0 && has_record(d, base + pe)) {  // AddPenalty needs a record (score.go:681-684)
       d.bp[base + pe] += (double)__popcll(same);
       d.sdirty[base + pe] = 1;
     }
@@ -974,7 +974,7 @@ __global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t no
   int nmT = 0;
   if (lane < d.T)
     for (int w = lane * d.Wt; w < (lane + 1) * d.Wt; ++w) nmT += __popcll(sgw[w]);
-  const uint64_t subv = valid ? d.sub[vcol] : 0;
+  const uint64_t subv = valid && edge_up(d, e) ? d.subA[vcol] : 0;  // topic peers: connected, announced
   uint64_t meshl = valid ? d.mesh[e] : 0;
   uint64_t fanl = valid ? d.fanout[e] : 0;
   double S = valid ? d.score1[e] : 0.0;
@@ -1257,4 +1257,205 @@ __global__ void k_read_deliv(Dev d, int slot, int64_t pubhop, int32_t* hop, int3
   hop[v] = (int32_t)(pubhop + d.age[(int64_t)v * d.S + slot]);
   const uint8_t f = d.ffrom[(int64_t)v * d.S + slot];
   from[v] = f == 255 ? -1 : d.col[d.rowptr[v] + f];
+}
+
+// ---------------------------------------------------------------- churn events
+// (gs_schedule_events, applied at the start of their hop)
+//
+// A connection goes down: one wave per directed edge e = (u -> v), run for
+// both directions.  handleDeadPeers + GossipSubRouter.RemovePeer (pubsub.go:
+// 521-551, gossipsub.go:534-547): out of the mesh and fanout, no pending
+// gossip, the RPCs u sent to v during the previous hop are lost (outbox and
+// forwarding sets of parity prv).  tracer.RemovePeer -> peerScore.RemovePeer
+// (score.go:602-635): a positive score drops the record, otherwise it is
+// retained for RetainScore with firstMessageDeliveries reset and the mesh
+// delivery penalty applied (lane = topic).
+__global__ __launch_bounds__(64) void k_edge_down(Dev d, const int32_t* __restrict__ edges, int64_t hop,
+                                                  int64_t now, int prv) {
+  __shared__ double sterm[64];
+  const int64_t e = edges[blockIdx.x];
+  const int lane = lane_id();
+  const int u = d.esrc[e], v = d.col[e];
+  double s = 0.0;
+  if (d.scoring && d.rstate != nullptr && d.rstate[e] == 1) s = edge_score_wave(d, e, sterm);
+  if (lane == 0) {
+    d.alive[e] = 0;
+    d.mesh[e] = 0;
+    d.fanout[e] = 0;
+    d.cPre[prv][e] = 0; d.cHb[prv][e] = 0; d.cGraftJoin[prv][e] = 0; d.cGraftHb[prv][e] = 0;
+    d.cPruneReply[prv][e] = 0; d.cPruneHb[prv][e] = 0; d.cIhave[prv][e] = 0;
+    d.cIwant[prv][e] = -1; d.cIresp[prv][e] = -1;
+    if (d.cSpam[prv] != nullptr) { d.cSpam[prv][e] = -1; d.cNSrv[prv][e] = 0; }
+    d.fwdRelay[prv][e] = 0;
+    d.fwdPub[prv][e] = 0;
+    d.sdirty[e] = 1;
+    if (is_traced(d, u)) trace_emit(d, hop, GS_TRACE_REMOVE_PEER, u, v, -1, -1, 0);  // trace.go:215
+  }
+  if (!d.scoring || d.rstate == nullptr || d.rstate[e] != 1) return;
+  const bool drop = s > 0;
+  for (int t = lane; t < d.T; t += 64) {
+    const int64_t i = tix(d, t, e);
+    if (drop) {
+      d.fmd[i] = 0; d.mmd[i] = 0; d.mfp[i] = 0; d.imd[i] = 0; d.dlt[i] = 0;
+      d.meshTime[i] = 0; d.graftTime[i] = 0; d.flags[i] = 0;
+      continue;
+    }
+    if (!d.tp[t].scored) continue;
+    const TopicP& tp = d.tp[t];
+    const uint32_t q = d.dlt[i];
+    const double mm = eff_mmd(tp, d.mmd[i], q);  // the pending mesh deliveries count
+    d.mmd[i] = mm;
+    d.fmd[i] = 0;
+    d.dlt[i] = 0;
+    const uint8_t fl = d.flags[i];
+    if ((fl & 1) && (fl & 2) && mm < tp.MmdThreshold) {
+      const double deficit = tp.MmdThreshold - mm;
+      d.mfp[i] += deficit * deficit;
+    }
+    d.flags[i] = fl & ~1;
+  }
+  if (lane == 0) {
+    if (drop) {
+      d.bp[e] = 0;
+      d.rstate[e] = 0;
+    } else {
+      d.rstate[e] = 2;
+      d.rexpire[e] = now + d.RetainScore;
+    }
+  }
+}
+
+// A connection comes back: AddPeer (gossipsub.go:505-532; peerScore.AddPeer
+// score.go:586-600 revives a retained record or starts an empty one).
+__global__ void k_edge_up(Dev d, const int32_t* __restrict__ edges, int n, int64_t hop) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int64_t e = edges[k];
+  d.alive[e] = 1;
+  if (d.rstate != nullptr) d.rstate[e] = 1;
+  d.sdirty[e] = 1;
+  if (is_traced(d, d.esrc[e])) trace_emit(d, hop, GS_TRACE_ADD_PEER, d.esrc[e], d.col[e], -1, -1, 0);
+}
+
+// ipColocationFactor (score.go:335-379) after the record set changed: per
+// observer (one wave per node, lane = edge) the peers with a record that share
+// the edge's IP.
+__global__ __launch_bounds__(64) void k_p6(Dev d, double* __restrict__ p6) {
+  const int v = d.n0 + blockIdx.x;
+  const int lane = lane_id();
+  const int64_t base = d.rowptr[v];
+  const int deg = (int)(d.rowptr[v + 1] - base);
+  const bool valid = lane < deg;
+  const int64_t e = base + lane;
+  const uint32_t ip = valid ? d.ipv4[d.col[e]] : 0u;
+  const bool rec = valid && ip != 0 && has_record(d, e);
+  int cnt = 0;
+  for (int j = 0; j < deg; ++j) {
+    const uint32_t ipj = (uint32_t)__builtin_amdgcn_readlane((int)ip, j);
+    const int recj = __builtin_amdgcn_readlane(rec ? 1 : 0, j);
+    cnt += (recj && ipj == ip) ? 1 : 0;
+  }
+  if (!valid) return;
+  double f = 0.0;
+  if (ip != 0 && !d.ipWL[d.col[e]] && cnt > d.IPThr) {
+    const double s = (double)(cnt - d.IPThr);
+    f = s * s;
+  }
+  p6[e] = f;
+}
+
+// Leave(topic) at node v (handleRemoveSubscription pubsub.go:665-686 ->
+// gossipsub.go:1062-1078): tracer.Leave, then for every mesh peer
+// tracer.Prune and a PRUNE RPC (sendPrune: a reply-group RPC of this hop).
+// One wave per (node, topic), lane = edge.
+__global__ __launch_bounds__(64) void k_leave(Dev d, const int32_t* __restrict__ pairs, int64_t hop, int cur) {
+  const int v = pairs[2 * blockIdx.x], t = pairs[2 * blockIdx.x + 1];
+  const int lane = lane_id();
+  const int64_t base = d.rowptr[v];
+  const int deg = (int)(d.rowptr[v + 1] - base);
+  const bool valid = lane < deg;
+  const int64_t e = base + lane;
+  const uint64_t bit = 1ull << t;
+  const bool traced = is_traced(d, v);
+  if (lane == 0 && traced) trace_emit(d, hop, d.router == 1 ? GS_TRACE_JOIN : GS_TRACE_LEAVE, v, -1, t, -1, 0);
+  if (d.router != 2) return;  // floodsub / randomsub: nothing else (randomsub.go:166-168 traces a Join)
+  const bool m = valid && (d.mesh[e] & bit);
+  const bool silent = behaves(d, v, GS_BEHAVE_NO_FORWARD);  // a squatter sends no control
+  if (m) {
+    d.mesh[e] &= ~bit;
+    stats_prune(d, e, t);
+    if (traced) trace_emit(d, hop, GS_TRACE_PRUNE, v, d.col[e], t, -1, 0);
+    if (!silent) {
+      d.cPruneReply[cur][e] |= bit;
+      d.cPre[cur][e] = (uint8_t)(d.cPre[cur][e] + 1);
+    }
+  }
+  const int np = __popcll(__ballot(m));
+  if (lane == 0 && np && !silent) ctr_add(d, C_PRUNES, (unsigned long long)np);
+}
+
+// Join(topic) at node v after the start (handleAddSubscription pubsub.go:
+// 692-713 -> gossipsub.go:1011-1060): reuse the fanout (dropping peers with a
+// negative score) topped up by getPeers, or getPeers(D); tracer.Join, then
+// tracer.Graft and one GRAFT RPC per peer.  Scores are exact: a memo below 0
+// is recomputed (the filter compares with 0).
+__global__ __launch_bounds__(64) void k_join_pairs(Dev d, const int32_t* __restrict__ pairs, int64_t hop,
+                                                   int64_t now, int cur) {
+  __shared__ double sterm[64];
+  const int v = pairs[2 * blockIdx.x], t = pairs[2 * blockIdx.x + 1];
+  const int lane = lane_id();
+  const int64_t base = d.rowptr[v];
+  const int deg = (int)(d.rowptr[v + 1] - base);
+  const bool valid = lane < deg;
+  const int64_t e = base + lane;
+  const uint64_t bit = 1ull << t;
+  const bool traced = is_traced(d, v);
+  if (lane == 0 && traced) trace_emit(d, hop, GS_TRACE_JOIN, v, -1, t, -1, 0);
+  if (d.router != 2) return;
+  const int vcol = valid ? d.col[e] : -1;
+  const bool inTopic = valid && edge_up(d, e) && ((d.subA[vcol] >> t) & 1);
+  const bool dir = valid && d.direct[e];
+  double s = valid ? d.score0[e] : 0.0;
+  if (d.scoring) {
+    unsigned long long xm = __ballot(valid && (d.sdirty[e] != 0 || !(s >= 0.0)));
+    while (xm) {
+      const int j = __ffsll((long long)xm) - 1;
+      xm &= xm - 1;
+      const double sj = edge_score_wave(d, base + j, sterm);
+      if (lane == j) s = sj;
+    }
+  } else {
+    s = 0.0;
+  }
+  const bool present = (d.fanoutPresent[v] >> t) & 1;
+  bool g;
+  if (present) {
+    const uint64_t fo = valid ? d.fanout[e] : 0;
+    g = valid && (fo & bit) && s >= 0;
+    const int have = __popcll(__ballot(g));
+    if (have < d.D) {
+      const uint64_t key = gs_key64(d.seed, GS_SITE_GP_JOIN, v, (uint32_t)hop, vcol, t);
+      g = g || select_k(inTopic && !g && !dir && s >= 0, key, d.D - have);
+    }
+    if (valid) d.fanout[e] = fo & ~bit;
+    if (lane == 0) {
+      d.fanoutPresent[v] &= ~bit;
+      d.lastpub[(int64_t)v * d.T + t] = INT64_MIN;
+    }
+  } else {
+    const uint64_t key = gs_key64(d.seed, GS_SITE_GP_JOIN, v, (uint32_t)hop, vcol, t);
+    g = select_k(inTopic && !dir && s >= 0, key, d.D);
+  }
+  const bool silent = behaves(d, v, GS_BEHAVE_NO_FORWARD);
+  if (g) {
+    d.mesh[e] |= bit;
+    stats_graft(d, e, t, now);
+    if (traced) trace_emit(d, hop, GS_TRACE_GRAFT, v, vcol, t, -1, 0);  // gossipsub.go:1057
+    if (!silent) {
+      d.cGraftJoin[cur][e] |= bit;
+      d.cPre[cur][e] = (uint8_t)(d.cPre[cur][e] + 1);
+    }
+  }
+  const int ng = __popcll(__ballot(g));
+  if (lane == 0 && ng && !silent) ctr_add(d, C_GRAFTS, (unsigned long long)ng);
 }

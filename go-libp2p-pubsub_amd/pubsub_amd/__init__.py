@@ -5,7 +5,7 @@ C-ABI in include/gossip_engine.h; the compute runs in the HIP library
 build/libgossip_engine.so (gfx950).
 """
 from ._abi import (GS_BEHAVE_GRAFT_SPAM, GS_BEHAVE_IHAVE_SPAM, GS_BEHAVE_IWANT_SPAM, GS_BEHAVE_NO_FORWARD, GS_MSG_IGNORE,  # noqa: F401
-                   GS_MSG_PHANTOM, GS_MSG_REJECT, GS_MSG_VALID, GS_ROUTER_FLOODSUB, GS_ROUTER_GOSSIPSUB,
+                   GS_EV_CONNECT, GS_EV_DISCONNECT, GS_EV_JOIN, GS_EV_LEAVE, GS_MSG_PHANTOM, GS_MSG_REJECT, GS_MSG_VALID, GS_ROUTER_FLOODSUB, GS_ROUTER_GOSSIPSUB,
                    GS_ROUTER_RANDOMSUB)
 from .params import (DefaultGossipSubParams, DefaultPeerGaterParams, GossipSubParams,  # noqa: F401
                      Hour, Microsecond, Millisecond, Minute, NewPeerGaterParams, PeerGaterParams,

@@ -27,6 +27,7 @@ GS_FLAG_RECORD_DELIVERIES = 1 << 2
 
 GS_MSG_VALID, GS_MSG_REJECT, GS_MSG_IGNORE, GS_MSG_PHANTOM = 0, 1, 2, 3
 GS_BEHAVE_NO_FORWARD, GS_BEHAVE_IWANT_SPAM, GS_BEHAVE_GRAFT_SPAM, GS_BEHAVE_IHAVE_SPAM = 1, 2, 4, 8
+GS_EV_DISCONNECT, GS_EV_CONNECT, GS_EV_LEAVE, GS_EV_JOIN = 0, 1, 2, 3
 REJECT_REASONS = ["blacklisted peer", "blacklisted source", "missing signature", "unexpected signature",
                   "unexpected auth info", "invalid signature", "validation queue full", "validation throttled",
                   "validation failed", "validation ignored", "self originated message"]  # tracer.go:27-38
@@ -155,6 +156,7 @@ ABI_FUNCTIONS = [
                                 C.POINTER(i64)]),
     ("gs_set_validation", C.c_int, [P, C.POINTER(u8), i32]),
     ("gs_set_behaviour", C.c_int, [P, C.POINTER(u8)]),
+    ("gs_schedule_events", C.c_int, [P, i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(i64)]),
     ("gs_step", C.c_int, [P, i64]),
     ("gs_sync", C.c_int, [P]),
     ("gs_set_topic_score_params", C.c_int, [P, i32, C.POINTER(TopicScoreParamsC)]),

@@ -230,6 +230,17 @@ class Engine:
         self.n_published += len(src)
         return ids
 
+    def schedule_events(self, kind, a, b, hop):
+        """Connection churn and subscription changes at the start of hop[i]
+        (gs_schedule_events): GS_EV_DISCONNECT / GS_EV_CONNECT of the connection
+        a[i] - b[i], GS_EV_LEAVE / GS_EV_JOIN of topic b[i] by node a[i]."""
+        kind = np.ascontiguousarray(kind, dtype=np.int32)
+        a = np.ascontiguousarray(a, dtype=np.int32)
+        b = np.ascontiguousarray(b, dtype=np.int32)
+        hop = np.ascontiguousarray(hop, dtype=np.int64)
+        _check(self.lib, self.lib.gs_schedule_events(self.h, len(kind), _ptr(kind, C.c_int32), _ptr(a, C.c_int32),
+                                                     _ptr(b, C.c_int32), _ptr(hop, C.c_int64)))
+
     def exchange_stats(self):
         """(host ms spent in the transport, bytes received from other ranks)."""
         ms, nb = C.c_double(), C.c_int64()

@@ -268,6 +268,36 @@ int gs_set_validation(gs_engine* eng, const uint8_t* topic_validator, int32_t qu
                                    (IHAVE spam, gossipsub_spam_test.go:196-222) */
 int gs_set_behaviour(gs_engine* eng, const uint8_t* behaviour /*[N]*/);
 
+/* Connection churn and subscription changes: a schedule of events, applied at
+ * the start of their hop in the order given (hops non-decreasing across calls,
+ * >= 1 and >= the current hop).
+ *   GS_EV_DISCONNECT (a, b): the connection between nodes a and b (an edge
+ *     pair of the graph) goes down.  Both hosts run handleDeadPeers
+ *     (pubsub.go:521-551): the peer leaves every topic map, then
+ *     GossipSubRouter.RemovePeer (gossipsub.go:534-547: mesh, fanout, pending
+ *     gossip dropped, tracer.RemovePeer -> peerScore.RemovePeer score.go:602-635:
+ *     a positive score is dropped, otherwise retained for RetainScore with
+ *     firstMessageDeliveries reset and the mesh delivery penalty applied).  RPCs
+ *     still in flight on the connection are lost.
+ *   GS_EV_CONNECT (a, b): the connection comes back: AddPeer on both hosts
+ *     (gossipsub.go:505-532, score.go:586-600 revives a retained record), the
+ *     hello packet's subscriptions known at once (pubsub.go:495-497).
+ *   GS_EV_LEAVE (a, topic b): node a unsubscribes (handleRemoveSubscription
+ *     pubsub.go:665-686): announce (the peers update their topic maps when it
+ *     arrives, next hop), then Leave (gossipsub.go:1062-1078: PRUNE every mesh
+ *     peer).
+ *   GS_EV_JOIN (a, topic b): node a subscribes (handleAddSubscription
+ *     pubsub.go:692-713): announce, then Join (gossipsub.go:1011-1060).
+ * An event that finds its state already (a connection down twice, a topic
+ * left twice) does nothing.  Not supported together with a partitioned engine
+ * or the peer gater (GS_EUNSUPPORTED). */
+#define GS_EV_DISCONNECT 0
+#define GS_EV_CONNECT 1
+#define GS_EV_LEAVE 2
+#define GS_EV_JOIN 3
+int gs_schedule_events(gs_engine* eng, int32_t n, const int32_t* kind, const int32_t* a, const int32_t* b,
+                       const int64_t* hop);
+
 /* Advances the simulation by `hops` lock-step hops. */
 int gs_step(gs_engine* eng, int64_t hops);
 /* Waits for all queued device work (no-op on the oracle). */

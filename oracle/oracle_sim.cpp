@@ -64,6 +64,7 @@ struct Node {
   std::map<int, std::set<int>> topics;   // p.topics (static subscriptions of peers)
   uint64_t mySubs = 0;                   // p.mySubs
   std::set<int64_t> seen;                // p.seenMessages (timecache, no expiry in-window)
+  std::set<int> dead;                    // neighbours whose connection is down (not in p.peers)
   // gossipsub router state — gossipsub.go:400-457
   std::map<int, std::set<int>> mesh, fanout;
   std::map<int, int64_t> lastpub;
@@ -103,6 +104,10 @@ struct Node {
   PruneEntry makePrune(int p, int topic);
   void heartbeat();
   void emitGossip(int topic, const std::set<int>& exclude);
+  void removePeer(int p);                // handleDeadPeers + RemovePeer
+  void addPeer(int p);                   // newPeerStream -> AddPeer + hello
+  void leaveTopic(int topic);            // handleRemoveSubscription -> Leave
+  void joinTopic(int topic);             // handleAddSubscription -> Join
   void applyIwantPenalties();
   void clearBackoff();
 };
@@ -128,6 +133,12 @@ struct Sim {
   int32_t valQueue = 0;            // validation queue entries per node per hop (0 = unlimited)
   std::vector<uint8_t> behave;     // GS_BEHAVE_* per node
   std::vector<uint8_t> msgKind;    // GS_MSG_* per message id
+  // churn / subscription events (gs_schedule_events), by hop
+  struct Event { int64_t hop; int32_t kind, a, b; };
+  std::vector<Event> sched;
+  size_t nextEvent = 0;
+  struct Ann { int node, topic; bool sub; };
+  std::vector<Ann> pendingAnn;     // subscription announcements arriving next hop
   int N = 0, T = 0;
   int64_t E = 0;
   std::vector<int64_t> rowptr;
@@ -177,6 +188,7 @@ struct Sim {
   }
   void start();
   void step();
+  void applyEvents(std::vector<std::map<int, std::vector<RPC>>>& inbox);
 };
 
 void Sim::emit(int type, int node, int peer, int topic, int64_t msg, int phase, int reason) {
@@ -206,6 +218,7 @@ double Node::Score(int p) { return sim->scoring ? score.score(p) : 0.0; }
 // simulator; pending gossip is piggybacked exactly as sendRPC does).
 void Node::sendRPC(int p, RPC rpc) {
   if ((behave & GS_BEHAVE_NO_FORWARD) && rpc.hasCtl) return;  // a squatter sends no control at all
+  if (dead.count(p)) return;  // gossipsub.go:1101-1104: no outbound queue for p
   auto g = gossip.find(p);
   if (g != gossip.end()) {  // piggybackGossip gossipsub.go:1736-1744
     rpc.hasCtl = true;
@@ -840,6 +853,123 @@ void Node::heartbeat() {
   mcache.Shift();
 }
 
+// handleDeadPeers (pubsub.go:521-551): the peer leaves every topic map, then
+// GossipSubRouter.RemovePeer (gossipsub.go:534-547) with tracer.RemovePeer
+// (trace.go:215) -> peerScore.RemovePeer (score.go:602-635), peerGater.RemovePeer.
+void Node::removePeer(int p) {
+  if (dead.count(p)) return;
+  dead.insert(p);
+  for (auto& kv : topics) kv.second.erase(p);
+  sim->emit(GS_TRACE_REMOVE_PEER, id, p, -1, -1, 0);
+  for (auto& kv : mesh) kv.second.erase(p);
+  for (auto& kv : fanout) kv.second.erase(p);
+  gossip.erase(p);
+  if (sim->scoring) score.RemovePeer(p, sim->now());
+  if (sim->gaterOn) gater.RemovePeer(p, sim->now());
+}
+
+// A new stream from p (pubsub.go:499-515): AddPeer (gossipsub.go:505-532,
+// tracer.AddPeer -> peerScore.AddPeer score.go:586-600, peerGater.AddPeer);
+// the hello packet's subscriptions (pubsub.go:495-497) are applied at once.
+void Node::addPeer(int p) {
+  if (!dead.count(p)) return;
+  dead.erase(p);
+  sim->emit(GS_TRACE_ADD_PEER, id, p, -1, -1, 0);
+  const int64_t e = sim->edgeIndex(id, p);
+  outbound[p] = sim->outboundE.empty() ? false : sim->outboundE[e] != 0;
+  if (sim->scoring) {
+    std::vector<uint32_t> ips;
+    if (!sim->ipv4.empty() && sim->ipv4[p] != 0) ips.push_back(sim->ipv4[p]);
+    score.AddPeer(p, ips);
+  }
+  if (sim->gaterOn) gater.AddPeer(p);
+  for (int t = 0; t < sim->T; ++t)
+    if ((sim->nodes[p].mySubs >> t) & 1) topics[t].insert(p);
+}
+
+// handleRemoveSubscription (pubsub.go:665-686): announce(topic, false), then
+// the router's Leave: gossipsub.go:1062-1078 (tracer.Leave, PRUNE to every mesh
+// peer), floodsub.go:106-108, randomsub.go:166-168 (which traces a Join).
+void Node::leaveTopic(int topic) {
+  const uint64_t bit = 1ull << topic;
+  if (!(mySubs & bit)) return;
+  mySubs &= ~bit;
+  if (sim->cfg.router == GS_ROUTER_RANDOMSUB) { sim->emit(GS_TRACE_JOIN, id, -1, topic, -1, 0); return; }
+  if (sim->cfg.router == GS_ROUTER_FLOODSUB) { sim->emit(GS_TRACE_LEAVE, id, -1, topic, -1, 0); return; }
+  auto gm = mesh.find(topic);
+  if (gm == mesh.end()) return;
+  sim->emit(GS_TRACE_LEAVE, id, -1, topic, -1, 0);
+  std::set<int> gmap = gm->second;
+  mesh.erase(gm);
+  for (int p : gmap) {
+    sim->emit(GS_TRACE_PRUNE, id, p, topic, -1, 0);  // tracer.Prune (gossipsub.go:1075)
+    if (sim->scoring) score.Prune(p, topic);
+    RPC r;  // sendPrune (gossipsub.go:1093-1097)
+    r.hasCtl = true;
+    r.ctl.prune.push_back(makePrune(p, topic));
+    sendRPC(p, std::move(r));
+  }
+}
+
+// handleAddSubscription (pubsub.go:692-713): announce(topic, true), then Join.
+void Node::joinTopic(int topic) {
+  const uint64_t bit = 1ull << topic;
+  if (mySubs & bit) return;
+  mySubs |= bit;
+  sim->emit(GS_TRACE_JOIN, id, -1, topic, -1, 0);  // tracer.Join gossipsub.go:1018, floodsub.go:103
+  join(topic);
+}
+
+// The events of this hop, at its start: first the subscription announcements
+// sent during the previous hop reach the peers that are still connected
+// (handleIncomingRPC processes subscriptions first, pubsub.go:915-941), then
+// the scheduled events: every disconnect, every connect, every leave, every
+// join (canonical order), each kind in schedule order.  A lost connection
+// drops what was in flight.
+void Sim::applyEvents(std::vector<std::map<int, std::vector<RPC>>>& inbox) {
+  for (const Ann& an : pendingAnn)
+    for (int p : nodes[an.node].nbrs) {
+      Node& np = nodes[p];
+      if (np.dead.count(an.node)) continue;
+      if (an.sub) np.topics[an.topic].insert(an.node); else np.topics[an.topic].erase(an.node);
+    }
+  pendingAnn.clear();
+  // one hop's events in four passes (disconnects, connects, leaves, joins),
+  // each in schedule order
+  size_t end = nextEvent;
+  while (end < sched.size() && sched[end].hop == hop) end++;
+  for (int pass = GS_EV_DISCONNECT; pass <= GS_EV_JOIN; ++pass)
+  for (size_t k = nextEvent; k < end; ++k) {
+    const Event& ev = sched[k];
+    if (ev.kind != pass) continue;
+    switch (ev.kind) {
+      case GS_EV_DISCONNECT:
+        if (nodes[ev.a].dead.count(ev.b)) break;
+        nodes[ev.a].removePeer(ev.b);
+        nodes[ev.b].removePeer(ev.a);
+        inbox[ev.a].erase(ev.b);
+        inbox[ev.b].erase(ev.a);
+        break;
+      case GS_EV_CONNECT:
+        if (!nodes[ev.a].dead.count(ev.b)) break;
+        nodes[ev.a].addPeer(ev.b);
+        nodes[ev.b].addPeer(ev.a);
+        break;
+      case GS_EV_LEAVE:
+        if (!((nodes[ev.a].mySubs >> ev.b) & 1)) break;
+        nodes[ev.a].leaveTopic(ev.b);
+        pendingAnn.push_back({ev.a, ev.b, false});
+        break;
+      case GS_EV_JOIN:
+        if ((nodes[ev.a].mySubs >> ev.b) & 1) break;
+        nodes[ev.a].joinTopic(ev.b);
+        pendingAnn.push_back({ev.a, ev.b, true});
+        break;
+    }
+  }
+  nextEvent = end;
+}
+
 void Sim::start() {
   nodes.assign(N, Node());
   if (record) deliv.assign(N, {});
@@ -888,6 +1018,7 @@ void Sim::step() {
   // Every per-node phase below touches only the node's own state (its router
   // maps, peerScore, mcache, outbox, counters and trace buffer) and reads
   // shared immutable data, so nodes run in parallel; the phase order is kept.
+  applyEvents(inbox);
   if (hop == 0) {  // Join: the GRAFTs it sends arrive in hop 1
 #pragma omp parallel for schedule(dynamic, 64)
     for (int u = 0; u < N; ++u)
@@ -1211,6 +1342,25 @@ int gs_set_behaviour(gs_engine* eng, const uint8_t* behaviour) {
   if (s.started) { set_error("behaviours must be set before the first step"); return GS_ESTATE; }
   s.behave.clear();
   if (behaviour) s.behave.assign(behaviour, behaviour + s.N);
+  return GS_OK;
+}
+
+int gs_schedule_events(gs_engine* eng, int32_t n, const int32_t* kind, const int32_t* a, const int32_t* b,
+                       const int64_t* hop) {
+  Sim& s = eng->sim;
+  if (n < 0 || (n > 0 && (!kind || !a || !b || !hop))) { set_error("gs_schedule_events: bad arguments"); return GS_EINVAL; }
+  if (!s.graphSet) { set_error("graph not set"); return GS_ESTATE; }
+  if (s.gaterOn) { set_error("connection churn with the peer gater is not supported"); return GS_EUNSUPPORTED; }
+  int64_t last = s.sched.empty() ? std::max<int64_t>(1, s.hop) : std::max(s.hop, s.sched.back().hop);
+  for (int32_t i = 0; i < n; ++i) {
+    bool ok = hop[i] >= last && hop[i] >= 1 && kind[i] >= GS_EV_DISCONNECT && kind[i] <= GS_EV_JOIN &&
+              a[i] >= 0 && a[i] < s.N;
+    if (ok && kind[i] <= GS_EV_CONNECT) ok = b[i] >= 0 && b[i] < s.N && s.edgeIndex(a[i], b[i]) >= 0;
+    if (ok && kind[i] >= GS_EV_LEAVE) ok = b[i] >= 0 && b[i] < s.T;
+    if (!ok) { set_error("gs_schedule_events: bad event (kind, nodes, topic or hop order)"); return GS_EINVAL; }
+    last = hop[i];
+  }
+  for (int32_t i = 0; i < n; ++i) s.sched.push_back({hop[i], kind[i], a[i], b[i]});
   return GS_OK;
 }
 

@@ -393,3 +393,108 @@ ADVERSARIAL = {
     "adversarial_mix_nogater": lambda lib, x=(): adversarial_mix(lib, gater=False, queue=0, seed=52, extra=x),
 }
 SCENARIOS.update(ADVERSARIAL)
+
+
+# ---------------------------------------------------------------- churn
+# Connection churn and subscription changes (gs_schedule_events): the
+# reference's RemovePeer / Prune / Graft tests restated, and a scored mix.
+from pubsub_amd import GS_EV_CONNECT, GS_EV_DISCONNECT, GS_EV_JOIN, GS_EV_LEAVE  # noqa: E402
+
+
+def _pairs_of(g, nodes):
+    """Every connection (a < b) touching one of `nodes`."""
+    rowptr, col, _ = g
+    out = set()
+    for u in nodes:
+        for v in col[rowptr[u]:rowptr[u + 1]]:
+            out.add((min(u, int(v)), max(u, int(v))))
+    return sorted(out)
+
+
+def churn_remove_peer(lib, extra=()):
+    """TestGossipsubRemovePeer (gossipsub_test.go:629-676): 20 hosts, denseConnect,
+    2 s of heartbeats, hosts 0-4 close (every connection down), a heartbeat, then
+    10 messages from hosts 5-19 that hosts 5-19 must all receive."""
+    n, seed = 20, 61
+    g = graphs.dense_connect(n, seed)
+    e = NewGossipSub(n, 1, g, graphs.all_subscribed(n, 1), WithRecordDeliveries(), WithSeed(seed),
+                     WithHop(HOP), WithMessageWindow(64), *extra, lib=lib)
+    pairs = _pairs_of(g, range(5))
+    e.schedule_events([GS_EV_DISCONNECT] * len(pairs), [a for a, _ in pairs], [b for _, b in pairs],
+                      [20] * len(pairs))
+    rng = np.random.default_rng(seed)
+    e.publish(5 + rng.integers(0, n - 5, 10), np.zeros(10, np.int32), 30 + np.arange(10))
+    return e, 60
+
+
+def churn_prune(lib, extra=()):
+    """TestGossipsubPrune (gossipsub_test.go:535-582): hosts 0-4 cancel their
+    subscription after the mesh formed (Leave -> PRUNE), 10 messages that
+    hosts 5-19 must all receive."""
+    n, seed = 20, 62
+    g = graphs.dense_connect(n, seed)
+    e = NewGossipSub(n, 1, g, graphs.all_subscribed(n, 1), WithRecordDeliveries(), WithSeed(seed),
+                     WithHop(HOP), WithMessageWindow(64), *extra, lib=lib)
+    e.schedule_events([GS_EV_LEAVE] * 5, list(range(5)), [0] * 5, [20] * 5)
+    rng = np.random.default_rng(seed)
+    e.publish(rng.integers(0, n, 10), np.zeros(10, np.int32), 21 + np.arange(10))
+    return e, 50
+
+
+def churn_graft(lib, extra=()):
+    """TestGossipsubGraft (gossipsub_test.go:584-627): a sparse graph whose hosts
+    subscribe one after another (Join -> GRAFT, announcements), then 100
+    messages that every host must receive."""
+    n, seed = 20, 63
+    g = graphs.sparse_connect(n, seed)
+    subs = np.zeros(n, dtype=np.uint64)
+    e = NewGossipSub(n, 1, g, subs, WithRecordDeliveries(), WithSeed(seed), WithHop(HOP), WithMessageWindow(256),
+                     *extra, lib=lib)
+    e.schedule_events([GS_EV_JOIN] * n, list(range(n)), [0] * n, list(range(10, 10 + n)))
+    rng = np.random.default_rng(seed)
+    e.publish(rng.integers(0, n, 100), np.zeros(100, np.int32), 45 + np.arange(100))
+    return e, 170
+
+
+def churn_scored(lib, n=240, k=16, topics=2, seed=65, msgs=400, hb=14, extra=()):
+    """A scored mix: 15% negative app scores and shared IPs (retained vs dropped
+    records, P6 recounted), random connections going down and coming back,
+    topics left and re-joined, Eth2 scoring with a RetainScore of 2 s."""
+    rng = np.random.default_rng(seed)
+    g = graphs.random_regular(n, k, seed)
+    subs = graphs.all_subscribed(n, topics)
+    sp = eth2_peer_score_params(topics)
+    sp.RetainScore = 2 * Second
+    thr = eth2_thresholds()
+    app = np.zeros(n)
+    app[rng.random(n) < 0.15] = -150.0
+    ipv4 = (rng.integers(0, 60, n) + (10 << 24)).astype(np.uint32)
+    e = NewGossipSub(n, topics, g, subs, WithPeerScore(sp, thr), WithRecordDeliveries(), WithSeed(seed),
+                     WithHop(HOP), WithMessageWindow(512), *extra, app_score=app, ipv4=ipv4, lib=lib)
+    pairs = _pairs_of(g, range(n))
+    ev = []
+    for h in range(12, hb * 10 - 10, 3):
+        for i in rng.choice(len(pairs), 4, replace=False):
+            a, b = pairs[i]
+            ev.append((h, GS_EV_DISCONNECT, a, b))
+            ev.append((h + int(rng.integers(5, 40)), GS_EV_CONNECT, a, b))
+        for _ in range(2):
+            a, t = int(rng.integers(0, n)), int(rng.integers(0, topics))
+            ev.append((h, GS_EV_LEAVE, a, t))
+            ev.append((h + int(rng.integers(3, 30)), GS_EV_JOIN, a, t))
+    ev.sort(key=lambda x: x[0])
+    e.schedule_events([x[1] for x in ev], [x[2] for x in ev], [x[3] for x in ev], [x[0] for x in ev])
+    src = rng.integers(0, n, msgs).astype(np.int32)
+    top = rng.integers(0, topics, msgs).astype(np.int32)
+    hops = (5 + (np.arange(msgs) * (hb * 10 - 20)) // msgs).astype(np.int64)
+    e.publish(src, top, hops)
+    return e, hb * 10 + 5
+
+
+CHURN = {
+    "churn_remove_peer": lambda lib, x=(): churn_remove_peer(lib, extra=x),
+    "churn_prune": lambda lib, x=(): churn_prune(lib, extra=x),
+    "churn_graft": lambda lib, x=(): churn_graft(lib, extra=x),
+    "churn_scored": lambda lib, x=(): churn_scored(lib, extra=x),
+}
+SCENARIOS.update(CHURN)
