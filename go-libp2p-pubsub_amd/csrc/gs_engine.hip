@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
 #include <tuple>
 #include <chrono>
 #include <cmath>
@@ -713,6 +714,7 @@ int gs_engine::applyEvents(int64_t h) {
   size_t end = nextEv;
   while (end < events.size() && events[end].hop == h) end++;
   std::vector<int32_t> down, up, leave, join;
+  std::map<int, uint64_t> leaveM, joinM;
   auto edgeOf = [&](int a, int b) -> int64_t {
     auto bgn = col.begin() + rowptr[a], fin = col.begin() + rowptr[a + 1];
     auto it = std::lower_bound(bgn, fin, b);
@@ -737,12 +739,19 @@ int gs_engine::applyEvents(int64_t h) {
         sub[ev.a] = joinEv ? (sub[ev.a] | bit) : (sub[ev.a] & ~bit);
         subChanged = true;
         pendAnn.push_back({ev.a, ev.b, joinEv});
-        auto& lst = joinEv ? join : leave;
-        lst.push_back(ev.a);
-        lst.push_back(ev.b);
+        (joinEv ? joinM : leaveM)[ev.a] |= bit;
       }
     }
   nextEv = end;
+  // one item per node: node, topic mask (lo, hi) — its topics run in one wave
+  for (auto* pr : {&leaveM, &joinM}) {
+    auto& lst = pr == &leaveM ? leave : join;
+    for (auto& kv : *pr) {
+      lst.push_back(kv.first);
+      lst.push_back((int32_t)(uint32_t)kv.second);
+      lst.push_back((int32_t)(uint32_t)(kv.second >> 32));
+    }
+  }
   if (subAChanged) HIPCHECK(hipMemcpyAsync(dSubA, subA.data(), (size_t)N * 8, hipMemcpyHostToDevice, stream));
   if (subChanged) HIPCHECK(hipMemcpyAsync(dSubOwn, sub.data(), (size_t)N * 8, hipMemcpyHostToDevice, stream));
   if (subAChanged || subChanged) HIPCHECK(hipStreamSynchronize(stream));  // pageable sources
@@ -762,12 +771,12 @@ int gs_engine::applyEvents(int64_t h) {
   if (!leave.empty()) {
     int rc = uploadList(leave);
     if (rc) return rc;
-    k_leave<<<(unsigned)(leave.size() / 2), 64, 0, stream>>>(d, dEv, h, cur);
+    k_leave<<<(unsigned)(leave.size() / 3), 64, 0, stream>>>(d, dEv, h, cur);
   }
   if (!join.empty()) {
     int rc = uploadList(join);
     if (rc) return rc;
-    k_join_pairs<<<(unsigned)(join.size() / 2), 64, 0, stream>>>(d, dEv, h, now, cur);
+    k_join_pairs<<<(unsigned)(join.size() / 3), 64, 0, stream>>>(d, dEv, h, now, cur);
   }
   HIPCHECK(hipGetLastError());
   return GS_OK;
@@ -942,7 +951,10 @@ int gs_engine::stepOne() {
           }));
   }
   if (refreshDue(now)) {
-    TIMED(this, GS_K_REFRESH, (k_refresh_rows<<<nblk(eOwn, GS_RG), 64, 0, stream>>>(d, now)));
+    if (churnOn)
+      TIMED(this, GS_K_REFRESH, (k_refresh_rows<true><<<nblk(eOwn, GS_RG), 64, 0, stream>>>(d, now)));
+    else
+      TIMED(this, GS_K_REFRESH, (k_refresh_rows<false><<<nblk(eOwn, GS_RG), 64, 0, stream>>>(d, now)));
     if (churnOn && p6Live() && nOwn) k_p6<<<nOwn, 64, 0, stream>>>(d, dP6w);  // expired records
     refreshedHop = h;
     hopsSinceFold = 0;

@@ -122,6 +122,9 @@ __global__ __launch_bounds__(64) void k_score_rows(Dev d, double* __restrict__ o
 // edge from the refreshed state into S0 (sdirty cleared): nothing but
 // refreshScores changed the state since the hop's message phase, so this is
 // the value the next S0 pass would compute.
+// CHURN: some connection may be down (gs_schedule_events): retained records
+// are not decayed and expire; the honest instantiation carries none of it.
+template <bool CHURN>
 __global__ __launch_bounds__(64) void k_refresh_rows(Dev d, int64_t now) {
   __shared__ double sT[GS_RG * 65];
   const int lane = lane_id();
@@ -135,7 +138,7 @@ __global__ __launch_bounds__(64) void k_refresh_rows(Dev d, int64_t now) {
   // churn: a retained record is not decayed; past its expiry it is dropped
   // (score.go:500-509); the host then recounts P6 (removeIPs)
   uint64_t frozen = 0;
-  if (d.rstate != nullptr) {
+  if (CHURN && d.rstate != nullptr) {
     for (int j = 0; j < ng; ++j) {
       const int64_t ej = e0 + j;
       const uint8_t st = d.rstate[ej];
@@ -176,7 +179,7 @@ __global__ __launch_bounds__(64) void k_refresh_rows(Dev d, int64_t now) {
       if (j0 + k >= ng) break;
       const int64_t i = (e0 + j0 + k) * T + tl;
       double term = 0.0;
-      if (act && ((frozen >> (j0 + k)) & 1)) {
+      if (CHURN && act && ((frozen >> (j0 + k)) & 1)) {
         term = topic_term(d, tp, i);  // not decayed: the stored record as it is
       } else if (act) {
         TermIn x;
@@ -218,13 +221,13 @@ __global__ __launch_bounds__(64) void k_refresh_rows(Dev d, int64_t now) {
   if (lane < ng) {
     const int64_t e = e0 + lane;
     double b = d.bp[e];
-    if (!((frozen >> lane) & 1)) {
+    if (!CHURN || !((frozen >> lane) & 1)) {
       b *= d.BPDecay;
       if (b < d.DecayToZero) b = 0;
       d.bp[e] = b;
     }
     double score = 0.0;
-    if (d.scoring && has_record(d, e)) {
+    if (d.scoring && (!CHURN || has_record(d, e))) {
       for (int t = 0; t < T; ++t)
         if ((scoredT >> t) & 1) score += sT[lane * 65 + t];
       score = score_tail(d, e, score);
@@ -557,7 +560,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
   const bool scoring = d.scoring != 0;
   // in-edge metadata (lane = in-edge)
   int u = 0, jr = -1, Ln = 0;
-  uint64_t relay = 0, pub = 0;
+  uint64_t relay = 0, pub = 0, relayAll = 0, pubAll = 0;
   bool gray = false;
   int irOff = 0, irN = 0;
   int64_t r = 0;
@@ -566,18 +569,20 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     u = d.col[e];
     r = d.rev[e];
     jr = (int)(r - d.rowptr[u]);
-    // what the sender sent (counted as transmissions even when v is not
-    // subscribed: a peer that left is still in the sender's mesh until its
-    // PRUNE arrives); only copies of v's own topics are handled (pubsub.go:959)
-    relay = d.fwdRelay[prv][r];
-    pub = d.fwdPub[prv][r];
+    // only copies of v's own topics are handled (pubsub.go:959); what the
+    // sender sent on other topics (a peer that left is still in the sender's
+    // mesh until its PRUNE arrives) only counts as transmitted (uSent below)
+    relayAll = d.fwdRelay[prv][r];
+    pubAll = d.fwdPub[prv][r];
+    relay = relayAll & sv;
+    pub = pubAll & sv;
     const int64_t ir = d.cIresp[prv][r];
     if (ir >= 0) {
       irOff = (int)(ir >> 24);
       irN = (int)(ir & 0xFFFFFF);
     }
     gray = d.router == 2 && scoring && !d.direct[e] && d.score0[e] < d.graylistThr;
-    if (relay | pub) Ln = d.fln[prv][u];
+    if (relayAll | pubAll) Ln = d.fln[prv][u];
   }
   GS_STAMP(0);
   const bool authV = d.nAuth[v] > 0;  // v authored a live message: author exclusion possible
@@ -812,7 +817,7 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
               nSent += sent;
               if (sent && isGray) ++nGray;  // one RPC per relayed message, all dropped
             }
-            sn[c] = sent && !isGray && ((sv >> t) & 1);
+            sn[c] = sent && !isGray;
             en[c] = (uint32_t)slot | ((uint32_t)i << 16);
           }
         }
@@ -848,6 +853,27 @@ __global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int h
     __syncthreads();
   };
   walk([&](int i, int slot) { deliver(i, slot, true); }, true);
+  if (__ballot(((relayAll | pubAll) & ~sv) != 0)) {
+    // copies of topics v is not subscribed to: transmitted, then ignored
+    // (churn runs only: a mesh or announced peer that has just left)
+    const uint64_t ru = relayAll & ~sv, pu = pubAll & ~sv;
+    if ((ru | pu) && valid) {
+      const uint32_t* L = d.fl[prv] + (int64_t)u * FC;
+      for (int k = 0; k < Ln; ++k) {
+        const uint32_t ent = L[k];
+        const int slot = (int)(ent & 0xFFFF), tag = (int)(ent >> 16);
+        const int t = (int)__umulhi((unsigned)slot, d.stMagic);
+        bool sent = tag == 255 ? ((pu >> t) & 1) : ((ru >> t) & 1);
+        sent = sent && tag != jr;
+        if (sent && d.router == 1) sent = (d.sel[(int64_t)u * d.S + slot] >> jr) & 1;
+        if (sent && authV && d.slotSrc[slot] == v) sent = false;
+        if (sent) {
+          ++nSent;
+          if (gray) ++nGray;
+        }
+      }
+    }
+  }
   // ---- pass 1b: IWANT responses (in the sender's reply RPCs, rare)
   nSent += irN;
   if (!gray) {

@@ -1367,95 +1367,118 @@ __global__ __launch_bounds__(64) void k_p6(Dev d, double* __restrict__ p6) {
 // Leave(topic) at node v (handleRemoveSubscription pubsub.go:665-686 ->
 // gossipsub.go:1062-1078): tracer.Leave, then for every mesh peer
 // tracer.Prune and a PRUNE RPC (sendPrune: a reply-group RPC of this hop).
-// One wave per (node, topic), lane = edge.
-__global__ __launch_bounds__(64) void k_leave(Dev d, const int32_t* __restrict__ pairs, int64_t hop, int cur) {
-  const int v = pairs[2 * blockIdx.x], t = pairs[2 * blockIdx.x + 1];
+// One wave per node (items: node, topic mask lo, hi), its topics ascending;
+// lane = edge.
+__global__ __launch_bounds__(64) void k_leave(Dev d, const int32_t* __restrict__ items, int64_t hop, int cur) {
+  const int v = items[3 * blockIdx.x];
+  const uint64_t mask = (uint64_t)(uint32_t)items[3 * blockIdx.x + 1] | ((uint64_t)(uint32_t)items[3 * blockIdx.x + 2] << 32);
   const int lane = lane_id();
   const int64_t base = d.rowptr[v];
   const int deg = (int)(d.rowptr[v + 1] - base);
   const bool valid = lane < deg;
   const int64_t e = base + lane;
-  const uint64_t bit = 1ull << t;
   const bool traced = is_traced(d, v);
-  if (lane == 0 && traced) trace_emit(d, hop, d.router == 1 ? GS_TRACE_JOIN : GS_TRACE_LEAVE, v, -1, t, -1, 0);
-  if (d.router != 2) return;  // floodsub / randomsub: nothing else (randomsub.go:166-168 traces a Join)
-  const bool m = valid && (d.mesh[e] & bit);
   const bool silent = behaves(d, v, GS_BEHAVE_NO_FORWARD);  // a squatter sends no control
-  if (m) {
-    d.mesh[e] &= ~bit;
-    stats_prune(d, e, t);
-    if (traced) trace_emit(d, hop, GS_TRACE_PRUNE, v, d.col[e], t, -1, 0);
+  uint64_t meshl = valid ? d.mesh[e] : 0;
+  uint64_t pruned = 0;
+  int np = 0;
+  for (uint64_t mm = mask; mm; mm &= mm - 1) {
+    const int t = __ffsll((long long)mm) - 1;
+    const uint64_t bit = 1ull << t;
+    if (lane == 0 && traced) trace_emit(d, hop, d.router == 1 ? GS_TRACE_JOIN : GS_TRACE_LEAVE, v, -1, t, -1, 0);
+    if (d.router != 2) continue;  // floodsub / randomsub (randomsub.go:166-168 traces a Join)
+    const bool m = valid && (meshl & bit);
+    if (m) {
+      meshl &= ~bit;
+      pruned |= bit;
+      stats_prune(d, e, t);
+      if (traced) trace_emit(d, hop, GS_TRACE_PRUNE, v, d.col[e], t, -1, 0);
+    }
+    np += __popcll(__ballot(m));
+  }
+  if (valid && pruned) {
+    d.mesh[e] = meshl;
     if (!silent) {
-      d.cPruneReply[cur][e] |= bit;
-      d.cPre[cur][e] = (uint8_t)(d.cPre[cur][e] + 1);
+      d.cPruneReply[cur][e] |= pruned;
+      d.cPre[cur][e] = (uint8_t)(d.cPre[cur][e] + __popcll(pruned));  // one sendPrune RPC per topic
     }
   }
-  const int np = __popcll(__ballot(m));
   if (lane == 0 && np && !silent) ctr_add(d, C_PRUNES, (unsigned long long)np);
 }
 
 // Join(topic) at node v after the start (handleAddSubscription pubsub.go:
 // 692-713 -> gossipsub.go:1011-1060): reuse the fanout (dropping peers with a
 // negative score) topped up by getPeers, or getPeers(D); tracer.Join, then
-// tracer.Graft and one GRAFT RPC per peer.  Scores are exact: a memo below 0
-// is recomputed (the filter compares with 0).
-__global__ __launch_bounds__(64) void k_join_pairs(Dev d, const int32_t* __restrict__ pairs, int64_t hop,
+// tracer.Graft and one GRAFT RPC per peer.  One wave per node, its topics
+// ascending.  Scores are exact: a memo below 0 or after a score change is
+// recomputed (the filter compares with 0).
+__global__ __launch_bounds__(64) void k_join_pairs(Dev d, const int32_t* __restrict__ items, int64_t hop,
                                                    int64_t now, int cur) {
   __shared__ double sterm[64];
-  const int v = pairs[2 * blockIdx.x], t = pairs[2 * blockIdx.x + 1];
+  const int v = items[3 * blockIdx.x];
+  const uint64_t mask = (uint64_t)(uint32_t)items[3 * blockIdx.x + 1] | ((uint64_t)(uint32_t)items[3 * blockIdx.x + 2] << 32);
   const int lane = lane_id();
   const int64_t base = d.rowptr[v];
   const int deg = (int)(d.rowptr[v + 1] - base);
   const bool valid = lane < deg;
   const int64_t e = base + lane;
-  const uint64_t bit = 1ull << t;
   const bool traced = is_traced(d, v);
-  if (lane == 0 && traced) trace_emit(d, hop, GS_TRACE_JOIN, v, -1, t, -1, 0);
-  if (d.router != 2) return;
+  const bool silent = behaves(d, v, GS_BEHAVE_NO_FORWARD);
   const int vcol = valid ? d.col[e] : -1;
-  const bool inTopic = valid && edge_up(d, e) && ((d.subA[vcol] >> t) & 1);
   const bool dir = valid && d.direct[e];
+  uint64_t meshl = valid ? d.mesh[e] : 0, fanl = valid ? d.fanout[e] : 0, grafted = 0;
+  uint64_t fpres = d.fanoutPresent[v];
   double s = valid ? d.score0[e] : 0.0;
-  if (d.scoring) {
-    unsigned long long xm = __ballot(valid && (d.sdirty[e] != 0 || !(s >= 0.0)));
-    while (xm) {
+  bool stale = valid && d.scoring && (d.sdirty[e] != 0 || !(s >= 0.0));
+  if (!d.scoring) s = 0.0;
+  int ng = 0;
+  for (uint64_t mm = mask; mm; mm &= mm - 1) {
+    const int t = __ffsll((long long)mm) - 1;
+    const uint64_t bit = 1ull << t;
+    if (lane == 0 && traced) trace_emit(d, hop, GS_TRACE_JOIN, v, -1, t, -1, 0);
+    if (d.router != 2) continue;
+    unsigned long long xm = __ballot(stale);
+    while (xm) {  // exact Score(p) where the memo may be off
       const int j = __ffsll((long long)xm) - 1;
       xm &= xm - 1;
       const double sj = edge_score_wave(d, base + j, sterm);
-      if (lane == j) s = sj;
+      if (lane == j) {
+        s = sj;
+        stale = false;
+      }
     }
-  } else {
-    s = 0.0;
-  }
-  const bool present = (d.fanoutPresent[v] >> t) & 1;
-  bool g;
-  if (present) {
-    const uint64_t fo = valid ? d.fanout[e] : 0;
-    g = valid && (fo & bit) && s >= 0;
-    const int have = __popcll(__ballot(g));
-    if (have < d.D) {
-      const uint64_t key = gs_key64(d.seed, GS_SITE_GP_JOIN, v, (uint32_t)hop, vcol, t);
-      g = g || select_k(inTopic && !g && !dir && s >= 0, key, d.D - have);
-    }
-    if (valid) d.fanout[e] = fo & ~bit;
-    if (lane == 0) {
-      d.fanoutPresent[v] &= ~bit;
-      d.lastpub[(int64_t)v * d.T + t] = INT64_MIN;
-    }
-  } else {
+    const bool inTopic = valid && edge_up(d, e) && ((d.subA[vcol] >> t) & 1);
     const uint64_t key = gs_key64(d.seed, GS_SITE_GP_JOIN, v, (uint32_t)hop, vcol, t);
-    g = select_k(inTopic && !dir && s >= 0, key, d.D);
+    bool g;
+    if ((fpres >> t) & 1) {
+      g = valid && (fanl & bit) && s >= 0;
+      const int have = __popcll(__ballot(g));
+      if (have < d.D) g = g || select_k(inTopic && !g && !dir && s >= 0, key, d.D - have);
+      fanl &= ~bit;
+      fpres &= ~bit;
+      if (lane == 0) d.lastpub[(int64_t)v * d.T + t] = INT64_MIN;
+    } else {
+      g = select_k(inTopic && !dir && s >= 0, key, d.D);
+    }
+    if (g) {
+      meshl |= bit;
+      grafted |= bit;
+      stats_graft(d, e, t, now);
+      stale = true;  // a graft may raise the score (P3 switched off)
+      if (traced) trace_emit(d, hop, GS_TRACE_GRAFT, v, vcol, t, -1, 0);  // gossipsub.go:1057
+    }
+    ng += __popcll(__ballot(g));
   }
-  const bool silent = behaves(d, v, GS_BEHAVE_NO_FORWARD);
-  if (g) {
-    d.mesh[e] |= bit;
-    stats_graft(d, e, t, now);
-    if (traced) trace_emit(d, hop, GS_TRACE_GRAFT, v, vcol, t, -1, 0);  // gossipsub.go:1057
-    if (!silent) {
-      d.cGraftJoin[cur][e] |= bit;
-      d.cPre[cur][e] = (uint8_t)(d.cPre[cur][e] + 1);
+  if (valid) {
+    d.mesh[e] = meshl;
+    d.fanout[e] = fanl;
+    if (grafted && !silent) {
+      d.cGraftJoin[cur][e] |= grafted;
+      d.cPre[cur][e] = (uint8_t)(d.cPre[cur][e] + __popcll(grafted));  // one sendGraft RPC per topic
     }
   }
-  const int ng = __popcll(__ballot(g));
-  if (lane == 0 && ng && !silent) ctr_add(d, C_GRAFTS, (unsigned long long)ng);
+  if (lane == 0) {
+    d.fanoutPresent[v] = fpres;
+    if (ng && !silent) ctr_add(d, C_GRAFTS, (unsigned long long)ng);
+  }
 }

@@ -924,8 +924,8 @@ void Node::joinTopic(int topic) {
 // sent during the previous hop reach the peers that are still connected
 // (handleIncomingRPC processes subscriptions first, pubsub.go:915-941), then
 // the scheduled events: every disconnect, every connect, every leave, every
-// join (canonical order), each kind in schedule order.  A lost connection
-// drops what was in flight.
+// join (canonical order); disconnects and connects in schedule order, leaves
+// and joins by (node, topic).  A lost connection drops what was in flight.
 void Sim::applyEvents(std::vector<std::map<int, std::vector<RPC>>>& inbox) {
   for (const Ann& an : pendingAnn)
     for (int p : nodes[an.node].nbrs) {
@@ -938,10 +938,15 @@ void Sim::applyEvents(std::vector<std::map<int, std::vector<RPC>>>& inbox) {
   // each in schedule order
   size_t end = nextEvent;
   while (end < sched.size() && sched[end].hop == hop) end++;
-  for (int pass = GS_EV_DISCONNECT; pass <= GS_EV_JOIN; ++pass)
-  for (size_t k = nextEvent; k < end; ++k) {
-    const Event& ev = sched[k];
-    if (ev.kind != pass) continue;
+  for (int pass = GS_EV_DISCONNECT; pass <= GS_EV_JOIN; ++pass) {
+  std::vector<Event> evs;
+  for (size_t k = nextEvent; k < end; ++k)
+    if (sched[k].kind == pass) evs.push_back(sched[k]);
+  if (pass >= GS_EV_LEAVE)  // leaves and joins of one hop in (node, topic) order
+    std::stable_sort(evs.begin(), evs.end(), [](const Event& x, const Event& y) {
+      return x.a != y.a ? x.a < y.a : x.b < y.b;
+    });
+  for (const Event& ev : evs) {
     switch (ev.kind) {
       case GS_EV_DISCONNECT:
         if (nodes[ev.a].dead.count(ev.b)) break;
@@ -966,6 +971,7 @@ void Sim::applyEvents(std::vector<std::map<int, std::vector<RPC>>>& inbox) {
         pendingAnn.push_back({ev.a, ev.b, true});
         break;
     }
+  }
   }
   nextEvent = end;
 }

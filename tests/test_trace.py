@@ -222,3 +222,31 @@ def test_gpu_trace_equals_oracle(oracle_path, name):
     bad = np.nonzero(got != ref)[0]
     assert len(bad) == 0, f"{len(bad)} events differ, first {got[bad[0]]} vs {ref[bad[0]]}"
     check_invariants(e, got, nodes)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["churn_scored", "churn_prune", "churn_graft"])
+def test_gpu_trace_equals_oracle_churn(oracle_path, name):
+    """RemovePeer / AddPeer / Leave / Join events of the churn scenarios
+    (trace.go:199-233, 399-414): the GPU stream equals the oracle's."""
+    nodes = [u for u in TRACED if u < 20] if name != "churn_scored" else TRACED
+    _, ref = traced_run(oracle_path, name, nodes)
+    _, got = traced_run(PRODUCT_LIB, name, nodes)
+    assert len(got) == len(ref), (len(got), len(ref))
+    bad = np.nonzero(got != ref)[0]
+    assert len(bad) == 0, f"{len(bad)} events differ, first {got[bad[0]]} vs {ref[bad[0]]}"
+
+
+@pytest.mark.parametrize("name", ["churn_scored", "churn_prune"])
+def test_oracle_churn_trace_types(oracle_path, name):
+    """The churn events appear in the trace: RemovePeer / AddPeer for every
+    connection change of a traced host, Leave / Join for its topic changes."""
+    nodes = [u for u in TRACED if u < 20] if name != "churn_scored" else TRACED
+    _, ev = traced_run(oracle_path, name, nodes)
+    types = set(ev["type"].tolist())
+    assert T("LEAVE") in types
+    if name == "churn_scored":
+        assert {T("REMOVE_PEER"), T("ADD_PEER"), T("JOIN")} <= types
+        rm = ev[ev["type"] == T("REMOVE_PEER")]
+        add = ev[(ev["type"] == T("ADD_PEER")) & (ev["hop"] > 0)]
+        assert len(rm) >= len(add) > 0  # every reconnect follows a disconnect
