@@ -16,6 +16,34 @@
 #include "../../include/gs_rng.h"
 
 #define GS_WAVE 64
+// Occupancy hints (waves per SIMD the register allocator must allow) of the
+// latency-bound node-wave kernels; -DGS_WPE_<K>=n overrides for experiments.
+#define GS_WPE_(n) __attribute__((amdgpu_waves_per_eu(n)))
+// heartbeat: 6 waves/SIMD (80 VGPRs) measured 43 -> 34 ms per launch at
+// config4 against the allocator's own 4 (97 VGPRs); 8 spills and loses
+#ifndef GS_WPE_HB
+#define GS_WPE_HB 6
+#endif
+#ifdef GS_WPE_HB
+#define GS_OCC_HB GS_WPE_(GS_WPE_HB)
+#else
+#define GS_OCC_HB
+#endif
+#ifdef GS_WPE_RF
+#define GS_OCC_RF GS_WPE_(GS_WPE_RF)
+#else
+#define GS_OCC_RF
+#endif
+#ifdef GS_WPE_PA
+#define GS_OCC_PA GS_WPE_(GS_WPE_PA)
+#else
+#define GS_OCC_PA
+#endif
+#ifdef GS_WPE_PB
+#define GS_OCC_PB GS_WPE_(GS_WPE_PB)
+#else
+#define GS_OCC_PB
+#endif
 #define GS_MAX_WPL 4   // words per lane in the node-wave kernels: W <= 256
 #define GS_QCAP 320    // phase A delivery queue (>= 63 pending + 256 appended per sub-round)
 #define GS_BMAP 32     // phase A: list blocks mapped to senders without a search (64 per entry)

@@ -256,6 +256,17 @@ static TopicP to_dev(const gs_topic_score_params& p, bool scored) {
 }
 
 static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+// k_score_rows over nEdges edges from d.e0 (lanes hold whole topic rows when
+// T divides 64)
+template <int MODE>
+static void score_rows(const Dev& d, int64_t nEdges, int T, double* out, hipStream_t s) {
+  const unsigned g = nblk(nEdges, score_wave_edges(T));
+  if (g == 0) return;
+  if (64 % T == 0)
+    k_score_rows<MODE, true><<<g, 64, 0, s>>>(d, out);
+  else
+    k_score_rows<MODE, false><<<g, 64, 0, s>>>(d, out);
+}
 
 // Launch `stmt` on g's stream; with profiling on, bracket it with HIP events
 // recorded on that same stream (so the measured interval is the kernel's).
@@ -839,8 +850,8 @@ int gs_engine::stepOne() {
   const int nOwn = n1 - n0;
   const int64_t eOwn = e1 - e0;
   const unsigned eb = nblk(eOwn, 256);
-  const unsigned sgb = nblk(eOwn, GS_SG), pb = nblk(eOwn * T, 256);
-  if (scoring) TIMED(this, GS_K_SCORE, (k_score_rows<1><<<sgb, 64, 0, stream>>>(d, nullptr)));
+  const unsigned pb = nblk(eOwn * T, 256);
+  if (scoring) TIMED(this, GS_K_SCORE, (score_rows<1>(d, eOwn, T, nullptr, stream)));
   if (h == 0 && gossip && nOwn) TIMED(this, GS_K_JOIN, (k_join<<<nOwn, 64, 0, stream>>>(d, h, now, cur)));
   if (gossip && !floodPublish && n > 0) {
     // Publish to a topic we have not joined: fanout (gossipsub.go:977-994)
@@ -928,7 +939,7 @@ int gs_engine::stepOne() {
     if (cfg.router == GS_ROUTER_RANDOMSUB) k_publish_rs<<<n, 64, 0, stream>>>(d, (int)b);
   }
   if (gossip) {
-    if (scoring) TIMED(this, GS_K_SCORE, (k_score_rows<2><<<sgb, 64, 0, stream>>>(d, nullptr)));
+    if (scoring) TIMED(this, GS_K_SCORE, (score_rows<2>(d, eOwn, T, nullptr, stream)));
     // MaxIHaveLength cuts are possible only if the messages (phantom ids
     // included) that can sit in one gossip window outnumber MaxIHaveLength:
     // published within HistoryGossip + 1 heartbeats plus the delivery age bound
@@ -951,10 +962,16 @@ int gs_engine::stepOne() {
           }));
   }
   if (refreshDue(now)) {
-    if (churnOn)
-      TIMED(this, GS_K_REFRESH, (k_refresh_rows<true><<<nblk(eOwn, GS_RG), 64, 0, stream>>>(d, now)));
+    const unsigned rb = nblk(eOwn, GS_RP / T);
+    const bool laneT = (64 % T) == 0;  // a lane keeps one topic
+    if (churnOn && laneT)
+      TIMED(this, GS_K_REFRESH, (k_refresh_rows<true, true><<<rb, 64, 0, stream>>>(d, now)));
+    else if (churnOn)
+      TIMED(this, GS_K_REFRESH, (k_refresh_rows<true, false><<<rb, 64, 0, stream>>>(d, now)));
+    else if (laneT)
+      TIMED(this, GS_K_REFRESH, (k_refresh_rows<false, true><<<rb, 64, 0, stream>>>(d, now)));
     else
-      TIMED(this, GS_K_REFRESH, (k_refresh_rows<false><<<nblk(eOwn, GS_RG), 64, 0, stream>>>(d, now)));
+      TIMED(this, GS_K_REFRESH, (k_refresh_rows<false, false><<<rb, 64, 0, stream>>>(d, now)));
     if (churnOn && p6Live() && nOwn) k_p6<<<nOwn, 64, 0, stream>>>(d, dP6w);  // expired records
     refreshedHop = h;
     hopsSinceFold = 0;
@@ -976,11 +993,11 @@ int gs_engine::stepOne() {
     // memo pass (k_score_rows<4>)
     int allExact = 1;
     if (scoring && refreshedHop == h)
-      TIMED(this, GS_K_SCORE, (k_score_rows<3><<<sgb, 64, 0, stream>>>(d, nullptr)));
+      TIMED(this, GS_K_SCORE, (score_rows<3>(d, eOwn, T, nullptr, stream)));
     else if (scoring && ticks % (uint64_t)d.OGT == 0)
-      TIMED(this, GS_K_SCORE, (k_score_rows<0><<<sgb, 64, 0, stream>>>(d, d.score1)));
+      TIMED(this, GS_K_SCORE, (score_rows<0>(d, eOwn, T, d.score1, stream)));
     else if (scoring) {
-      TIMED(this, GS_K_SCORE, (k_score_rows<4><<<sgb, 64, 0, stream>>>(d, nullptr)));
+      TIMED(this, GS_K_SCORE, (score_rows<4>(d, eOwn, T, nullptr, stream)));
       allExact = 0;
     }
     const int newhead = (head + R - 1) % R;
@@ -1685,7 +1702,7 @@ int gs_read_counters(gs_engine* g, gs_counters* out) {
 int gs_read_scores(gs_engine* g, double* score) {
   if (!g->graphSet) { gs_set_error("graph not set"); return GS_ESTATE; }
   NEED_STARTED(g);
-  k_score_rows<0><<<nblk(g->E, GS_SG), 64, 0, g->stream>>>(g->d, g->dScoreTmp);
+  score_rows<0>(g->d, g->E, g->d.T, g->dScoreTmp, g->stream);
   HIPCHECK(hipMemcpyAsync(score, g->dScoreTmp, g->E * 8, hipMemcpyDeviceToHost, g->stream));
   HIPCHECK(hipStreamSynchronize(g->stream));
   return GS_OK;

@@ -1,8 +1,8 @@
 // gs_kernels.h — HIP kernels of the gossip engine (gfx950, wave64).
 //
 // Kernel map (one hop):
-//   k_score_rows   wave/32 edges peerScore.score (+ memos)  score.go:256-333
-//   k_refresh_rows wave/32 edges refreshScores (+ exact S0) score.go:495-556
+//   k_score_rows   wave/64 edges peerScore.score (+ memos)  score.go:256-333
+//   k_refresh_rows wave/1024 pairs refreshScores (+ exact S0) score.go:495-556
 //   k_join         wave/node     Join at hop 0              gossipsub.go:1011-1060
 //   k_fanout_pub   wave/pair     Publish fanout creation    gossipsub.go:977-994
 //   k_fwd          thread/edge   forwarding-target snapshot gossipsub.go:953-999, floodsub.go:85, randomsub.go:115
@@ -22,10 +22,10 @@
 #include "gs_device.h"
 
 // ---------------------------------------------------------------- score
-// peerScore.score (score.go:256-333) of a group of GS_SG consecutive edges per
-// wave.  Lane = topic: the topic terms of one edge are one contiguous row of
-// each state array (full lines); terms go to LDS and lane j then adds edge j's
-// terms in ascending topic order, exactly as the reference's loop does.
+// peerScore.score (score.go:256-333) of score_wave_edges(T) consecutive edges
+// per wave.  The topic terms of one edge are one contiguous row of each state
+// array (full lines), loaded by T lanes; terms go to LDS and lane j then adds
+// edge j's terms in ascending topic order, exactly as the reference's loop does.
 // Only the edges that need it are computed, so a sparse recompute costs the
 // rows it touches, not the whole table.
 //   MODE 0: every edge -> out
@@ -48,20 +48,25 @@
 //     of the exact score, so every heartbeat threshold test — 0, Gossip- and
 //     PublishThreshold, all <= 0 — decides exactly).  k_heartbeat recomputes
 //     the few scores it needs as values (Dhi ranking) from the same rule.
-#define GS_SG 16  // edges per wave
-#define GS_SB 8   // edges per load batch
-// refresh: one load batch per wave, so no wave issues a batch's loads behind
-// its own previous batch's stores (on gfx9 vmcnt counts both)
-#ifndef GS_RG
-#define GS_RG 16
+#define GS_SB 8   // passes per load batch
+#ifndef GS_RB
+#define GS_RB 8   // refresh: pairs per lane per load batch
 #endif
-template <int MODE>
+#define GS_RP 1024  // (edge, topic) pairs of one wave's LDS term table
+__device__ __forceinline__ int rp_pad(int pl) { return pl + (pl >> 6); }
+// Edges per wave of k_score_rows: lane = edge for the need test, and the
+// needy edges' T-topic rows fill the lanes in passes of 64 / T edges.
+__host__ __device__ __forceinline__ int score_wave_edges(int T) { return T * 64 <= GS_RP ? 64 : GS_RP / T; }
+template <int MODE, bool LANE_T>
 __global__ __launch_bounds__(64) void k_score_rows(Dev d, double* __restrict__ out) {
-  __shared__ double sT[GS_SG * 65];  // [edge][topic], row stride 65: conflict-free column reads
+  __shared__ double sT[GS_RP + GS_RP / 64];  // [edge][topic], padded: conflict-free column reads
+  __shared__ int sList[64];
   const int lane = lane_id();
-  const int64_t e0 = d.e0 + (int64_t)blockIdx.x * GS_SG;
+  const int T = d.T;
+  const int sgw = score_wave_edges(T);
+  const int64_t e0 = d.e0 + (int64_t)blockIdx.x * sgw;
   const int64_t e = e0 + lane;
-  const bool in = lane < GS_SG && e < d.e1;
+  const bool in = lane < sgw && e < d.e1;
   double s0 = 0.0;
   bool need = false;
   if (in) {
@@ -84,32 +89,40 @@ __global__ __launch_bounds__(64) void k_score_rows(Dev d, double* __restrict__ o
     return;
   }
   if (MODE >= 2 && in && !need) d.score1[e] = s0;
-  unsigned long long m = __ballot(need);
+  const unsigned long long m = __ballot(need);
   if (!m) return;
-  const int T = d.T;
-  const int tl = lane < T ? lane : 0;
-  const bool scoredL = lane < T && d.tp[tl].scored;
-  const uint64_t scoredT = __ballot(scoredL);
-  while (m) {
-    // GS_SB edges per batch: every load of the batch in flight at once
+  const int nNeed = __popcll(m);
+  if (need) sList[__popcll(m & ((1ull << lane) - 1))] = lane;
+  __syncthreads();
+  // LANE_T (T divides 64): lane = (edge of the pass, topic); else one edge
+  // per pass, lane = topic
+  const int G = LANE_T ? 64 / T : 1;
+  const int gi = LANE_T ? lane / T : 0;
+  const int tl = LANE_T ? (lane & (T - 1)) : (lane < T ? lane : 0);
+  const bool lt = LANE_T || lane < T;
+  const bool scoredL = lt && d.tp[tl].scored;
+  const uint64_t scoredT = __ballot(lane < T && d.tp[lane < T ? lane : 0].scored);
+  const int P = (nNeed + G - 1) / G;
+  for (int p0 = 0; p0 < P; p0 += GS_SB) {
+    // GS_SB passes per batch: every load of the batch in flight at once
     int js[GS_SB];
 #pragma unroll
     for (int k = 0; k < GS_SB; ++k) {
-      js[k] = m ? __ffsll((long long)m) - 1 : -1;
-      m &= m - 1;
+      const int q = (p0 + k) * G + gi;
+      js[k] = (lt && q < nNeed) ? sList[q] : -1;
     }
     TermIn x[GS_SB];
 #pragma unroll
-    for (int k = 0; k < GS_SB; ++k) x[k] = term_load(d, (e0 + (js[k] < 0 ? js[0] : js[k])) * T + tl);
+    for (int k = 0; k < GS_SB; ++k) x[k] = term_load(d, (e0 + (js[k] < 0 ? sList[0] : js[k])) * T + tl);
 #pragma unroll
     for (int k = 0; k < GS_SB; ++k)
-      if (js[k] >= 0) sT[js[k] * 65 + lane] = scoredL ? term_eval(d.tp[tl], x[k]) : 0.0;
+      if (js[k] >= 0) sT[rp_pad(js[k] * T + tl)] = scoredL ? term_eval(d.tp[tl], x[k]) : 0.0;
   }
   __syncthreads();
-  if (lane < GS_SG && need) {
+  if (need) {
     double score = 0.0;
     for (int t = 0; t < T; ++t)
-      if ((scoredT >> t) & 1) score += sT[lane * 65 + t];
+      if ((scoredT >> t) & 1) score += sT[rp_pad(lane * T + t)];
     score = has_record(d, e) ? score_tail(d, e, score) : 0.0;
     if (MODE == 0) out[e] = score;
     if (MODE == 1 || MODE == 3) { d.score0[e] = score; d.sdirty[e] = 0; }
@@ -117,55 +130,41 @@ __global__ __launch_bounds__(64) void k_score_rows(Dev d, double* __restrict__ o
   }
 }
 
-// refreshScores — score.go:495-556 (every peer is connected: no retention
-// path), GS_RG edges per wave, lane = topic, and the exact score of every
-// edge from the refreshed state into S0 (sdirty cleared): nothing but
-// refreshScores changed the state since the hop's message phase, so this is
-// the value the next S0 pass would compute.
+// refreshScores — score.go:495-556, and the exact score of every edge from
+// the refreshed state into S0 (sdirty cleared): nothing but refreshScores
+// changed the state since the hop's message phase, so this is the value the
+// next S0 pass would compute.
+// A wave owns GS_RP consecutive (edge, topic) pairs — GS_RP / T whole edges —
+// and lane l takes pairs l, l + 64, ...: every lane busy for any T (at T = 1
+// a wave covers 1024 edges, at T = 64 sixteen, one topic per lane).  LANE_T:
+// T divides 64, so a lane's topic is fixed (lane % T) and its params stay in
+// registers; otherwise each pair finds its own.  Terms go to LDS (one pad
+// word per 64: conflict-free at T = 64) and the sum per edge runs in
+// ascending topic order, as the reference's loop does.
 // CHURN: some connection may be down (gs_schedule_events): retained records
 // are not decayed and expire; the honest instantiation carries none of it.
-template <bool CHURN>
-__global__ __launch_bounds__(64) void k_refresh_rows(Dev d, int64_t now) {
-  __shared__ double sT[GS_RG * 65];
+template <bool CHURN, bool LANE_T>
+__global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t now) {
+  __shared__ double sT[GS_RP + GS_RP / 64];
   const int lane = lane_id();
-  const int64_t e0 = d.e0 + (int64_t)blockIdx.x * GS_RG;
-  const int ng = (int)min((int64_t)GS_RG, d.e1 - e0);
   const int T = d.T;
+  const int epw = GS_RP / T;
+  const int64_t e0 = d.e0 + (int64_t)blockIdx.x * epw;
+  const int ng = (int)min((int64_t)epw, d.e1 - e0);
+  const int np = ng * T;
+  const int64_t p0 = e0 * T;
   const int tl = lane < T ? lane : 0;
-  const TopicP& tp = d.tp[tl];
-  const bool act = lane < T && tp.scored;
-  const uint64_t scoredT = __ballot(act);
-  // churn: a retained record is not decayed; past its expiry it is dropped
-  // (score.go:500-509); the host then recounts P6 (removeIPs)
-  uint64_t frozen = 0;
-  if (CHURN && d.rstate != nullptr) {
-    for (int j = 0; j < ng; ++j) {
-      const int64_t ej = e0 + j;
-      const uint8_t st = d.rstate[ej];
-      if (st == 1) continue;
-      frozen |= 1ull << j;
-      if (st == 2 && now > d.rexpire[ej]) {
-        for (int t = lane; t < T; t += 64) {
-          const int64_t i = ej * T + t;
-          d.fmd[i] = 0; d.mmd[i] = 0; d.mfp[i] = 0; d.imd[i] = 0; d.dlt[i] = 0;
-          d.meshTime[i] = 0; d.graftTime[i] = 0; d.flags[i] = 0;
-        }
-        if (lane == 0) {
-          d.bp[ej] = 0;
-          d.rstate[ej] = 0;
-        }
-      }
-    }
-    __syncthreads();  // the dropped records' zeros before the loads below
-  }
-  for (int j0 = 0; j0 < ng; j0 += GS_SB) {
-    uint32_t q[GS_SB];
-    double fmd[GS_SB], mmd[GS_SB], mfp[GS_SB], imd[GS_SB];
-    int64_t gt[GS_SB];
-    uint8_t fl[GS_SB];
+  const uint64_t scoredT = __ballot(lane < T && d.tp[tl].scored);
+  const int tLane = LANE_T ? (lane & (T - 1)) : 0;
+  for (int k0 = 0; 64 * k0 < np; k0 += GS_RB) {
+    uint32_t q[GS_RB];
+    double fmd[GS_RB], mmd[GS_RB], mfp[GS_RB], imd[GS_RB];
+    int64_t gt[GS_RB];
+    uint8_t fl[GS_RB];
 #pragma unroll
-    for (int k = 0; k < GS_SB; ++k) {
-      const int64_t i = (e0 + min(j0 + k, ng - 1)) * T + tl;
+    for (int k = 0; k < GS_RB; ++k) {
+      const int pl = min(lane + 64 * (k0 + k), np - 1);
+      const int64_t i = p0 + pl;
       q[k] = d.dlt[i];
       fmd[k] = d.fmd[i];
       mmd[k] = d.mmd[i];
@@ -175,12 +174,30 @@ __global__ __launch_bounds__(64) void k_refresh_rows(Dev d, int64_t now) {
       fl[k] = d.flags[i];
     }
 #pragma unroll
-    for (int k = 0; k < GS_SB; ++k) {
-      if (j0 + k >= ng) break;
-      const int64_t i = (e0 + j0 + k) * T + tl;
+    for (int k = 0; k < GS_RB; ++k) {
+      const int pl = lane + 64 * (k0 + k);
+      if (pl >= np) break;
+      const int64_t i = p0 + pl;
+      int t = tLane;
+      int64_t e = 0;
+      if (!LANE_T || CHURN) {
+        pair_split(d, i, e, t);
+        if (LANE_T) t = tLane;
+      }
+      const TopicP& tp = d.tp[t];
+      const bool act = (scoredT >> t) & 1;
       double term = 0.0;
-      if (CHURN && act && ((frozen >> (j0 + k)) & 1)) {
-        term = topic_term(d, tp, i);  // not decayed: the stored record as it is
+      uint8_t st = 1;
+      if (CHURN && d.rstate != nullptr) st = d.rstate[e];
+      if (CHURN && st != 1) {
+        // a retained record is not decayed; past its expiry it is dropped
+        // (score.go:500-509); the host then recounts P6 (removeIPs)
+        if (st == 2 && now > d.rexpire[e]) {
+          d.fmd[i] = 0; d.mmd[i] = 0; d.mfp[i] = 0; d.imd[i] = 0; d.dlt[i] = 0;
+          d.meshTime[i] = 0; d.graftTime[i] = 0; d.flags[i] = 0;
+        } else if (act) {
+          term = topic_term(d, tp, i);  // the stored record as it is
+        }
       } else if (act) {
         TermIn x;
         x.q = 0;
@@ -214,22 +231,32 @@ __global__ __launch_bounds__(64) void k_refresh_rows(Dev d, int64_t now) {
         }
         term = term_eval(tp, x);
       }
-      sT[(j0 + k) * 65 + lane] = term;
+      sT[rp_pad(pl)] = term;
     }
   }
   __syncthreads();
-  if (lane < ng) {
-    const int64_t e = e0 + lane;
+  for (int j = lane; j < ng; j += 64) {
+    const int64_t e = e0 + j;
+    bool frozen = false, dropped = false;
+    if (CHURN && d.rstate != nullptr) {
+      const uint8_t st = d.rstate[e];
+      frozen = st != 1;
+      dropped = st == 2 && now > d.rexpire[e];
+    }
     double b = d.bp[e];
-    if (!CHURN || !((frozen >> lane) & 1)) {
+    if (dropped) {
+      b = 0;
+      d.bp[e] = 0;
+      d.rstate[e] = 0;
+    } else if (!frozen) {
       b *= d.BPDecay;
       if (b < d.DecayToZero) b = 0;
       d.bp[e] = b;
     }
     double score = 0.0;
-    if (d.scoring && (!CHURN || has_record(d, e))) {
+    if (d.scoring && !dropped && (!CHURN || has_record(d, e))) {
       for (int t = 0; t < T; ++t)
-        if ((scoredT >> t) & 1) score += sT[lane * 65 + t];
+        if ((scoredT >> t) & 1) score += sT[rp_pad(j * T + t)];
       score = score_tail(d, e, score);
     }
     d.score0[e] = score;
@@ -514,7 +541,7 @@ __device__ __forceinline__ int wave_min_int(int x) {
 //     RejectValidationQueueFull (not seen; the gater's throttle counter);
 //   * an IWANT spammer re-requests every message it received, per sender.
 template <int WPL, bool NARROW, bool ADV>
-__global__ __launch_bounds__(64) void k_phase_a(Dev d, int64_t h, int cur, int head, WMask amR, WMask amW,
+__global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int cur, int head, WMask amR, WMask amW,
                                                 int nR, int nY) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
   const int nCnt = (d.T * d.maxDeg + 7) & ~7;

@@ -168,7 +168,7 @@ __device__ __forceinline__ int lane_prefix(int x, int* total) {
 // squatters, the dynamic peertx hash, phantom ids and the cuts; the honest
 // instantiation carries none of them.
 template <int WPL, bool ADV>
-__global__ __launch_bounds__(64) void k_phase_b(Dev d, int64_t h, int64_t now, int cur, int head, int cutModeArg) {
+__global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int64_t now, int cur, int head, int cutModeArg) {
   const int cutMode = ADV ? cutModeArg : 0;
   __shared__ uint64_t scache[64 * WPL];  // v's mcache windows (handleIWant, step 2)
   uint64_t* const sseen = scache;        // then v's seen row (handleIHave, step 3)
@@ -947,7 +947,7 @@ __device__ __forceinline__ uint64_t emit_gossip(const Dev& d, int v, int t, int6
 // maintenance, sendGraftPrune (outbox), mcache.Shift.  Scores are the
 // heartbeat memo (score1, computed after applyIwantPenalties); emitGossip
 // re-scores peers whose stats changed during this heartbeat (live Score()).
-__global__ __launch_bounds__(64) void k_heartbeat(Dev d, int64_t hop, int64_t now, uint64_t ticks, int cur,
+__global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, int64_t now, uint64_t ticks, int cur,
                                                   int head, int newhead, int allExact) {
   __shared__ int plst[64];
   __shared__ int obs[64];

@@ -1,0 +1,15 @@
+#!/bin/bash
+# GPU tests, then the config4 and config3 benches, each step time-limited and
+# chained with && (a failing step ends the call).
+set -o pipefail
+cd "$(dirname "$0")/.."
+OUT=gpurun_out/${1:-tb}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    > "$OUT/pytest_gpu.log" 2>&1 &&
+timeout -k 10 600 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline \
+    > "$OUT/bench_c4.json" 2> "$OUT/bench_c4.err" &&
+timeout -k 10 600 python -u bench.py --workload config3 --steps 3 --warmup 1 --no-cpu-baseline \
+    > "$OUT/bench_c3.json" 2> "$OUT/bench_c3.err" &&
+echo done
