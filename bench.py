@@ -174,6 +174,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="partition", choices=["partition", "replicas"])
     ap.add_argument("--peers", type=int, default=0, help="override the workload's peer count (rehearsals)")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "torch"],
+                    help="partitioned ranks' exchange: the product library's native RCCL transport "
+                         "(include/gs_transport.h) or torch.distributed collectives")
     ap.add_argument("--lib", default=None, help="timing experiments only: another build of the product library "
                     "(results are labelled with it)")
     args = ap.parse_args()
@@ -210,8 +213,13 @@ def main():
         else:
             dist.init_process_group(backend)
         if partitioned:
-            from pubsub_amd.transport import TorchTransport
-            extra = (WithPartition(rank, world, TorchTransport(memory="device")),)
+            if backend == "nccl" and args.transport == "rccl":
+                from pubsub_amd.transport import RcclTransport
+                transport = RcclTransport(rank, world, device=local)
+            else:  # gloo rehearsals stage through host memory
+                from pubsub_amd.transport import TorchTransport
+                transport = TorchTransport(memory="device")
+            extra = (WithPartition(rank, world, transport),)
 
     wl = dict(WORKLOADS[args.workload])
     if args.peers:
@@ -335,7 +343,8 @@ def main():
     if args.lib:
         out["experiment_lib"] = os.path.basename(args.lib)
     if partitioned:
-        out["exchange"] = {"rank0_host_ms_per_step": round((x1[0] - x0[0]) / args.steps, 3),
+        out["exchange"] = {"transport": type(extra[0][1][2]).__name__,
+                           "rank0_host_ms_per_step": round((x1[0] - x0[0]) / args.steps, 3),
                            "rank0_bytes_in_per_step": (x1[1] - x0[1]) // args.steps,
                            "rank0_nodes": eng.node_range[1] - eng.node_range[0]}
     if not args.no_cpu_baseline and world == 1:

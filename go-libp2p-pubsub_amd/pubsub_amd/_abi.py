@@ -182,6 +182,16 @@ ABI_FUNCTIONS = [
     ("gs_read_kernel_stats", C.c_int, [P, C.POINTER(f64), C.POINTER(i64)]),
 ]
 
+# include/gs_transport.h (product library only; bound by transport.RcclTransport)
+GS_RCCL_ID_BYTES = 128
+RCCL_FUNCTIONS = [
+    ("gs_rccl_get_unique_id", C.c_int, [C.POINTER(u8)]),
+    ("gs_rccl_create", C.c_int, [i32, i32, C.POINTER(u8), i32, C.POINTER(P)]),
+    ("gs_rccl_transport", C.c_int, [P, C.POINTER(TransportC)]),
+    ("gs_rccl_stats", C.c_int, [P, C.POINTER(i64), C.POINTER(i64)]),
+    ("gs_rccl_destroy", C.c_int, [P]),
+]
+
 KERNEL_NAMES = ["score", "refresh", "join", "fanout", "fwd", "phase_a", "publish", "phase_b",
                 "hb_pre", "heartbeat"]
 

@@ -148,3 +148,52 @@ def _alltoallv_p2p(out, inp, out_splits, in_splits, rank, world, group):
 
 def _global(rank, group):
     return rank if group is None else dist.get_global_rank(group, rank)
+
+
+class RcclTransport:
+    """The product library's native RCCL transport (include/gs_transport.h):
+    the same gs_transport semantics as TorchTransport with the collectives
+    issued by C++ (ncclAllGather, grouped ncclSend / ncclRecv) on the engine's
+    device buffers — what a cgo host uses.  The communicator
+    id is made on rank 0 and handed to the other ranks through `group`
+    (torch.distributed, any backend) or given as `uid` (bytes)."""
+
+    def __init__(self, rank, world, device=0, group=None, uid=None, lib=None):
+        from .engine import PRODUCT_LIB
+        self.lib = C.CDLL(lib or PRODUCT_LIB, mode=C.RTLD_LOCAL)
+        for name, res, args in _abi.RCCL_FUNCTIONS + [("gs_last_error", C.c_char_p, [])]:
+            fn = getattr(self.lib, name)  # AttributeError = missing export: fail loudly
+            fn.restype, fn.argtypes = res, args
+        n = _abi.GS_RCCL_ID_BYTES
+        idbuf = (C.c_uint8 * n)()
+        if uid is None:
+            if rank == 0:
+                self._check(self.lib.gs_rccl_get_unique_id(idbuf))
+            if world > 1:
+                obj = [bytes(idbuf)]
+                dist.broadcast_object_list(obj, src=0, group=group)
+                C.memmove(idbuf, obj[0], n)
+        else:
+            C.memmove(idbuf, bytes(uid), n)
+        self.uid = bytes(idbuf)
+        self.h = C.c_void_p()
+        self._check(self.lib.gs_rccl_create(int(rank), int(world), idbuf, int(device), C.byref(self.h)))
+        self.c = _abi.TransportC()
+        self._check(self.lib.gs_rccl_transport(self.h, C.byref(self.c)))
+        self.rank, self.world = rank, world
+
+    def _check(self, rc):
+        if rc != _abi.GS_OK:
+            from .engine import GossipEngineError
+            raise GossipEngineError(rc, self.lib.gs_last_error().decode(errors="replace"))
+
+    @property
+    def calls(self):
+        c, b = C.c_int64(), C.c_int64()
+        self._check(self.lib.gs_rccl_stats(self.h, C.byref(c), C.byref(b)))
+        return c.value
+
+    def close(self):
+        if self.h:
+            self.lib.gs_rccl_destroy(self.h)
+            self.h = C.c_void_p()

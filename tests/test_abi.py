@@ -82,3 +82,33 @@ def test_product_fails_loudly_without_gpu():
     with pytest.raises(GossipEngineError) as ei:
         NewFloodSub(10, 1, g, graphs.all_subscribed(10, 1))
     assert ei.value.code == _abi.GS_EDEVICE
+
+
+def test_product_exports_transport_header():
+    """include/gs_transport.h (native RCCL transport) is product-only and bound
+    by pubsub_amd.transport.RcclTransport."""
+    if not os.path.exists(PRODUCT_LIB):
+        pytest.skip("product library not built")
+    src = open(os.path.join(REPO, "include", "gs_transport.h")).read()
+    names = set(re.findall(r"^[a-z_0-9 \*]+?\b(gs_[a-z_0-9]+)\(", src, re.M))
+    assert names == {n for n, _, _ in _abi.RCCL_FUNCTIONS}
+    lib = C.CDLL(PRODUCT_LIB)
+    for name in names:
+        assert hasattr(lib, name), f"product library does not export {name}"
+
+
+def test_rccl_transport_refuses_bad_arguments_and_no_gpu():
+    if not os.path.exists(PRODUCT_LIB):
+        pytest.skip("product library not built")
+    import torch
+    lib = C.CDLL(PRODUCT_LIB)
+    for name, res, args in _abi.RCCL_FUNCTIONS:
+        getattr(lib, name).restype, getattr(lib, name).argtypes = res, args
+    idb = (C.c_uint8 * _abi.GS_RCCL_ID_BYTES)()
+    h = C.c_void_p()
+    assert lib.gs_rccl_create(2, 2, idb, 0, C.byref(h)) == _abi.GS_EINVAL  # rank >= world
+    assert lib.gs_rccl_create(0, 0, idb, 0, C.byref(h)) == _abi.GS_EINVAL
+    assert lib.gs_rccl_transport(None, None) == _abi.GS_EINVAL
+    assert lib.gs_rccl_destroy(None) == _abi.GS_OK
+    if torch.cuda.device_count() == 0:
+        assert lib.gs_rccl_create(0, 1, idb, 0, C.byref(h)) == _abi.GS_EDEVICE
