@@ -29,8 +29,10 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "go-libp2p-pubsub_amd"))
 
-from pubsub_amd import (Millisecond, NewGossipSub, WithDevice, WithHop, WithMessageWindow,  # noqa: E402
-                        WithPartition, WithPeerScore, WithSeed, eth2_peer_score_params, eth2_thresholds)
+from pubsub_amd import (GS_BEHAVE_GRAFT_SPAM, GS_BEHAVE_IHAVE_SPAM, GS_BEHAVE_IWANT_SPAM,  # noqa: E402
+                        GS_MSG_PHANTOM, GS_MSG_REJECT, DefaultPeerGaterParams, Millisecond, NewGossipSub,
+                        WithBehaviour, WithDevice, WithHop, WithMessageWindow, WithPartition, WithPeerGater,
+                        WithPeerScore, WithSeed, WithValidation, eth2_peer_score_params, eth2_thresholds)
 from pubsub_amd import graphs  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
@@ -40,25 +42,61 @@ MSGS_PER_ROUND = 1000
 WORKLOADS = {
     "config4": dict(n=1_000_000, k=32, topics=64, slots=256),
     "config3": dict(n=1_000_000, k=32, topics=1, slots=10048),
+    # BASELINE configs[4] (the adversarial run) on ONE GPU: 1M peers (the
+    # 10M-peer figure is the 8-GPU node's; --peers raises it), 20% Sybils split
+    # over IWANT spam, GRAFT spam, phantom-IHAVE spam and invalid publishing,
+    # 20 Sybils per shared IP, the peer gater, a topic validator with a
+    # 32-entry queue per hop.  50 msgs/round: an honest node keeps one
+    # mcache.peertx entry per (message, IWANT spammer) it served, and its
+    # table holds 4096 (the capacity limit of this build).
+    "config5": dict(n=1_000_000, k=32, topics=1, slots=10240, msgs=50, adversarial=True),
 }
 
 
-def build_engine(wl, rounds, seed, device, lib=None, n=None, msgs_per_round=MSGS_PER_ROUND, extra=()):
+def build_engine(wl, rounds, seed, device, lib=None, n=None, msgs_per_round=None, extra=()):
     n = n or wl["n"]
     T = wl["topics"]
+    msgs_per_round = msgs_per_round or wl.get("msgs", MSGS_PER_ROUND)
     g = graphs.random_regular_fast(n, wl["k"], seed)
     subs = graphs.all_subscribed(n, T)
     opts = [WithPeerScore(eth2_peer_score_params(T), eth2_thresholds()), WithHop(100 * Millisecond),
             WithMessageWindow(wl["slots"]), WithSeed(seed)]
     if lib is None or "libgossip_engine" in os.path.basename(lib):
         opts.append(WithDevice(device))
-    eng = NewGossipSub(n, T, g, subs, *opts, *extra, lib=lib)
+    kw = {}
+    rng = np.random.default_rng(seed + 7)
     per_hop = msgs_per_round // HOPS_PER_ROUND
     hops = np.repeat(np.arange(1, rounds * HOPS_PER_ROUND + 1, dtype=np.int64), per_hop)
-    rng = np.random.default_rng(seed + 7)
     src = rng.integers(0, n, len(hops)).astype(np.int32)
     top = (np.arange(len(hops)) % T).astype(np.int32)
-    eng.publish(src, top, hops)
+    kind = None
+    if wl.get("adversarial"):
+        # the config-5 mix (tests/scenarios.py adversarial_mix, at scale)
+        arng = np.random.default_rng(seed + 11)
+        sybil = arng.random(n) < 0.2
+        ids = np.flatnonzero(sybil)
+        kind_of = arng.integers(0, 4, len(ids))  # 0 IWANT spam, 1 GRAFT spam, 2 phantom IHAVE, 3 invalid
+        beh = np.zeros(n, np.uint8)
+        beh[ids[kind_of == 0]] = GS_BEHAVE_IWANT_SPAM
+        beh[ids[kind_of == 1]] = GS_BEHAVE_GRAFT_SPAM
+        beh[ids[kind_of == 2]] = GS_BEHAVE_IHAVE_SPAM
+        ipv4 = (np.arange(n) + (10 << 24)).astype(np.uint32)
+        ipv4[ids] = (192 << 24) + (np.arange(len(ids)) // 20).astype(np.uint32)  # 20 Sybils per IP
+        kw["ipv4"] = ipv4
+        opts += [WithBehaviour(beh), WithValidation([1] * T, 32), WithPeerGater(DefaultPeerGaterParams())]
+        honest = np.flatnonzero(~sybil)
+        src = honest[rng.integers(0, len(honest), len(hops))].astype(np.int32)
+        kind = np.zeros(len(hops), np.uint8)
+        r = rng.random(len(hops))
+        inv, ph = ids[kind_of == 3], ids[kind_of == 2]
+        sel = r < 1 / 3  # a third invalid messages, a sixth phantom ids
+        src[sel] = inv[rng.integers(0, len(inv), int(sel.sum()))]
+        kind[sel] = GS_MSG_REJECT
+        sel = (r >= 1 / 3) & (r < 0.5)
+        src[sel] = ph[rng.integers(0, len(ph), int(sel.sum()))]
+        kind[sel] = GS_MSG_PHANTOM
+    eng = NewGossipSub(n, T, g, subs, *opts, *extra, lib=lib, **kw)
+    eng.publish(src, top, hops, kind=kind)
     eng.schedule = (top, hops)
     return eng, g
 
@@ -76,7 +114,7 @@ def active_words(eng, wl, hop):
             slots[idx] = t * St + np.arange(len(idx)) % St
         eng.sched_slots = slots
     slots = eng.sched_slots
-    max_age = 3 * HOPS_PER_ROUND
+    max_age = (13 if wl.get("adversarial") else 3) * HOPS_PER_ROUND  # gs_engine setWindow
     live = (hops >= hop - 1 - max_age) & (hops <= hop - 1)
     return len(np.unique(slots[live] // 64))
 
@@ -161,7 +199,8 @@ def cpu_baseline(wl, seconds=20.0):
             "extrapolation": f"per-peer linear: rounds/s x {n}/{wl['n']} (labelled estimate, not measured)",
             "cpu_model": cpu_info(), "nproc": os.cpu_count(),
             "sample": f"oracle/ (C++ restatement, OpenMP {threads} threads), {n} peers k={wl['k']}, "
-                      f"{wl['topics']} topics, Eth2 scoring, {MSGS_PER_ROUND} msgs/round, {hops} hops "
+                      f"{wl['topics']} topics, Eth2 scoring, {wl.get('msgs', MSGS_PER_ROUND)} msgs/round"
+                      f"{' (config-5 adversarial mix)' if wl.get('adversarial') else ''}, {hops} hops "
                       f"after 1 warm-up round, {dt:.1f} s"}
 
 
@@ -253,7 +292,8 @@ def main():
     kstats = eng.kernel_stats()
     eng.set_profiling(False)
     ev_keys = ("deliveries", "duplicates", "transmissions", "grafts_sent", "prunes_sent",
-               "ihave_sent", "iwant_sent", "iwant_served", "promises_broken", "graylisted")
+               "ihave_sent", "iwant_sent", "iwant_served", "promises_broken", "graylisted",
+               "rejected", "throttled", "gated")
     events = {k: c1[k] - c0[k] for k in ev_keys}
     if dist is not None:
         import torch
@@ -265,6 +305,7 @@ def main():
         dist.all_reduce(dv, op=dist.ReduceOp.SUM)
         events = dict(zip(ev_keys, (int(x) for x in dv.tolist())))
     deliveries = events["deliveries"]
+    msgs_round = wl.get("msgs", MSGS_PER_ROUND)
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -293,7 +334,7 @@ def main():
         return None, None
 
     traffic, traffic_src = pmc_traffic(dom)
-    if bytes_per_launch:
+    if bytes_per_launch and avg_ms > 0:
         achieved = bytes_per_launch / (avg_ms / 1e3) / 1e9
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
@@ -326,11 +367,13 @@ def main():
         "vs_baseline": None,
         "dtype": "f64+u64",
         "data": "synthetic (seeded random 32-regular graph, seeded publish schedule)",
-        "config": {"workload": args.workload + ": " + ("1M peers, 64 topics" if wl["topics"] == 64
-                                                        else "1M peers, 1 topic") +
-                   ", k=32, gossipsub v1.1 + Eth2 scoring, 1000 msgs/round, 10 hops/round",
+        "config": {"workload": f"{args.workload}: {wl['n'] / 1e6:g}M peers, {wl['topics']} topic"
+                   f"{'s' if wl['topics'] > 1 else ''}, k=32, gossipsub v1.1 + Eth2 scoring, "
+                   f"{msgs_round} msgs/round, 10 hops/round" +
+                   (", 20% Sybils (IWANT / GRAFT / phantom-IHAVE spam, invalid messages, 20 per IP), "
+                    "peer gater, validation queue 32" if wl.get("adversarial") else ""),
                    "peers": wl["n"], "topics": wl["topics"], "degree": wl["k"],
-                   "msgs_per_round": MSGS_PER_ROUND, "hops_per_round": HOPS_PER_ROUND,
+                   "msgs_per_round": msgs_round, "hops_per_round": HOPS_PER_ROUND,
                    "parallelism": f"partition{world}" if partitioned else f"replicas{world}"},
         "rounds_per_sec": rounds_per_s * (1 if partitioned else world),
         "hops_per_sec": rounds_per_s * HOPS_PER_ROUND,
