@@ -317,10 +317,6 @@ int gs_engine::start() {
   n1 = part[rank + 1];
   e0 = rowptr[n0];
   e1 = rowptr[n1];
-  if (world > 1 && (behaveAll & GS_BEHAVE_IWANT_SPAM)) {
-    gs_set_error("IWANT spammers need an unpartitioned engine (their request lists are not exchanged)");
-    return GS_EUNSUPPORTED;
-  }
   if (world > 1 && cfg.router == GS_ROUTER_RANDOMSUB) {
     gs_set_error("a partitioned engine supports floodsub and gossipsub (randomsub target masks are not exchanged)");
     return GS_EUNSUPPORTED;

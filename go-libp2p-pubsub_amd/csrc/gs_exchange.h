@@ -9,8 +9,9 @@
 //   - the sender's frontier list fl[u] / fln[u] (the payload of its RPCs),
 //   - the forwarding sets fwdRelay[r] / fwdPub[r] (the sender's mesh, fanout,
 //     direct and flood-publish choice for that edge),
-//   - the control outbox of edge r (GRAFT / PRUNE / IHAVE / IWANT entries) and
-//     the slot-id arena lists its IWANT records point at,
+//   - the control outbox of edge r (GRAFT / PRUNE / IHAVE / IWANT entries, an
+//     IWANT spammer's re-request list) and the slot-id arena lists its
+//     records point at,
 //   - after a heartbeat, the sender's IHAVE payload row gw[u].
 // Each rank keeps a full-size mirror of these arrays: its own nodes' entries
 // are written by its kernels, every other entry by the unpack kernels below.
@@ -26,14 +27,17 @@
 #pragma once
 #include "gs_device.h"
 
-struct XRec {  // 80 bytes
+struct XRec {  // 96 bytes
   int32_t e;   // the sender's edge (receiver reads it as rev[e'])
   uint8_t pre, hb;
-  uint16_t pad;
+  uint8_t nsrv;  // reply RPCs carrying served messages (IWANT-spam runs)
+  uint8_t pad;
   uint64_t relay, pub, gj, ghb, prep, phb, ihave;
   int64_t iwant, iresp;
+  int64_t spam;  // an IWANT spammer's re-request list (arena record), -1 = none
+  int64_t pad2;
 };
-static_assert(sizeof(XRec) == 80, "XRec layout");
+static_assert(sizeof(XRec) == 96, "XRec layout");
 
 __device__ __forceinline__ bool x_needed(const Dev& d, int cur, int64_t e, int& dest) {
   dest = d.nodeRank[d.col[e]];
@@ -72,6 +76,12 @@ __global__ void k_x_pack(Dev d, int cur, const int64_t* __restrict__ off, unsign
     x.ihave = d.cIhave[cur][e];
     x.iwant = d.cIwant[cur][e];
     x.iresp = d.cIresp[cur][e];
+    x.spam = d.cSpam[cur] != nullptr ? d.cSpam[cur][e] : -1;
+    x.nsrv = d.cNSrv[cur] != nullptr ? d.cNSrv[cur][e] : 0;
+    if (d.cSpam[cur] != nullptr) {
+      d.cSpam[cur][e] = -1;
+      d.cNSrv[cur][e] = 0;
+    }
     d.cPre[cur][e] = 0;
     d.cHb[cur][e] = 0;
     d.cGraftJoin[cur][e] = 0;
@@ -83,8 +93,10 @@ __global__ void k_x_pack(Dev d, int cur, const int64_t* __restrict__ off, unsign
     d.cIresp[cur][e] = -1;
   } else {
     x.gj = x.ghb = x.prep = x.phb = x.ihave = 0;
-    x.iwant = x.iresp = -1;
+    x.iwant = x.iresp = x.spam = -1;
+    x.nsrv = 0;
   }
+  x.pad2 = 0;
   d.xmark[e] = 0;
   out[k] = x;
 }
@@ -105,6 +117,10 @@ __global__ void k_x_unpack(Dev d, int cur, const XRec* __restrict__ in, int64_t 
   d.cIhave[cur][e] = x.ihave;
   d.cIwant[cur][e] = x.iwant;
   d.cIresp[cur][e] = x.iresp;
+  if (d.cSpam[cur] != nullptr) {
+    d.cSpam[cur][e] = x.spam;
+    d.cNSrv[cur][e] = x.nsrv;
+  }
 }
 
 // Frontier lists of the owned nodes: one wave per node, entries appended at a

@@ -40,7 +40,7 @@ def _worker(rank, world, port, name, oracle, q):
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
         from pubsub_amd import WithEventTracer
         tr = TorchTransport(memory="device")
-        traced = [u for u in TRACED if u < 20]
+        traced = [0, 1] if name.startswith("spam_") else [u for u in TRACED if u < 20]  # spam pairs: 2 nodes
         e, hops = scenarios.SCENARIOS[name](PRODUCT_LIB, (WithPartition(rank, world, tr), WithEventTracer(traced)))
         e.step(hops)
         got = scenarios.snapshot(e, range(e.n_published))
@@ -102,6 +102,11 @@ def run_partitioned(world, name, oracle):
     (2, "gossipsub_negative_app"),
     (3, "gossipsub_dense_dhi"),
     (2, "gossipsub_flood_publish"),
+    # the adversarial model across ranks: IWANT-spam re-request lists, served
+    # replies, GRAFT / IHAVE spam, the gater and the validation queue
+    (2, "spam_iwant"),
+    (2, "adversarial_mix"),
+    (3, "adversarial_mix_nogater"),
 ])
 def test_partitioned_engine_matches_oracle(world, name, oracle_path):
     res = run_partitioned(world, name, oracle_path)
