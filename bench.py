@@ -46,10 +46,9 @@ WORKLOADS = {
     # 10M-peer figure is the 8-GPU node's; --peers raises it), 20% Sybils split
     # over IWANT spam, GRAFT spam, phantom-IHAVE spam and invalid publishing,
     # 20 Sybils per shared IP, the peer gater, a topic validator with a
-    # 32-entry queue per hop.  50 msgs/round: an honest node keeps one
-    # mcache.peertx entry per (message, IWANT spammer) it served, and its
-    # table holds 4096 (the capacity limit of this build).
-    "config5": dict(n=1_000_000, k=32, topics=1, slots=10240, msgs=50, adversarial=True),
+    # 32-entry queue per hop.  500 msgs/round: the adversarial delivery
+    # window keeps 200 hops of messages alive (10240 slots).
+    "config5": dict(n=1_000_000, k=32, topics=1, slots=10240, msgs=500, adversarial=True),
 }
 
 

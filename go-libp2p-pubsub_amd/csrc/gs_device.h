@@ -154,6 +154,9 @@ struct Dev {
   int64_t* cSpam[2];     // [E] IWANT-spam request list (arena record), -1 = none
   int32_t* pmaskRow;     // [N] row of an IWANT spammer in pmask, -1 = none (nullptr: no spammers)
   uint64_t* pmask;       // [spammers][S] drec.peers: in-edges whose duplicate was counted
+  uint8_t* pflag[2];     // IWANT-spam runs: per arena entry, the served verdict of that request
+  int32_t* spamRow;      // [E] row of in-edge e in spamCnt when col[e] is an IWANT spammer, else -1
+  uint32_t* spamCnt;     // [rows][S / 4] mcache.peertx counts of those requesters, one byte per slot
   uint8_t* cNSrv[2];     // [E] reply RPCs carrying served messages (0..2)
   // peer gater (peer_gater.go), one per node; stats per (observer, IP) kept on
   // the observer's first edge to a peer of that IP (gGrp = its in-row index)
@@ -235,6 +238,29 @@ __device__ __forceinline__ bool behaves(const Dev& d, int v, unsigned bit) {
 __device__ __forceinline__ bool is_traced(const Dev& d, int v) { return d.traced != nullptr && d.traced[v] != 0; }
 __device__ __forceinline__ bool edge_up(const Dev& d, int64_t e) { return d.alive == nullptr || d.alive[e] != 0; }
 // Score(p) of an observer without a record of p is 0 (score.go:246-249)
+// mcache.peertx (mcache.go:66-80) of a requester that is an IWANT spammer: a
+// byte per (in-edge, slot) in HBM instead of the node's LDS hash, which would
+// need an entry per (message, spammer).  A count only matters while its
+// message is cached (GetForPeer), so it is cleared when the slot is recycled
+// (k_retire) rather than at mcache.Shift.  Saturates at 255 (> GossipRetransmission).
+__device__ __forceinline__ uint32_t* spam_word(const Dev& d, int row, int slot) {
+  return d.spamCnt + (int64_t)row * (d.S >> 2) + (slot >> 2);
+}
+__device__ __forceinline__ int spam_incr(const Dev& d, int row, int slot) {
+  uint32_t* w = spam_word(d, row, slot);
+  const int sh = (slot & 3) * 8;
+  uint32_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), assumed;
+  do {
+    assumed = old;
+    if (((assumed >> sh) & 0xFF) == 0xFF) return 0xFF;
+    old = atomicCAS(w, assumed, assumed + (1u << sh));
+  } while (old != assumed);
+  return (int)((assumed >> sh) & 0xFF) + 1;
+}
+__device__ __forceinline__ int spam_count(const Dev& d, int row, int slot) {
+  const uint32_t x = __hip_atomic_load(spam_word(d, row, slot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return (int)((x >> ((slot & 3) * 8)) & 0xFF);
+}
 __device__ __forceinline__ bool has_record(const Dev& d, int64_t e) { return d.rstate == nullptr || d.rstate[e] != 0; }
 __device__ __forceinline__ void set_err(const Dev& d, int code);
 __device__ __forceinline__ void trace_emit(const Dev& d, int64_t hop, int type, int node, int peer, int topic,

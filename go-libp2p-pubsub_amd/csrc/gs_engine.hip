@@ -96,6 +96,7 @@ struct gs_engine {
   uint64_t topicVal = 0;
   int32_t valQueue = 0;
   std::vector<uint8_t> behaveH;
+  std::vector<int32_t> spamRowH;  // host copy of Dev::spamRow
   uint8_t behaveAll = 0;               // OR of every node's bits
   bool anyPhantom = false;             // a published id is advertised only (GS_MSG_PHANTOM)
   bool gaterOn = false;
@@ -454,8 +455,10 @@ int gs_engine::start() {
   const size_t NQ = (size_t)N * GS_TABLE;
   x.promMid = dalloc<int64_t>(NQ); x.promExp = dalloc<int64_t>(NQ); x.promSlot = dalloc<int32_t>(NQ);
   x.promEdge = dalloc<uint8_t>(NQ); x.promN = dalloc<int32_t>(N);
-  // mcache.peertx: 512 entries per node; an IWANT spammer's requests add one
-  // per (message, spammer) to every neighbour's table, so spam runs get 4096
+  // mcache.peertx: 512 entries per node.  With IWANT spammers present the
+  // honest requests grow too (messages dropped by validation queues come back
+  // through gossip), so those runs get 4096; the spammers' own requests, one
+  // per (message, spammer), are counted in spamCnt instead
   x.ptxCap = (behaveAll & GS_BEHAVE_IWANT_SPAM) ? 4096 : GS_PTX;
   x.ptxHBits = 13;  // the dynamic hash of the 4096-entry table: 8192 slots (32 KiB)
   x.ptx = dalloc<uint64_t>((size_t)N * x.ptxCap); x.ptxN = dalloc<int32_t>(N);
@@ -507,6 +510,9 @@ int gs_engine::start() {
   x.cSpam[0] = x.cSpam[1] = nullptr;
   x.pmaskRow = nullptr;
   x.pmask = nullptr;
+  x.spamRow = nullptr;
+  x.spamCnt = nullptr;
+  x.pflag[0] = x.pflag[1] = nullptr;
   x.cNSrv[0] = x.cNSrv[1] = nullptr;
   if (behaveAll) {
     uint8_t* b = dalloc<uint8_t>(N); chk(b);
@@ -524,6 +530,16 @@ int gs_engine::start() {
       x.pmaskRow = dalloc<int32_t>(N); chk(x.pmaskRow);
       x.pmask = dalloc<uint64_t>((size_t)nsp * S); chk(x.pmask);
       if (ok) HIPCHECK(hipMemcpyAsync(x.pmaskRow, row.data(), (size_t)N * 4, hipMemcpyHostToDevice, stream));
+      // peertx counts of the owned edges whose peer is an IWANT spammer
+      spamRowH.assign((size_t)E, -1);
+      int64_t nrow = 0;
+      for (int64_t ee = e0; ee < e1; ++ee)
+        if (behaveH[col[ee]] & GS_BEHAVE_IWANT_SPAM) spamRowH[ee] = (int32_t)nrow++;
+      if (nrow > INT32_MAX) { gs_set_error("too many IWANT-spammer edges"); return GS_ECAPACITY; }
+      x.spamRow = dalloc<int32_t>(E); chk(x.spamRow);
+      for (int k = 0; k < 2; ++k) { x.pflag[k] = dalloc<uint8_t>((size_t)poolSeg * world); chk(x.pflag[k]); }
+      x.spamCnt = dalloc<uint32_t>((size_t)std::max<int64_t>(nrow, 1) * (S / 4)); chk(x.spamCnt);
+      if (ok) HIPCHECK(hipMemcpyAsync(x.spamRow, spamRowH.data(), (size_t)E * 4, hipMemcpyHostToDevice, stream));
     }
   }
   x.gater = gaterOn ? 1 : 0;

@@ -1393,6 +1393,23 @@ __global__ void k_retire(Dev d, int cur, const int32_t* __restrict__ words, int 
   const int v = d.n0 + (int)(k / nwords);
   const int w = words[k % nwords];
   d.seen[(int64_t)v * d.W + w] &= ~d.pubmask[cur][w];
+  if (d.spamRow != nullptr && d.pubmask[cur][w]) {
+    // a recycled slot starts with no peertx counts from v's spammer peers
+    const uint64_t pm = d.pubmask[cur][w];
+    for (int64_t e = d.rowptr[v]; e < d.rowptr[v + 1]; ++e) {
+      const int row = d.spamRow[e];
+      if (row < 0) continue;
+      uint32_t* c = d.spamCnt + (int64_t)row * (d.S >> 2) + w * 16;
+      for (int q = 0; q < 16; ++q) {
+        const uint32_t b = (uint32_t)(pm >> (4 * q)) & 0xFu;
+        if (!b) continue;
+        uint32_t m = 0;
+        for (int j = 0; j < 4; ++j)
+          if ((b >> j) & 1) m |= 0xFFu << (8 * j);
+        c[q] &= ~m;
+      }
+    }
+  }
   if (d.pmaskRow != nullptr && d.pmaskRow[v] >= 0) {  // a recycled slot starts a fresh record
     uint64_t y = d.pubmask[cur][w];
     while (y) {

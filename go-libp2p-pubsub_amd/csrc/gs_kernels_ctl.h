@@ -356,7 +356,7 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
   long long cServed = 0;
   int nSrv = 0;  // reply RPCs carrying served messages to this sender
   if (__ballot(gateIWant || gateSpam)) {
-    __shared__ int sSpOff[64], sSpN[64], sItI[64], sCntS[64];
+    __shared__ int sSpOff[64], sSpN[64], sItI[64], sCntS[64], sRow[64];
     // the peertx hash: static, or a larger dynamic table (IWANT-spam runs)
     extern __shared__ __attribute__((aligned(16))) uint32_t smemH[];
     const bool big = ADV && d.ptxCap > GS_PTX;
@@ -380,6 +380,7 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
     sSpOff[lane] = gateSpam ? (int)(spRec >> 24) : 0;
     sSpN[lane] = nS;
     sItI[lane] = itI;
+    sRow[lane] = (ADV && d.spamRow != nullptr && valid) ? d.spamRow[e] : -1;  // a spammer's counts: spamCnt
     sCnt[lane] = 0;
     sCntS[lane] = 0;
     sCur[lane] = 0;
@@ -410,20 +411,39 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
     auto cached = [&](int slot) {
       return ((scache[slot >> 6] >> (slot & 63)) & 1) && !(ADV && d.slotKind[slot] == GS_MSG_PHANTOM);
     };
-    // pass a: increments and per-sender served counts
-    for (int b = lane; b < totalItems; b += 64) {
-      int i, off, cnt;
-      bool sp;
-      item(b, i, off, cnt, sp);
-      int c = 0;
-      for (int q = 0; q < cnt; ++q) {
-        const int slot = d.pool[prv][off + q];
-        if (!cached(slot)) continue;
-        const uint64_t key = ((uint64_t)(uint32_t)slot << 32) | ((uint64_t)i << 8);
-        const int count = ptx_incr(d, hT, hbits, key);
-        if (count >= 1 && count <= d.GR) ++c;
+    // pass a: increments and per-sender served counts.  A spammer's two lists
+    // may name the same message (a copy dropped by the validation queue stays
+    // unseen, so it is asked for again after the IHAVE): its re-request RPC was
+    // sent first (phase A of the previous hop), so that list is counted first,
+    // and each request's own verdict is kept (pflag) for pass b.
+    const bool flags = ADV && d.pflag[0] != nullptr;
+    auto passA = [&](int which) {  // 0: IHAVE-reply lists, 1: spam lists, 2: both
+      for (int b = lane; b < totalItems; b += 64) {
+        int i, off, cnt;
+        bool sp;
+        item(b, i, off, cnt, sp);
+        if (which != 2 && sp != (which == 1)) continue;
+        int c = 0;
+        for (int q = 0; q < cnt; ++q) {
+          const int slot = d.pool[prv][off + q];
+          bool srv = false;
+          if (cached(slot)) {
+            const uint64_t key = ((uint64_t)(uint32_t)slot << 32) | ((uint64_t)i << 8);
+            const int count = (ADV && sRow[i] >= 0) ? spam_incr(d, sRow[i], slot) : ptx_incr(d, hT, hbits, key);
+            srv = count >= 1 && count <= d.GR;
+          }
+          if (srv) ++c;
+          if (flags) d.pflag[prv][off + q] = srv ? 1 : 0;
+        }
+        if (c) atomicAdd(sp ? &sCntS[i] : &sCnt[i], c);
       }
-      if (c) atomicAdd(sp ? &sCntS[i] : &sCnt[i], c);
+    };
+    if (flags) {
+      passA(1);
+      __syncthreads();
+      passA(0);
+    } else {
+      passA(2);
     }
     __syncthreads();
     int totalServed;
@@ -442,18 +462,24 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
         if (myServed) respRec = ((int64_t)(poolBase + myOff) << 24) | (int64_t)myServed;
         cServed = totalServed;
         __syncthreads();
-        // pass b: write the served ids (the counts are final now; an id is in
-        // at most one of a sender's two lists)
+        // pass b: write the served ids (without two lists per sender a request's
+        // verdict is its final count: an id is asked for at most once)
         for (int b = lane; b < totalItems; b += 64) {
           int i, off, cnt;
           bool sp;
           item(b, i, off, cnt, sp);
           for (int q = 0; q < cnt; ++q) {
             const int slot = d.pool[prv][off + q];
-            if (!cached(slot)) continue;
-            const uint64_t key = ((uint64_t)(uint32_t)slot << 32) | ((uint64_t)i << 8);
-            const int count = ptx_count(hT, hbits, key);
-            if (count >= 1 && count <= d.GR) d.pool[cur][sOut[i] + atomicAdd(&sCur[i], 1)] = slot;
+            bool srv;
+            if (flags) {
+              srv = d.pflag[prv][off + q] != 0;
+            } else {
+              if (!cached(slot)) continue;
+              const uint64_t key = ((uint64_t)(uint32_t)slot << 32) | ((uint64_t)i << 8);
+              const int count = (ADV && sRow[i] >= 0) ? spam_count(d, sRow[i], slot) : ptx_count(hT, hbits, key);
+              srv = count >= 1 && count <= d.GR;
+            }
+            if (srv) d.pool[cur][sOut[i] + atomicAdd(&sCur[i], 1)] = slot;
           }
         }
       }

@@ -23,9 +23,9 @@ def light(e):
     return s
 
 
-def main(name):
+def main(name, lib=None):
     a, hops = scenarios.SCENARIOS[name](ORACLE)
-    b, _ = scenarios.SCENARIOS[name](PRODUCT_LIB)
+    b, _ = scenarios.SCENARIOS[name](lib or PRODUCT_LIB)
     for h in range(hops):
         a.step(1)
         b.step(1)
@@ -53,4 +53,4 @@ def main(name):
 
 
 if __name__ == "__main__":
-    sys.exit(main(sys.argv[1] if len(sys.argv) > 1 else "gossipsub_scored"))
+    sys.exit(main(sys.argv[1] if len(sys.argv) > 1 else "gossipsub_scored", sys.argv[2] if len(sys.argv) > 2 else None))

@@ -337,7 +337,7 @@ def sinkhole(lib, extra=()):
 
 
 def adversarial_mix(lib, n=400, k=16, seed=51, sybil_frac=0.2, queue=6, msgs=600, hb=10, gater=True,
-                    extra=()):
+                    window=2048, extra=()):
     """A config-5-like mix: 20% Sybils split over IWANT spam,
     GRAFT spam, phantom-IHAVE spam and invalid-message publishing, 20 Sybils
     per shared IP (P6), the peer gater, topic validator with a bounded queue,
@@ -355,7 +355,7 @@ def adversarial_mix(lib, n=400, k=16, seed=51, sybil_frac=0.2, queue=6, msgs=600
     ipv4[ids] = (192 << 24) + (np.arange(len(ids)) // 20).astype(np.uint32)
     sp = eth2_peer_score_params(1)
     thr = eth2_thresholds()
-    opts = [WithPeerScore(sp, thr), WithHop(HOP), WithMessageWindow(2048), WithSeed(seed), WithBehaviour(beh),
+    opts = [WithPeerScore(sp, thr), WithHop(HOP), WithMessageWindow(window), WithSeed(seed), WithBehaviour(beh),
             WithValidation([1], queue), WithRecordDeliveries()]
     if gater:
         opts.append(WithPeerGater(DefaultPeerGaterParams()))
@@ -393,6 +393,12 @@ ADVERSARIAL = {
     "adversarial_mix_nogater": lambda lib, x=(): adversarial_mix(lib, gater=False, queue=0, seed=52, extra=x),
 }
 SCENARIOS.update(ADVERSARIAL)
+# bench.py config5 at a size the oracle finishes in seconds: degree 32, one
+# topic x 10240 slots (W = 160, 3 words per lane), validation queue 32, ~60
+# messages per hop, the ADV instantiations of phase A / phase B
+HEAVY["c5shape"] = lambda lib, x=(): adversarial_mix(lib, n=2000, k=32, seed=53, queue=32, msgs=4000, hb=10,
+                                                     window=10240, extra=x)
+SCENARIOS["c5shape"] = HEAVY["c5shape"]
 
 
 # ---------------------------------------------------------------- churn
