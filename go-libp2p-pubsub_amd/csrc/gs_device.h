@@ -188,6 +188,8 @@ struct Dev {
   double* score1;  // after the message phase (S1) / heartbeat memo
   uint8_t* sdirty; // [E] a score-lowering change (graft/prune/penalty/refresh) since score0
   int64_t* backoff;  // [T][E], 0 = none
+  uint64_t* boMask;  // [E] bit t: backoff of (e, t) is set (the heartbeat's candidate filter
+                     // reads one coalesced word per edge instead of a strided expiry per topic)
   double *fmd, *mmd, *mfp, *imd;  // per-(edge, topic) rows (tix)
   int32_t anyImd;                 // 0: no invalid delivery ever recorded, imd is all 0 (P4 = 0)
   uint32_t* dlt;                  // [E][T]: deliveries not yet folded into fmd / mmd,
@@ -519,6 +521,7 @@ __device__ __forceinline__ void add_backoff(const Dev& d, int64_t e, int t, int6
   const int64_t expire = now + interval;
   const int64_t cur = d.backoff[i];
   if (cur == 0 || cur < expire) d.backoff[i] = expire;
+  d.boMask[e] |= 1ull << t;  // the edge's observer only: no other wave writes it
 }
 
 // ---- slot-id arena: compact IWANT request / response payloads ----------

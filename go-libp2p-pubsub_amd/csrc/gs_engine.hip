@@ -481,6 +481,7 @@ int gs_engine::start() {
   x.score0 = dalloc<double>(E); x.score1 = dalloc<double>(E);
   x.sdirty = dalloc<uint8_t>(E, 1); chk(x.sdirty);
   x.backoff = dalloc<int64_t>(TE);
+  x.boMask = dalloc<uint64_t>(E); chk(x.boMask);
   x.fmd = dalloc<double>(TE); x.mmd = dalloc<double>(TE); x.mfp = dalloc<double>(TE); x.imd = dalloc<double>(TE);
   x.dlt = dalloc<uint32_t>(TE); chk(x.dlt);
   x.graftTime = dalloc<int64_t>(TE); x.meshTime = dalloc<int64_t>(TE); x.flags = dalloc<uint8_t>(TE);

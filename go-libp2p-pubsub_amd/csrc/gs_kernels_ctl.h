@@ -872,9 +872,16 @@ __global__ __launch_bounds__(64) void k_hb_pre(Dev d, int64_t now, uint64_t tick
     d.iasked[e] = 0;
   }
   if (ticks % 15 == 0) {  // v's in-edges own the contiguous pairs [base*T, (base+deg)*T)
-    for (int64_t i = base * d.T + lane; i < (base + deg) * d.T; i += 64) {
-      const int64_t be = d.backoff[i];
-      if (be != 0 && be + 2000000000LL < now) d.backoff[i] = 0;
+    for (int j = 0; j < deg; ++j) {  // one edge's topics per step (lane = topic), its mask rebuilt
+      const int64_t i = (base + j) * d.T + lane;
+      bool set = false;
+      if (lane < d.T) {
+        const int64_t be = d.backoff[i];
+        if (be != 0 && be + 2000000000LL < now) d.backoff[i] = 0;
+        else set = be != 0;
+      }
+      const uint64_t m = __ballot(set);
+      if (lane == 0) d.boMask[base + j] = m;
     }
   }
   if (!d.scoring) return;
@@ -1003,6 +1010,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
   const uint64_t subv = valid && edge_up(d, e) ? d.subA[vcol] : 0;  // topic peers: connected, announced
   uint64_t meshl = valid ? d.mesh[e] : 0;
   uint64_t fanl = valid ? d.fanout[e] : 0;
+  uint64_t boM = valid ? d.boMask[e] : 0;  // topics in backoff with this peer
   double S = valid ? d.score1[e] : 0.0;
   const uint64_t joined = d.sub[v];
   if (d.scoring && !allExact) {
@@ -1044,6 +1052,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
       stats_prune(d, e, t);
       meshl &= ~bit;
       add_backoff(d, e, t, now, d.PruneBackoff);
+      boM |= bit;
       toprune |= bit;
       dirty = true;
       m = false;
@@ -1051,7 +1060,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
     int cnt = __popcll(__ballot(m));
     // do we have enough peers?
     if (cnt < d.Dlo) {
-      const bool bo = valid && d.backoff[tix(d, t, e)] != 0;
+      const bool bo = (boM & bit) != 0;
       const bool cand = inTopic && !m && !bo && !dir && S >= 0;
       const uint64_t key = gs_key64(d.seed, GS_SITE_GP_DLO, v, hw, vcol, t);
       if (select_k_lds(cand, key, d.D - cnt, (uint64_t*)sterm)) {
@@ -1122,6 +1131,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
         stats_prune(d, e, t);
         meshl &= ~bit;
         add_backoff(d, e, t, now, d.PruneBackoff);
+        boM |= bit;
         toprune |= bit;
         dirty = true;
         m = false;
@@ -1133,7 +1143,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
     if (cnt >= d.Dlo) {
       const int outb = __popcll(__ballot(m && ob));
       if (outb < d.Dout) {
-        const bool bo = valid && d.backoff[tix(d, t, e)] != 0;
+        const bool bo = (boM & bit) != 0;
         const bool cand = inTopic && !m && !bo && !dir && ob && S >= 0;
         const uint64_t key = gs_key64(d.seed, GS_SITE_GP_DOUT, v, hw, vcol, t);
         if (select_k_lds(cand, key, d.Dout - outb, (uint64_t*)sterm)) {
@@ -1159,7 +1169,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
       const unsigned long long ml = __ballot(m && rank == cnt / 2);
       const double median = lane_getf(S, __ffsll((long long)ml) - 1);
       if (median < d.oppThr) {
-        const bool bo = valid && d.backoff[tix(d, t, e)] != 0;
+        const bool bo = (boM & bit) != 0;
         const bool cand = inTopic && !m && !bo && !dir && S > median;
         const uint64_t key = gs_key64(d.seed, GS_SITE_GP_OPPORTUNISTIC, v, hw, vcol, t);
         if (select_k_lds(cand, key, d.OGP, (uint64_t*)sterm)) {
@@ -1173,7 +1183,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
     }
     // a GRAFT spammer re-GRAFTs the topic peers it is in backoff with, leaving
     // its own mesh as it is (gossipsub_spam_test.go:449-500)
-    if (graftSpam && ticks > 1 && inTopic && !m) {
+    if (graftSpam && ticks > 1 && inTopic && !m && (boM & bit)) {
       const int64_t be = d.backoff[tix(d, t, e)];
       if (be != 0 && be > now) spamGraft |= bit;
     }

@@ -15,9 +15,10 @@ def main():
     ap.add_argument("--workload", default="config4", choices=sorted(bench.WORKLOADS))
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--rounds", type=int, default=1)
+    ap.add_argument("--lib", default=None, help="another build of the product library (experiments)")
     a = ap.parse_args()
     wl = bench.WORKLOADS[a.workload]
-    eng, _ = bench.build_engine(wl, a.warmup + a.rounds + 1, 3, 0)
+    eng, _ = bench.build_engine(wl, a.warmup + a.rounds + 1, 3, 0, lib=a.lib)
     eng.step(1 + a.warmup * bench.HOPS_PER_ROUND)
     eng.sync()
     print("warm", eng.counters(), flush=True)
