@@ -511,7 +511,12 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
     for (int w = lane; w < W; w += 64) sseen[w] = d.seen[(int64_t)v * W + w];
     const uint64_t tm = gateIHave ? (ihaveT & sv) : 0ull;
     int totalItems;
-    sIt[lane] = lane_prefix(__popcll(tm), &totalItems);
+    // An item is (sender, topic), or with long topic windows (Wt > 16 words,
+    // config3's 157) (sender, topic, 16-word chunk), so the lanes share the
+    // words of one topic; with cuts an item stays a whole topic (the cut is
+    // per (sender, topic)).  At most 64 items per sender either way.
+    const int nCh = (cutMode || Wt <= 16) ? 1 : (Wt + 15) >> 4;
+    sIt[lane] = lane_prefix(__popcll(tm) * nCh, &totalItems);
     sTm[lane] = tm;
     sNode[lane] = u;
     sCnt[lane] = 0;
@@ -592,14 +597,16 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
         __syncthreads();
       }
     }
-    // the advertised wants of item b: fn(w, want) per word with a want
-    auto wants = [&](int b, int uu, int t, auto&& fn) {
+    // the advertised wants of item b (topic t, chunk ch): fn(w, want) per word
+    // with a want
+    auto wants = [&](int b, int uu, int t, int ch, auto&& fn) {
       int ci = -1;
       if (nCut && ((cBits[b >> 5] >> (b & 31)) & 1))
         for (int c = 0; c < nCut; ++c)
           if (cItem[c] == b) ci = c;
-      const int wEnd = (t + 1) * Wt;
-      for (int w0 = t * Wt; w0 < wEnd; w0 += 4) {
+      const int wBeg = nCh > 1 ? t * Wt + 16 * ch : t * Wt;
+      const int wEnd = nCh > 1 ? min(wBeg + 16, (t + 1) * Wt) : (t + 1) * Wt;
+      for (int w0 = wBeg; w0 < wEnd; w0 += 4) {
         uint64_t g[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) g[q] = d.gw[(int64_t)uu * W + min(w0 + q, wEnd - 1)];
@@ -629,11 +636,11 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
     for (int b = lane; b < totalItems; b += 64) {
       int k;
       const int i = item_sender(sIt, b, k);
-      const int t = kth_bit(sTm[i], k);
+      const int t = kth_bit(sTm[i], k / nCh), ch = k % nCh;
       const int uu = sNode[i];
       int c = 0;
       uint64_t bestKey = ~0ull;
-      wants(b, uu, t, [&](int w, uint64_t want) {
+      wants(b, uu, t, ch, [&](int w, uint64_t want) {
         c += __popcll(want);
         uint64_t y = want;
         while (y) {
@@ -657,10 +664,10 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
       if (!((sHas[b >> 5] >> (b & 31)) & 1)) continue;
       int k;
       const int i = item_sender(sIt, b, k);
-      const int t = kth_bit(sTm[i], k);
+      const int t = kth_bit(sTm[i], k / nCh), ch = k % nCh;
       const int uu = sNode[i];
       const uint64_t best = sKey[i];
-      wants(b, uu, t, [&](int w, uint64_t want) {
+      wants(b, uu, t, ch, [&](int w, uint64_t want) {
         uint64_t y = want;
         while (y) {
           const int bb = __ffsll((long long)y) - 1;
@@ -739,11 +746,11 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
           if (!((sHas[b >> 5] >> (b & 31)) & 1)) continue;
           int k;
           const int i = item_sender(sIt, b, k);
-          const int t = kth_bit(sTm[i], k);
+          const int t = kth_bit(sTm[i], k / nCh), ch = k % nCh;
           const int uu = sNode[i];
           const long long bestMid = sMid[i];
           const bool cutI = (cutSenders >> i) & 1;
-          wants(b, uu, t, [&](int w, uint64_t want) {
+          wants(b, uu, t, ch, [&](int w, uint64_t want) {
             uint64_t y = want;
             while (y) {
               const int bb = __ffsll((long long)y) - 1;

@@ -35,6 +35,20 @@ __global__ void k_rmw4(uint32_t* __restrict__ p, size_t n) {
     p[i] = p[i] + 1u;
 }
 
+// phase A's list walk pattern: 400-byte lists (100 four-byte entries) at an
+// 8576-byte row stride (FC = 2144 entries), read as 16-byte blocks, one list
+// per half-wave here; each list is read once
+__global__ void k_lists(const uint8_t* __restrict__ p, int nlist, unsigned long long* out, unsigned long long magic) {
+  const int l = blockIdx.x * 2 + (threadIdx.x >> 5);
+  const int b = threadIdx.x & 31;
+  unsigned long long acc = 0;
+  if (l < nlist && b < 25) {
+    const uint4 x = *(const uint4*)(p + (size_t)l * 8576 + 16 * b);
+    acc = x.x + x.w;
+  }
+  if (acc == magic) out[0] = acc;  // a runtime value: the loads cannot be proven dead
+}
+
 int main() {
   const size_t GiB = 1ull << 30;
   uint8_t* buf = nullptr;
@@ -52,8 +66,11 @@ int main() {
   k_write<uint64_t><<<grid, blk>>>((uint64_t*)(buf + GiB), GiB / 8);
   k_write<uint4><<<grid, blk>>>((uint4*)(buf + 2 * GiB), GiB / 16);
   k_rmw4<<<grid, blk>>>((uint32_t*)(buf + 3 * GiB), GiB / 4);
+  const int nlist = 400000;  // 400000 * 8576 B = 3.4 GB of rows, 160 MB of lists
+  k_lists<<<nlist / 2, 64>>>(buf, nlist, out, 0x123456789ull);
   CHECK(hipDeviceSynchronize());
-  printf("each kernel streams %zu bytes (rmw4: read and write)\n", GiB);
+  printf("each kernel streams %zu bytes (rmw4: read and write); k_lists reads %d lists of 400 B "
+         "(%d bytes, %d bytes of 128-B lines)\n", GiB, nlist, nlist * 400, nlist * 512);
   CHECK(hipFree(buf));
   CHECK(hipFree(out));
   return 0;
