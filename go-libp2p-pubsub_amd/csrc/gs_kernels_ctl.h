@@ -186,8 +186,9 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
   unsigned long long* const sKey = (unsigned long long*)(sH + 192);
   long long* const sMid = (long long*)(sH + 320);
   int* const sSlot = (int*)(sH + 448);
-  uint32_t* const sHas = (uint32_t*)(sH + 512);  // step 3: items with a want (<= 64 senders x 64 topics)
-  static_assert(512 + 64 * 64 / 32 <= GS_PTXH, "step-3 arrays must fit in the peertx hash");
+  uint32_t* const sHas = (uint32_t*)(sH + 512);  // step 3: items with a want (<= 64 senders x 64 items)
+  uint32_t* const sCand = (uint32_t*)(sH + 640); // step 3: items that held their sender's smallest key
+  static_assert(640 + 64 * 64 / 32 <= GS_PTXH, "step-3 arrays must fit in the peertx hash");
   const int v = d.n0 + blockIdx.x;
   const int lane = lane_id();
   const int prv = cur ^ 1;
@@ -361,8 +362,20 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
     extern __shared__ __attribute__((aligned(16))) uint32_t smemH[];
     const bool big = ADV && d.ptxCap > GS_PTX;
     unsigned int* const hT = big ? (unsigned int*)(smemH + GS_CUTLDS / 4) : sH;
-    const int hbits = big ? d.ptxHBits : 10;
     const int ptxCap = ADV ? d.ptxCap : GS_PTX;  // the honest instantiation always has GS_PTX
+    const int nI = gateIWant ? (int)(iwRec & 0xFFFFFF) : 0;
+    const int nS = gateSpam ? (int)(spRec & 0xFFFFFF) : 0;
+    // the large table is sized to this node's load (entries it holds plus the
+    // keys this hop can add, at most half full), so a lightly loaded node
+    // clears and writes back a small table; lookups use the same size
+    int hbits = 10;
+    if (big) {
+      int tot;
+      (void)lane_prefix(nI + nS, &tot);
+      const int need = 2 * (d.ptxN[v] + tot);
+      hbits = 10;
+      while (hbits < d.ptxHBits && (1 << hbits) < need) ++hbits;
+    }
     const int hN = 1 << hbits;
     for (int w = lane; w < W; w += 64) {
       uint64_t x = 0;
@@ -370,8 +383,6 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
       scache[w] = x;
     }
     for (int k = lane; k < hN; k += 64) hT[k] = 0u;
-    const int nI = gateIWant ? (int)(iwRec & 0xFFFFFF) : 0;
-    const int nS = gateSpam ? (int)(spRec & 0xFFFFFF) : 0;
     const int itI = (nI + 15) >> 4, itS = (nS + 15) >> 4;
     int totalItems;
     sIt[lane] = lane_prefix(itI + itS, &totalItems);
@@ -528,7 +539,7 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
     // The wanted words of item (sender i, topic t): the advertised window of
     // the sender minus v's seen row, four words loaded at once.
     const int nHas = (totalItems + 31) >> 5;
-    for (int k = lane; k < nHas; k += 64) sHas[k] = 0u;
+    for (int k = lane; k < nHas; k += 64) sHas[k] = sCand[k] = 0u;
     // ---- MaxIHaveLength cuts (cutMode: the host saw that a topic may hold
     // more gossip ids than that).  Item cut: a sender with more than
     // MaxIHaveLength ids of a topic advertised its own keyed subset to v
@@ -653,15 +664,18 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
       });
       if (c) {
         atomicAdd(&sCnt[i], c);
-        atomicMin(&sKey[i], bestKey);
+        // an item whose key was the sender's smallest when it got there is a
+        // candidate for pass a2 (a superset of the items holding the final one)
+        if (bestKey <= atomicMin(&sKey[i], bestKey)) atomicOr(&sCand[b >> 5], 1u << (b & 31));
         atomicOr(&sHas[b >> 5], 1u << (b & 31));
       }
     }
     __syncthreads();
     GS_STAMPB(5);
-    // pass a2: the smallest mid among the wants holding the smallest key
+    // pass a2: the smallest mid among the wants holding the smallest key (only
+    // the candidate items can hold it)
     for (int b = lane; b < totalItems; b += 64) {
-      if (!((sHas[b >> 5] >> (b & 31)) & 1)) continue;
+      if (!((sCand[b >> 5] >> (b & 31)) & 1)) continue;
       int k;
       const int i = item_sender(sIt, b, k);
       const int t = kth_bit(sTm[i], k / nCh), ch = k % nCh;
