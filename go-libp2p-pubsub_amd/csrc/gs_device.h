@@ -14,6 +14,7 @@
 
 #include "../../include/gossip_engine.h"
 #include "../../include/gs_rng.h"
+#include "../../include/gs_rpcsize.h"
 
 #define GS_WAVE 64
 // Occupancy hints (waves per SIMD the register allocator must allow) of the
@@ -78,6 +79,15 @@ struct TopicP {  // TopicScoreParams (score_params.go:98-148) + scored flag
   int32_t pad;
 };
 
+// RPC byte accounting (gs_set_rpc_accounting): per topic, the sizes of the
+// RPC parts that carry it (include/gs_rpcsize.h)
+struct AcctT {
+  int32_t msgF;       // RPC.publish entry of a message of the topic
+  int32_t graftEnt;   // ControlMessage.graft entry
+  int32_t pruneEnt;   // ControlMessage.prune entry (makePrune: topic + backoff)
+  int32_t ihaveHead;  // ControlIHave topicID field (the ids add acctIdF each)
+};
+
 struct Dev {
   // sizes
   int32_t N, T, Wt, W, St, S, R, HL, HG;
@@ -90,6 +100,13 @@ struct Dev {
   int32_t n0, n1, rank, world;
   int64_t e0, e1;
   uint8_t* xmark;   // [E] forwarding set changed since its parity was exchanged (world > 1)
+  // RPC byte accounting (gs_set_rpc_accounting); rpcB == nullptr: off
+  unsigned long long* rpcB;    // [E] bytes of the RPCs sent over the sender's edge e
+  unsigned long long* rpcN;    // [E] RPCs sent over edge e
+  unsigned long long* rpcBin;  // [E] payload RPCs received over in-edge e (the receiver's row)
+  unsigned long long* rpcNin;
+  const AcctT* acc;            // [T]
+  int32_t acctIdF;             // one message id inside an IHAVE / IWANT
   // EventTracer of the hosts with traced[u] != 0 (gs_set_trace); nullptr = off
   const uint8_t* traced;
   gs_trace_event* trace;
@@ -262,6 +279,11 @@ __device__ __forceinline__ int spam_incr(const Dev& d, int row, int slot) {
 __device__ __forceinline__ int spam_count(const Dev& d, int row, int slot) {
   const uint32_t x = __hip_atomic_load(spam_word(d, row, slot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return (int)((x >> ((slot & 3) * 8)) & 0xFF);
+}
+// count one or more RPCs of `bytes` in total sent over the sender's edge e
+__device__ __forceinline__ void acct_send(const Dev& d, int64_t e, int64_t bytes, int n) {
+  d.rpcB[e] += (unsigned long long)bytes;
+  d.rpcN[e] += (unsigned long long)n;
 }
 __device__ __forceinline__ bool has_record(const Dev& d, int64_t e) { return d.rstate == nullptr || d.rstate[e] != 0; }
 __device__ __forceinline__ void set_err(const Dev& d, int code);

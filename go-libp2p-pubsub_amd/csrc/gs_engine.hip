@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include "../../include/gs_rpcsize.h"
 #include <map>
 #include <tuple>
 #include <chrono>
@@ -133,6 +134,20 @@ struct gs_engine {
   // trace events (gs_set_trace / gs_trace_read)
   std::vector<uint8_t> traceMask;
   int64_t traceCap = 0;
+  // RPC byte accounting (gs_set_rpc_accounting)
+  bool acctOn = false;
+  std::vector<int32_t> acctMsg, acctTl;
+  int32_t acctIdLen = 0;
+  std::vector<int64_t> acctPend;        // (edge, bytes) pairs sent by the host side this hop
+  int64_t* dAcctPend = nullptr;
+  int64_t acctPendCap = 0;
+  int64_t helloBytes(uint64_t subs) const {  // getHelloPacket: one SubOpts per subscribed topic
+    int64_t b = 0;
+    for (int t = 0; t < T; ++t)
+      if ((subs >> t) & 1) b += gs_pb_field(gs_pb_subopts(acctTl[t]));
+    return b;
+  }
+  int flushAcct();
   std::vector<gs_trace_event> tracePending;  // converted, canonical order from traceOut
   size_t traceOut = 0;
   int drainTrace();
@@ -633,8 +648,58 @@ int gs_engine::start() {
     const int rc = enableChurn();
     if (rc) return rc;
   }
+  x.rpcB = x.rpcN = x.rpcBin = x.rpcNin = nullptr;
+  x.acc = nullptr;
+  if (acctOn) {
+    if (world > 1) {
+      gs_set_error("RPC byte accounting needs an unpartitioned engine");
+      return GS_EUNSUPPORTED;
+    }
+    x.rpcB = dalloc<unsigned long long>(E); x.rpcN = dalloc<unsigned long long>(E);
+    x.rpcBin = dalloc<unsigned long long>(E); x.rpcNin = dalloc<unsigned long long>(E);
+    AcctT* ac = dalloc<AcctT>(T);
+    chk(x.rpcB); chk(x.rpcN); chk(x.rpcBin); chk(x.rpcNin); chk(ac);
+    if (!ok) { gs_set_error("device allocation failed (RPC accounting)"); return GS_ENOMEM; }
+    const uint64_t bo = (uint64_t)(gp.PruneBackoff / kSec);
+    std::vector<AcctT> ah(T);
+    for (int t = 0; t < T; ++t) {
+      ah[t].msgF = (int32_t)gs_pb_field(acctMsg[t]);
+      ah[t].graftEnt = (int32_t)gs_pb_field(gs_pb_graft(acctTl[t]));
+      ah[t].pruneEnt = (int32_t)gs_pb_field(gs_pb_prune(acctTl[t], bo));
+      ah[t].ihaveHead = (int32_t)gs_pb_field(acctTl[t]);
+    }
+    x.acctIdF = (int32_t)gs_pb_field(acctIdLen);
+    // the hello packet of every connection present at the start (pubsub.go:495)
+    std::vector<unsigned long long> hb((size_t)E), hn((size_t)E, 1ull);
+    for (int u = 0; u < N; ++u)
+      for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) hb[e] = (unsigned long long)helloBytes(sub[u]);
+    HIPCHECK(hipMemcpyAsync(ac, ah.data(), (size_t)T * sizeof(AcctT), hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipMemcpyAsync(x.rpcB, hb.data(), (size_t)E * 8, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipMemcpyAsync(x.rpcN, hn.data(), (size_t)E * 8, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipStreamSynchronize(stream));  // pageable sources
+    x.acc = ac;
+  }
   started = true;
   return uploadMessages();
+}
+
+// host-side RPCs of this hop (hello packets, subscription announcements): one
+// (edge, bytes) pair each, added on the device
+int gs_engine::flushAcct() {
+  if (acctPend.empty()) return GS_OK;
+  if ((int64_t)acctPend.size() > acctPendCap) {
+    int64_t* p = nullptr;
+    HIPCHECK(hipMalloc(&p, acctPend.size() * 2 * 8));
+    allocs.push_back(p);
+    dAcctPend = p;
+    acctPendCap = (int64_t)acctPend.size() * 2;
+  }
+  HIPCHECK(hipMemcpyAsync(dAcctPend, acctPend.data(), acctPend.size() * 8, hipMemcpyHostToDevice, stream));
+  const int n = (int)(acctPend.size() / 2);
+  k_acct_add<<<nblk(n, 256), 256, 0, stream>>>(d, dAcctPend, n);
+  HIPCHECK(hipStreamSynchronize(stream));  // acctPend is pageable
+  acctPend.clear();
+  return GS_OK;
 }
 
 int gs_engine::uploadMessages() {
@@ -756,10 +821,16 @@ int gs_engine::applyEvents(int64_t h) {
         auto& lst = pass == GS_EV_CONNECT ? up : down;
         lst.push_back((int32_t)ab);
         lst.push_back((int32_t)ba);
+        if (acctOn && want) {  // hello packets both ways (pubsub.go:534)
+          acctPend.insert(acctPend.end(), {ab, helloBytes(sub[ev.a]), ba, helloBytes(sub[ev.b])});
+        }
       } else {
         const uint64_t bit = 1ull << ev.b;
         const bool joinEv = pass == GS_EV_JOIN;
         if (((sub[ev.a] & bit) != 0) == joinEv) continue;
+        if (acctOn)  // announce (pubsub.go:775-792) to every connected peer
+          for (int64_t e = rowptr[ev.a]; e < rowptr[ev.a + 1]; ++e)
+            if (aliveH[e]) acctPend.insert(acctPend.end(), {e, gs_pb_field(gs_pb_subopts(acctTl[ev.b]))});
         sub[ev.a] = joinEv ? (sub[ev.a] | bit) : (sub[ev.a] & ~bit);
         subChanged = true;
         pendAnn.push_back({ev.a, ev.b, joinEv});
@@ -776,12 +847,18 @@ int gs_engine::applyEvents(int64_t h) {
       lst.push_back((int32_t)(uint32_t)(kv.second >> 32));
     }
   }
+  if (acctOn) {
+    const int rc = flushAcct();
+    if (rc) return rc;
+  }
   if (subAChanged) HIPCHECK(hipMemcpyAsync(dSubA, subA.data(), (size_t)N * 8, hipMemcpyHostToDevice, stream));
   if (subChanged) HIPCHECK(hipMemcpyAsync(dSubOwn, sub.data(), (size_t)N * 8, hipMemcpyHostToDevice, stream));
   if (subAChanged || subChanged) HIPCHECK(hipStreamSynchronize(stream));  // pageable sources
   if (!down.empty()) {
     int rc = uploadList(down);
     if (rc) return rc;
+    // the payload RPCs in flight on a closed connection were sent (and lost)
+    if (acctOn) k_acct_drop<<<nblk((int64_t)down.size(), 256), 256, 0, stream>>>(d, dEv, (int)down.size(), prv);
     k_edge_down<<<(unsigned)down.size(), 64, 0, stream>>>(d, dEv, h, now, prv);
     recChanged = true;
   }
@@ -916,7 +993,8 @@ int gs_engine::stepOne() {
     // instantiation: the honest path keeps its LDS budget and code
     const bool adv = topicVal != 0 || gaterOn || behaveAll != 0;
     const bool hasUnc = d.needAge || (adv && d.pmaskRow != nullptr);
-    size_t lds = (narrow ? 2 : 4) * nCnt + 16 * (size_t)nR + (size_t)nYp + (hasUnc ? 4 * nCnt : 0);
+    size_t lds = (narrow ? 2 : 4) * nCnt + 16 * (size_t)nR + (size_t)nYp + (hasUnc ? 4 * nCnt : 0) +
+                 (acctOn ? 512 : 0);
     if (adv) lds += 4 * nCnt + 4 * 64 * 4 + 8 * 64 + 8 * (size_t)nR;
     TIMED(this, GS_K_PHASE_A, launch_wpl(W, [&](auto w) {
             if (!nOwn) return;
@@ -1637,6 +1715,53 @@ int gs_partition_range(const gs_engine* g, int32_t* node_begin, int32_t* node_en
   const std::vector<int32_t> part = partition_bounds(g->rowptr, g->N, g->world);
   *node_begin = part[g->rank];
   *node_end = part[g->rank + 1];
+  return GS_OK;
+}
+
+int gs_set_rpc_accounting(gs_engine* g, const int32_t* msg_size, int32_t id_len, const int32_t* topic_len) {
+  if (g->started) { gs_set_error("gs_set_rpc_accounting: before the first step"); return GS_ESTATE; }
+  if (!msg_size || !topic_len || id_len < 0) { gs_set_error("gs_set_rpc_accounting: bad arguments"); return GS_EINVAL; }
+  for (int t = 0; t < g->T; ++t)
+    if (msg_size[t] < 0 || topic_len[t] < 0) { gs_set_error("gs_set_rpc_accounting: negative size"); return GS_EINVAL; }
+  g->acctOn = true;
+  g->acctMsg.assign(msg_size, msg_size + g->T);
+  g->acctTl.assign(topic_len, topic_len + g->T);
+  g->acctIdLen = id_len;
+  return GS_OK;
+}
+
+int gs_read_rpc_bytes(gs_engine* g, int64_t* bytes, int64_t* rpcs) {
+  if (!g->acctOn) { gs_set_error("gs_read_rpc_bytes: accounting is off"); return GS_ESTATE; }
+  const int64_t E = g->E;
+  if (!g->started) {
+    for (int64_t e = 0; e < E; ++e) {
+      if (bytes) bytes[e] = 0;
+      if (rpcs) rpcs[e] = 0;
+    }
+    return GS_OK;
+  }
+  // sender-side sums plus the payload RPCs counted at the receiver (in-edge
+  // rev[e] of col[e] carries what u sent over e)
+  std::vector<unsigned long long> b(E), n(E), bi(E), ni(E), fb(E, 0ull), fn(E, 0ull);
+  if (g->hop > 0) {  // the last hop's payload RPCs, sent but not received yet
+    unsigned long long* t = nullptr;
+    HIPCHECK(hipMalloc(&t, (size_t)E * 16));
+    k_acct_inflight<<<nblk(E, 256), 256, 0, g->stream>>>(g->d, (int)((g->hop - 1) & 1), t, t + E);
+    HIPCHECK(hipMemcpyAsync(fb.data(), t, (size_t)E * 8, hipMemcpyDeviceToHost, g->stream));
+    HIPCHECK(hipMemcpyAsync(fn.data(), t + E, (size_t)E * 8, hipMemcpyDeviceToHost, g->stream));
+    HIPCHECK(hipStreamSynchronize(g->stream));
+    HIPCHECK(hipFree(t));
+  }
+  HIPCHECK(hipStreamSynchronize(g->stream));
+  HIPCHECK(hipMemcpy(b.data(), g->d.rpcB, (size_t)E * 8, hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(n.data(), g->d.rpcN, (size_t)E * 8, hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(bi.data(), g->d.rpcBin, (size_t)E * 8, hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(ni.data(), g->d.rpcNin, (size_t)E * 8, hipMemcpyDeviceToHost));
+  for (int64_t e = 0; e < E; ++e) {
+    const int64_t r = g->rev[e];
+    if (bytes) bytes[e] = (int64_t)(b[e] + bi[r] + fb[r]);
+    if (rpcs) rpcs[e] = (int64_t)(n[e] + ni[r] + fn[r]);
+  }
   return GS_OK;
 }
 

@@ -335,6 +335,11 @@ __global__ __launch_bounds__(64) void k_join(Dev d, int64_t hop, int64_t now, in
     d.mesh[e] = meshl;
     d.cGraftJoin[cur][e] = gj;
     d.cPre[cur][e] = (uint8_t)__popcll(gj);
+    if (d.rpcB != nullptr && gj) {  // one sendGraft RPC per topic (gossipsub.go:1080-1084)
+      int64_t b = 0;
+      for (uint64_t m = gj; m; m &= m - 1) b += gs_pb_field(d.acc[__ffsll((long long)m) - 1].graftEnt);
+      acct_send(d, e, b, __popcll(gj));
+    }
   }
   int g = wave_sum_int(valid ? __popcll(gj) : 0);
   if (lane == 0 && g) ctr_add(d, C_GRAFTS, (unsigned long long)g);
@@ -546,8 +551,11 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
   extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
   const int nCnt = (d.T * d.maxDeg + 7) & ~7;
   const int nCntW = NARROW ? nCnt / 2 : nCnt;             // LDS words of the counter table
-  uint32_t* scnt = smem32;  // [MD][T] copies | fresh << 16 (NARROW: u16 copies | fresh << 8)
-  uint64_t* sD = (uint64_t*)(smem32 + nCntW);             // [nR] delivered young slots (non-graylisted)
+  // RPC accounting: payload bytes / RPCs per sender, ahead of the other tables
+  uint32_t* const sAccB = smem32;
+  uint32_t* const sAccN = smem32 + 64;
+  uint32_t* scnt = smem32 + (d.rpcB != nullptr ? 128 : 0);  // [MD][T] copies | fresh << 16 (NARROW: u16 copies | fresh << 8)
+  uint64_t* sD = (uint64_t*)(scnt + nCntW);               // [nR] delivered young slots (non-graylisted)
   uint64_t* sYm = sD + nR;                                // [nR] young-slot mask of each amR word
   uint8_t* sFirst = (uint8_t*)(sYm + nR);                 // [nY] lowest deliverer per young slot
   uint32_t* sUnc = (uint32_t*)(sFirst + nY);              // [MD][T] uncredited duplicates (needAge / pmask)
@@ -614,6 +622,11 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
   GS_STAMP(0);
   const bool authV = d.nAuth[v] > 0;  // v authored a live message: author exclusion possible
   for (int k = lane; k < nCntW / 4; k += 64) ((uint4*)scnt)[k] = make_uint4(0, 0, 0, 0);
+  const bool acct = d.rpcB != nullptr;
+  if (acct) {
+    sAccB[lane] = 0u;
+    sAccN[lane] = 0u;
+  }
   if (hasUnc)
     for (int k = lane; k < nCnt / 4; k += 64) ((uint4*)sUnc)[k] = make_uint4(0, 0, 0, 0);
   for (int k = lane; k < nR; k += 64) {
@@ -823,6 +836,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
         uint32_t en[4];
         bool sn[4];
         {
+          uint32_t accB = 0, accN = 0;
           const int i = si[rr] < 0 ? 0 : si[rr];
           const int snd = sSnd[i];
           const int uu = snd & 0xFFFFFF;
@@ -843,9 +857,17 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
             if (count) {
               nSent += sent;
               if (sent && isGray) ++nGray;  // one RPC per relayed message, all dropped
+              if (acct && sent) {  // rpcWithMessages: RPC = one publish entry
+                accB += (uint32_t)d.acc[t].msgF;
+                ++accN;
+              }
             }
             sn[c] = sent && !isGray;
             en[c] = (uint32_t)slot | ((uint32_t)i << 16);
+          }
+          if (accN) {
+            atomicAdd(&sAccB[i], accB);
+            atomicAdd(&sAccN[i], accN);
           }
         }
         // c-major positions (delivery order does not matter: every update is
@@ -880,6 +902,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
     __syncthreads();
   };
   walk([&](int i, int slot) { deliver(i, slot, true); }, true);
+  uint32_t myAccB = 0, myAccN = 0;  // RPC accounting of the copies below (lane = sender)
   if (__ballot(((relayAll | pubAll) & ~sv) != 0)) {
     // copies of topics v is not subscribed to: transmitted, then ignored
     // (churn runs only: a mesh or announced peer that has just left)
@@ -897,6 +920,10 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
         if (sent) {
           ++nSent;
           if (gray) ++nGray;
+          if (acct) {
+            myAccB += (uint32_t)d.acc[t].msgF;
+            ++myAccN;
+          }
         }
       }
     }
@@ -1289,6 +1316,8 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
           each([&](int slot) { d.pool[cur][p++] = slot; });
           d.cSpam[cur][base + lane] = ((int64_t)off << 24) | (int64_t)n;
           d.cPre[cur][base + lane] = (uint8_t)(d.cPre[cur][base + lane] + 1);
+          // RPC{control: {iwant: [{n ids}]}}
+          if (acct) acct_send(d, base + lane, gs_pb_field(gs_pb_field((int64_t)n * d.acctIdF)), 1);
           ctr_add(d, C_IWANT_SENT, (unsigned long long)n);
         }
       }
@@ -1352,6 +1381,13 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
     }
   }
   GS_STAMP(4);
+  if (acct && valid) {  // the payload RPCs received from each sender this hop
+    const uint32_t nn = sAccN[lane] + myAccN;
+    if (nn) {
+      d.rpcBin[base + lane] += (unsigned long long)(sAccB[lane] + myAccB);
+      d.rpcNin[base + lane] += (unsigned long long)nn;
+    }
+  }
   if (lane == 0) d.fln[cur][v] = behaves(d, v, GS_BEHAVE_NO_FORWARD) ? 0 : (running < FC ? running : FC);
   const long long deliv = (long long)wave_sum_ll(nDeliv);
   const unsigned long long copies = wave_sum_ll(nCopies), s2 = wave_sum_ll(nSent), s3 = wave_sum_ll(nGray);
@@ -1515,6 +1551,63 @@ __device__ __forceinline__ double gdecay(double x, double f, double z) {
   x *= f;
   return x < z ? 0.0 : x;
 }
+// RPC accounting: the payload RPCs in flight to v over its in-edge e, sent by
+// u = col[e] in the hop of parity p (phase A counts payload at the receiver:
+// this adds what a disconnect drops and what the last hop has sent but
+// nobody has received yet).  The same filter as phase A's list walk.
+__device__ __forceinline__ void inflight_payload(const Dev& d, int64_t e, int p, unsigned long long& b,
+                                                 unsigned long long& n) {
+  const int v = d.esrc[e];
+  const int u = d.col[e];
+  const int64_t r = d.rev[e];
+  const int jr = (int)(r - d.rowptr[u]);
+  const uint64_t ru = d.fwdRelay[p][r], pu = d.fwdPub[p][r];
+  b = n = 0;
+  if (!(ru | pu)) return;
+  const int Ln = d.fln[p][u];
+  const uint32_t* L = d.fl[p] + (int64_t)u * d.FC;
+  const bool authV = d.nAuth[v] > 0;
+  for (int k = 0; k < Ln; ++k) {
+    const uint32_t ent = L[k];
+    const int slot = (int)(ent & 0xFFFF), tag = (int)(ent >> 16);
+    const int t = (int)__umulhi((unsigned)slot, d.stMagic);
+    bool sent = tag == 255 ? ((pu >> t) & 1) : ((ru >> t) & 1);
+    sent = sent && tag != jr;
+    if (sent && d.router == 1) sent = (d.sel[(int64_t)u * d.S + slot] >> jr) & 1;
+    if (sent && authV && d.slotSrc[slot] == v) sent = false;
+    if (sent) {
+      b += (unsigned long long)d.acc[t].msgF;
+      ++n;
+    }
+  }
+}
+__global__ void k_acct_drop(Dev d, const int32_t* __restrict__ edges, int n, int p) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int64_t e = edges[k];
+  unsigned long long b, c;
+  inflight_payload(d, e, p, b, c);
+  d.rpcBin[e] += b;  // distinct edges in the list
+  d.rpcNin[e] += c;
+}
+__global__ void k_acct_inflight(Dev d, int p, unsigned long long* __restrict__ tb, unsigned long long* __restrict__ tn) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.E) return;
+  unsigned long long b, c;
+  inflight_payload(d, e, p, b, c);
+  tb[e] = b;
+  tn[e] = c;
+}
+
+// RPC accounting: (edge, bytes) pairs of the host-side RPCs of a hop
+__global__ void k_acct_add(Dev d, const int64_t* __restrict__ pairs, int n) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  // one edge may get several (a node announcing two topics): atomics
+  atomicAdd(&d.rpcB[pairs[2 * k]], (unsigned long long)pairs[2 * k + 1]);
+  atomicAdd(&d.rpcN[pairs[2 * k]], 1ull);
+}
+
 __global__ void k_gater_decay(Dev d) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < d.n1 - d.n0) {

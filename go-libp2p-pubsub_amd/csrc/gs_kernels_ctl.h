@@ -244,6 +244,7 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
   // score); a sender whose RPCs carry neither is handled in its own lane.
   bool gateIWant = false, gateIHave = false, prunesHb = false, gateSpam = false;
   uint64_t pruneOut = 0;
+  uint64_t joinRej = 0, hbPr = 0;  // RPC accounting: the join GRAFTs answered by a PRUNE, the heartbeat RPC's
   int nRep1 = 0;
   long long cPrunes = 0, cGray = 0;
   const bool heavy = ctl && !gl && (gJoin | gHb | pRep | pHb) != 0;
@@ -332,8 +333,11 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
         }
         prune_topics(d, ei, v, pHb_i, now, meshcnt, mE, dirty);
       }
+      const uint64_t jrej = pOut;
       pOut |= prunes;
       if (lane == i) {
+        joinRej = jrej;
+        hbPr = prunes;
         meshE = mE;
         ph = ph_i;
         pruneOut = pOut;
@@ -356,6 +360,8 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
   int64_t respRec = -1;
   long long cServed = 0;
   int nSrv = 0;  // reply RPCs carrying served messages to this sender
+  __shared__ uint32_t sSrvB[64], sSrvBS[64];  // RPC accounting: served message bytes per list
+  uint32_t srvB = 0, srvBS = 0;
   if (__ballot(gateIWant || gateSpam)) {
     __shared__ int sSpOff[64], sSpN[64], sItI[64], sCntS[64], sRow[64];
     // the peertx hash: static, or a larger dynamic table (IWANT-spam runs)
@@ -391,6 +397,8 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
     sSpOff[lane] = gateSpam ? (int)(spRec >> 24) : 0;
     sSpN[lane] = nS;
     sItI[lane] = itI;
+    sSrvB[lane] = 0u;
+    sSrvBS[lane] = 0u;
     sRow[lane] = (ADV && d.spamRow != nullptr && valid) ? d.spamRow[e] : -1;  // a spammer's counts: spamCnt
     sCnt[lane] = 0;
     sCntS[lane] = 0;
@@ -490,12 +498,18 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
               const int count = (ADV && sRow[i] >= 0) ? spam_count(d, sRow[i], slot) : ptx_count(hT, hbits, key);
               srv = count >= 1 && count <= d.GR;
             }
-            if (srv) d.pool[cur][sOut[i] + atomicAdd(&sCur[i], 1)] = slot;
+            if (srv) {
+              d.pool[cur][sOut[i] + atomicAdd(&sCur[i], 1)] = slot;
+              if (d.rpcB != nullptr)
+                atomicAdd(sp ? &sSrvBS[i] : &sSrvB[i], (uint32_t)d.acc[(int)__umulhi((unsigned)slot, d.stMagic)].msgF);
+            }
           }
         }
       }
     }
     __syncthreads();
+    srvB = sSrvB[lane];
+    srvBS = sSrvBS[lane];
     {  // peertx table back to its list form
       __syncthreads();
       int kept = 0;
@@ -862,6 +876,22 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
         if (iwantRec >= 0) d.cIwant[cur][e] = iwantRec;
         if (respRec >= 0) d.cIresp[cur][e] = respRec;
         if (nSrv && d.cNSrv[cur] != nullptr) d.cNSrv[cur][e] = (uint8_t)nSrv;
+        if (d.rpcB != nullptr) {
+          // HandleRPC's replies (gossipsub.go:602-607, rpcWithControl): a PRUNE
+          // per rejected join GRAFT; the served messages of each IWANT list
+          // with an empty control message (2 bytes); IWANT + PRUNEs for the
+          // heartbeat RPC
+          int64_t b = 0;
+          for (uint64_t m = joinRej; m; m &= m - 1) b += gs_pb_field(d.acc[__ffsll((long long)m) - 1].pruneEnt);
+          if (srvB) b += (int64_t)srvB + 2;
+          if (srvBS) b += (int64_t)srvBS + 2;
+          if (iwantAny || prunesHb) {
+            int64_t body = iwantAny ? gs_pb_field((int64_t)(iwantRec & 0xFFFFFF) * d.acctIdF) : 0;
+            for (uint64_t m = hbPr; m; m &= m - 1) body += d.acc[__ffsll((long long)m) - 1].pruneEnt;
+            b += gs_pb_field(body);
+          }
+          acct_send(d, e, b, nReplies);
+        }
       }
     }
   }
@@ -1250,6 +1280,22 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
   }
   tograft |= spamGraft;
   if (behaves(d, v, GS_BEHAVE_NO_FORWARD)) tograft = toprune = ihave = 0;  // a squatter sends nothing
+  if (d.rpcB != nullptr) {
+    // the heartbeat RPC (sendGraftPrune + piggybacked gossip / flush): IHAVE
+    // entries of min(ids, MaxIHaveLength) ids, GRAFT and PRUNE entries
+    if (lane < d.T) sterm[lane] = (double)min(nmT, d.MaxIHaveLength);
+    __syncthreads();
+    if (valid && (tograft | toprune | ihave)) {
+      int64_t body = 0;
+      for (uint64_t m = ihave; m; m &= m - 1) {
+        const int t = __ffsll((long long)m) - 1;
+        body += gs_pb_field(d.acc[t].ihaveHead + (int64_t)sterm[t] * d.acctIdF);
+      }
+      for (uint64_t m = tograft; m; m &= m - 1) body += d.acc[__ffsll((long long)m) - 1].graftEnt;
+      for (uint64_t m = toprune; m; m &= m - 1) body += d.acc[__ffsll((long long)m) - 1].pruneEnt;
+      acct_send(d, e, gs_pb_field(body), 1);
+    }
+  }
   if (valid) {
     d.mesh[e] = meshl;
     d.fanout[e] = fanl;
@@ -1458,6 +1504,11 @@ __global__ __launch_bounds__(64) void k_leave(Dev d, const int32_t* __restrict__
     if (!silent) {
       d.cPruneReply[cur][e] |= pruned;
       d.cPre[cur][e] = (uint8_t)(d.cPre[cur][e] + __popcll(pruned));  // one sendPrune RPC per topic
+      if (d.rpcB != nullptr) {
+        int64_t b = 0;
+        for (uint64_t m = pruned; m; m &= m - 1) b += gs_pb_field(d.acc[__ffsll((long long)m) - 1].pruneEnt);
+        acct_send(d, e, b, __popcll(pruned));
+      }
     }
   }
   if (lane == 0 && np && !silent) ctr_add(d, C_PRUNES, (unsigned long long)np);
@@ -1532,6 +1583,11 @@ __global__ __launch_bounds__(64) void k_join_pairs(Dev d, const int32_t* __restr
     if (grafted && !silent) {
       d.cGraftJoin[cur][e] |= grafted;
       d.cPre[cur][e] = (uint8_t)(d.cPre[cur][e] + __popcll(grafted));  // one sendGraft RPC per topic
+      if (d.rpcB != nullptr) {
+        int64_t b = 0;
+        for (uint64_t m = grafted; m; m &= m - 1) b += gs_pb_field(d.acc[__ffsll((long long)m) - 1].graftEnt);
+        acct_send(d, e, b, __popcll(grafted));
+      }
     }
   }
   if (lane == 0) {

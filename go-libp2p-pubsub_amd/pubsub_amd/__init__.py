@@ -15,4 +15,4 @@ from .params import (DefaultGossipSubParams, DefaultPeerGaterParams, GossipSubPa
 from .engine import (PRODUCT_LIB, Engine, GossipEngineError, NewFloodSub, NewGossipSub,  # noqa: F401
                      NewRandomSub, PROTOCOLS, WithDevice, WithEventTracer, encode_trace, WithDirectPeers, WithFloodPublish, WithGossipSubParams,
                      WithHop, WithMessageWindow, WithPartition, WithPeerScore, WithRecordDeliveries, WithSeed,
-                     WithBehaviour, WithPeerGater, WithValidation, load)
+                     WithBehaviour, WithPeerGater, WithRPCAccounting, WithValidation, load)

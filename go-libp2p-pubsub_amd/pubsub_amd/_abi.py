@@ -175,6 +175,8 @@ ABI_FUNCTIONS = [
       C.POINTER(i64), C.POINTER(u8)]),
     ("gs_read_behaviour_penalty", C.c_int, [P, C.POINTER(f64)]),
     ("gs_read_deliveries", C.c_int, [P, i64, C.POINTER(i32), C.POINTER(i32)]),
+    ("gs_set_rpc_accounting", C.c_int, [P, C.POINTER(i32), i32, C.POINTER(i32)]),
+    ("gs_read_rpc_bytes", C.c_int, [P, C.POINTER(i64), C.POINTER(i64)]),
     ("gs_set_trace", C.c_int, [P, C.POINTER(u8), i64]),
     ("gs_trace_read", C.c_int, [P, P, i64, C.POINTER(i64)]),
     ("gs_trace_encode", C.c_int, [P, i64, i32, i64, C.POINTER(C.c_char_p), C.c_char_p, P, i64, C.POINTER(i64)]),

@@ -88,6 +88,16 @@ def WithDevice(dev):
     return ("device", int(dev))
 
 
+def WithRPCAccounting(msg_size, id_len=40, topic_len=None):
+    """Per-edge RPC byte accounting (gs_set_rpc_accounting, SURVEY.md §8(f)
+    rank 3): every RPC a host sends is measured as RPC.Size() (gossipsub.go:
+    1121-1137) with messages of topic t msg_size[t] bytes (a scalar: all
+    topics), ids id_len bytes, topic names topic_len[t] bytes (default: the
+    decimal index's length, as the trace encoder names topics).  Read with
+    Engine.rpc_bytes()."""
+    return ("rpc_acct", (msg_size, int(id_len), topic_len))
+
+
 def WithEventTracer(nodes, capacity=1 << 22):
     """EventTracer (pubsub.go:418, trace.go) for the hosts in `nodes` (indices
     or a bool mask): their PublishMessage / DeliverMessage / DuplicateMessage /
@@ -179,6 +189,14 @@ class Engine:
             nodes = np.asarray(nodes)
             mask[np.nonzero(nodes)[0] if nodes.dtype == bool else nodes] = 1
             _check(self.lib, self.lib.gs_set_trace(h, _ptr(mask, C.c_uint8), cap))
+        acct = opts.get("rpc_acct")
+        if acct is not None:
+            ms, idl, tl = acct
+            ms = np.ascontiguousarray(np.broadcast_to(np.asarray(ms, dtype=np.int32), (num_topics,)))
+            tl = (np.array([len(str(t)) for t in range(num_topics)], dtype=np.int32) if tl is None
+                  else np.ascontiguousarray(np.broadcast_to(np.asarray(tl, dtype=np.int32), (num_topics,))))
+            _check(self.lib, self.lib.gs_set_rpc_accounting(h, _ptr(ms, C.c_int32), idl, _ptr(tl, C.c_int32)))
+        self.rpc_acct = acct is not None
         self.router = router
         self.hop_ns = cfg.hop_ns
         self.rank, self.world, self.transport = opts.get("partition", (0, 1, None))
@@ -314,6 +332,13 @@ class Engine:
         cnt = np.zeros(n, dtype=np.int64)
         _check(self.lib, self.lib.gs_read_kernel_stats(self.h, _ptr(ms, C.c_double), _ptr(cnt, C.c_int64)))
         return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(_abi.KERNEL_NAMES)}
+
+    def rpc_bytes(self):
+        """(bytes[E], rpcs[E]) sent over every directed edge since the start."""
+        b = np.empty(self.E, dtype=np.int64)
+        n = np.empty(self.E, dtype=np.int64)
+        _check(self.lib, self.lib.gs_read_rpc_bytes(self.h, _ptr(b, C.c_int64), _ptr(n, C.c_int64)))
+        return b, n
 
     def trace_events(self, chunk=1 << 16):
         """Every recorded event since the last call, in canonical order

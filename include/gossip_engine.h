@@ -339,6 +339,23 @@ int gs_partition_range(const gs_engine* eng, int32_t* node_begin, int32_t* node_
 /* Host time spent in the transport and bytes received from other ranks. */
 int gs_read_exchange_stats(gs_engine* eng, double* host_ms, int64_t* bytes_in);
 
+/* ---- RPC byte accounting ---------------------- */
+/* The reference's sendRPC measures every outgoing RPC (out.Size(),
+ * gossipsub.go:1121-1137); pubsub.go sends the hello packet (pubsub.go:495,
+ * 534) and subscription announcements (pubsub.go:775-792).  With accounting
+ * on, the engine sums the protobuf size (include/gs_rpcsize.h) and the count of
+ * every RPC each host sends, per directed edge: forwarded and published
+ * messages, GRAFT / PRUNE / IHAVE / IWANT control, IWANT replies, hellos (for
+ * every connection at the start and on every reconnect) and announcements.
+ * Sizes: a message of topic t is msg_size[t] bytes (its Message.Size()),
+ * every message id id_len bytes, topic t's name topic_len[t] bytes.  Before
+ * the first step; not on a partitioned engine. */
+int gs_set_rpc_accounting(gs_engine* eng, const int32_t* msg_size /*[T]*/, int32_t id_len,
+                          const int32_t* topic_len /*[T]*/);
+/* bytes[e], rpcs[e]: totals sent by node u to col[e] (rowptr[u] <= e <
+ * rowptr[u+1]) since the start (either array may be NULL). */
+int gs_read_rpc_bytes(gs_engine* eng, int64_t* bytes /*[E]*/, int64_t* rpcs /*[E]*/);
+
 /* ---- readbacks (host arrays sized by the caller) ----------------------- */
 /* A partitioned engine reports its own nodes / edges only: counters count its
  * nodes' events, per-edge arrays are valid on its edges [rowptr[node_begin],

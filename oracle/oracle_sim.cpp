@@ -25,6 +25,7 @@
 
 #include "oracle_core.hpp"
 #include "../include/gs_trace.h"
+#include "../include/gs_rpcsize.h"
 
 namespace oracle {
 
@@ -161,6 +162,20 @@ struct Sim {
   // EventTracer (trace.go:61-499) of the hosts with traced[u] != 0
   std::vector<uint8_t> traced;
   std::vector<gs_trace_event> events;  // drained from the nodes' buffers by gs_trace_read
+  // RPC byte accounting (gs_set_rpc_accounting): RPC.Size() and count of every
+  // RPC a host sends, per directed edge (the sender's row)
+  bool acct = false;
+  std::vector<int32_t> acctMsg, acctTl;
+  int32_t acctId = 0;
+  std::vector<int64_t> rpcBytes, rpcCount;
+  void account(int u, int p, int64_t bytes) {
+    if (!acct) return;
+    const int e = edgeIndex(u, p);
+    rpcBytes[e] += bytes;  // edges of u: only u's own (parallel) node loop writes them
+    rpcCount[e] += 1;
+  }
+  int64_t rpcSize(const RPC& r) const;    // pb/rpc.pb.go Size() of r
+  int64_t helloSize(uint64_t subs) const;
   size_t traceRead = 0;
   // Events go to the tracing host's own buffer, so nodes run in parallel
   // (OpenMP over nodes in every per-node phase; the canonical event order
@@ -189,6 +204,7 @@ struct Sim {
   void start();
   void step();
   void applyEvents(std::vector<std::map<int, std::vector<RPC>>>& inbox);
+  void announce(int a, int topic);
 };
 
 void Sim::emit(int type, int node, int peer, int topic, int64_t msg, int phase, int reason) {
@@ -212,6 +228,29 @@ gs_counters Sim::total() const {
   return c;
 }
 
+// RPC.Size() (include/gs_rpcsize.h): publish entries, then the control message
+// when the RPC carries one (rpcWithControl always does).
+int64_t Sim::rpcSize(const RPC& r) const {
+  int64_t s = 0;
+  for (int64_t mid : r.publish) s += gs_pb_field(acctMsg[msgs[mid].topic]);
+  if (r.hasCtl) {
+    int64_t c = 0;
+    for (const IHaveEntry& ih : r.ctl.ihave) c += gs_pb_field(gs_pb_ihave(acctTl[ih.topic], (int64_t)ih.mids.size(), acctId));
+    if (!r.ctl.iwant.empty()) c += gs_pb_field(gs_pb_iwant((int64_t)r.ctl.iwant.size(), acctId));
+    for (int t : r.ctl.graft) c += gs_pb_field(gs_pb_graft(acctTl[t]));
+    for (const PruneEntry& pe : r.ctl.prune) c += gs_pb_field(gs_pb_prune(acctTl[pe.topic], pe.backoff));
+    s += gs_pb_field(c);
+  }
+  return s;
+}
+// getHelloPacket (pubsub.go:853-866 area): one SubOpts per subscribed topic
+int64_t Sim::helloSize(uint64_t subs) const {
+  int64_t s = 0;
+  for (int t = 0; t < T; ++t)
+    if ((subs >> t) & 1) s += gs_pb_field(gs_pb_subopts(acctTl[t]));
+  return s;
+}
+
 double Node::Score(int p) { return sim->scoring ? score.score(p) : 0.0; }
 
 // sendRPC / doSendRPC — gossipsub.go:1092-1156 (queues never drop in the
@@ -225,6 +264,7 @@ void Node::sendRPC(int p, RPC rpc) {
     rpc.ctl.ihave = g->second;
     gossip.erase(g);
   }
+  sim->account(id, p, sim->acct ? sim->rpcSize(rpc) : 0);
   ctr.grafts_sent += (int64_t)rpc.ctl.graft.size();
   ctr.prunes_sent += (int64_t)rpc.ctl.prune.size();
   ctr.ihave_sent += (int64_t)rpc.ctl.ihave.size();
@@ -926,6 +966,13 @@ void Node::joinTopic(int topic) {
 // the scheduled events: every disconnect, every connect, every leave, every
 // join (canonical order); disconnects and connects in schedule order, leaves
 // and joins by (node, topic).  A lost connection drops what was in flight.
+// announce (pubsub.go:775-792): one SubOpts RPC to every connected peer
+void Sim::announce(int a, int topic) {
+  if (!acct) return;
+  for (int p : nodes[a].nbrs)
+    if (!nodes[a].dead.count(p)) account(a, p, gs_pb_field(gs_pb_subopts(acctTl[topic])));
+}
+
 void Sim::applyEvents(std::vector<std::map<int, std::vector<RPC>>>& inbox) {
   for (const Ann& an : pendingAnn)
     for (int p : nodes[an.node].nbrs) {
@@ -959,14 +1006,18 @@ void Sim::applyEvents(std::vector<std::map<int, std::vector<RPC>>>& inbox) {
         if (!nodes[ev.a].dead.count(ev.b)) break;
         nodes[ev.a].addPeer(ev.b);
         nodes[ev.b].addPeer(ev.a);
+        account(ev.a, ev.b, acct ? helloSize(nodes[ev.a].mySubs) : 0);  // hello packets (pubsub.go:534)
+        account(ev.b, ev.a, acct ? helloSize(nodes[ev.b].mySubs) : 0);
         break;
       case GS_EV_LEAVE:
         if (!((nodes[ev.a].mySubs >> ev.b) & 1)) break;
+        announce(ev.a, ev.b);
         nodes[ev.a].leaveTopic(ev.b);
         pendingAnn.push_back({ev.a, ev.b, false});
         break;
       case GS_EV_JOIN:
         if ((nodes[ev.a].mySubs >> ev.b) & 1) break;
+        announce(ev.a, ev.b);
         nodes[ev.a].joinTopic(ev.b);
         pendingAnn.push_back({ev.a, ev.b, true});
         break;
@@ -1009,6 +1060,15 @@ void Sim::start() {
       for (int t = 0; t < T; ++t)
         if (!subs.empty() && ((subs[v] >> t) & 1)) nd.topics[t].insert(v);
     }
+  }
+  if (acct) {  // the hello packet of every connection (pubsub.go:495)
+    rpcBytes.assign(E, 0);
+    rpcCount.assign(E, 0);
+    for (int u = 0; u < N; ++u)
+      for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) {
+        rpcBytes[e] += helloSize(subs.empty() ? 0 : subs[u]);
+        rpcCount[e] += 1;
+      }
   }
   started = true;
 }
@@ -1497,6 +1557,29 @@ int gs_partition_range(const gs_engine* g, int32_t* node_begin, int32_t* node_en
   *node_end = g->sim.N;
   return GS_OK;
 }
+int gs_set_rpc_accounting(gs_engine* g, const int32_t* msg_size, int32_t id_len, const int32_t* topic_len) {
+  Sim& sim = g->sim;
+  if (sim.started) { set_error("gs_set_rpc_accounting: before the first step"); return GS_ESTATE; }
+  if (!msg_size || !topic_len || id_len < 0) { set_error("gs_set_rpc_accounting: bad arguments"); return GS_EINVAL; }
+  for (int t = 0; t < sim.T; ++t)
+    if (msg_size[t] < 0 || topic_len[t] < 0) { set_error("gs_set_rpc_accounting: negative size"); return GS_EINVAL; }
+  sim.acct = true;
+  sim.acctMsg.assign(msg_size, msg_size + sim.T);
+  sim.acctTl.assign(topic_len, topic_len + sim.T);
+  sim.acctId = id_len;
+  return GS_OK;
+}
+
+int gs_read_rpc_bytes(gs_engine* g, int64_t* bytes, int64_t* rpcs) {
+  Sim& sim = g->sim;
+  if (!sim.acct) { set_error("gs_read_rpc_bytes: accounting is off"); return GS_ESTATE; }
+  for (int64_t e = 0; e < sim.E; ++e) {
+    if (bytes) bytes[e] = sim.started ? sim.rpcBytes[e] : 0;
+    if (rpcs) rpcs[e] = sim.started ? sim.rpcCount[e] : 0;
+  }
+  return GS_OK;
+}
+
 int gs_set_trace(gs_engine* g, const uint8_t* node_mask, int64_t capacity) {
   (void)capacity;  // the oracle keeps every event
   if (g->sim.started) { set_error("tracing must be set before the first step"); return GS_ESTATE; }

@@ -159,6 +159,8 @@ def snapshot(e, msg_ids):
                scores=e.scores(), bp=e.behaviour_penalty())
     out.update({"ts_" + k: v for k, v in e.topic_stats().items()})
     out["deliv"] = [e.deliveries(i) for i in msg_ids]
+    if getattr(e, "rpc_acct", False):
+        out["rpc_bytes"], out["rpc_count"] = e.rpc_bytes()
     return out
 
 
@@ -504,3 +506,30 @@ CHURN = {
     "churn_scored": lambda lib, x=(): churn_scored(lib, extra=x),
 }
 SCENARIOS.update(CHURN)
+
+
+# ---------------------------------------------------------------- RPC bytes
+# Per-edge RPC byte accounting (gs_set_rpc_accounting)
+# on top of scenarios that send every RPC kind: forwarded / published messages
+# (floodsub, randomsub, gossipsub, fanout), GRAFT / PRUNE / IHAVE / IWANT,
+# served replies, IWANT spam, squatters, hellos and announcements under churn.
+# Message sizes straddle the one-byte varint boundary per topic.
+from pubsub_amd import WithRPCAccounting  # noqa: E402
+
+
+def _acct(T):
+    return WithRPCAccounting(np.array([120 + 5 * t for t in range(T)], np.int32), id_len=30)
+
+
+ACCT = {
+    "acct_floodsub": lambda lib, x=(): floodsub_dense(lib, extra=(_acct(1),) + tuple(x)),
+    "acct_randomsub": lambda lib, x=(): randomsub(lib, 100, extra=(_acct(1),) + tuple(x)),
+    "acct_multitopic": lambda lib, x=(): gossipsub_scored(lib, n=200, topics=3, sub_frac=0.7, seed=7, msgs=240,
+                                                          extra=(_acct(3),) + tuple(x)),
+    "acct_graylist_direct": lambda lib, x=(): gossipsub_scored(lib, n=300, k=20, seed=23, app_neg_frac=0.15,
+                                                               app_neg=-400.0, direct_frac=0.03,
+                                                               extra=(_acct(1),) + tuple(x)),
+    "acct_adversarial": lambda lib, x=(): adversarial_mix(lib, extra=(_acct(1),) + tuple(x)),
+    "acct_churn": lambda lib, x=(): churn_scored(lib, extra=(_acct(2),) + tuple(x)),
+}
+SCENARIOS.update(ACCT)
