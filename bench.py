@@ -215,6 +215,8 @@ def main():
     ap.add_argument("--transport", default="rccl", choices=["rccl", "torch"],
                     help="partitioned ranks' exchange: the product library's native RCCL transport "
                          "(include/gs_transport.h) or torch.distributed collectives")
+    ap.add_argument("--rpc-accounting", action="store_true",
+                    help="also sum RPC bytes per edge (gs_set_rpc_accounting; 1 KB messages, 40-byte ids)")
     ap.add_argument("--lib", default=None, help="timing experiments only: another build of the product library "
                     "(results are labelled with it)")
     args = ap.parse_args()
@@ -265,6 +267,9 @@ def main():
     rounds = args.warmup + args.steps + 1
     t_setup = time.perf_counter()
     # partitioned ranks simulate ONE graph and schedule (same seed); replicas differ
+    if args.rpc_accounting:
+        from pubsub_amd import WithRPCAccounting
+        extra = tuple(extra) + (WithRPCAccounting(1000, id_len=40),)
     eng, g = build_engine(wl, rounds, 3 if partitioned else 3 + rank, local, extra=extra, lib=args.lib)
     # hop 0 (Join) + warm-up rounds: meshes form, the message window fills
     eng.step(1 + args.warmup * HOPS_PER_ROUND)
@@ -384,6 +389,10 @@ def main():
     }
     if args.lib:
         out["experiment_lib"] = os.path.basename(args.lib)
+    if args.rpc_accounting:
+        rb, rn = eng.rpc_bytes()
+        out["rpc_accounting"] = {"bytes_total": int(rb.sum()), "rpcs_total": int(rn.sum()),
+                                 "bytes_per_peer_per_round": float(rb.sum()) / wl["n"] / (rounds - 1)}
     if partitioned:
         out["exchange"] = {"transport": type(extra[0][1][2]).__name__,
                            "rank0_host_ms_per_step": round((x1[0] - x0[0]) / args.steps, 3),

@@ -103,8 +103,6 @@ struct Dev {
   // RPC byte accounting (gs_set_rpc_accounting); rpcB == nullptr: off
   unsigned long long* rpcB;    // [E] bytes of the RPCs sent over the sender's edge e
   unsigned long long* rpcN;    // [E] RPCs sent over edge e
-  unsigned long long* rpcBin;  // [E] payload RPCs received over in-edge e (the receiver's row)
-  unsigned long long* rpcNin;
   const AcctT* acc;            // [T]
   int32_t acctIdF;             // one message id inside an IHAVE / IWANT
   // EventTracer of the hosts with traced[u] != 0 (gs_set_trace); nullptr = off

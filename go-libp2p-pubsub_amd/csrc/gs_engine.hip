@@ -648,7 +648,7 @@ int gs_engine::start() {
     const int rc = enableChurn();
     if (rc) return rc;
   }
-  x.rpcB = x.rpcN = x.rpcBin = x.rpcNin = nullptr;
+  x.rpcB = x.rpcN = nullptr;
   x.acc = nullptr;
   if (acctOn) {
     if (world > 1) {
@@ -656,9 +656,8 @@ int gs_engine::start() {
       return GS_EUNSUPPORTED;
     }
     x.rpcB = dalloc<unsigned long long>(E); x.rpcN = dalloc<unsigned long long>(E);
-    x.rpcBin = dalloc<unsigned long long>(E); x.rpcNin = dalloc<unsigned long long>(E);
     AcctT* ac = dalloc<AcctT>(T);
-    chk(x.rpcB); chk(x.rpcN); chk(x.rpcBin); chk(x.rpcNin); chk(ac);
+    chk(x.rpcB); chk(x.rpcN); chk(ac);
     if (!ok) { gs_set_error("device allocation failed (RPC accounting)"); return GS_ENOMEM; }
     const uint64_t bo = (uint64_t)(gp.PruneBackoff / kSec);
     std::vector<AcctT> ah(T);
@@ -857,8 +856,6 @@ int gs_engine::applyEvents(int64_t h) {
   if (!down.empty()) {
     int rc = uploadList(down);
     if (rc) return rc;
-    // the payload RPCs in flight on a closed connection were sent (and lost)
-    if (acctOn) k_acct_drop<<<nblk((int64_t)down.size(), 256), 256, 0, stream>>>(d, dEv, (int)down.size(), prv);
     k_edge_down<<<(unsigned)down.size(), 64, 0, stream>>>(d, dEv, h, now, prv);
     recChanged = true;
   }
@@ -993,8 +990,7 @@ int gs_engine::stepOne() {
     // instantiation: the honest path keeps its LDS budget and code
     const bool adv = topicVal != 0 || gaterOn || behaveAll != 0;
     const bool hasUnc = d.needAge || (adv && d.pmaskRow != nullptr);
-    size_t lds = (narrow ? 2 : 4) * nCnt + 16 * (size_t)nR + (size_t)nYp + (hasUnc ? 4 * nCnt : 0) +
-                 (acctOn ? 512 : 0);
+    size_t lds = (narrow ? 2 : 4) * nCnt + 16 * (size_t)nR + (size_t)nYp + (hasUnc ? 4 * nCnt : 0);
     if (adv) lds += 4 * nCnt + 4 * 64 * 4 + 8 * 64 + 8 * (size_t)nR;
     TIMED(this, GS_K_PHASE_A, launch_wpl(W, [&](auto w) {
             if (!nOwn) return;
@@ -1098,6 +1094,8 @@ int gs_engine::stepOne() {
     head = newhead;
     heartbeats++;
   }
+  // RPC accounting: this hop's forwarded and published messages, one RPC each
+  if (acctOn && nOwn) k_acct_payload<<<nOwn, 64, 0, stream>>>(d, cur);
   HIPCHECK(hipGetLastError());
   if (world > 1) {
     const int rc = exchange(cur, heartbeatDue(now));
@@ -1740,27 +1738,13 @@ int gs_read_rpc_bytes(gs_engine* g, int64_t* bytes, int64_t* rpcs) {
     }
     return GS_OK;
   }
-  // sender-side sums plus the payload RPCs counted at the receiver (in-edge
-  // rev[e] of col[e] carries what u sent over e)
-  std::vector<unsigned long long> b(E), n(E), bi(E), ni(E), fb(E, 0ull), fn(E, 0ull);
-  if (g->hop > 0) {  // the last hop's payload RPCs, sent but not received yet
-    unsigned long long* t = nullptr;
-    HIPCHECK(hipMalloc(&t, (size_t)E * 16));
-    k_acct_inflight<<<nblk(E, 256), 256, 0, g->stream>>>(g->d, (int)((g->hop - 1) & 1), t, t + E);
-    HIPCHECK(hipMemcpyAsync(fb.data(), t, (size_t)E * 8, hipMemcpyDeviceToHost, g->stream));
-    HIPCHECK(hipMemcpyAsync(fn.data(), t + E, (size_t)E * 8, hipMemcpyDeviceToHost, g->stream));
-    HIPCHECK(hipStreamSynchronize(g->stream));
-    HIPCHECK(hipFree(t));
-  }
+  std::vector<unsigned long long> b(E), n(E);
   HIPCHECK(hipStreamSynchronize(g->stream));
   HIPCHECK(hipMemcpy(b.data(), g->d.rpcB, (size_t)E * 8, hipMemcpyDeviceToHost));
   HIPCHECK(hipMemcpy(n.data(), g->d.rpcN, (size_t)E * 8, hipMemcpyDeviceToHost));
-  HIPCHECK(hipMemcpy(bi.data(), g->d.rpcBin, (size_t)E * 8, hipMemcpyDeviceToHost));
-  HIPCHECK(hipMemcpy(ni.data(), g->d.rpcNin, (size_t)E * 8, hipMemcpyDeviceToHost));
   for (int64_t e = 0; e < E; ++e) {
-    const int64_t r = g->rev[e];
-    if (bytes) bytes[e] = (int64_t)(b[e] + bi[r] + fb[r]);
-    if (rpcs) rpcs[e] = (int64_t)(n[e] + ni[r] + fn[r]);
+    if (bytes) bytes[e] = (int64_t)b[e];
+    if (rpcs) rpcs[e] = (int64_t)n[e];
   }
   return GS_OK;
 }

@@ -551,10 +551,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
   extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
   const int nCnt = (d.T * d.maxDeg + 7) & ~7;
   const int nCntW = NARROW ? nCnt / 2 : nCnt;             // LDS words of the counter table
-  // RPC accounting: payload bytes / RPCs per sender, ahead of the other tables
-  uint32_t* const sAccB = smem32;
-  uint32_t* const sAccN = smem32 + 64;
-  uint32_t* scnt = smem32 + (d.rpcB != nullptr ? 128 : 0);  // [MD][T] copies | fresh << 16 (NARROW: u16 copies | fresh << 8)
+  uint32_t* scnt = smem32;  // [MD][T] copies | fresh << 16 (NARROW: u16 copies | fresh << 8)
   uint64_t* sD = (uint64_t*)(scnt + nCntW);               // [nR] delivered young slots (non-graylisted)
   uint64_t* sYm = sD + nR;                                // [nR] young-slot mask of each amR word
   uint8_t* sFirst = (uint8_t*)(sYm + nR);                 // [nY] lowest deliverer per young slot
@@ -623,10 +620,6 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
   const bool authV = d.nAuth[v] > 0;  // v authored a live message: author exclusion possible
   for (int k = lane; k < nCntW / 4; k += 64) ((uint4*)scnt)[k] = make_uint4(0, 0, 0, 0);
   const bool acct = d.rpcB != nullptr;
-  if (acct) {
-    sAccB[lane] = 0u;
-    sAccN[lane] = 0u;
-  }
   if (hasUnc)
     for (int k = lane; k < nCnt / 4; k += 64) ((uint4*)sUnc)[k] = make_uint4(0, 0, 0, 0);
   for (int k = lane; k < nR; k += 64) {
@@ -836,7 +829,6 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
         uint32_t en[4];
         bool sn[4];
         {
-          uint32_t accB = 0, accN = 0;
           const int i = si[rr] < 0 ? 0 : si[rr];
           const int snd = sSnd[i];
           const int uu = snd & 0xFFFFFF;
@@ -857,17 +849,9 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
             if (count) {
               nSent += sent;
               if (sent && isGray) ++nGray;  // one RPC per relayed message, all dropped
-              if (acct && sent) {  // rpcWithMessages: RPC = one publish entry
-                accB += (uint32_t)d.acc[t].msgF;
-                ++accN;
-              }
             }
             sn[c] = sent && !isGray;
             en[c] = (uint32_t)slot | ((uint32_t)i << 16);
-          }
-          if (accN) {
-            atomicAdd(&sAccB[i], accB);
-            atomicAdd(&sAccN[i], accN);
           }
         }
         // c-major positions (delivery order does not matter: every update is
@@ -902,7 +886,6 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
     __syncthreads();
   };
   walk([&](int i, int slot) { deliver(i, slot, true); }, true);
-  uint32_t myAccB = 0, myAccN = 0;  // RPC accounting of the copies below (lane = sender)
   if (__ballot(((relayAll | pubAll) & ~sv) != 0)) {
     // copies of topics v is not subscribed to: transmitted, then ignored
     // (churn runs only: a mesh or announced peer that has just left)
@@ -920,10 +903,6 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
         if (sent) {
           ++nSent;
           if (gray) ++nGray;
-          if (acct) {
-            myAccB += (uint32_t)d.acc[t].msgF;
-            ++myAccN;
-          }
         }
       }
     }
@@ -1381,13 +1360,6 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
     }
   }
   GS_STAMP(4);
-  if (acct && valid) {  // the payload RPCs received from each sender this hop
-    const uint32_t nn = sAccN[lane] + myAccN;
-    if (nn) {
-      d.rpcBin[base + lane] += (unsigned long long)(sAccB[lane] + myAccB);
-      d.rpcNin[base + lane] += (unsigned long long)nn;
-    }
-  }
   if (lane == 0) d.fln[cur][v] = behaves(d, v, GS_BEHAVE_NO_FORWARD) ? 0 : (running < FC ? running : FC);
   const long long deliv = (long long)wave_sum_ll(nDeliv);
   const unsigned long long copies = wave_sum_ll(nCopies), s2 = wave_sum_ll(nSent), s3 = wave_sum_ll(nGray);
@@ -1551,52 +1523,43 @@ __device__ __forceinline__ double gdecay(double x, double f, double z) {
   x *= f;
   return x < z ? 0.0 : x;
 }
-// RPC accounting: the payload RPCs in flight to v over its in-edge e, sent by
-// u = col[e] in the hop of parity p (phase A counts payload at the receiver:
-// this adds what a disconnect drops and what the last hop has sent but
-// nobody has received yet).  The same filter as phase A's list walk.
-__device__ __forceinline__ void inflight_payload(const Dev& d, int64_t e, int p, unsigned long long& b,
-                                                 unsigned long long& n) {
-  const int v = d.esrc[e];
-  const int u = d.col[e];
-  const int64_t r = d.rev[e];
-  const int jr = (int)(r - d.rowptr[u]);
-  const uint64_t ru = d.fwdRelay[p][r], pu = d.fwdPub[p][r];
-  b = n = 0;
-  if (!(ru | pu)) return;
+// RPC accounting: the payload RPCs u sent in the hop of parity p (its list and
+// forwarding sets; forwarded and published messages, one RPC each,
+// rpcWithMessages), counted at the end of the hop — the filter of phase A's
+// list walk seen from the sender.  A wave per sender, lane = out-edge, the
+// list's entries broadcast one at a time.
+__global__ __launch_bounds__(64) void k_acct_payload(Dev d, int p) {
+  const int u = d.n0 + blockIdx.x;
+  const int lane = lane_id();
+  const int64_t base = d.rowptr[u];
+  const int deg = (int)(d.rowptr[u + 1] - base);
+  const bool valid = lane < deg;
+  const int64_t e = base + lane;
+  const uint64_t ru = valid ? d.fwdRelay[p][e] : 0, pu = valid ? d.fwdPub[p][e] : 0;
+  if (!__ballot((ru | pu) != 0)) return;
+  const int w = valid ? d.col[e] : 0;
+  const bool authW = valid && d.nAuth[w] > 0;  // the receiver authored a live message
   const int Ln = d.fln[p][u];
   const uint32_t* L = d.fl[p] + (int64_t)u * d.FC;
-  const bool authV = d.nAuth[v] > 0;
-  for (int k = 0; k < Ln; ++k) {
-    const uint32_t ent = L[k];
-    const int slot = (int)(ent & 0xFFFF), tag = (int)(ent >> 16);
-    const int t = (int)__umulhi((unsigned)slot, d.stMagic);
-    bool sent = tag == 255 ? ((pu >> t) & 1) : ((ru >> t) & 1);
-    sent = sent && tag != jr;
-    if (sent && d.router == 1) sent = (d.sel[(int64_t)u * d.S + slot] >> jr) & 1;
-    if (sent && authV && d.slotSrc[slot] == v) sent = false;
-    if (sent) {
-      b += (unsigned long long)d.acc[t].msgF;
-      ++n;
+  unsigned long long b = 0, n = 0;
+  for (int k0 = 0; k0 < Ln; k0 += 64) {
+    const uint32_t mine = k0 + lane < Ln ? L[k0 + lane] : 0u;
+    const int cnt = min(64, Ln - k0);
+    for (int k = 0; k < cnt; ++k) {
+      const uint32_t ent = (uint32_t)lane_get((int)mine, k);
+      const int slot = (int)(ent & 0xFFFF), tag = (int)(ent >> 16);
+      const int t = (int)__umulhi((unsigned)slot, d.stMagic);
+      bool sent = tag == 255 ? ((pu >> t) & 1) : ((ru >> t) & 1);
+      sent = sent && tag != lane;  // not back to the deliverer (gossipsub.go:1003)
+      if (sent && d.router == 1) sent = (d.sel[(int64_t)u * d.S + slot] >> lane) & 1;
+      if (sent && authW && d.slotSrc[slot] == w) sent = false;  // never to the author
+      if (sent) {
+        b += (unsigned long long)d.acc[t].msgF;
+        ++n;
+      }
     }
   }
-}
-__global__ void k_acct_drop(Dev d, const int32_t* __restrict__ edges, int n, int p) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  const int64_t e = edges[k];
-  unsigned long long b, c;
-  inflight_payload(d, e, p, b, c);
-  d.rpcBin[e] += b;  // distinct edges in the list
-  d.rpcNin[e] += c;
-}
-__global__ void k_acct_inflight(Dev d, int p, unsigned long long* __restrict__ tb, unsigned long long* __restrict__ tn) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= d.E) return;
-  unsigned long long b, c;
-  inflight_payload(d, e, p, b, c);
-  tb[e] = b;
-  tn[e] = c;
+  if (valid && n) acct_send(d, e, (int64_t)b, (int)n);
 }
 
 // RPC accounting: (edge, bytes) pairs of the host-side RPCs of a hop
