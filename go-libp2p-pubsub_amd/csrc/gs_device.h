@@ -199,6 +199,11 @@ struct Dev {
   uint64_t* fanout;
   uint64_t* fwdRelay[2];
   uint64_t* fwdPub[2];
+  // the same sets in the receiver's order: fwdIn[p][rev[e]] = {relay, pub} of
+  // edge e, so a receiver reads its in-edges' sets as one coalesced row
+  // (maintained by k_fwd on change, k_edge_down and the exchange)
+  ulonglong2* fwdIn[2];
+  uint8_t* jrIn;  // [E] position of the receiver in the sender's row: rev[e] - rowptr[col[e]]
   double* score0;  // hop-start score memo (S0)
   double* score1;  // after the message phase (S1) / heartbeat memo
   uint8_t* sdirty; // [E] a score-lowering change (graft/prune/penalty/refresh) since score0
@@ -223,7 +228,8 @@ struct Dev {
   uint64_t* cPruneHb[2];
   uint64_t* cIhave[2];
   int64_t* cIwant[2];  // IWANT request list: arena record (off << 24 | count), -1 = none
-  int64_t* cIresp[2];  // messages served for an IWANT: arena record, -1 = none
+  int64_t* cIresp[2];  // messages served for an IWANT: arena record, -1 = none;
+                       // indexed by the receiver's in-edge (rev of the sender's edge)
   int32_t* pool[2];    // slot-id arena for IWANT lists / responses
   unsigned long long* poolCnt;  // [2] bump pointers
   int64_t poolCap;     // ids per arena

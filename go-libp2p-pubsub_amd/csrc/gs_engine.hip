@@ -404,6 +404,7 @@ int gs_engine::start() {
   int32_t* dRev = dalloc<int32_t>(E); chk(dRev);
   uint8_t* dOut = dalloc<uint8_t>(E); chk(dOut);
   uint8_t* dDir = dalloc<uint8_t>(E); chk(dDir);
+  uint8_t* dJrIn = dalloc<uint8_t>(E); chk(dJrIn);
   uint64_t* dSub = dalloc<uint64_t>(N); chk(dSub);
   dSubA = dalloc<uint64_t>(N); chk(dSubA);
   double* dApp = dalloc<double>(N); chk(dApp);
@@ -414,6 +415,11 @@ int gs_engine::start() {
   HIPCHECK(hipMemcpyAsync(dCol, col.data(), E * 4, hipMemcpyHostToDevice, stream));
   HIPCHECK(hipMemcpyAsync(dEsrc, esrc.data(), E * 4, hipMemcpyHostToDevice, stream));
   HIPCHECK(hipMemcpyAsync(dRev, rev.data(), E * 4, hipMemcpyHostToDevice, stream));
+  {
+    std::vector<uint8_t> jr(E);
+    for (int64_t e = 0; e < E; ++e) jr[e] = (uint8_t)(rev[e] - rowptr[col[e]]);
+    HIPCHECK(hipMemcpy(dJrIn, jr.data(), E, hipMemcpyHostToDevice));
+  }
   HIPCHECK(hipMemcpyAsync(dOut, outbound.data(), E, hipMemcpyHostToDevice, stream));
   HIPCHECK(hipMemcpyAsync(dDir, direct.data(), E, hipMemcpyHostToDevice, stream));
   HIPCHECK(hipMemcpyAsync(dSub, sub.data(), N * 8, hipMemcpyHostToDevice, stream));
@@ -426,7 +432,7 @@ int gs_engine::start() {
   std::vector<TopicP> htp(T);
   for (int t = 0; t < T; ++t) htp[t] = to_dev(tps[t], scoring && tscored[t]);
   HIPCHECK(hipMemcpyAsync(dTp, htp.data(), T * sizeof(TopicP), hipMemcpyHostToDevice, stream));
-  x.rowptr = dRowptr; x.col = dCol; x.esrc = dEsrc; x.rev = dRev; x.outbound = dOut; x.direct = dDir;
+  x.rowptr = dRowptr; x.col = dCol; x.esrc = dEsrc; x.rev = dRev; x.outbound = dOut; x.direct = dDir; x.jrIn = dJrIn;
   x.sub = dSub; x.subA = dSubA; x.app = dApp; x.p6 = dP6; x.tp = dTp;
   x.alive = nullptr; x.rstate = nullptr; x.rexpire = nullptr; x.ipv4 = nullptr; x.ipWL = nullptr;
   x.RetainScore = sp.RetainScore; x.IPThr = sp.IPColocationFactorThreshold;
@@ -483,7 +489,8 @@ int gs_engine::start() {
   chk(x.mesh); chk(x.fanout);
   for (int k = 0; k < 2; ++k) {
     x.fwdRelay[k] = dalloc<uint64_t>(E); x.fwdPub[k] = dalloc<uint64_t>(E);
-    chk(x.fwdRelay[k]); chk(x.fwdPub[k]);
+    x.fwdIn[k] = dalloc<ulonglong2>(E);
+    chk(x.fwdRelay[k]); chk(x.fwdPub[k]); chk(x.fwdIn[k]);
     x.cPre[k] = dalloc<uint8_t>(E); x.cHb[k] = dalloc<uint8_t>(E);
     x.cGraftJoin[k] = dalloc<uint64_t>(E); x.cGraftHb[k] = dalloc<uint64_t>(E);
     x.cPruneReply[k] = dalloc<uint64_t>(E); x.cPruneHb[k] = dalloc<uint64_t>(E);

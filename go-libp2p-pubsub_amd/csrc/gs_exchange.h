@@ -75,7 +75,7 @@ __global__ void k_x_pack(Dev d, int cur, const int64_t* __restrict__ off, unsign
     x.phb = d.cPruneHb[cur][e];
     x.ihave = d.cIhave[cur][e];
     x.iwant = d.cIwant[cur][e];
-    x.iresp = d.cIresp[cur][e];
+    x.iresp = d.cIresp[cur][d.rev[e]];
     x.spam = d.cSpam[cur] != nullptr ? d.cSpam[cur][e] : -1;
     x.nsrv = d.cNSrv[cur] != nullptr ? d.cNSrv[cur][e] : 0;
     if (d.cSpam[cur] != nullptr) {
@@ -90,7 +90,7 @@ __global__ void k_x_pack(Dev d, int cur, const int64_t* __restrict__ off, unsign
     d.cPruneHb[cur][e] = 0;
     d.cIhave[cur][e] = 0;
     d.cIwant[cur][e] = -1;
-    d.cIresp[cur][e] = -1;
+    d.cIresp[cur][d.rev[e]] = -1;
   } else {
     x.gj = x.ghb = x.prep = x.phb = x.ihave = 0;
     x.iwant = x.iresp = x.spam = -1;
@@ -108,6 +108,7 @@ __global__ void k_x_unpack(Dev d, int cur, const XRec* __restrict__ in, int64_t 
   const int64_t e = x.e;
   d.fwdRelay[cur][e] = x.relay;
   d.fwdPub[cur][e] = x.pub;
+  d.fwdIn[cur][d.rev[e]] = make_ulonglong2(x.relay, x.pub);
   d.cPre[cur][e] = x.pre;
   d.cHb[cur][e] = x.hb;
   d.cGraftJoin[cur][e] = x.gj;
@@ -116,7 +117,7 @@ __global__ void k_x_unpack(Dev d, int cur, const XRec* __restrict__ in, int64_t 
   d.cPruneHb[cur][e] = x.phb;
   d.cIhave[cur][e] = x.ihave;
   d.cIwant[cur][e] = x.iwant;
-  d.cIresp[cur][e] = x.iresp;
+  d.cIresp[cur][d.rev[e]] = x.iresp;
   if (d.cSpam[cur] != nullptr) {
     d.cSpam[cur][e] = x.spam;
     d.cNSrv[cur][e] = x.nsrv;

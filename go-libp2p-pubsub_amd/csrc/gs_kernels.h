@@ -402,11 +402,13 @@ __global__ void k_fwd(Dev d, int cur) {
     }
   }
   if (!edge_up(d, e)) relay = pub = 0;  // no connection: nothing is sent
+  if (d.fwdRelay[cur][e] == relay && d.fwdPub[cur][e] == pub) return;
   // partitioned engine: a forwarding set that changed since this parity was
   // last exchanged must reach the receiver's rank (gs_exchange.h)
-  if (d.xmark && (d.fwdRelay[cur][e] != relay || d.fwdPub[cur][e] != pub)) d.xmark[e] = 1;
+  if (d.xmark) d.xmark[e] = 1;
   d.fwdRelay[cur][e] = relay;
   d.fwdPub[cur][e] = pub;
+  d.fwdIn[cur][d.rev[e]] = make_ulonglong2(relay, pub);
 }
 
 __global__ void k_pubmask(Dev d, int b, int n, int cur) {
@@ -600,15 +602,16 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
     const int64_t e = base + lane;
     u = d.col[e];
     r = d.rev[e];
-    jr = (int)(r - d.rowptr[u]);
+    jr = d.jrIn[e];
     // only copies of v's own topics are handled (pubsub.go:959); what the
     // sender sent on other topics (a peer that left is still in the sender's
     // mesh until its PRUNE arrives) only counts as transmitted (uSent below)
-    relayAll = d.fwdRelay[prv][r];
-    pubAll = d.fwdPub[prv][r];
+    const ulonglong2 fw = d.fwdIn[prv][e];
+    relayAll = fw.x;
+    pubAll = fw.y;
     relay = relayAll & sv;
     pub = pubAll & sv;
-    const int64_t ir = d.cIresp[prv][r];
+    const int64_t ir = d.cIresp[prv][e];
     if (ir >= 0) {
       irOff = (int)(ir >> 24);
       irN = (int)(ir & 0xFFFFFF);

@@ -859,7 +859,7 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
     d.cPruneHb[prv][r] = 0;
     d.cIhave[prv][r] = 0;
     d.cIwant[prv][r] = -1;
-    d.cIresp[prv][r] = -1;
+    d.cIresp[prv][e] = -1;
     if (ADV && d.cSpam[prv] != nullptr) {
       d.cSpam[prv][r] = -1;
       d.cNSrv[prv][r] = 0;
@@ -874,7 +874,7 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
         d.cPre[cur][e] = (uint8_t)(d.cPre[cur][e] + nReplies);
         d.cPruneReply[cur][e] |= pruneOut;
         if (iwantRec >= 0) d.cIwant[cur][e] = iwantRec;
-        if (respRec >= 0) d.cIresp[cur][e] = respRec;
+        if (respRec >= 0) d.cIresp[cur][r] = respRec;
         if (nSrv && d.cNSrv[cur] != nullptr) d.cNSrv[cur][e] = (uint8_t)nSrv;
         if (d.rpcB != nullptr) {
           // HandleRPC's replies (gossipsub.go:602-607, rpcWithControl): a PRUNE
@@ -1387,10 +1387,11 @@ __global__ __launch_bounds__(64) void k_edge_down(Dev d, const int32_t* __restri
     d.fanout[e] = 0;
     d.cPre[prv][e] = 0; d.cHb[prv][e] = 0; d.cGraftJoin[prv][e] = 0; d.cGraftHb[prv][e] = 0;
     d.cPruneReply[prv][e] = 0; d.cPruneHb[prv][e] = 0; d.cIhave[prv][e] = 0;
-    d.cIwant[prv][e] = -1; d.cIresp[prv][e] = -1;
+    d.cIwant[prv][e] = -1; d.cIresp[prv][d.rev[e]] = -1;
     if (d.cSpam[prv] != nullptr) { d.cSpam[prv][e] = -1; d.cNSrv[prv][e] = 0; }
     d.fwdRelay[prv][e] = 0;
     d.fwdPub[prv][e] = 0;
+    d.fwdIn[prv][d.rev[e]] = make_ulonglong2(0ull, 0ull);
     d.sdirty[e] = 1;
     if (is_traced(d, u)) trace_emit(d, hop, GS_TRACE_REMOVE_PEER, u, v, -1, -1, 0);  // trace.go:215
   }
