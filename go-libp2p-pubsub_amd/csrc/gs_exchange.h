@@ -42,7 +42,8 @@ static_assert(sizeof(XRec) == 96, "XRec layout");
 __device__ __forceinline__ bool x_needed(const Dev& d, int cur, int64_t e, int& dest) {
   dest = d.nodeRank[d.col[e]];
   if (dest == d.rank) return false;
-  return d.xmark[e] || d.cPre[cur][e] || d.cHb[cur][e];
+  const int64_t ri = d.rev[e];  // outbox records are indexed by the receiver's in-edge
+  return d.xmark[e] || d.cPre[cur][ri] || d.cHb[cur][ri];
 }
 
 // Records per destination rank.
@@ -61,36 +62,37 @@ __global__ void k_x_pack(Dev d, int cur, const int64_t* __restrict__ off, unsign
   int dest;
   if (!x_needed(d, cur, e, dest)) return;
   const int64_t k = off[dest] + (int64_t)atomicAdd(&cursor[dest], 1ull);
+  const int64_t ri = d.rev[e];
   XRec x;
   x.e = (int32_t)e;
-  x.pre = d.cPre[cur][e];
-  x.hb = d.cHb[cur][e];
+  x.pre = d.cPre[cur][ri];
+  x.hb = d.cHb[cur][ri];
   x.pad = 0;
   x.relay = d.fwdRelay[cur][e];
   x.pub = d.fwdPub[cur][e];
   if (x.pre | x.hb) {
-    x.gj = d.cGraftJoin[cur][e];
-    x.ghb = d.cGraftHb[cur][e];
-    x.prep = d.cPruneReply[cur][e];
-    x.phb = d.cPruneHb[cur][e];
-    x.ihave = d.cIhave[cur][e];
-    x.iwant = d.cIwant[cur][e];
-    x.iresp = d.cIresp[cur][d.rev[e]];
-    x.spam = d.cSpam[cur] != nullptr ? d.cSpam[cur][e] : -1;
-    x.nsrv = d.cNSrv[cur] != nullptr ? d.cNSrv[cur][e] : 0;
+    x.gj = d.cGraftJoin[cur][ri];
+    x.ghb = d.cGraftHb[cur][ri];
+    x.prep = d.cPruneReply[cur][ri];
+    x.phb = d.cPruneHb[cur][ri];
+    x.ihave = d.cIhave[cur][ri];
+    x.iwant = d.cIwant[cur][ri];
+    x.iresp = d.cIresp[cur][ri];
+    x.spam = d.cSpam[cur] != nullptr ? d.cSpam[cur][ri] : -1;
+    x.nsrv = d.cNSrv[cur] != nullptr ? d.cNSrv[cur][ri] : 0;
     if (d.cSpam[cur] != nullptr) {
-      d.cSpam[cur][e] = -1;
-      d.cNSrv[cur][e] = 0;
+      d.cSpam[cur][ri] = -1;
+      d.cNSrv[cur][ri] = 0;
     }
-    d.cPre[cur][e] = 0;
-    d.cHb[cur][e] = 0;
-    d.cGraftJoin[cur][e] = 0;
-    d.cGraftHb[cur][e] = 0;
-    d.cPruneReply[cur][e] = 0;
-    d.cPruneHb[cur][e] = 0;
-    d.cIhave[cur][e] = 0;
-    d.cIwant[cur][e] = -1;
-    d.cIresp[cur][d.rev[e]] = -1;
+    d.cPre[cur][ri] = 0;
+    d.cHb[cur][ri] = 0;
+    d.cGraftJoin[cur][ri] = 0;
+    d.cGraftHb[cur][ri] = 0;
+    d.cPruneReply[cur][ri] = 0;
+    d.cPruneHb[cur][ri] = 0;
+    d.cIhave[cur][ri] = 0;
+    d.cIwant[cur][ri] = -1;
+    d.cIresp[cur][ri] = -1;
   } else {
     x.gj = x.ghb = x.prep = x.phb = x.ihave = 0;
     x.iwant = x.iresp = x.spam = -1;
@@ -106,21 +108,22 @@ __global__ void k_x_unpack(Dev d, int cur, const XRec* __restrict__ in, int64_t 
   if (k >= n) return;
   const XRec x = in[k];
   const int64_t e = x.e;
+  const int64_t ri = d.rev[e];
   d.fwdRelay[cur][e] = x.relay;
   d.fwdPub[cur][e] = x.pub;
-  d.fwdIn[cur][d.rev[e]] = make_ulonglong2(x.relay, x.pub);
-  d.cPre[cur][e] = x.pre;
-  d.cHb[cur][e] = x.hb;
-  d.cGraftJoin[cur][e] = x.gj;
-  d.cGraftHb[cur][e] = x.ghb;
-  d.cPruneReply[cur][e] = x.prep;
-  d.cPruneHb[cur][e] = x.phb;
-  d.cIhave[cur][e] = x.ihave;
-  d.cIwant[cur][e] = x.iwant;
-  d.cIresp[cur][d.rev[e]] = x.iresp;
+  d.fwdIn[cur][ri] = make_ulonglong2(x.relay, x.pub);
+  d.cPre[cur][ri] = x.pre;
+  d.cHb[cur][ri] = x.hb;
+  d.cGraftJoin[cur][ri] = x.gj;
+  d.cGraftHb[cur][ri] = x.ghb;
+  d.cPruneReply[cur][ri] = x.prep;
+  d.cPruneHb[cur][ri] = x.phb;
+  d.cIhave[cur][ri] = x.ihave;
+  d.cIwant[cur][ri] = x.iwant;
+  d.cIresp[cur][ri] = x.iresp;
   if (d.cSpam[cur] != nullptr) {
-    d.cSpam[cur][e] = x.spam;
-    d.cNSrv[cur][e] = x.nsrv;
+    d.cSpam[cur][ri] = x.spam;
+    d.cNSrv[cur][ri] = x.nsrv;
   }
 }
 

@@ -333,8 +333,8 @@ __global__ __launch_bounds__(64) void k_join(Dev d, int64_t hop, int64_t now, in
   if (silent) gj = 0;
   if (valid) {
     d.mesh[e] = meshl;
-    d.cGraftJoin[cur][e] = gj;
-    d.cPre[cur][e] = (uint8_t)__popcll(gj);
+    d.cGraftJoin[cur][d.rev[e]] = gj;
+    d.cPre[cur][d.rev[e]] = (uint8_t)__popcll(gj);
     if (d.rpcB != nullptr && gj) {  // one sendGraft RPC per topic (gossipsub.go:1080-1084)
       int64_t b = 0;
       for (uint64_t m = gj; m; m &= m - 1) b += gs_pb_field(d.acc[__ffsll((long long)m) - 1].graftEnt);
@@ -597,11 +597,9 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
   uint64_t relay = 0, pub = 0, relayAll = 0, pubAll = 0;
   bool gray = false;
   int irOff = 0, irN = 0;
-  int64_t r = 0;
   if (valid) {
     const int64_t e = base + lane;
     u = d.col[e];
-    r = d.rev[e];
     jr = d.jrIn[e];
     // only copies of v's own topics are handled (pubsub.go:959); what the
     // sender sent on other topics (a peer that left is still in the sender's
@@ -663,11 +661,11 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
       }
     }
     sGThr[lane] = thr;
-    if (valid && thr >= 0 && (d.cPre[prv][r] != 0 || d.cHb[prv][r] != 0)) {
+    if (valid && thr >= 0 && (d.cPre[prv][base + lane] != 0 || d.cHb[prv][base + lane] != 0)) {
       const double uu = gs_key_to_unit(gs_key64(d.seed, GS_SITE_GATER, v, u, (uint32_t)h, 0xFFFFFFFFu));
       ctlGated = !(uu < thr);
     }
-    if (valid && d.cNSrv[prv] != nullptr) nSrvRpc = d.cNSrv[prv][r];
+    if (valid && d.cNSrv[prv] != nullptr) nSrvRpc = d.cNSrv[prv][base + lane];
     else if (irN) nSrvRpc = 1;
   }
   // per-sender view for the block-parallel walk
@@ -1296,8 +1294,9 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
         } else {
           int p = (int)off;
           each([&](int slot) { d.pool[cur][p++] = slot; });
-          d.cSpam[cur][base + lane] = ((int64_t)off << 24) | (int64_t)n;
-          d.cPre[cur][base + lane] = (uint8_t)(d.cPre[cur][base + lane] + 1);
+          const int64_t rl = d.rev[base + lane];  // the receiver's in-edge
+          d.cSpam[cur][rl] = ((int64_t)off << 24) | (int64_t)n;
+          d.cPre[cur][rl] = (uint8_t)(d.cPre[cur][rl] + 1);
           // RPC{control: {iwant: [{n ids}]}}
           if (acct) acct_send(d, base + lane, gs_pb_field(gs_pb_field((int64_t)n * d.acctIdF)), 1);
           ctr_add(d, C_IWANT_SENT, (unsigned long long)n);

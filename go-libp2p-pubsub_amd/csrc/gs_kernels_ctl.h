@@ -204,8 +204,8 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
   int npre = 0, hb = 0;
   if (valid) {
     r = d.rev[e];
-    npre = d.cPre[prv][r];
-    hb = d.cHb[prv][r];
+    npre = d.cPre[prv][e];
+    hb = d.cHb[prv][e];
   }
   const bool ctl = npre != 0 || hb != 0;
   const unsigned long long cmask = __ballot(ctl);
@@ -217,13 +217,13 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
   bool gl = false;
   if (valid) meshE = d.mesh[e];
   if (ctl) {
-    gJoin = d.cGraftJoin[prv][r];
-    gHb = d.cGraftHb[prv][r];
-    pRep = d.cPruneReply[prv][r];
-    pHb = d.cPruneHb[prv][r];
-    ihaveT = d.cIhave[prv][r];
-    iwRec = d.cIwant[prv][r];
-    if (ADV && d.cSpam[prv] != nullptr) spRec = d.cSpam[prv][r];  // IWANT spam RPC (an extra reply-group RPC)
+    gJoin = d.cGraftJoin[prv][e];
+    gHb = d.cGraftHb[prv][e];
+    pRep = d.cPruneReply[prv][e];
+    pHb = d.cPruneHb[prv][e];
+    ihaveT = d.cIhave[prv][e];
+    iwRec = d.cIwant[prv][e];
+    if (ADV && d.cSpam[prv] != nullptr) spRec = d.cSpam[prv][e];  // IWANT spam RPC (an extra reply-group RPC)
     ph = d.peerhave[e];
     ia = d.iasked[e];
     u = d.col[e];
@@ -851,18 +851,18 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
   GS_STAMPB(3);
   // ---- step 4: consume the outbox entries, per-edge state, reply RPCs
   if (ctl) {
-    d.cPre[prv][r] = 0;
-    d.cHb[prv][r] = 0;
-    d.cGraftJoin[prv][r] = 0;
-    d.cGraftHb[prv][r] = 0;
-    d.cPruneReply[prv][r] = 0;
-    d.cPruneHb[prv][r] = 0;
-    d.cIhave[prv][r] = 0;
-    d.cIwant[prv][r] = -1;
+    d.cPre[prv][e] = 0;
+    d.cHb[prv][e] = 0;
+    d.cGraftJoin[prv][e] = 0;
+    d.cGraftHb[prv][e] = 0;
+    d.cPruneReply[prv][e] = 0;
+    d.cPruneHb[prv][e] = 0;
+    d.cIhave[prv][e] = 0;
+    d.cIwant[prv][e] = -1;
     d.cIresp[prv][e] = -1;
     if (ADV && d.cSpam[prv] != nullptr) {
-      d.cSpam[prv][r] = -1;
-      d.cNSrv[prv][r] = 0;
+      d.cSpam[prv][e] = -1;
+      d.cNSrv[prv][e] = 0;
     }
     if (!gl) {
       d.mesh[e] = meshE;
@@ -871,11 +871,11 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
       // one reply per control RPC that produced one (HandleRPC, gossipsub.go:602-607)
       const int nReplies = nRep1 + nSrv + ((iwantAny || prunesHb) ? 1 : 0);
       if (nReplies && !silent) {
-        d.cPre[cur][e] = (uint8_t)(d.cPre[cur][e] + nReplies);
-        d.cPruneReply[cur][e] |= pruneOut;
-        if (iwantRec >= 0) d.cIwant[cur][e] = iwantRec;
+        d.cPre[cur][r] = (uint8_t)(d.cPre[cur][r] + nReplies);
+        d.cPruneReply[cur][r] |= pruneOut;
+        if (iwantRec >= 0) d.cIwant[cur][r] = iwantRec;
         if (respRec >= 0) d.cIresp[cur][r] = respRec;
-        if (nSrv && d.cNSrv[cur] != nullptr) d.cNSrv[cur][e] = (uint8_t)nSrv;
+        if (nSrv && d.cNSrv[cur] != nullptr) d.cNSrv[cur][r] = (uint8_t)nSrv;
         if (d.rpcB != nullptr) {
           // HandleRPC's replies (gossipsub.go:602-607, rpcWithControl): a PRUNE
           // per rejected join GRAFT; the served messages of each IWANT list
@@ -1300,10 +1300,11 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
     d.mesh[e] = meshl;
     d.fanout[e] = fanl;
     if (tograft | toprune | ihave) {
-      d.cGraftHb[cur][e] = tograft;
-      d.cPruneHb[cur][e] = toprune;
-      d.cIhave[cur][e] = ihave;
-      d.cHb[cur][e] = 1;
+      const int64_t re = d.rev[e];  // outbox records are indexed by the receiver's in-edge
+      d.cGraftHb[cur][re] = tograft;
+      d.cPruneHb[cur][re] = toprune;
+      d.cIhave[cur][re] = ihave;
+      d.cHb[cur][re] = 1;
     }
   }
   const int g = wave_sum_int(__popcll(tograft));
@@ -1382,16 +1383,17 @@ __global__ __launch_bounds__(64) void k_edge_down(Dev d, const int32_t* __restri
   double s = 0.0;
   if (d.scoring && d.rstate != nullptr && d.rstate[e] == 1) s = edge_score_wave(d, e, sterm);
   if (lane == 0) {
+    const int64_t re = d.rev[e];
     d.alive[e] = 0;
     d.mesh[e] = 0;
     d.fanout[e] = 0;
-    d.cPre[prv][e] = 0; d.cHb[prv][e] = 0; d.cGraftJoin[prv][e] = 0; d.cGraftHb[prv][e] = 0;
-    d.cPruneReply[prv][e] = 0; d.cPruneHb[prv][e] = 0; d.cIhave[prv][e] = 0;
-    d.cIwant[prv][e] = -1; d.cIresp[prv][d.rev[e]] = -1;
-    if (d.cSpam[prv] != nullptr) { d.cSpam[prv][e] = -1; d.cNSrv[prv][e] = 0; }
+    d.cPre[prv][re] = 0; d.cHb[prv][re] = 0; d.cGraftJoin[prv][re] = 0; d.cGraftHb[prv][re] = 0;
+    d.cPruneReply[prv][re] = 0; d.cPruneHb[prv][re] = 0; d.cIhave[prv][re] = 0;
+    d.cIwant[prv][re] = -1; d.cIresp[prv][re] = -1;
+    if (d.cSpam[prv] != nullptr) { d.cSpam[prv][re] = -1; d.cNSrv[prv][re] = 0; }
     d.fwdRelay[prv][e] = 0;
     d.fwdPub[prv][e] = 0;
-    d.fwdIn[prv][d.rev[e]] = make_ulonglong2(0ull, 0ull);
+    d.fwdIn[prv][re] = make_ulonglong2(0ull, 0ull);
     d.sdirty[e] = 1;
     if (is_traced(d, u)) trace_emit(d, hop, GS_TRACE_REMOVE_PEER, u, v, -1, -1, 0);  // trace.go:215
   }
@@ -1503,8 +1505,9 @@ __global__ __launch_bounds__(64) void k_leave(Dev d, const int32_t* __restrict__
   if (valid && pruned) {
     d.mesh[e] = meshl;
     if (!silent) {
-      d.cPruneReply[cur][e] |= pruned;
-      d.cPre[cur][e] = (uint8_t)(d.cPre[cur][e] + __popcll(pruned));  // one sendPrune RPC per topic
+      const int64_t re = d.rev[e];
+      d.cPruneReply[cur][re] |= pruned;
+      d.cPre[cur][re] = (uint8_t)(d.cPre[cur][re] + __popcll(pruned));  // one sendPrune RPC per topic
       if (d.rpcB != nullptr) {
         int64_t b = 0;
         for (uint64_t m = pruned; m; m &= m - 1) b += gs_pb_field(d.acc[__ffsll((long long)m) - 1].pruneEnt);
@@ -1582,8 +1585,9 @@ __global__ __launch_bounds__(64) void k_join_pairs(Dev d, const int32_t* __restr
     d.mesh[e] = meshl;
     d.fanout[e] = fanl;
     if (grafted && !silent) {
-      d.cGraftJoin[cur][e] |= grafted;
-      d.cPre[cur][e] = (uint8_t)(d.cPre[cur][e] + __popcll(grafted));  // one sendGraft RPC per topic
+      const int64_t re = d.rev[e];
+      d.cGraftJoin[cur][re] |= grafted;
+      d.cPre[cur][re] = (uint8_t)(d.cPre[cur][re] + __popcll(grafted));  // one sendGraft RPC per topic
       if (d.rpcB != nullptr) {
         int64_t b = 0;
         for (uint64_t m = grafted; m; m &= m - 1) b += gs_pb_field(d.acc[__ffsll((long long)m) - 1].graftEnt);
