@@ -653,7 +653,7 @@ __device__ __forceinline__ void select_kth(F&& each, int k, uint32_t* hist, unsi
     const int incl = wave_incl_sum(sum);
     const int excl = incl - sum;
     const bool mine = excl < kk && kk <= incl;
-    int digit = 0, below = 0;
+    int digit = 0, below = 0, inBin = 0;
     if (mine) {
       const uint32_t cs[4] = {c0, c1, c2, c3};
       int acc = excl, dd = 0;
@@ -663,6 +663,7 @@ __device__ __forceinline__ void select_kth(F&& each, int k, uint32_t* hist, unsi
       }
       digit = 4 * lane + dd;
       below = acc;
+      inBin = (int)cs[dd];
     }
     const unsigned long long m = __ballot(mine);
     __syncthreads();
@@ -674,8 +675,29 @@ __device__ __forceinline__ void select_kth(F&& each, int k, uint32_t* hist, unsi
     const int src = __ffsll((long long)m) - 1;
     digit = lane_get(digit, src);
     below = lane_get(below, src);
+    inBin = lane_get(inBin, src);
     prefix |= (unsigned long long)digit << sh;
     kk -= below;
+    if (inBin == 1) {
+      // the k-th candidate is the only one left with this prefix: one more
+      // pass reads its whole key and id (usually after 2 of the 8 digits)
+      const unsigned long long pm = ~0ull << sh;
+      unsigned long long bk = 0;
+      long long bi = 0;
+      bool found = false;
+      each([&](unsigned long long key, long long id) {
+        if ((key & pm) == prefix) {
+          bk = key;
+          bi = id;
+          found = true;
+        }
+      });
+      const unsigned long long f = __ballot(found);
+      const int fl = __ffsll((long long)f) - 1;
+      K = lane_get64(bk, fl);
+      M = (long long)lane_get64((uint64_t)bi, fl);
+      return;
+    }
   }
   K = prefix;
   long long prev = INT64_MIN;  // the kk-th smallest id among the keys equal to K

@@ -14,7 +14,9 @@ LIB = os.path.join(REPO, "go-libp2p-pubsub_amd", "build", os.environ.get("GS_STA
 
 def main():
     wl = bench.WORKLOADS[sys.argv[1] if len(sys.argv) > 1 else "config4"]
-    eng, _ = bench.build_engine(wl, 4, 3, 0, lib=LIB)
+    # publish schedule of `rounds` rounds (bench.py: warm-up + steps + 1)
+    rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 4
+    eng, _ = bench.build_engine(wl, rounds, 3, 0, lib=LIB)
     hops = int(sys.argv[2]) if len(sys.argv) > 2 else 1 + 2 * bench.HOPS_PER_ROUND + 3
     eng.step(hops)
     raw = C.CDLL(LIB)
