@@ -538,9 +538,9 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
     int totalItems;
     // An item is (sender, topic), or with long topic windows (Wt > 16 words,
     // config3's 157) (sender, topic, 16-word chunk), so the lanes share the
-    // words of one topic; with cuts an item stays a whole topic (the cut is
-    // per (sender, topic)).  At most 64 items per sender either way.
-    const int nCh = (cutMode || Wt <= 16) ? 1 : (Wt + 15) >> 4;
+    // words of one topic; a cut is decided per (sender, topic) item tb = b / nCh
+    // and applied to each of its chunks.  At most 64 items per sender.
+    const int nCh = Wt <= 16 ? 1 : (Wt + 15) >> 4;
     sIt[lane] = lane_prefix(__popcll(tm) * nCh, &totalItems);
     sTm[lane] = tm;
     sNode[lane] = u;
@@ -575,18 +575,20 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
       for (int k = lane; k < 128; k += 64) cBits[k] = 0u;
       if (lane == 0) *cN = 0;
       __syncthreads();
-      for (int b = lane; b < totalItems; b += 64) {
+      // cuts are per (sender, topic): topic item tb covers items tb*nCh ..
+      const int totalT = totalItems / nCh;
+      for (int tb = lane; tb < totalT; tb += 64) {
         int k;
-        const int i = item_sender(sIt, b, k);
-        const int t = kth_bit(sTm[i], k);
+        const int i = item_sender(sIt, tb * nCh, k);
+        const int t = kth_bit(sTm[i], k / nCh);
         const int uu = sNode[i];
         int nm = 0;
         for (int w = t * Wt; w < (t + 1) * Wt; ++w) nm += __popcll(d.gw[(int64_t)uu * W + w]);
         if (nm > d.MaxIHaveLength) {
           const int pos = atomicAdd(cN, 1);
           if (pos < GS_CUTS) {
-            cItem[pos] = b;
-            atomicOr(&cBits[b >> 5], 1u << (b & 31));
+            cItem[pos] = tb;
+            atomicOr(&cBits[tb >> 5], 1u << (tb & 31));
           } else {
             set_err(d, E_TRUNCATE);
           }
@@ -595,10 +597,10 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
       __syncthreads();
       nCut = min(*cN, GS_CUTS);
       for (int c = 0; c < nCut; ++c) {
-        const int b = cItem[c];
+        const int tb = cItem[c];
         int k;
-        const int i = item_sender(sIt, b, k);
-        const int t = kth_bit(sTm[i], k);
+        const int i = item_sender(sIt, tb * nCh, k);
+        const int t = kth_bit(sTm[i], k / nCh);
         const int uu = sNode[i];
         // every gossip id of the sender's topic t, lane-strided over words
         auto each = [&](auto&& fn) {
@@ -626,9 +628,10 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
     // with a want
     auto wants = [&](int b, int uu, int t, int ch, auto&& fn) {
       int ci = -1;
-      if (nCut && ((cBits[b >> 5] >> (b & 31)) & 1))
+      const int tb = b / nCh;  // the (sender, topic) item
+      if (nCut && ((cBits[tb >> 5] >> (tb & 31)) & 1))
         for (int c = 0; c < nCut; ++c)
-          if (cItem[c] == b) ci = c;
+          if (cItem[c] == tb) ci = c;
       const int wBeg = nCh > 1 ? t * Wt + 16 * ch : t * Wt;
       const int wEnd = nCh > 1 ? min(wBeg + 16, (t + 1) * Wt) : (t + 1) * Wt;
       for (int w0 = wBeg; w0 < wEnd; w0 += 4) {
@@ -719,7 +722,7 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
         cm &= cm - 1;
         const int uu = sNode[i];
         const int kk = lane_get(myWant, i);
-        const int b0 = sIt[i];
+        const int b0 = sIt[i] / nCh;  // its first (sender, topic) item
         const int nItems = __popcll(sTm[i]);
         // every want of sender i over its items, lane-strided over words
         auto each = [&](auto&& fn) {
