@@ -26,3 +26,17 @@ def test_oracle_reproduces_golden(oracle_path, name):
 def test_gpu_reproduces_golden(name):
     from pubsub_amd import PRODUCT_LIB
     assert digest(scenarios.run(PRODUCT_LIB, name)) == GOLDEN[name]
+
+
+# Races show up as run-to-run differences before they show up as a wrong
+# digest: the scenarios with the most cross-lane LDS and global atomics in
+# phase B (IWANT serving, IHAVE handling, spam, cuts) run three more times.
+RACE_PRONE = ["gossipsub_dense_dhi", "c5shape", "adversarial_mix", "spam_ihave_2t"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", [n for n in RACE_PRONE if n in GOLDEN])
+def test_gpu_golden_repeatable(name):
+    from pubsub_amd import PRODUCT_LIB
+    for _ in range(3):
+        assert digest(scenarios.run(PRODUCT_LIB, name)) == GOLDEN[name]
