@@ -418,7 +418,10 @@ int gs_engine::start() {
   {
     std::vector<uint8_t> jr(E);
     for (int64_t e = 0; e < E; ++e) jr[e] = (uint8_t)(rev[e] - rowptr[col[e]]);
-    HIPCHECK(hipMemcpy(dJrIn, jr.data(), E, hipMemcpyHostToDevice));
+    // on the engine's (non-blocking) stream, after dalloc's memset; the host
+    // buffer must outlive the copy
+    HIPCHECK(hipMemcpyAsync(dJrIn, jr.data(), E, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
   }
   HIPCHECK(hipMemcpyAsync(dOut, outbound.data(), E, hipMemcpyHostToDevice, stream));
   HIPCHECK(hipMemcpyAsync(dDir, direct.data(), E, hipMemcpyHostToDevice, stream));
