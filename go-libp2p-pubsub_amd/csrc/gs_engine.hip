@@ -566,6 +566,8 @@ int gs_engine::start() {
       for (int k = 0; k < 2; ++k) { x.pflag[k] = dalloc<uint8_t>((size_t)poolSeg * world); chk(x.pflag[k]); }
       x.spamCnt = dalloc<uint32_t>((size_t)std::max<int64_t>(nrow, 1) * (S / 4)); chk(x.spamCnt);
       if (ok) HIPCHECK(hipMemcpyAsync(x.spamRow, spamRowH.data(), (size_t)E * 4, hipMemcpyHostToDevice, stream));
+      // `row` is pageable and dies with this block: the copy must have read it
+      HIPCHECK(hipStreamSynchronize(stream));
     }
   }
   x.gater = gaterOn ? 1 : 0;
@@ -643,7 +645,7 @@ int gs_engine::start() {
       HIPCHECK(hipStreamSynchronize(stream));
     }
     x.nodeRank = nr;
-    HIPCHECK(hipHostMalloc((void**)&xHost, (size_t)(world + 2) * 8, hipHostMallocDefault));
+    HIPCHECK(hipHostMalloc((void**)&xHost, (size_t)(world + 3) * 8, hipHostMallocDefault));
   }
   if (!ok) {
     gs_set_error("device allocation failed (state); reduce num_nodes or slots_per_topic");
@@ -1221,7 +1223,13 @@ int gs_engine::exchange(int cur, bool hb) {
   HIPCHECK(hipMemcpyAsync(xHost, xCnt, (size_t)world * 8, hipMemcpyDeviceToHost, stream));
   HIPCHECK(hipMemcpyAsync(xHost + world, bump, 8, hipMemcpyDeviceToHost, stream));
   HIPCHECK(hipMemcpyAsync(xHost + world + 1, d.poolCnt + cur, 8, hipMemcpyDeviceToHost, stream));
+  // this rank's device error word travels with the sizes below, so every rank
+  // stops at the same hop (a rank returning alone would leave the others
+  // waiting in the next hop's collectives)
+  xHost[world + 2] = 0;
+  HIPCHECK(hipMemcpyAsync(xHost + world + 2, d.err, 4, hipMemcpyDeviceToHost, stream));
   HIPCHECK(hipStreamSynchronize(stream));
+  const int32_t myErr = (int32_t)xHost[world + 2];
   const int64_t nEnt = (int64_t)xHost[world];
   const int64_t poolBase = (int64_t)rank * poolSeg;
   const int64_t nPool = std::max<int64_t>(0, std::min<int64_t>((int64_t)xHost[world + 1], x_poolEnd()) - poolBase);
@@ -1257,15 +1265,27 @@ int gs_engine::exchange(int cur, bool hb) {
     k_x_pack<<<nblk(eOwn, 256), 256, 0, stream>>>(d, cur, xOff, cursor, (XRec*)xSendE);
   }
   HIPCHECK(hipStreamSynchronize(stream));  // sendOff is pageable; the transport reads the buffers
-  // 3. sizes of every rank: [bcast bytes, list entries, arena ids, gw rows?, records to rank 0..world-1]
-  const int nS = 4 + world;
+  // 3. sizes of every rank: [bcast bytes, list entries, arena ids, gw rows?,
+  //    records to rank 0..world-1, device error word]
+  const int nS = 5 + world;
   std::vector<int64_t> mine(nS), all((size_t)nS * world);
   mine[0] = (int64_t)bcast; mine[1] = nEnt; mine[2] = nPool; mine[3] = hb ? 1 : 0;
   for (int r = 0; r < world; ++r) mine[4 + r] = sendRec[r];
+  mine[4 + world] = myErr;
   const auto t0 = std::chrono::steady_clock::now();
   if (tr.allgather_i64(tr.user, mine.data(), nS, all.data()) != 0) {
     gs_set_error("transport allgather_i64 failed");
     return GS_EDEVICE;
+  }
+  if (myErr) return deviceErrorText(myErr, hop);
+  for (int r = 0; r < world; ++r) {
+    const int32_t err = (int32_t)all[(size_t)r * nS + 4 + world];
+    if (!err) continue;
+    const int rc = deviceErrorCode(err);  // the failing rank's code and text
+    g_err = "hop " + std::to_string(hop) + ": rank " + std::to_string(r) + ": " + g_err;
+    stickyRc = rc;
+    stickyMsg = g_err;
+    return rc;
   }
   int64_t chunk = 8;
   for (int r = 0; r < world; ++r) chunk = std::max<int64_t>(chunk, all[(size_t)r * nS]);
@@ -1333,7 +1353,9 @@ int gs_engine::drainTrace() {
   const int64_t k = std::min<int64_t>((int64_t)cnt, traceCap);
   std::vector<gs_trace_event> ev((size_t)k);
   if (k) HIPCHECK(hipMemcpy(ev.data(), d.trace, (size_t)k * sizeof(gs_trace_event), hipMemcpyDeviceToHost));
-  HIPCHECK(hipMemset(d.traceN, 0, 8));
+  // on the engine's stream: the next hop's appends are queued there too, and a
+  // null-stream memset is not ordered against a non-blocking stream
+  HIPCHECK(hipMemsetAsync(d.traceN, 0, 8, stream));
   struct Key {
     int64_t hop, msg;
     int32_t node, peer;
@@ -1599,7 +1621,13 @@ int gs_schedule_events(gs_engine* g, int32_t n, const int32_t* kind, const int32
   if (n < 0 || (n > 0 && (!kind || !a || !b || !hop))) { gs_set_error("gs_schedule_events: bad arguments"); return GS_EINVAL; }
   if (!g->graphSet) { gs_set_error("graph not set"); return GS_ESTATE; }
   if (g->gaterOn) { gs_set_error("connection churn with the peer gater is not supported"); return GS_EUNSUPPORTED; }
-  if (g->world > 1) { gs_set_error("connection churn needs an unpartitioned engine"); return GS_EUNSUPPORTED; }
+  if (n > 0 && !g->churnWindow && !g->mId.empty()) {
+    // late joiners catch up through gossip: the wide message window is chosen
+    // when the first churn is scheduled, and it cannot change once messages
+    // hold slots (gs_set_behaviour / gs_set_validation have the same rule)
+    gs_set_error("connection churn must first be scheduled before the first publish");
+    return GS_ESTATE;
+  }
   int64_t last = g->events.empty() ? std::max<int64_t>(1, g->hop) : std::max(g->hop, g->events.back().hop);
   auto isEdge = [&](int x, int y) {
     auto bgn = g->col.begin() + g->rowptr[x], fin = g->col.begin() + g->rowptr[x + 1];
@@ -1866,6 +1894,55 @@ int gs_read_topic_stats(gs_engine* g, double* fmd, double* mmd, double* mfp, dou
   return copy_back_pairs(g, flags, (const uint8_t*)g->d.flags);
 }
 int gs_read_behaviour_penalty(gs_engine* g, double* bp) { return copy_back(g, bp, g->d.bp, g->E * 8); }
+
+int gs_read_topic_stats_edges(gs_engine* g, int64_t n, const int64_t* edges, double* fmd, double* mmd,
+                              double* mfp, double* imd, int64_t* mesh_time, int64_t* graft_time,
+                              uint8_t* flags) {
+  if (n < 0 || (n > 0 && (!edges || !fmd || !mmd || !mfp || !imd || !mesh_time || !graft_time || !flags))) {
+    gs_set_error("gs_read_topic_stats_edges: bad arguments");
+    return GS_EINVAL;
+  }
+  for (int64_t i = 0; i < n; ++i)
+    if (edges[i] < 0 || edges[i] >= g->E) { gs_set_error("gs_read_topic_stats_edges: edge out of range"); return GS_EINVAL; }
+  const int64_t nk = n * g->T;
+  if (!g->started || nk == 0) {
+    std::fill(fmd, fmd + nk, 0.0); std::fill(mmd, mmd + nk, 0.0);
+    std::fill(mfp, mfp + nk, 0.0); std::fill(imd, imd + nk, 0.0);
+    std::fill(mesh_time, mesh_time + nk, 0); std::fill(graft_time, graft_time + nk, 0);
+    std::fill(flags, flags + nk, 0);
+    return GS_OK;
+  }
+  int64_t* dE = nullptr;
+  uint8_t* dOut = nullptr;
+  HIPCHECK(hipMalloc(&dE, (size_t)n * 8));
+  if (hipMalloc(&dOut, (size_t)nk * 49) != hipSuccess) {
+    (void)hipFree(dE);
+    gs_set_error("device allocation failed (gs_read_topic_stats_edges)");
+    return GS_ENOMEM;
+  }
+  std::vector<uint8_t> h((size_t)nk * 49);
+  hipError_t rc = hipMemcpyAsync(dE, edges, (size_t)n * 8, hipMemcpyHostToDevice, g->stream);
+  if (rc == hipSuccess) {
+    k_gather_pairs<<<nblk(nk, 256), 256, 0, g->stream>>>(g->d, dE, n, dOut);
+    rc = hipMemcpyAsync(h.data(), dOut, h.size(), hipMemcpyDeviceToHost, g->stream);
+  }
+  if (rc == hipSuccess) rc = hipStreamSynchronize(g->stream);
+  (void)hipFree(dE);
+  (void)hipFree(dOut);
+  if (rc != hipSuccess) {
+    gs_set_error(std::string("HIP error: ") + hipGetErrorString(rc) + " (gs_read_topic_stats_edges)");
+    return GS_EDEVICE;
+  }
+  const size_t b8 = (size_t)nk * 8;
+  std::memcpy(fmd, h.data(), b8);
+  std::memcpy(mmd, h.data() + b8, b8);
+  std::memcpy(mfp, h.data() + 2 * b8, b8);
+  std::memcpy(imd, h.data() + 3 * b8, b8);
+  std::memcpy(mesh_time, h.data() + 4 * b8, b8);
+  std::memcpy(graft_time, h.data() + 5 * b8, b8);
+  std::memcpy(flags, h.data() + 6 * b8, (size_t)nk);
+  return GS_OK;
+}
 
 int gs_read_deliveries(gs_engine* g, int64_t id, int32_t* hop, int32_t* from) {
   if (!g->record) { gs_set_error("GS_FLAG_RECORD_DELIVERIES not set"); return GS_ESTATE; }

@@ -279,6 +279,35 @@ __global__ void k_fold_all(Dev d) {
   d.dlt[p] = 0;
 }
 
+// gs_read_topic_stats_edges: the counters of n chosen edges, out[i*T + t],
+// pending deliveries applied (eff_fmd / eff_mmd) without writing them back.
+// Output arrays are packed after each other in `out` (8-byte fields first).
+__global__ void k_gather_pairs(Dev d, const int64_t* __restrict__ edges, int64_t n, uint8_t* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nk = n * d.T;
+  if (k >= nk) return;
+  const int64_t e = edges[k / d.T];
+  const int t = (int)(k % d.T);
+  double* o = (double*)out;
+  int64_t* oi = (int64_t*)out;
+  uint8_t* of = out + 48 * nk;
+  if (e < d.e0 || e >= d.e1) {
+    for (int a = 0; a < 6; ++a) o[a * nk + k] = 0.0;
+    of[k] = 0;
+    return;
+  }
+  const int64_t i = tix(d, t, e);
+  const TopicP& tp = d.tp[t];
+  const uint32_t q = d.dlt[i];
+  o[k] = eff_fmd(tp, d.fmd[i], q);
+  o[nk + k] = eff_mmd(tp, d.mmd[i], q);
+  o[2 * nk + k] = d.mfp[i];
+  o[3 * nk + k] = d.imd[i];
+  oi[4 * nk + k] = d.meshTime[i];
+  oi[5 * nk + k] = d.graftTime[i];
+  of[k] = d.flags[i];
+}
+
 // Folds the pending deliveries of topic t into fmd / mmd.
 __global__ void k_fold(Dev d, int t) {
   const int64_t e = d.e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -174,6 +174,9 @@ ABI_FUNCTIONS = [
      [P, C.POINTER(f64), C.POINTER(f64), C.POINTER(f64), C.POINTER(f64), C.POINTER(i64),
       C.POINTER(i64), C.POINTER(u8)]),
     ("gs_read_behaviour_penalty", C.c_int, [P, C.POINTER(f64)]),
+    ("gs_read_topic_stats_edges", C.c_int,
+     [P, i64, C.POINTER(i64), C.POINTER(f64), C.POINTER(f64), C.POINTER(f64), C.POINTER(f64), C.POINTER(i64),
+      C.POINTER(i64), C.POINTER(u8)]),
     ("gs_read_deliveries", C.c_int, [P, i64, C.POINTER(i32), C.POINTER(i32)]),
     ("gs_set_rpc_accounting", C.c_int, [P, C.POINTER(i32), i32, C.POINTER(i32)]),
     ("gs_read_rpc_bytes", C.c_int, [P, C.POINTER(i64), C.POINTER(i64)]),

@@ -158,6 +158,7 @@ class Engine:
         cfg.flags = flags
         cfg.device = opts.get("device", 0)
         self.N, self.T = num_nodes, num_topics
+        self.score_params = score[0] if score is not None else None
         gsp_c = gsp.to_c()
         psp_c = topics_c = scored_c = thr_c = None
         if score is not None:
@@ -314,6 +315,22 @@ class Engine:
             self.h, _ptr(fmd, C.c_double), _ptr(mmd, C.c_double), _ptr(mfp, C.c_double),
             _ptr(imd, C.c_double), _ptr(mt, C.c_int64), _ptr(gt, C.c_int64), _ptr(fl, C.c_uint8)))
         sh = (self.T, self.E)
+        return dict(fmd=fmd.reshape(sh), mmd=mmd.reshape(sh), mfp=mfp.reshape(sh), imd=imd.reshape(sh),
+                    mesh_time=mt.reshape(sh), graft_time=gt.reshape(sh), flags=fl.reshape(sh))
+
+    def topic_stats_at(self, edges):
+        """topic_stats() of the given edges only, shape (len(edges), T) per field
+        (gs_read_topic_stats_edges): spot checks at full size."""
+        edges = np.ascontiguousarray(edges, dtype=np.int64)
+        n = len(edges) * self.T
+        fmd, mmd, mfp, imd = (np.empty(n, dtype=np.float64) for _ in range(4))
+        mt, gt = np.empty(n, dtype=np.int64), np.empty(n, dtype=np.int64)
+        fl = np.empty(n, dtype=np.uint8)
+        _check(self.lib, self.lib.gs_read_topic_stats_edges(
+            self.h, len(edges), _ptr(edges, C.c_int64), _ptr(fmd, C.c_double), _ptr(mmd, C.c_double),
+            _ptr(mfp, C.c_double), _ptr(imd, C.c_double), _ptr(mt, C.c_int64), _ptr(gt, C.c_int64),
+            _ptr(fl, C.c_uint8)))
+        sh = (len(edges), self.T)
         return dict(fmd=fmd.reshape(sh), mmd=mmd.reshape(sh), mfp=mfp.reshape(sh), imd=imd.reshape(sh),
                     mesh_time=mt.reshape(sh), graft_time=gt.reshape(sh), flags=fl.reshape(sh))
 

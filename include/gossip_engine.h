@@ -254,7 +254,12 @@ int gs_publish_ex(gs_engine* eng, int32_t n, const int32_t* src, const int32_t* 
  * the validation queue: at most queue_per_hop received messages enter
  * validation per node per hop (0 = unlimited); later fresh copies are
  * dropped with RejectValidationQueueFull (validation.go:236-241), which is
- * what drives the peer gater (peer_gater.go:413-420).  Before the first step. */
+ * what drives the peer gater (peer_gater.go:413-420).  Before the first step.
+ * Signature policy: the model is StrictNoSign (unsigned messages).  Only topics
+ * with a validator pass through the queue; under the reference's default
+ * StrictSign every received message would (validation.Push, validation.go:233
+ * queues when a topic has validators OR the message carries a signature), so
+ * queue-full drops and the gater inputs they feed occur more often there. */
 int gs_set_validation(gs_engine* eng, const uint8_t* topic_validator, int32_t queue_per_hop);
 /* Per-node behaviour bits (simulated attackers, restating the reference's
  * attack mocks).  Before the first step; NULL = all honest. */
@@ -376,6 +381,13 @@ int gs_read_topic_stats(gs_engine* eng, double* fmd, double* mmd, double* mfp,
                         double* imd, int64_t* mesh_time, int64_t* graft_time,
                         uint8_t* flags);
 int gs_read_behaviour_penalty(gs_engine* eng, double* bp /*[E]*/);
+/* The same counters for n chosen edges only, edge-major: out[i*T + t] is
+ * (edges[i], t).  For spot checks at sizes where the full T*E readback is too
+ * large (1M peers x 64 topics = 2.05e9 pairs).  An edge outside this rank's
+ * range (partitioned engine) reads 0; an edge outside [0, E) is GS_EINVAL. */
+int gs_read_topic_stats_edges(gs_engine* eng, int64_t n, const int64_t* edges, double* fmd,
+                              double* mmd, double* mfp, double* imd, int64_t* mesh_time,
+                              int64_t* graft_time, uint8_t* flags);
 /* Per node: hop of first delivery of message `id` (-1: never) and the node it
  * was first received from (-1: origin or never).  Valid while the message's
  * slot has not been recycled. */

@@ -25,7 +25,27 @@ ops_obj* ops_new(const gs_peer_score_params* p) {
   return o;
 }
 void ops_free(ops_obj* o) { delete o; }
-void ops_set_app_score(ops_obj* o, int p, double v) { o->app[p] = v; }
+void ops_set_app_score(ops_obj* o, int p, double v) {
+  if (p >= (int)o->app.size()) o->app.resize((size_t)p + 1, 0.0);
+  o->app[p] = v;
+}
+// State injection (tests/test_fullsize_gpu.py): the engine's counters of one
+// (edge, topic) become peer p's TopicStats, so score() (score.go:256-333) is
+// recomputed by the oracle's own code from state the oracle cannot simulate
+// at full size.  flags: bit0 inMesh, bit1 meshMessageDeliveriesActive.
+void ops_set_stats(ops_obj* o, int p, int topic, int flags, int64_t graft_time, int64_t mesh_time, double fmd,
+                   double mmd, double mfp, double imd) {
+  TopicStats& ts = o->ps.peerStats[p].topics[topic];
+  ts.inMesh = (flags & 1) != 0;
+  ts.meshMessageDeliveriesActive = (flags & 2) != 0;
+  ts.graftTime = graft_time;
+  ts.meshTime = mesh_time;
+  ts.firstMessageDeliveries = fmd;
+  ts.meshMessageDeliveries = mmd;
+  ts.meshFailurePenalty = mfp;
+  ts.invalidMessageDeliveries = imd;
+}
+void ops_set_behaviour_penalty(ops_obj* o, int p, double bp) { o->ps.peerStats[p].behaviourPenalty = bp; }
 void ops_set_topic(ops_obj* o, int topic, const gs_topic_score_params* tp) { o->ps.topics[topic] = *tp; }
 void ops_set_topic_score_params(ops_obj* o, int topic, const gs_topic_score_params* tp) {
   o->ps.SetTopicScoreParams(topic, *tp);

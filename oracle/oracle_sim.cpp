@@ -1519,6 +1519,40 @@ int gs_read_topic_stats(gs_engine* eng, double* fmd, double* mmd, double* mfp, d
   return GS_OK;
 }
 
+int gs_read_topic_stats_edges(gs_engine* eng, int64_t n, const int64_t* edges, double* fmd, double* mmd,
+                              double* mfp, double* imd, int64_t* mesh_time, int64_t* graft_time, uint8_t* flags) {
+  Sim& s = eng->sim;
+  if (n < 0 || (n > 0 && (!edges || !fmd || !mmd || !mfp || !imd || !mesh_time || !graft_time || !flags))) {
+    set_error("gs_read_topic_stats_edges: bad arguments");
+    return GS_EINVAL;
+  }
+  for (int64_t i = 0; i < n; ++i)
+    if (edges[i] < 0 || edges[i] >= s.E) { set_error("gs_read_topic_stats_edges: edge out of range"); return GS_EINVAL; }
+  const int64_t nk = n * s.T;
+  std::fill(fmd, fmd + nk, 0.0); std::fill(mmd, mmd + nk, 0.0);
+  std::fill(mfp, mfp + nk, 0.0); std::fill(imd, imd + nk, 0.0);
+  std::fill(mesh_time, mesh_time + nk, 0); std::fill(graft_time, graft_time + nk, 0);
+  std::fill(flags, flags + nk, 0);
+  if (!s.started) return GS_OK;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t e = edges[i];
+    const int u = (int)(std::upper_bound(s.rowptr.begin(), s.rowptr.end(), e) - s.rowptr.begin()) - 1;
+    auto ps = s.nodes[u].score.peerStats.find(s.col[e]);
+    if (ps == s.nodes[u].score.peerStats.end()) continue;
+    for (auto& ts : ps->second.topics) {
+      const int64_t k = i * s.T + ts.first;
+      fmd[k] = ts.second.firstMessageDeliveries;
+      mmd[k] = ts.second.meshMessageDeliveries;
+      mfp[k] = ts.second.meshFailurePenalty;
+      imd[k] = ts.second.invalidMessageDeliveries;
+      mesh_time[k] = ts.second.meshTime;
+      graft_time[k] = ts.second.graftTime;
+      flags[k] = (ts.second.inMesh ? 1 : 0) | (ts.second.meshMessageDeliveriesActive ? 2 : 0);
+    }
+  }
+  return GS_OK;
+}
+
 int gs_read_behaviour_penalty(gs_engine* eng, double* bp) {
   Sim& s = eng->sim;
   std::fill(bp, bp + s.E, 0.0);

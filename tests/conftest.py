@@ -52,6 +52,8 @@ def olib(oracle_path):
         "ops_duplicate": (None, [P, i64, i32, i32, i64]), "ops_reject": (None, [P, i64, i32, i32, i32, i64]),
         "ops_gc": (None, [P, i64]), "ops_expire_head": (None, [P, i64]),
         "ops_topic_stats": (C.c_int, [P, i32, i32, C.POINTER(f64)]),
+        "ops_set_stats": (None, [P, i32, i32, i32, i64, i64, f64, f64, f64, f64]),
+        "ops_set_behaviour_penalty": (None, [P, i32, f64]),
         "omc_new": (P, [i32, i32]), "omc_free": (None, [P]), "omc_put": (None, [P, i64, i32]),
         "omc_get": (C.c_int, [P, i64]), "omc_get_for_peer": (C.c_int, [P, i64, i32]),
         "omc_gossip_ids": (C.c_int, [P, i32, C.POINTER(i64), i32]), "omc_len": (C.c_int, [P]),

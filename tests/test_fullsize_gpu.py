@@ -1,0 +1,128 @@
+"""The benchmarked configurations at their BASELINE.json sizes, on the GPU.
+
+The oracle cannot simulate 1M peers in a test's time, so these runs are checked
+by what holds at any size, plus a true oracle check of score():
+  * every subscriber gets every message exactly once (deliveries =
+    published x (N - 1) once the schedule has drained; the seen set makes a
+    second first delivery impossible);
+  * every copy on the wire is a delivery or a duplicate (deliveries +
+    duplicates = transmissions, nothing graylisted in these honest runs);
+  * no device error (a capacity or model error raises in step());
+  * score() of a few thousand sampled edges, recomputed by the oracle's own
+    PeerScore from the engine's counters (tests/score_check.py, pinned on
+    the oracle by tests/test_score_check.py), equals gs_read_scores bit for
+    bit: a21 at E x T = 2.05e9 (edge, topic) pairs;
+  * router-specific closed forms (floodsub / randomsub transmissions).
+The engines are built by bench.build_engine, i.e. exactly the benchmarked
+workload (graph, schedule, params), with the schedule cut to a few rounds."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+import bench  # noqa: E402
+from score_check import oracle_scores, sample_edges  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+H = bench.HOPS_PER_ROUND
+
+
+def _drain_and_check(e, rounds, extra_hops):
+    """Join + `rounds` rounds of publishes + extra hops; the common properties."""
+    e.step(1 + rounds * H + extra_hops)
+    c = e.counters()
+    published = rounds * bench.MSGS_PER_ROUND
+    assert c["published"] == published
+    assert c["deliveries"] == published * (e.N - 1), c
+    assert c["graylisted"] == 0, c
+    assert c["deliveries"] + c["duplicates"] == c["transmissions"], c
+    return c
+
+
+def _score_check(olib, e, n=3000, seed=7):
+    edges = sample_edges(e.E, n, seed, must=[0, e.E - 1])
+    got, st = oracle_scores(olib, e.score_params, e, edges)
+    want = e.scores()[edges]
+    bad = np.flatnonzero(got.view(np.uint64) != want.view(np.uint64))
+    assert len(bad) == 0, f"{len(bad)} of {len(edges)} scores differ, first edge {edges[bad[0]]}: " \
+                          f"engine {want[bad[0]]!r} oracle {got[bad[0]]!r}"
+    # the sample is not trivial: mesh members with time in mesh and deliveries
+    assert (st["flags"] & 1).mean() > 0.05, (st["flags"] & 1).mean()
+    assert (st["fmd"] > 0).mean() > 0.05 and (st["mesh_time"] > 0).any()
+    return got
+
+
+def test_config4_full_size(olib):
+    """BASELINE configs[3] on one GPU: 1M peers, k = 32, 64 topics, Eth2
+    scoring, 1000 msgs/round; 2 rounds of publishes after Join, drained."""
+    wl = bench.WORKLOADS["config4"]
+    e, g = bench.build_engine(wl, 2, 3, 0)
+    _drain_and_check(e, 2, 3 * H)
+    scores = _score_check(olib, e)
+    assert np.isfinite(scores).all()
+    mesh = e.mesh()
+    sizes = np.add.reduceat(np.bitwise_count(mesh).astype(np.int64), g[0][:-1]) / wl["topics"]
+    from pubsub_amd.params import GossipSubParams
+    gp = GossipSubParams()
+    assert gp.Dlo <= np.median(sizes) <= gp.Dhi, np.median(sizes)  # meshes maintained per (node, topic)
+
+
+def test_config3_full_size_with_ihave_cuts(olib):
+    """BASELINE configs[2]: 1M peers, one topic x 10048 slots, 1000 msgs per
+    heartbeat.  Nine rounds of publishes reach the steady state in which a
+    gossip window holds more ids than MaxIHaveLength (5000): phase B runs
+    its cut instantiation and the receivers take the senders' keyed subsets
+    (gossipsub.go:650-653, 1702-1709)."""
+    wl = bench.WORKLOADS["config3"]
+    rounds = 9
+    e, _ = bench.build_engine(wl, rounds, 3, 0)
+    # the engine's cut-mode bound (gs_engine.hip stepOne): messages published
+    # within HistoryGossip + 1 heartbeats plus the delivery age bound
+    per_hop = bench.MSGS_PER_ROUND // H
+    window = (5 + 1) * H + 3 * H + 2
+    assert per_hop * window > 5000
+    # the gossip windows (5 heartbeats of mcache) hold ~5000 ids plus the late
+    # ones: real cuts from round ~7
+    c = _drain_and_check(e, rounds, 3 * H)
+    assert c["ihave_sent"] > 0 and c["iwant_sent"] > 0
+    _score_check(olib, e)
+
+
+@pytest.mark.parametrize("size", ["100", "N"])
+def test_config2_randomsub_100k(size):
+    """BASELINE configs[1], the randomsub leg: 100k peers, random 32-regular
+    graph, 1 topic, 10,000 messages at hop 0.  size = 100 samples
+    max(6, ceil(sqrt(100))) = 10 targets per forward (randomsub.go:115-149);
+    size = N degenerates to floodsub (every candidate)."""
+    from pubsub_amd import NewRandomSub, WithMessageWindow, WithSeed, graphs
+    n, k, m = 100_000, 32, 10_000
+    rowptr, col, outbound = graphs.random_regular_fast(n, k, 2)
+    deg = np.diff(rowptr)
+    assert deg.min() >= 12  # every holder has more than 10 candidates
+    rs = 100 if size == "100" else n
+    e = NewRandomSub(n, 1, (rowptr, col, outbound), graphs.all_subscribed(n, 1), rs, WithSeed(2),
+                     WithMessageWindow(10_048))
+    rng = np.random.default_rng(2)
+    e.publish(rng.integers(0, n, m).astype(np.int32), np.zeros(m, np.int32), np.zeros(m, np.int64))
+    e.step(40)
+    c = e.counters()
+    assert c["published"] == m
+    assert c["duplicates"] == c["transmissions"] - c["deliveries"]
+    if size == "N":
+        # floodsub's closed form (tests/test_scale_gpu.py)
+        assert c["deliveries"] == m * (n - 1)
+        assert c["transmissions"] == m * (int(deg.sum()) - (n - 1))
+    else:
+        # every holder (the author, then every first receiver) sends exactly
+        # 10 copies: its candidates (all but the sender and the author) number
+        # at least deg - 2 > 10, and the keyed shuffle takes 10 of them
+        assert c["transmissions"] == 10 * (m + c["deliveries"])
+        # a node is missed only if none of its ~32 holders picked it
+        assert c["deliveries"] > 0.999 * m * (n - 1)
+        assert c["deliveries"] <= m * (n - 1)

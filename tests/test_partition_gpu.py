@@ -117,6 +117,60 @@ def test_partitioned_engine_matches_oracle(world, name, oracle_path):
     assert not bad, "\n".join(bad)
 
 
+def _err_worker(rank, world, port, q):
+    """Rank 0 traces node 0 with a 16-event buffer, so its device error word
+    gets E_TRACE within a few hops; rank 1 has no device error of its own."""
+    try:
+        sys.path.insert(0, HERE)
+        sys.path.insert(0, os.path.join(os.path.dirname(HERE), "go-libp2p-pubsub_amd"))
+        import torch
+        import torch.distributed as dist
+
+        import scenarios
+        from pubsub_amd import PRODUCT_LIB, GossipEngineError, WithEventTracer, WithPartition, _abi
+        from pubsub_amd.transport import TorchTransport
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        tr = TorchTransport(memory="device")
+        e, hops = scenarios.SCENARIOS["gossipsub_scored"](
+            PRODUCT_LIB, (WithPartition(rank, world, tr), WithEventTracer([0], capacity=16)))
+        try:
+            e.step(hops)
+            q.put((rank, None, e.hop))
+        except GossipEngineError as ex:
+            q.put((rank, (ex.code, str(ex)), e.hop))
+        dist.destroy_process_group()
+        del _abi
+    except Exception as ex:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, ("raised", f"{ex!r}\n{traceback.format_exc()}"), -1))
+
+
+@pytest.mark.gpu
+def test_partitioned_device_error_stops_every_rank():
+    """A device error on one rank: every rank returns it at the
+    same hop instead of the healthy ranks waiting in the next exchange."""
+    from pubsub_amd import _abi
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_err_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted((q.get(timeout=180) for _ in range(world)), key=lambda r: r[0])
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    assert all(r[1] is not None for r in res), res
+    assert all(r[1][0] == _abi.GS_ECAPACITY for r in res), res
+    assert res[0][2] == res[1][2], res            # both stopped at the same hop
+    assert "rank 0" in res[1][1][1], res          # rank 1 names the failing rank
+
+
 class _NoTransport:
     """gs_transport whose callbacks fail (never reached in this test)."""
 

@@ -225,6 +225,19 @@ def test_gpu_trace_equals_oracle(oracle_path, name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["gossipsub_scored", "churn_scored"])
+def test_gpu_trace_repeatable(oracle_path, name):
+    """traced_run drains between steps: the device's event counter is reset on
+    the engine's stream before the next hop appends (gs_engine.hip drainTrace).
+    Three more runs must each reproduce the oracle's stream."""
+    nodes = TRACED
+    _, ref = traced_run(oracle_path, name, nodes)
+    for _ in range(3):
+        _, got = traced_run(PRODUCT_LIB, name, nodes)
+        assert len(got) == len(ref) and not np.any(got != ref)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", ["churn_scored", "churn_prune", "churn_graft"])
 def test_gpu_trace_equals_oracle_churn(oracle_path, name):
     """RemovePeer / AddPeer / Leave / Join events of the churn scenarios
