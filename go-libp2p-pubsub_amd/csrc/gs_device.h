@@ -46,6 +46,9 @@
 #define GS_OCC_PB
 #endif
 #define GS_MAX_WPL 4   // words per lane in the node-wave kernels: W <= 256
+#ifndef GS_SBATCH
+#define GS_SBATCH 2    // edge_scores_batch: edges whose loads are in flight together (<= 4)
+#endif
 #define GS_QCAP 320    // phase A delivery queue (>= 63 pending + 256 appended per sub-round)
 #define GS_BMAP 32     // phase A: list blocks mapped to senders without a search (64 per entry)
 #define GS_TABLE 64    // promise table entries per node (one per lane)
@@ -507,6 +510,59 @@ __device__ __forceinline__ double edge_score_wave(const Dev& d, int64_t e, doubl
   for (int t = 0; t < d.T; ++t)
     if ((scoredT >> t) & 1) score += lds[t];
   return has_record(d, e) ? score_tail_v(d, score, app, p6, b) : 0.0;
+}
+
+// edge_score_wave for every edge rowBase + j with bit j of `mask` (wave-
+// uniform): GS_SBATCH edges per pass with all their loads in flight at once (lane
+// = topic), instead of one memory round trip per edge.  Lane j receives its
+// edge's score in S; other lanes keep theirs.  lds: 4 * 64 doubles.
+__device__ __forceinline__ void edge_scores_batch(const Dev& d, int64_t rowBase, unsigned long long mask, double& S,
+                                                  double* lds) {
+  const int lane = lane_id();
+  const bool mine = (mask >> lane) & 1;
+  if (!d.scoring) {
+    if (mine) S = 0.0;
+    return;
+  }
+  const int T = d.T;
+  const int tl = lane < T ? lane : 0;
+  const bool sc = lane < T && d.tp[tl].scored;
+  const uint64_t scoredT = __ballot(sc);
+  double app = 0.0, p6 = 0.0, b = 0.0;
+  bool rec = false;
+  if (mine) {  // the tail inputs of the lane's own edge
+    const int64_t e = rowBase + lane;
+    app = d.app[d.col[e]];
+    p6 = d.p6[e];
+    b = d.bp[e];
+    rec = has_record(d, e);
+  }
+  while (mask) {
+    int js[GS_SBATCH];
+#pragma unroll
+    for (int k = 0; k < GS_SBATCH; ++k) {
+      js[k] = mask ? __ffsll((long long)mask) - 1 : -1;
+      mask &= mask ? mask - 1 : 0ull;
+    }
+    TermIn x[GS_SBATCH];
+#pragma unroll
+    for (int k = 0; k < GS_SBATCH; ++k) x[k] = term_load(d, tix(d, tl, rowBase + (js[k] < 0 ? js[0] : js[k])));
+    __syncthreads();  // the previous pass's sums are done with lds
+#pragma unroll
+    for (int k = 0; k < GS_SBATCH; ++k) lds[k * 64 + lane] = (js[k] >= 0 && sc) ? term_eval(d.tp[tl], x[k]) : 0.0;
+    __syncthreads();
+    int kb = -1;
+#pragma unroll
+    for (int k = 0; k < GS_SBATCH; ++k)
+      if (lane == js[k]) kb = k;
+    if (kb >= 0) {
+      double score = 0.0;
+      for (int t = 0; t < T; ++t)
+        if ((scoredT >> t) & 1) score += lds[kb * 64 + t];
+      S = rec ? score_tail_v(d, score, app, p6, b) : 0.0;
+    }
+  }
+  __syncthreads();
 }
 
 // peerScore.Graft — score.go:640-658 (scored topics only)

@@ -599,7 +599,7 @@ int gs_engine::start() {
     }
   }
 #ifdef GS_STAMPS
-  x.stamps = dalloc<unsigned long long>((size_t)(N / 1024 + 1) * 16);  // phase A | phase B
+  x.stamps = dalloc<unsigned long long>((size_t)(N / 1024 + 1) * 24);  // phase A | phase B | heartbeat
 #endif
   x.pad = dalloc<double>(256 * 64 * 2); chk(x.pad);
   x.ctr = dalloc<unsigned long long>((size_t)C_NCOUNTERS * GS_CTR_SPREAD); x.err = dalloc<int32_t>(1);

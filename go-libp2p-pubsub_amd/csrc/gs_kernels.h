@@ -523,7 +523,18 @@ __device__ __forceinline__ int wave_min_int(int x) {
     if ((blockIdx.x & 1023) == 0 && lane == 0)                                                 \
       d.stamps[((int64_t)d.N / 1024 + 1) * 8 + (blockIdx.x >> 10) * 8 + (k)] = clock64();      \
   } while (0)
+// heartbeat: stamp k = value v (a clock or an accumulated cycle count)
+#define GS_STAMPH(k, v)                                                                        \
+  do {                                                                                         \
+    if ((blockIdx.x & 1023) == 0 && lane == 0)                                                 \
+      d.stamps[((int64_t)d.N / 1024 + 1) * 16 + (blockIdx.x >> 10) * 8 + (k)] = (v);           \
+  } while (0)
+#define GS_CLK() clock64()
 #else
+#define GS_STAMPH(k, v) \
+  do {                  \
+  } while (0)
+#define GS_CLK() 0ull
 #define GS_STAMP(k) \
   do {              \
   } while (0)

@@ -1005,7 +1005,7 @@ __device__ __forceinline__ uint64_t emit_gossip(const Dev& d, int v, int t, int6
   // is switched off; weights validated w1 >= 0, w3 <= 0), so a cached score
   // already at or above the threshold stays a correct decision after one.
   unsigned long long dm = __ballot(base && (dirty || (dirtyUp && !(Slive >= d.gossipThr))));
-  while (dm) {
+  while (dm) {  // rare (a peer pruned earlier in this heartbeat): one edge at a time
     const int j = __ffsll((long long)dm) - 1;
     dm &= dm - 1;
     const double s = edge_score_wave(d, rowBase + j, lds);
@@ -1048,15 +1048,39 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
   const bool valid = lane < deg;
   const int64_t e = base + lane;
   const int vcol = valid ? d.col[e] : -1;
+  GS_STAMPH(0, GS_CLK());
   // mcache.GetGossipIDs windows 0..HG-1 (mcache.go:82-92): this heartbeat's
   // IHAVE payload, kept as the node's gw row for the receivers' handleIHave
-  for (int w = lane; w < d.W; w += 64) {
-    uint64_t x = 0;
-    for (int k = 0; k < d.HG; ++k) x |= d.hist[((int64_t)((head + k) % d.R) * d.N + v) * d.W + w];
-    sgw[w] = x;
-    d.gw[(int64_t)v * d.W + w] = x;
+  {
+    // windows in pairs, the pair's 2 x GS_MAX_WPL loads in flight at once
+    uint64_t x[GS_MAX_WPL] = {};
+    for (int k0 = 0; k0 < d.HG; k0 += 2) {
+      uint64_t y[2][GS_MAX_WPL];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const uint64_t* src = d.hist + ((int64_t)((head + k0 + k) % d.R) * d.N + v) * d.W;
+#pragma unroll
+        for (int j = 0; j < GS_MAX_WPL; ++j) {
+          const int w = lane + 64 * j;
+          y[k][j] = (k0 + k < d.HG && w < d.W) ? src[w] : 0ull;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int j = 0; j < GS_MAX_WPL; ++j) x[j] |= y[k][j];
+    }
+#pragma unroll
+    for (int j = 0; j < GS_MAX_WPL; ++j) {
+      const int w = lane + 64 * j;
+      if (w < d.W) {
+        sgw[w] = x[j];
+        d.gw[(int64_t)v * d.W + w] = x[j];
+      }
+    }
   }
   __syncthreads();
+  GS_STAMPH(1, GS_CLK());
   // lane t: message ids of topic t in the gossip windows (emitGossip's mids)
   int nmT = 0;
   if (lane < d.T)
@@ -1078,14 +1102,11 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
       if (__popcll(__ballot(mt)) > d.Dhi) needX |= mt;
     }
     const bool exact = valid && (d.sdirty[e] != 0 || !(d.score0[e] >= 0.0));
-    unsigned long long xm = __ballot(needX && !exact);
-    while (xm) {
-      const int j = __ffsll((long long)xm) - 1;
-      xm &= xm - 1;
-      const double sj = edge_score_wave(d, base + j, sterm);
-      if (lane == j) S = sj;
-    }
+    __syncthreads();  // sgw (read for nmT above) becomes the batch's term table
+    edge_scores_batch(d, base, __ballot(needX && !exact), S, (double*)sgw);
   }
+  GS_STAMPH(2, GS_CLK());
+  unsigned long long cyMesh = 0, cyEmit = 0;  // GS_STAMPS: cycles in mesh maintenance / emitGossip
   double Slive = S;  // live Score(p) for emitGossip
   const bool dir = valid && d.direct[e];
   const bool ob = valid && d.outbound[e];
@@ -1097,6 +1118,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
   uint64_t spamGraft = 0;  // GRAFTs without a mesh change (not traced as Graft)
   for (int t = 0; t < d.T; ++t) {
     if (!((joined >> t) & 1)) continue;
+    const unsigned long long c0 = GS_CLK();
     const uint64_t bit = 1ull << t;
     const bool inTopic = valid && ((subv >> t) & 1);
     bool m = valid && (meshl & bit);
@@ -1241,18 +1263,24 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
       const int64_t be = d.backoff[tix(d, t, e)];
       if (be != 0 && be > now) spamGraft |= bit;
     }
-    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, m, dir, Slive, dirty, dirtyUp, base, sterm,
+    const unsigned long long c1 = GS_CLK();
+    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, m, dir, Slive, dirty, dirtyUp, base, (double*)sgw,
                          lane_get(nmT, t));
+    cyMesh += c1 - c0;
+    cyEmit += GS_CLK() - c1;
   }
+  GS_STAMPH(3, GS_CLK());
+  GS_STAMPH(6, cyMesh);
+  GS_STAMPH(7, cyEmit);
   // expire fanout for topics we haven't published to in a while
   uint64_t fpres = d.fanoutPresent[v];
-  for (int t = 0; t < d.T; ++t) {
-    const int64_t lp = d.lastpub[(int64_t)v * d.T + t];
-    if (lp != INT64_MIN && lp + d.FanoutTTL < now) {
-      fpres &= ~(1ull << t);
-      fanl &= ~(1ull << t);
-      if (lane == 0) d.lastpub[(int64_t)v * d.T + t] = INT64_MIN;
-    }
+  {
+    const int64_t lp = lane < d.T ? d.lastpub[(int64_t)v * d.T + lane] : INT64_MIN;  // lane = topic
+    const bool expired = lp != INT64_MIN && lp + d.FanoutTTL < now;
+    const uint64_t xm = __ballot(expired);
+    fpres &= ~xm;
+    fanl &= ~xm;
+    if (expired) d.lastpub[(int64_t)v * d.T + lane] = INT64_MIN;
   }
   // maintain our fanout for topics we are publishing but have not joined
   for (int t = 0; t < d.T; ++t) {
@@ -1273,9 +1301,10 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
         f = true;
       }
     }
-    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, f, dir, Slive, dirty, dirtyUp, base, sterm,
+    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, f, dir, Slive, dirty, dirtyUp, base, (double*)sgw,
                          lane_get(nmT, t));
   }
+  GS_STAMPH(4, GS_CLK());
   // sendGraftPrune + flush: one heartbeat RPC per peer with any control
   if (valid && is_traced(d, v)) {  // prunePeer / graftPeer, gossipsub.go:1334, 1343
     for (uint64_t m = toprune; m; m &= m - 1) trace_emit(d, hop, GS_TRACE_PRUNE, v, vcol, __ffsll((long long)m) - 1, -1, 4);
@@ -1345,6 +1374,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
     if (lane == 0) d.ptxN[v] = kept;
   }
   for (int w = lane; w < d.W; w += 64) d.hist[((int64_t)newhead * d.N + v) * d.W + w] = 0;
+  GS_STAMPH(5, GS_CLK());
 }
 
 // gs_read_deliveries gather

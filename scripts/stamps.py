@@ -20,11 +20,14 @@ def main():
     hops = int(sys.argv[2]) if len(sys.argv) > 2 else 1 + 2 * bench.HOPS_PER_ROUND + 3
     eng.step(hops)
     raw = C.CDLL(LIB)
-    n = (eng.N // 1024 + 1) * 16
+    n = (eng.N // 1024 + 1) * 24
     buf = np.zeros(n, dtype=np.uint64)
     raw.gs_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]
     rc = raw.gs_debug_stamps(eng.h, buf.ctypes.data_as(C.POINTER(C.c_uint64)), n)
     assert rc == 0
+    K = eng.N // 1024 + 1
+    hbbuf = buf[16 * K:]
+    buf = buf[:16 * K]
     s = buf.reshape(-1, 8)[: len(buf) // 16, :5].astype(np.int64)
     s = s[(s[:, 0] > 0) & (s[:, 4] > 0)]
     d = np.diff(s, axis=1)
@@ -40,6 +43,14 @@ def main():
     c = buf.reshape(-1, 8)[: len(buf) // 16, 5:8].astype(np.int64)
     print("copies/node mean", c[:, 0].mean(), "pass-1 list-load cycles mean", c[:, 1].mean(), "pass-1 delivery-drain cycles mean",
           c[:, 2].mean())
+    hb = hbbuf.reshape(-1, 8).astype(np.int64)
+    hb = hb[(hb[:, 0] > 0) & (hb[:, 5] > 0)]
+    if len(hb):
+        dh = np.diff(hb[:, :6], axis=1)
+        print("heartbeat samples", len(hb))
+        for i, nm in enumerate(["gw windows", "exact scores", "topic loop", "fanout", "outbox + shift"]):
+            print(f"  {nm}: mean {dh[:, i].mean():.0f} cycles  p50 {np.median(dh[:, i]):.0f}  p99 {np.percentile(dh[:, i], 99):.0f}")
+        print(f"  topic loop split: mesh maintenance {hb[:, 6].mean():.0f}, emitGossip {hb[:, 7].mean():.0f}")
     bb = buf.reshape(-1, 8)[len(buf) // 16:].astype(np.int64)
     bb = bb[(bb[:, 0] > 0) & (bb[:, 4] > 0)]
     b = bb[:, :5]
