@@ -663,10 +663,8 @@ int gs_engine::start() {
   x.rpcB = x.rpcN = nullptr;
   x.acc = nullptr;
   if (acctOn) {
-    if (world > 1) {
-      gs_set_error("RPC byte accounting needs an unpartitioned engine");
-      return GS_EUNSUPPORTED;
-    }
+    // partitioned: every RPC is counted by its sender's rank, on the sender's
+    // (owned) edge; gs_read_rpc_bytes returns the owned edges
     x.rpcB = dalloc<unsigned long long>(E); x.rpcN = dalloc<unsigned long long>(E);
     AcctT* ac = dalloc<AcctT>(T);
     chk(x.rpcB); chk(x.rpcN); chk(ac);
@@ -697,6 +695,15 @@ int gs_engine::start() {
 // host-side RPCs of this hop (hello packets, subscription announcements): one
 // (edge, bytes) pair each, added on the device
 int gs_engine::flushAcct() {
+  if (world > 1) {  // a partitioned rank counts what its own nodes send
+    size_t k = 0;
+    for (size_t i = 0; i + 1 < acctPend.size(); i += 2)
+      if (acctPend[i] >= e0 && acctPend[i] < e1) {
+        acctPend[k++] = acctPend[i];
+        acctPend[k++] = acctPend[i + 1];
+      }
+    acctPend.resize(k);
+  }
   if (acctPend.empty()) return GS_OK;
   if ((int64_t)acctPend.size() > acctPendCap) {
     int64_t* p = nullptr;
@@ -830,8 +837,12 @@ int gs_engine::applyEvents(int64_t h) {
         if (aliveH[ab] == want) continue;
         aliveH[ab] = aliveH[ba] = want;
         auto& lst = pass == GS_EV_CONNECT ? up : down;
-        lst.push_back((int32_t)ab);
-        lst.push_back((int32_t)ba);
+        // a partitioned rank launches the pairs with a side it owns (the
+        // kernels do only that side)
+        if (world == 1 || (ab >= e0 && ab < e1) || (ba >= e0 && ba < e1)) {
+          lst.push_back((int32_t)ab);
+          lst.push_back((int32_t)ba);
+        }
         if (acctOn && want) {  // hello packets both ways (pubsub.go:534)
           acctPend.insert(acctPend.end(), {ab, helloBytes(sub[ev.a]), ba, helloBytes(sub[ev.b])});
         }
@@ -850,9 +861,11 @@ int gs_engine::applyEvents(int64_t h) {
     }
   nextEv = end;
   // one item per node: node, topic mask (lo, hi) — its topics run in one wave
+  // (a partitioned rank: its own nodes)
   for (auto* pr : {&leaveM, &joinM}) {
     auto& lst = pr == &leaveM ? leave : join;
     for (auto& kv : *pr) {
+      if (kv.first < n0 || kv.first >= n1) continue;
       lst.push_back(kv.first);
       lst.push_back((int32_t)(uint32_t)kv.second);
       lst.push_back((int32_t)(uint32_t)(kv.second >> 32));
@@ -1100,9 +1113,13 @@ int gs_engine::stepOne() {
       allExact = 0;
     }
     const int newhead = (head + R - 1) % R;
-    if (nOwn)
+    // nodes of degree <= 32: two topics per wave (one per half-wave)
+    if (nOwn && d.maxDeg <= 32)
       TIMED(this, GS_K_HEARTBEAT,
-            (k_heartbeat<<<nOwn, 64, 0, stream>>>(d, h, now, ticks, cur, head, newhead, allExact)));
+            (k_heartbeat<true><<<nOwn, 64, 0, stream>>>(d, h, now, ticks, cur, head, newhead, allExact)));
+    else if (nOwn)
+      TIMED(this, GS_K_HEARTBEAT,
+            (k_heartbeat<false><<<nOwn, 64, 0, stream>>>(d, h, now, ticks, cur, head, newhead, allExact)));
     head = newhead;
     heartbeats++;
   }
@@ -1781,8 +1798,9 @@ int gs_read_rpc_bytes(gs_engine* g, int64_t* bytes, int64_t* rpcs) {
   HIPCHECK(hipMemcpy(b.data(), g->d.rpcB, (size_t)E * 8, hipMemcpyDeviceToHost));
   HIPCHECK(hipMemcpy(n.data(), g->d.rpcN, (size_t)E * 8, hipMemcpyDeviceToHost));
   for (int64_t e = 0; e < E; ++e) {
-    if (bytes) bytes[e] = (int64_t)b[e];
-    if (rpcs) rpcs[e] = (int64_t)n[e];
+    const bool own = e >= g->e0 && e < g->e1;  // a partitioned rank reports its own edges
+    if (bytes) bytes[e] = own ? (int64_t)b[e] : 0;
+    if (rpcs) rpcs[e] = own ? (int64_t)n[e] : 0;
   }
   return GS_OK;
 }

@@ -1580,7 +1580,8 @@ __global__ __launch_bounds__(64) void k_acct_payload(Dev d, int p) {
   const uint64_t ru = valid ? d.fwdRelay[p][e] : 0, pu = valid ? d.fwdPub[p][e] : 0;
   if (!__ballot((ru | pu) != 0)) return;
   const int w = valid ? d.col[e] : 0;
-  const bool authW = valid && d.nAuth[w] > 0;  // the receiver authored a live message
+  // the receiver authored a live message (nAuth is kept for owned nodes only)
+  const bool authW = valid && (d.world > 1 || d.nAuth[w] > 0);
   const int Ln = d.fln[p][u];
   const uint32_t* L = d.fl[p] + (int64_t)u * d.FC;
   unsigned long long b = 0, n = 0;

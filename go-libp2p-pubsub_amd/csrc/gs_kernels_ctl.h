@@ -1028,12 +1028,304 @@ __device__ __forceinline__ uint64_t emit_gossip(const Dev& d, int v, int t, int6
   return sel ? (1ull << t) : 0;
 }
 
+// select_k per half-wave: each half (lanes 0..31, 32..63) selects its own k
+// (a lane-varying value, uniform within the half) of its own candidates; the
+// same radix selection and the same "lowest lanes first" tie rule as select_k.
+// Works under divergence: a half that is not executing contributes nothing.
+__device__ __forceinline__ bool select_k_half(bool cand, uint64_t key, int k) {
+  const int lane = lane_id();
+  const int sh = lane & 32, bl = lane & 31;
+  uint32_t act = (uint32_t)(__ballot(cand) >> sh);
+  int n = __popc(act);
+  if (k <= 0 || n <= k) return cand;
+  uint32_t sel = 0;
+  int need = k;
+  for (int b = 63; b >= 0; --b) {
+    const uint32_t z = (uint32_t)(__ballot(((act >> bl) & 1) && !((key >> b) & 1)) >> sh);
+    const int nz = __popc(z);
+    if (nz <= need) {
+      sel |= z;
+      need -= nz;
+      act &= ~z;
+      n -= nz;
+    } else {
+      act = z;
+      n = nz;
+    }
+    if (need == 0) break;
+    if (n == need) {
+      sel |= act;
+      need = 0;
+      break;
+    }
+  }
+  while (need > 0 && act) {
+    sel |= act & (~act + 1);
+    act &= act - 1;
+    need--;
+  }
+  return (sel >> bl) & 1;
+}
+// number of lanes of this lane's half with x set
+__device__ __forceinline__ int half_count(bool x) {
+  const unsigned long long b = __ballot(x);
+  return __popc((uint32_t)(b >> (lane_id() & 32)));
+}
+
+// The joined-topic loop of k_heartbeat<true>: pairs of joined topics (ta, tb)
+// ascending, half h = lane >> 5 handles topic (ta, tb)[h] of every edge (lane
+// & 31).  Per pair:
+//   1. mesh maintenance decisions of both topics (they read the heartbeat memo
+//      S and the topic's own mesh / backoff bits only, so the two topics are
+//      independent): negative-score prune, Dlo graft, Dhi prune (serially per
+//      half: it ranks by value through LDS), Dout graft, opportunistic graft;
+//   2. ta's stats writes (peerScore.Prune / Graft, backoff), then emitGossip's
+//      live-score refresh for ta's candidates; tb's writes, then tb's refresh
+//      starting from ta's live-score state — the serial topic order, so every
+//      live score emitGossip compares equals the serial loop's;
+//   3. both topics' IHAVE peer selections (key draw + select) at once.
+__device__ __forceinline__ void hb_pair(const Dev& d, int v, int64_t base, int deg, bool vm, int64_t e, int vcol,
+                                        int64_t hop, int64_t now, uint64_t ticks, int head, uint64_t joined,
+                                        uint64_t subv, double S, bool dir, bool ob, bool graftSpam, int nmT,
+                                        uint64_t& meshl, uint64_t& boM, double& Slive, bool& dirty, bool& dirtyUp,
+                                        uint64_t& tograft, uint64_t& toprune, uint64_t& ihave, uint64_t& spamGraft,
+                                        int* plst, int* obs, int* posOf, double* lds, unsigned long long& cyMesh,
+                                        unsigned long long& cyEmit, unsigned long long& cySel) {
+  const int lane = lane_id();
+  const int h = lane >> 5;
+  const uint32_t hw = (uint32_t)hop;
+  const bool noFwd = behaves(d, v, GS_BEHAVE_NO_FORWARD);
+  const bool ihaveSpam = behaves(d, v, GS_BEHAVE_IHAVE_SPAM);
+  const bool oppTick = ticks % d.OGT == 0;
+  uint64_t jm = joined;
+  while (jm) {
+    const unsigned long long c0 = GS_CLK();
+    const int ta = __ffsll((long long)jm) - 1;
+    jm &= jm - 1;
+    const int tb = jm ? __ffsll((long long)jm) - 1 : -1;
+    if (jm) jm &= jm - 1;
+    const int t = h ? tb : ta;  // this half's topic, -1: none
+    const bool act = t >= 0;
+    const int tt = act ? t : 0;
+    const uint64_t bit = act ? 1ull << t : 0ull;
+    const bool inTopic = vm && act && ((subv >> tt) & 1);
+    bool m = vm && act && (meshl & bit);
+    bool pr = false, gr = false;  // pruned / grafted at t in this pass
+    // ---- 1. decisions
+    if (m && (S < 0 || (graftSpam && ticks == 1))) {
+      pr = true;
+      m = false;
+    }
+    bool bo = (boM & bit) != 0 || pr;  // a prune adds backoff
+    int cnt = half_count(m);
+    if (cnt < d.Dlo) {
+      const bool cand = inTopic && !m && !bo && !dir && S >= 0;
+      const uint64_t key = gs_key64(d.seed, GS_SITE_GP_DLO, v, hw, vcol, tt);
+      if (select_k_half(cand, key, d.D - cnt)) {
+        gr = true;
+        m = true;
+      }
+      cnt = half_count(m);
+    }
+    // too many peers: ranked by value through LDS, one half at a time
+    const int cntA = lane_get(cnt, 0), cntB = lane_get(cnt, 32);
+    for (int hh = 0; hh < 2; ++hh) {
+      if ((hh ? cntB : cntA) <= d.Dhi) continue;
+      const int cnth = hh ? cntB : cntA;
+      const bool mh = m && h == hh;
+      const uint64_t k1 = gs_key64(d.seed, GS_SITE_DHI_SHUFFLE, v, hw, vcol, tt);
+      int rank1 = 0;
+      unsigned long long mm = __ballot(mh);
+      while (mm) {
+        const int j = __ffsll((long long)mm) - 1;
+        mm &= mm - 1;
+        const double sj = lane_getf(S, j);
+        const uint64_t kj = lane_get64(k1, j);
+        if (sj > S || (sj == S && (kj < k1 || (kj == k1 && j < lane)))) rank1++;
+      }
+      const bool tail = mh && rank1 >= d.Dscore;
+      const uint64_t k2 = gs_key64(d.seed, GS_SITE_DHI_TAIL, v, hw, vcol, tt);
+      int rank2 = 0;
+      mm = __ballot(tail);
+      while (mm) {
+        const int j = __ffsll((long long)mm) - 1;
+        mm &= mm - 1;
+        const uint64_t kj = lane_get64(k2, j);
+        if (kj < k2 || (kj == k2 && j < lane)) rank2++;
+      }
+      const int pos = tail ? d.Dscore + rank2 : rank1;
+      if (mh) plst[pos] = lane;
+      obs[lane] = ob ? 1 : 0;
+      __syncthreads();
+      if (lane == 0) {
+        // keep D_out outbound peers among the first D (gossipsub.go:1389-1429)
+        int outbound = 0;
+        for (int i = 0; i < d.D; ++i) outbound += obs[plst[i]];
+        if (outbound < d.Dout) {
+          if (outbound > 0) {
+            int ih = outbound;
+            for (int i = 1; i < d.D && ih > 0; ++i) {
+              if (obs[plst[i]]) {
+                const int p = plst[i];
+                for (int j = i; j > 0; --j) plst[j] = plst[j - 1];
+                plst[0] = p;
+                ih--;
+              }
+            }
+          }
+          int ineed = d.Dout - outbound;
+          for (int i = d.D; i < cnth && ineed > 0; ++i) {
+            if (obs[plst[i]]) {
+              const int p = plst[i];
+              for (int j = i; j > 0; --j) plst[j] = plst[j - 1];
+              plst[0] = p;
+              ineed--;
+            }
+          }
+        }
+        for (int i = 0; i < cnth; ++i) posOf[plst[i]] = i;
+      }
+      __syncthreads();
+      if (mh && posOf[lane] >= d.D) {
+        pr = true;
+        bo = true;
+        m = false;
+      }
+      __syncthreads();
+    }
+    cnt = half_count(m);
+    // do we have enough outbound peers?
+    if (cnt >= d.Dlo) {
+      const int outb = half_count(m && ob);
+      if (outb < d.Dout) {
+        const bool cand = inTopic && !m && !bo && !dir && ob && S >= 0;
+        const uint64_t key = gs_key64(d.seed, GS_SITE_GP_DOUT, v, hw, vcol, tt);
+        if (select_k_half(cand, key, d.Dout - outb)) {
+          gr = true;
+          m = true;
+        }
+        cnt = half_count(m);
+      }
+    }
+    // opportunistic grafting (median of the memoised mesh scores), one half at a time
+    if (oppTick) {
+      const int ca = lane_get(cnt, 0), cb = lane_get(cnt, 32);
+      for (int hh = 0; hh < 2; ++hh) {
+        const int cnth = hh ? cb : ca;
+        if (cnth <= 1) continue;
+        const bool mh = m && h == hh;
+        int rank = 0;
+        unsigned long long mm = __ballot(mh);
+        while (mm) {
+          const int j = __ffsll((long long)mm) - 1;
+          mm &= mm - 1;
+          const double sj = lane_getf(S, j);
+          if (sj < S || (sj == S && j < lane)) rank++;
+        }
+        const unsigned long long ml = __ballot(mh && rank == cnth / 2);
+        const double median = lane_getf(S, __ffsll((long long)ml) - 1);
+        if (median < d.oppThr) {
+          const bool cand = h == hh && inTopic && !m && !bo && !dir && S > median;
+          const uint64_t key = gs_key64(d.seed, GS_SITE_GP_OPPORTUNISTIC, v, hw, vcol, tt);
+          if (select_k_half(cand, key, d.OGP)) {
+            gr = true;
+            m = true;
+          }
+        }
+      }
+    }
+    // a GRAFT spammer re-GRAFTs the topic peers it is in backoff with
+    if (graftSpam && ticks > 1 && inTopic && !m && bo) {
+      if (pr) {
+        spamGraft |= bit;  // the backoff just added expires after now
+      } else {
+        const int64_t be = d.backoff[tix(d, tt, e)];
+        if (be != 0 && be > now) spamGraft |= bit;
+      }
+    }
+    const unsigned long long c1 = GS_CLK();
+    // ---- 2. stats writes and emitGossip's live scores, in topic order
+    const int nm = act ? __shfl(nmT, tt) : 0;  // message ids of t in the gossip windows
+    const bool emits = nm > 0 && !noFwd && !ihaveSpam;
+    const bool baseE = emits && vm && inTopic && !m && !dir;
+    bool cand = false;
+    for (int hh = 0; hh < 2; ++hh) {
+      if (h == hh) {
+        if (pr) {
+          stats_prune(d, e, tt);
+          add_backoff(d, e, tt, now, d.PruneBackoff);
+        }
+        if (gr) stats_graft(d, e, tt, now);
+        dirty = dirty || pr;
+        dirtyUp = dirtyUp || gr;
+      }
+      unsigned long long dm = __ballot(h == hh && baseE && (dirty || (dirtyUp && !(Slive >= d.gossipThr))));
+      while (dm) {  // rare (a peer pruned earlier in this heartbeat): one edge at a time
+        const int j = __ffsll((long long)dm) - 1;
+        dm &= dm - 1;
+        const double sj = edge_score_wave(d, base + (j & 31), lds);
+        if (lane == j) {
+          Slive = sj;
+          dirty = false;
+          dirtyUp = false;
+        }
+      }
+      if (h == hh) cand = baseE && Slive >= d.gossipThr;
+      // the other half continues from this half's live-score state
+      const double sx = __shfl_xor(Slive, 32);
+      const bool dx = __shfl_xor((int)dirty, 32) != 0, ux = __shfl_xor((int)dirtyUp, 32) != 0;
+      if (h != hh) {
+        Slive = sx;
+        dirty = dx;
+        dirtyUp = ux;
+      }
+    }
+    // ---- 3. IHAVE peer selection of both topics
+    const unsigned long long c2 = GS_CLK();
+    uint64_t ih = 0;
+    if (ihaveSpam) {
+      ih = (nm > 0 && !noFwd && vm && inTopic) ? bit : 0;  // every topic peer, any score
+    } else if (emits) {
+      const int n = half_count(cand);
+      int target = d.Dlazy;
+      const int factor = (int)(d.GossipFactor * (double)n);
+      if (factor > target) target = factor;
+      bool sel = cand;
+      if (target < n) {
+        const uint64_t key = gs_key64(d.seed, GS_SITE_EMIT_PEERS, v, hw, vcol, tt);
+        sel = select_k_half(cand, key, target);
+      }
+      ih = sel ? bit : 0;
+    }
+    // ---- merge the two halves' topic bits into both halves
+    const uint64_t clr = bit | (uint64_t)__shfl_xor((unsigned long long)bit, 32);
+    const uint64_t mb = m ? bit : 0, pb = pr ? bit : 0, gb = gr ? bit : 0;
+    const uint64_t mAll = mb | (uint64_t)__shfl_xor((unsigned long long)mb, 32);
+    const uint64_t pAll = pb | (uint64_t)__shfl_xor((unsigned long long)pb, 32);
+    meshl = (meshl & ~clr) | mAll;
+    boM |= pAll;
+    toprune |= pAll;
+    tograft |= gb | (uint64_t)__shfl_xor((unsigned long long)gb, 32);
+    ihave |= ih | (uint64_t)__shfl_xor((unsigned long long)ih, 32);
+    spamGraft |= (uint64_t)__shfl_xor((unsigned long long)spamGraft, 32);
+    cyMesh += c1 - c0;
+    cyEmit += c2 - c1;
+    cySel += GS_CLK() - c2;
+  }
+}
+
 // ---------------------------------------------------------------- heartbeat
 // GossipSubRouter.heartbeat (gossipsub.go:1299-1552) for one node: mesh
 // maintenance per joined topic (ascending), emitGossip, fanout expiry and
 // maintenance, sendGraftPrune (outbox), mcache.Shift.  Scores are the
 // heartbeat memo (score1, computed after applyIwantPenalties); emitGossip
 // re-scores peers whose stats changed during this heartbeat (live Score()).
+// PAIR (every node has at most 32 peers): the joined topics are handled two at
+// a time, one per half-wave: lanes 32..63 mirror the edges of lanes 0..31 for
+// the topic loop (mesh maintenance and emitGossip's peer selection of topic
+// t0 + 1 next to t0's), with the live-score bookkeeping of emitGossip kept in
+// the serial topic order (hb_pair below).
+template <bool PAIR>
 __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, int64_t now, uint64_t ticks, int cur,
                                                   int head, int newhead, int allExact) {
   __shared__ int plst[64];
@@ -1045,9 +1337,11 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
   const int lane = lane_id();
   const int64_t base = d.rowptr[v];
   const int deg = (int)(d.rowptr[v + 1] - base);
-  const bool valid = lane < deg;
-  const int64_t e = base + lane;
-  const int vcol = valid ? d.col[e] : -1;
+  const int el = PAIR ? (lane & 31) : lane;  // the lane's edge (PAIR: both halves)
+  const bool valid = lane < deg;             // PAIR: deg <= 32, the lower half only
+  const bool vm = el < deg;                  // valid, mirrored into the upper half
+  const int64_t e = base + el;
+  const int vcol = vm ? d.col[e] : -1;
   GS_STAMPH(0, GS_CLK());
   // mcache.GetGossipIDs windows 0..HG-1 (mcache.go:82-92): this heartbeat's
   // IHAVE payload, kept as the node's gw row for the receivers' handleIHave
@@ -1085,11 +1379,11 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
   int nmT = 0;
   if (lane < d.T)
     for (int w = lane * d.Wt; w < (lane + 1) * d.Wt; ++w) nmT += __popcll(sgw[w]);
-  const uint64_t subv = valid && edge_up(d, e) ? d.subA[vcol] : 0;  // topic peers: connected, announced
-  uint64_t meshl = valid ? d.mesh[e] : 0;
+  const uint64_t subv = vm && edge_up(d, e) ? d.subA[vcol] : 0;  // topic peers: connected, announced
+  uint64_t meshl = vm ? d.mesh[e] : 0;
   uint64_t fanl = valid ? d.fanout[e] : 0;
-  uint64_t boM = valid ? d.boMask[e] : 0;  // topics in backoff with this peer
-  double S = valid ? d.score1[e] : 0.0;
+  uint64_t boM = vm ? d.boMask[e] : 0;  // topics in backoff with this peer
+  double S = vm ? d.score1[e] : 0.0;
   const uint64_t joined = d.sub[v];
   if (d.scoring && !allExact) {
     // score1 is exact only where k_score_rows<4> recomputed it; the Dhi
@@ -1104,18 +1398,25 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
     const bool exact = valid && (d.sdirty[e] != 0 || !(d.score0[e] >= 0.0));
     __syncthreads();  // sgw (read for nmT above) becomes the batch's term table
     edge_scores_batch(d, base, __ballot(needX && !exact), S, (double*)sgw);
+    if (PAIR) S = __shfl(S, el);  // the upper half mirrors the exact scores
   }
   GS_STAMPH(2, GS_CLK());
-  unsigned long long cyMesh = 0, cyEmit = 0;  // GS_STAMPS: cycles in mesh maintenance / emitGossip
+  unsigned long long cyMesh = 0, cyEmit = 0, cySel = 0;  // GS_STAMPS: cycles in mesh maintenance / emitGossip
   double Slive = S;  // live Score(p) for emitGossip
-  const bool dir = valid && d.direct[e];
-  const bool ob = valid && d.outbound[e];
+  const bool dir = vm && d.direct[e];
+  const bool ob = vm && d.outbound[e];
   bool dirty = false;    // a PRUNE lowered the peer's score since Slive
   bool dirtyUp = false;  // a GRAFT (never lowers it) changed it since Slive
   uint64_t tograft = 0, toprune = 0, ihave = 0;
   const uint32_t hw = (uint32_t)hop;
   const bool graftSpam = behaves(d, v, GS_BEHAVE_GRAFT_SPAM);
   uint64_t spamGraft = 0;  // GRAFTs without a mesh change (not traced as Graft)
+  if constexpr (PAIR) {
+    hb_pair(d, v, base, deg, vm, e, vcol, hop, now, ticks, head, joined, subv, S, dir, ob, graftSpam, nmT, meshl, boM,
+            Slive, dirty, dirtyUp, tograft, toprune, ihave, spamGraft, plst, obs, posOf, (double*)sgw, cyMesh, cyEmit,
+            cySel);
+    if (!valid) tograft = toprune = ihave = spamGraft = 0;  // the mirror half is done
+  } else
   for (int t = 0; t < d.T; ++t) {
     if (!((joined >> t) & 1)) continue;
     const unsigned long long c0 = GS_CLK();
@@ -1272,6 +1573,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
   GS_STAMPH(3, GS_CLK());
   GS_STAMPH(6, cyMesh);
   GS_STAMPH(7, cyEmit);
+  GS_STAMPH(4, cySel);  // PAIR: the selection part of cyEmit
   // expire fanout for topics we haven't published to in a while
   uint64_t fpres = d.fanoutPresent[v];
   {
@@ -1304,7 +1606,6 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
     ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, f, dir, Slive, dirty, dirtyUp, base, (double*)sgw,
                          lane_get(nmT, t));
   }
-  GS_STAMPH(4, GS_CLK());
   // sendGraftPrune + flush: one heartbeat RPC per peer with any control
   if (valid && is_traced(d, v)) {  // prunePeer / graftPeer, gossipsub.go:1334, 1343
     for (uint64_t m = toprune; m; m &= m - 1) trace_emit(d, hop, GS_TRACE_PRUNE, v, vcol, __ffsll((long long)m) - 1, -1, 4);
@@ -1413,20 +1714,29 @@ __global__ __launch_bounds__(64) void k_edge_down(Dev d, const int32_t* __restri
   const int64_t e = edges[blockIdx.x];
   const int lane = lane_id();
   const int u = d.esrc[e], v = d.col[e];
+  const int64_t re = d.rev[e];
+  // A partitioned rank does the part it owns: u's side of the connection
+  // (edge e: its state and what it was about to send) and, at re = rev[e] in
+  // v's in-edge order, the RPCs u sent to v in the previous hop (their records
+  // live with the receiver).  Unpartitioned: both.
+  const bool ownE = e >= d.e0 && e < d.e1;
+  const bool ownR = re >= d.e0 && re < d.e1;
   double s = 0.0;
-  if (d.scoring && d.rstate != nullptr && d.rstate[e] == 1) s = edge_score_wave(d, e, sterm);
-  if (lane == 0) {
-    const int64_t re = d.rev[e];
-    d.alive[e] = 0;
-    d.mesh[e] = 0;
-    d.fanout[e] = 0;
+  if (ownE && d.scoring && d.rstate != nullptr && d.rstate[e] == 1) s = edge_score_wave(d, e, sterm);
+  if (lane == 0 && ownR) {
     d.cPre[prv][re] = 0; d.cHb[prv][re] = 0; d.cGraftJoin[prv][re] = 0; d.cGraftHb[prv][re] = 0;
     d.cPruneReply[prv][re] = 0; d.cPruneHb[prv][re] = 0; d.cIhave[prv][re] = 0;
     d.cIwant[prv][re] = -1; d.cIresp[prv][re] = -1;
     if (d.cSpam[prv] != nullptr) { d.cSpam[prv][re] = -1; d.cNSrv[prv][re] = 0; }
+    d.fwdIn[prv][re] = make_ulonglong2(0ull, 0ull);
+  }
+  if (!ownE) return;
+  if (lane == 0) {
+    d.alive[e] = 0;
+    d.mesh[e] = 0;
+    d.fanout[e] = 0;
     d.fwdRelay[prv][e] = 0;
     d.fwdPub[prv][e] = 0;
-    d.fwdIn[prv][re] = make_ulonglong2(0ull, 0ull);
     d.sdirty[e] = 1;
     if (is_traced(d, u)) trace_emit(d, hop, GS_TRACE_REMOVE_PEER, u, v, -1, -1, 0);  // trace.go:215
   }
@@ -1470,6 +1780,7 @@ __global__ void k_edge_up(Dev d, const int32_t* __restrict__ edges, int n, int64
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   const int64_t e = edges[k];
+  if (e < d.e0 || e >= d.e1) return;  // another rank's connection side
   d.alive[e] = 1;
   if (d.rstate != nullptr) d.rstate[e] = 1;
   d.sdirty[e] = 1;

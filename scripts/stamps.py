@@ -46,11 +46,13 @@ def main():
     hb = hbbuf.reshape(-1, 8).astype(np.int64)
     hb = hb[(hb[:, 0] > 0) & (hb[:, 5] > 0)]
     if len(hb):
-        dh = np.diff(hb[:, :6], axis=1)
+        cols = [0, 1, 2, 3, 5]
+        dh = np.diff(hb[:, cols], axis=1)
         print("heartbeat samples", len(hb))
-        for i, nm in enumerate(["gw windows", "exact scores", "topic loop", "fanout", "outbox + shift"]):
+        for i, nm in enumerate(["gw windows", "exact scores", "topic loop", "fanout + outbox + shift"]):
             print(f"  {nm}: mean {dh[:, i].mean():.0f} cycles  p50 {np.median(dh[:, i]):.0f}  p99 {np.percentile(dh[:, i], 99):.0f}")
-        print(f"  topic loop split: mesh maintenance {hb[:, 6].mean():.0f}, emitGossip {hb[:, 7].mean():.0f}")
+        print(f"  topic loop split: mesh maintenance {hb[:, 6].mean():.0f}, emitGossip {hb[:, 7].mean():.0f}"
+              f" (paired: stats + live scores {hb[:, 7].mean():.0f}, peer selection {hb[:, 4].mean():.0f})")
     bb = buf.reshape(-1, 8)[len(buf) // 16:].astype(np.int64)
     bb = bb[(bb[:, 0] > 0) & (bb[:, 4] > 0)]
     b = bb[:, :5]

@@ -107,6 +107,17 @@ def run_partitioned(world, name, oracle):
     (2, "spam_iwant"),
     (2, "adversarial_mix"),
     (3, "adversarial_mix_nogater"),
+    # per-edge RPC byte accounting, counted by the sender's rank
+    (2, "acct_floodsub"),
+    (3, "acct_multitopic"),
+    (2, "acct_adversarial"),
+    # connection churn and subscription changes: each rank takes its side of
+    # every connection event and its own nodes' leaves / joins
+    (2, "churn_remove_peer"),
+    (2, "churn_prune"),
+    (3, "churn_graft"),
+    (2, "churn_scored"),
+    (3, "acct_churn"),
 ])
 def test_partitioned_engine_matches_oracle(world, name, oracle_path):
     res = run_partitioned(world, name, oracle_path)
