@@ -15,6 +15,7 @@
 #include "../../include/gossip_engine.h"
 #include "../../include/gs_rng.h"
 #include "../../include/gs_rpcsize.h"
+#include "../../include/gs_trace.h"
 
 #define GS_WAVE 64
 // Occupancy hints (waves per SIMD the register allocator must allow) of the
@@ -113,6 +114,7 @@ struct Dev {
   gs_trace_event* trace;
   unsigned long long* traceN;
   int64_t traceCap;
+  int32_t traceRpc;  // gs_set_trace_rpc: RECV_RPC / SEND_RPC blocks of the traced hosts
   const uint8_t* nodeRank;  // [N] owning rank of every node (world > 1)
   uint32_t seed;
   int64_t hop_ns;
@@ -311,6 +313,49 @@ __device__ __forceinline__ void trace_emit(const Dev& d, int64_t hop, int type, 
   e.phase = (uint8_t)phase;
   e.reason = (uint8_t)reason;
   d.trace[k] = e;
+}
+
+// ---- RPC trace events (gs_set_trace_rpc, include/gs_trace.h) -------------
+// One RPC sent by `snd` to `rcv` in hop `hop`: a SEND_RPC block for a traced
+// sender (its send phase sPhase) and a RECV_RPC block for a traced receiver,
+// stamped hop + 1 (the receiver handles it in the next hop; the host holds it
+// back until that hop ran, and drops it if the connection closed at its start).
+// A block is the RPC event and its nItems items, contiguous in the buffer;
+// gen(put) must call put(kind, topic, msg) exactly nItems times.  One lane.
+template <class G>
+__device__ void rpc_trace(const Dev& d, int64_t hop, int snd, int rcv, int sPhase, int rPhase, int64_t ord, int nItems,
+                          G&& gen) {
+  for (int dir = 0; dir < 2; ++dir) {
+    const int node = dir ? rcv : snd, peer = dir ? snd : rcv;
+    if (!is_traced(d, node)) continue;
+    const unsigned long long k = atomicAdd(d.traceN, (unsigned long long)(1 + nItems));
+    if ((int64_t)(k + 1 + nItems) > d.traceCap) {
+      set_err(d, E_TRACE);
+      continue;
+    }
+    gs_trace_event e;
+    e.hop = dir ? hop + 1 : hop;
+    e.msg = ord;
+    e.type = dir ? GS_TRACE_RECV_RPC : GS_TRACE_SEND_RPC;
+    e.node = node;
+    e.peer = peer;
+    e.topic = -1;
+    e.phase = (uint8_t)(dir ? rPhase : sPhase);
+    e.reason = 0;
+    d.trace[k] = e;
+    unsigned long long j = k + 1;
+    e.type = GS_TRACE_RPC_ITEM;
+    gen([&](int kind, int topic, int64_t msg) {
+      if (j > k + (unsigned long long)nItems) return;  // never more than reserved
+      e.reason = (uint8_t)kind;
+      e.topic = (int16_t)topic;
+      e.msg = msg;
+      d.trace[j++] = e;
+    });
+  }
+}
+__device__ __forceinline__ bool rpc_traced(const Dev& d, int a, int b) {
+  return d.traceRpc && (is_traced(d, a) || is_traced(d, b));
 }
 
 // Index of (edge e, topic t) in the per-(edge, topic) arrays: one row of T

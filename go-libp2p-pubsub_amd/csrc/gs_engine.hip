@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include "../../include/gs_rpcsize.h"
 #include <map>
 #include <tuple>
@@ -149,6 +150,20 @@ struct gs_engine {
   }
   int flushAcct();
   std::vector<gs_trace_event> tracePending;  // converted, canonical order from traceOut
+  // RPC events (gs_set_trace_rpc): RECV blocks of hops not run yet, and the
+  // connections closed at the start of a hop (their in-flight RPCs are lost)
+  bool traceRpc = false;
+  std::vector<gs_trace_event> traceFuture;
+  std::vector<std::array<int64_t, 3>> rpcDowns;  // (hop, receiver, sender)
+  // an RPC block recorded on the host: hello packets and announcements
+  void hostRpc(int type, int node, int peer, int64_t h, int64_t ord, int topicSub, uint64_t subs, int subFlag) {
+    if (!traceRpc || traceMask.empty() || !traceMask[node] || node < n0 || node >= n1) return;
+    tracePending.push_back(gs_trace_event{h, ord, type, node, peer, -1, 0, 0});
+    for (int t = 0; t < T; ++t)
+      if (((subs >> t) & 1) || t == topicSub)
+        tracePending.push_back(gs_trace_event{h, t == topicSub ? subFlag : 1, GS_TRACE_RPC_ITEM, node, peer,
+                                              (int16_t)t, 0, GS_RPC_ITEM_SUB});
+  }
   size_t traceOut = 0;
   int drainTrace();
   int64_t x_poolEnd() const { return (int64_t)(rank + 1) * poolSeg; }
@@ -612,6 +627,7 @@ int gs_engine::start() {
   x.trace = nullptr;
   x.traceN = nullptr;
   x.traceCap = 0;
+  x.traceRpc = traceRpc && !traceMask.empty();
   if (!traceMask.empty()) {
     uint8_t* tm = dalloc<uint8_t>(N); chk(tm);
     x.trace = dalloc<gs_trace_event>((size_t)traceCap); chk(x.trace);
@@ -630,6 +646,13 @@ int gs_engine::start() {
         tracePending.push_back(gs_trace_event{0, -1, GS_TRACE_ADD_PEER, u, col[e], -1, 0, 0});
       for (int t = 0; t < T; ++t)
         if ((sub[u] >> t) & 1) tracePending.push_back(gs_trace_event{0, -1, GS_TRACE_JOIN, u, -1, (int16_t)t, 0, 0});
+      // the hello packet of every peer (pubsub.go:495; its RecvRPC at time 0)
+      for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e)
+        hostRpc(GS_TRACE_RECV_RPC, u, col[e], 0, GS_RPC_ORD(0, GS_RPC_O_HELLO), -1, sub[col[e]], 1);
+    }
+    if (traceRpc && world > 1) {
+      gs_set_error("RPC trace events need an unpartitioned engine");
+      return GS_EUNSUPPORTED;
     }
   }
   if (world > 1) {
@@ -813,6 +836,11 @@ int gs_engine::applyEvents(int64_t h) {
   const int cur = (int)(h & 1), prv = cur ^ 1;
   bool subAChanged = false, subChanged = false, recChanged = false;
   for (const Ann& an : pendAnn) {
+    if (traceRpc)  // RecvRPC of the announcement at every still-connected peer
+      for (int64_t e = rowptr[an.node]; e < rowptr[an.node + 1]; ++e)
+        if (aliveH[e])
+          hostRpc(GS_TRACE_RECV_RPC, col[e], an.node, h, GS_RPC_ORD(0, GS_RPC_O_ANNOUNCE + an.topic), an.topic, 0,
+                  an.sub ? 1 : 0);
     const uint64_t bit = 1ull << an.topic;
     subA[an.node] = an.sub ? (subA[an.node] | bit) : (subA[an.node] & ~bit);
     subAChanged = true;
@@ -846,6 +874,14 @@ int gs_engine::applyEvents(int64_t h) {
         if (acctOn && want) {  // hello packets both ways (pubsub.go:534)
           acctPend.insert(acctPend.end(), {ab, helloBytes(sub[ev.a]), ba, helloBytes(sub[ev.b])});
         }
+        if (traceRpc && want) {  // the hellos' RecvRPC
+          hostRpc(GS_TRACE_RECV_RPC, ev.a, ev.b, h, GS_RPC_ORD(0, GS_RPC_O_HELLO), -1, sub[ev.b], 1);
+          hostRpc(GS_TRACE_RECV_RPC, ev.b, ev.a, h, GS_RPC_ORD(0, GS_RPC_O_HELLO), -1, sub[ev.a], 1);
+        }
+        if (traceRpc && !want) {  // RPCs in flight on the connection are lost
+          rpcDowns.push_back({h, ev.a, ev.b});
+          rpcDowns.push_back({h, ev.b, ev.a});
+        }
       } else {
         const uint64_t bit = 1ull << ev.b;
         const bool joinEv = pass == GS_EV_JOIN;
@@ -853,6 +889,11 @@ int gs_engine::applyEvents(int64_t h) {
         if (acctOn)  // announce (pubsub.go:775-792) to every connected peer
           for (int64_t e = rowptr[ev.a]; e < rowptr[ev.a + 1]; ++e)
             if (aliveH[e]) acctPend.insert(acctPend.end(), {e, gs_pb_field(gs_pb_subopts(acctTl[ev.b]))});
+        if (traceRpc)
+          for (int64_t e = rowptr[ev.a]; e < rowptr[ev.a + 1]; ++e)
+            if (aliveH[e])
+              hostRpc(GS_TRACE_SEND_RPC, ev.a, col[e], h, GS_RPC_ORD(0, GS_RPC_O_ANNOUNCE + ev.b), ev.b, 0,
+                      joinEv ? 1 : 0);
         sub[ev.a] = joinEv ? (sub[ev.a] | bit) : (sub[ev.a] & ~bit);
         subChanged = true;
         pendAnn.push_back({ev.a, ev.b, joinEv});
@@ -1125,6 +1166,7 @@ int gs_engine::stepOne() {
   }
   // RPC accounting: this hop's forwarded and published messages, one RPC each
   if (acctOn && nOwn) k_acct_payload<<<nOwn, 64, 0, stream>>>(d, cur);
+  if (traceRpc && nOwn) k_trace_payload<<<nOwn, 64, 0, stream>>>(d, cur, h);
   HIPCHECK(hipGetLastError());
   if (world > 1) {
     const int rc = exchange(cur, heartbeatDue(now));
@@ -1388,14 +1430,34 @@ int gs_engine::drainTrace() {
       delivered.push_back(Key{e.hop, e.msg, e.node, e.peer});
   std::sort(delivered.begin(), delivered.end());
   std::vector<gs_trace_event> keep(tracePending.begin() + traceOut, tracePending.end());
+  std::vector<gs_trace_event> all;
+  all.swap(traceFuture);
   for (auto e : ev) {
     if (e.type == GS_TRACE_COPY) {
       if (std::binary_search(delivered.begin(), delivered.end(), Key{e.hop, e.msg, e.node, e.peer})) continue;
       e.type = GS_TRACE_DUPLICATE_MESSAGE;
     }
-    keep.push_back(e);
+    all.push_back(e);
   }
-  std::stable_sort(keep.begin(), keep.end(), gs_trace_less);
+  // RPC blocks: a RECV stamped with a hop that has not run yet waits for it;
+  // one whose connection closed at the start of its hop was lost in flight
+  for (size_t i = 0; i < all.size();) {
+    size_t j = i + 1;
+    if (gs_trace_is_rpc(all[i]))
+      while (j < all.size() && all[j].type == GS_TRACE_RPC_ITEM) ++j;
+    const gs_trace_event& hd = all[i];
+    bool drop = false;
+    if (hd.hop >= hop) {
+      traceFuture.insert(traceFuture.end(), all.begin() + i, all.begin() + j);
+      drop = true;
+    } else if (hd.type == GS_TRACE_RECV_RPC) {
+      const std::array<int64_t, 3> k{hd.hop, hd.node, hd.peer};
+      drop = std::find(rpcDowns.begin(), rpcDowns.end(), k) != rpcDowns.end();
+    }
+    if (!drop) keep.insert(keep.end(), all.begin() + i, all.begin() + j);
+    i = j;
+  }
+  gs_trace_canonical(keep, cfg.seed, gp.MaxIHaveLength);
   tracePending.swap(keep);
   traceOut = 0;
   return GS_OK;
@@ -1811,6 +1873,12 @@ int gs_set_trace(gs_engine* g, const uint8_t* node_mask, int64_t capacity) {
   if (node_mask) g->traceMask.assign(node_mask, node_mask + g->N);
   else g->traceMask.clear();
   g->traceCap = capacity;
+  return GS_OK;
+}
+
+int gs_set_trace_rpc(gs_engine* g, int32_t on) {
+  if (g->started) { gs_set_error("tracing must be set before the first step"); return GS_ESTATE; }
+  g->traceRpc = on != 0;
   return GS_OK;
 }
 

@@ -369,6 +369,14 @@ __global__ __launch_bounds__(64) void k_join(Dev d, int64_t hop, int64_t now, in
       for (uint64_t m = gj; m; m &= m - 1) b += gs_pb_field(d.acc[__ffsll((long long)m) - 1].graftEnt);
       acct_send(d, e, b, __popcll(gj));
     }
+    if (gj && rpc_traced(d, u, v))
+      for (uint64_t m = gj; m; m &= m - 1) {
+        const int t = __ffsll((long long)m) - 1;
+        rpc_trace(d, hop, u, v, 0, 3, GS_RPC_ORD(0, t), 2, [&](auto put) {
+          put(GS_RPC_ITEM_CTL, -1, -1);
+          put(GS_RPC_ITEM_GRAFT, t, -1);
+        });
+      }
   }
   int g = wave_sum_int(valid ? __popcll(gj) : 0);
   if (lane == 0 && g) ctr_add(d, C_GRAFTS, (unsigned long long)g);
@@ -1340,6 +1348,11 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
           // RPC{control: {iwant: [{n ids}]}}
           if (acct) acct_send(d, base + lane, gs_pb_field(gs_pb_field((int64_t)n * d.acctIdF)), 1);
           ctr_add(d, C_IWANT_SENT, (unsigned long long)n);
+          if (rpc_traced(d, v, u))
+            rpc_trace(d, h, v, u, 2, 3, GS_RPC_ORD(2, GS_RPC_O_SPAM), 1 + n, [&](auto put) {
+              put(GS_RPC_ITEM_CTL, -1, -1);
+              for (int q = 0; q < n; ++q) put(GS_RPC_ITEM_IWANT, -1, d.slotMid[d.pool[cur][off + q]]);
+            });
         }
       }
     }
@@ -1606,6 +1619,42 @@ __global__ __launch_bounds__(64) void k_acct_payload(Dev d, int p) {
 }
 
 // RPC accounting: (edge, bytes) pairs of the host-side RPCs of a hop
+// RPC trace of this hop's payload RPCs (gs_set_trace_rpc): one RPC per
+// forwarded or published message and receiver, the walk of k_acct_payload;
+// only senders that are traced or have a traced peer do any work.
+__global__ __launch_bounds__(64) void k_trace_payload(Dev d, int p, int64_t hop) {
+  const int u = d.n0 + blockIdx.x;
+  const int lane = lane_id();
+  const int64_t base = d.rowptr[u];
+  const int deg = (int)(d.rowptr[u + 1] - base);
+  const bool valid = lane < deg;
+  const int64_t e = base + lane;
+  const int w = valid ? d.col[e] : 0;
+  const bool tr = valid && (is_traced(d, u) || is_traced(d, w));
+  if (!__ballot(tr)) return;
+  const uint64_t ru = valid ? d.fwdRelay[p][e] : 0, pu = valid ? d.fwdPub[p][e] : 0;
+  const int Ln = d.fln[p][u];
+  const uint32_t* L = d.fl[p] + (int64_t)u * d.FC;
+  for (int k0 = 0; k0 < Ln; k0 += 64) {
+    const uint32_t mine = k0 + lane < Ln ? L[k0 + lane] : 0u;
+    const int cnt = min(64, Ln - k0);
+    for (int k = 0; k < cnt; ++k) {
+      const uint32_t ent = (uint32_t)lane_get((int)mine, k);
+      const int slot = (int)(ent & 0xFFFF), tag = (int)(ent >> 16);
+      const int t = (int)__umulhi((unsigned)slot, d.stMagic);
+      bool sent = tr && (tag == 255 ? ((pu >> t) & 1) : ((ru >> t) & 1));
+      sent = sent && tag != lane;  // not back to the deliverer (gossipsub.go:1003)
+      if (sent && d.router == 1) sent = (d.sel[(int64_t)u * d.S + slot] >> lane) & 1;
+      if (sent && d.slotSrc[slot] == w) sent = false;  // never to the author
+      if (sent) {
+        const int sp = tag == 255 ? 1 : 2;  // local publish / forward
+        const int64_t mid = d.slotMid[slot];
+        rpc_trace(d, hop, u, w, sp, 2, GS_RPC_ORD(sp, mid), 1, [&](auto put) { put(GS_RPC_ITEM_MSG, t, mid); });
+      }
+    }
+  }
+}
+
 __global__ void k_acct_add(Dev d, const int64_t* __restrict__ pairs, int n) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;

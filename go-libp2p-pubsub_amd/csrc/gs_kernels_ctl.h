@@ -360,6 +360,7 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
   int64_t respRec = -1;
   long long cServed = 0;
   int nSrv = 0;  // reply RPCs carrying served messages to this sender
+  int srvR = 0, srvS = 0;  // messages served for the sender's IWANT list / its IWANT-spam list
   __shared__ uint32_t sSrvB[64], sSrvBS[64];  // RPC accounting: served message bytes per list
   uint32_t srvB = 0, srvBS = 0;
   if (__ballot(gateIWant || gateSpam)) {
@@ -468,6 +469,8 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
     int totalServed;
     const int myServed = sCnt[lane] + sCntS[lane];
     nSrv = (sCnt[lane] > 0 ? 1 : 0) + (sCntS[lane] > 0 ? 1 : 0);
+    srvR = sCnt[lane];
+    srvS = sCntS[lane];
     const int myOff = lane_prefix(myServed, &totalServed);
     if (lane == 0 && totalServed) sBase = atomicAdd(&d.poolCnt[cur], (unsigned long long)totalServed);
     __syncthreads();
@@ -894,6 +897,58 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
             b += gs_pb_field(body);
           }
           acct_send(d, e, b, nReplies);
+        }
+        if (rpc_traced(d, v, u)) {
+          // HandleRPC's replies (gossipsub.go:602-607), each named by the RPC it
+          // answers (include/gs_trace.h): a PRUNE per rejected join GRAFT, the
+          // served messages of the spam and IWANT lists, IWANT + PRUNEs for
+          // the heartbeat RPC
+          for (uint64_t m = joinRej; m; m &= m - 1) {
+            const int t = __ffsll((long long)m) - 1;
+            rpc_trace(d, h, v, u, 3, 3, GS_RPC_ORD(3, t), 2, [&](auto put) {
+              put(GS_RPC_ITEM_CTL, -1, -1);
+              put(GS_RPC_ITEM_PRUNE, t, -1);
+            });
+          }
+          // the served ids of one request list: by each request's verdict
+          // (pflag) when spam lists exist, else the whole served record
+          auto served = [&](int64_t reqRec, bool useFlags, auto put) {
+            if (useFlags) {
+              const int64_t off = reqRec >> 24;
+              const int n = (int)(reqRec & 0xFFFFFF);
+              for (int q = 0; q < n; ++q)
+                if (d.pflag[prv][off + q]) {
+                  const int slot = d.pool[prv][off + q];
+                  put(GS_RPC_ITEM_MSG, (int)__umulhi((unsigned)slot, d.stMagic), d.slotMid[slot]);
+                }
+            } else {
+              const int64_t off = respRec >> 24;
+              const int n = (int)(respRec & 0xFFFFFF);
+              for (int q = 0; q < n; ++q) {
+                const int slot = d.pool[cur][off + q];
+                put(GS_RPC_ITEM_MSG, (int)__umulhi((unsigned)slot, d.stMagic), d.slotMid[slot]);
+              }
+            }
+          };
+          const bool useFlags = ADV && d.pflag[0] != nullptr;
+          if (srvS > 0 && respRec >= 0)
+            rpc_trace(d, h, v, u, 3, 2, GS_RPC_ORD(3, GS_RPC_O_ANS_SPAM), 1 + srvS, [&](auto put) {
+              put(GS_RPC_ITEM_CTL, -1, -1);
+              served(spRec, true, put);
+            });
+          if (srvR > 0 && respRec >= 0)
+            rpc_trace(d, h, v, u, 3, 2, GS_RPC_ORD(3, GS_RPC_O_ANS_REPLY), 1 + srvR, [&](auto put) {
+              put(GS_RPC_ITEM_CTL, -1, -1);
+              served(iwRec, useFlags, put);
+            });
+          if (iwantAny || prunesHb) {
+            const int nIw = iwantAny ? (int)(iwantRec & 0xFFFFFF) : 0;
+            rpc_trace(d, h, v, u, 3, 3, GS_RPC_ORD(3, GS_RPC_O_ANS_HB), 1 + nIw + __popcll(hbPr), [&](auto put) {
+              put(GS_RPC_ITEM_CTL, -1, -1);
+              for (int q = 0; q < nIw; ++q) put(GS_RPC_ITEM_IWANT, -1, d.slotMid[d.pool[cur][(iwantRec >> 24) + q]]);
+              for (uint64_t m = hbPr; m; m &= m - 1) put(GS_RPC_ITEM_PRUNE, __ffsll((long long)m) - 1, -1);
+            });
+          }
         }
       }
     }
@@ -1638,6 +1693,33 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
       d.cPruneHb[cur][re] = toprune;
       d.cIhave[cur][re] = ihave;
       d.cHb[cur][re] = 1;
+      if (rpc_traced(d, v, vcol)) {
+        // the heartbeat RPC (sendGraftPrune with the piggybacked gossip): its
+        // IHAVE ids are the gossip windows of each topic (every id: the host
+        // applies emitGossip's MaxIHaveLength cut, include/gs_trace.h)
+        auto gwWord = [&](int w) {
+          uint64_t x = 0;
+          for (int k = 0; k < d.HG; ++k) x |= d.hist[((int64_t)((head + k) % d.R) * d.N + v) * d.W + w];
+          return x;
+        };
+        int nIh = 0;
+        for (uint64_t m = ihave; m; m &= m - 1) {
+          const int t = __ffsll((long long)m) - 1;
+          for (int w = t * d.Wt; w < (t + 1) * d.Wt; ++w) nIh += __popcll(gwWord(w));
+        }
+        rpc_trace(d, hop, v, vcol, 4, 3, GS_RPC_ORD(4, 0), 1 + __popcll(tograft) + __popcll(toprune) + nIh,
+                  [&](auto put) {
+                    put(GS_RPC_ITEM_CTL, -1, -1);
+                    for (uint64_t m = tograft; m; m &= m - 1) put(GS_RPC_ITEM_GRAFT, __ffsll((long long)m) - 1, -1);
+                    for (uint64_t m = toprune; m; m &= m - 1) put(GS_RPC_ITEM_PRUNE, __ffsll((long long)m) - 1, -1);
+                    for (uint64_t m = ihave; m; m &= m - 1) {
+                      const int t = __ffsll((long long)m) - 1;
+                      for (int w = t * d.Wt; w < (t + 1) * d.Wt; ++w)
+                        for (uint64_t y = gwWord(w); y; y &= y - 1)
+                          put(GS_RPC_ITEM_IHAVE, t, d.slotMid[(int64_t)w * 64 + __ffsll((long long)y) - 1]);
+                    }
+                  });
+      }
     }
   }
   const int g = wave_sum_int(__popcll(tograft));
@@ -1857,6 +1939,14 @@ __global__ __launch_bounds__(64) void k_leave(Dev d, const int32_t* __restrict__
         for (uint64_t m = pruned; m; m &= m - 1) b += gs_pb_field(d.acc[__ffsll((long long)m) - 1].pruneEnt);
         acct_send(d, e, b, __popcll(pruned));
       }
+      if (rpc_traced(d, v, d.col[e]))
+        for (uint64_t m = pruned; m; m &= m - 1) {
+          const int t = __ffsll((long long)m) - 1;
+          rpc_trace(d, hop, v, d.col[e], 0, 3, GS_RPC_ORD(0, GS_RPC_O_LEAVE + t), 2, [&](auto put) {
+            put(GS_RPC_ITEM_CTL, -1, -1);
+            put(GS_RPC_ITEM_PRUNE, t, -1);
+          });
+        }
     }
   }
   if (lane == 0 && np && !silent) ctr_add(d, C_PRUNES, (unsigned long long)np);
@@ -1937,6 +2027,14 @@ __global__ __launch_bounds__(64) void k_join_pairs(Dev d, const int32_t* __restr
         for (uint64_t m = grafted; m; m &= m - 1) b += gs_pb_field(d.acc[__ffsll((long long)m) - 1].graftEnt);
         acct_send(d, e, b, __popcll(grafted));
       }
+      if (rpc_traced(d, v, vcol))
+        for (uint64_t m = grafted; m; m &= m - 1) {
+          const int t = __ffsll((long long)m) - 1;
+          rpc_trace(d, hop, v, vcol, 0, 3, GS_RPC_ORD(0, t), 2, [&](auto put) {
+            put(GS_RPC_ITEM_CTL, -1, -1);
+            put(GS_RPC_ITEM_GRAFT, t, -1);
+          });
+        }
     }
   }
   if (lane == 0) {

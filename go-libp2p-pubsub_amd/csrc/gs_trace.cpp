@@ -11,7 +11,9 @@
 // Host code only; no device involvement.
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/gossip_engine.h"
@@ -156,6 +158,143 @@ std::vector<Field> sub_fields(const gs_trace_event& e, const std::string& topic,
   }
 }
 
+// ---- RPCMeta (trace.go:310-383, pb/trace.proto RPCMeta) of an RPC event's
+// items ev[1..n): messages, subscriptions, then the control message when the
+// RPC carries one (ihave per topic, one iwant entry, graft, prune).
+struct Meta {
+  std::vector<std::pair<int64_t, int>> msgs;  // (id, topic)
+  std::vector<std::pair<int, bool>> subs;     // (topic, subscribe)
+  bool ctl = false;
+  std::vector<std::pair<int, std::vector<int64_t>>> ihave;
+  std::vector<int64_t> iwant;
+  std::vector<int> graft, prune;
+};
+Meta collect(const gs_trace_event* it, int64_t n) {
+  Meta m;
+  for (int64_t i = 0; i < n; ++i) {
+    const gs_trace_event& x = it[i];
+    switch (x.reason) {
+      case GS_RPC_ITEM_MSG: m.msgs.push_back({x.msg, x.topic}); break;
+      case GS_RPC_ITEM_SUB: m.subs.push_back({x.topic, x.msg != 0}); break;
+      case GS_RPC_ITEM_CTL: m.ctl = true; break;
+      case GS_RPC_ITEM_IHAVE:
+        if (m.ihave.empty() || m.ihave.back().first != x.topic) m.ihave.push_back({x.topic, {}});
+        m.ihave.back().second.push_back(x.msg);
+        break;
+      case GS_RPC_ITEM_IWANT: m.iwant.push_back(x.msg); break;
+      case GS_RPC_ITEM_GRAFT: m.graft.push_back(x.topic); break;
+      case GS_RPC_ITEM_PRUNE: m.prune.push_back(x.topic); break;
+      default: break;
+    }
+  }
+  return m;
+}
+std::string meta_pb(const Meta& m, const std::function<std::string(int)>& tn) {
+  std::string o;
+  for (auto& mm : m.msgs) {  // MessageMeta{messageID=1, topic=2}
+    std::string b;
+    put_bytes(b, 1, msg_bytes(mm.first));
+    put_bytes(b, 2, tn(mm.second));
+    put_bytes(o, 1, b);
+  }
+  for (auto& sm : m.subs) {  // SubMeta{subscribe=1, topic=2}
+    std::string b;
+    put_int(b, 1, sm.second ? 1 : 0);
+    put_bytes(b, 2, tn(sm.first));
+    put_bytes(o, 2, b);
+  }
+  if (m.ctl) {  // ControlMeta{ihave=1, iwant=2, graft=3, prune=4}
+    std::string c;
+    for (auto& ih : m.ihave) {
+      std::string b;
+      put_bytes(b, 1, tn(ih.first));
+      for (int64_t id : ih.second) put_bytes(b, 2, msg_bytes(id));
+      put_bytes(c, 1, b);
+    }
+    if (!m.iwant.empty()) {
+      std::string b;
+      for (int64_t id : m.iwant) put_bytes(b, 1, msg_bytes(id));
+      put_bytes(c, 2, b);
+    }
+    for (int t : m.graft) {
+      std::string b;
+      put_bytes(b, 1, tn(t));
+      put_bytes(c, 3, b);
+    }
+    for (int t : m.prune) {  // peers: none (no PX records), an empty repeated field
+      std::string b;
+      put_bytes(b, 1, tn(t));
+      put_bytes(c, 4, b);
+    }
+    put_bytes(o, 3, c);
+  }
+  return o;
+}
+std::string meta_json(const Meta& m, const std::function<std::string(int)>& tn) {
+  std::string o = "{";
+  bool first = true;
+  auto sep = [&]() {
+    if (!first) o += ",";
+    first = false;
+  };
+  auto ids = [&](const std::vector<int64_t>& v) {
+    std::string a = "[";
+    for (size_t i = 0; i < v.size(); ++i) a += (i ? ",\"" : "\"") + b64(msg_bytes(v[i])) + "\"";
+    return a + "]";
+  };
+  if (!m.msgs.empty()) {
+    sep();
+    o += "\"messages\":[";
+    for (size_t i = 0; i < m.msgs.size(); ++i)
+      o += std::string(i ? "," : "") + "{\"messageID\":\"" + b64(msg_bytes(m.msgs[i].first)) + "\",\"topic\":" +
+           jstr(tn(m.msgs[i].second)) + "}";
+    o += "]";
+  }
+  if (!m.subs.empty()) {
+    sep();
+    o += "\"subscription\":[";
+    for (size_t i = 0; i < m.subs.size(); ++i)
+      o += std::string(i ? "," : "") + "{\"subscribe\":" + (m.subs[i].second ? "true" : "false") +
+           ",\"topic\":" + jstr(tn(m.subs[i].first)) + "}";
+    o += "]";
+  }
+  if (m.ctl) {
+    sep();
+    std::string c = "{";
+    bool cf = true;
+    auto csep = [&]() {
+      if (!cf) c += ",";
+      cf = false;
+    };
+    if (!m.ihave.empty()) {
+      csep();
+      c += "\"ihave\":[";
+      for (size_t i = 0; i < m.ihave.size(); ++i)
+        c += std::string(i ? "," : "") + "{\"topic\":" + jstr(tn(m.ihave[i].first)) +
+             (m.ihave[i].second.empty() ? "" : ",\"messageIDs\":" + ids(m.ihave[i].second)) + "}";
+      c += "]";
+    }
+    if (!m.iwant.empty()) {
+      csep();
+      c += "\"iwant\":[{\"messageIDs\":" + ids(m.iwant) + "}]";
+    }
+    if (!m.graft.empty()) {
+      csep();
+      c += "\"graft\":[";
+      for (size_t i = 0; i < m.graft.size(); ++i) c += std::string(i ? "," : "") + "{\"topic\":" + jstr(tn(m.graft[i])) + "}";
+      c += "]";
+    }
+    if (!m.prune.empty()) {
+      csep();
+      c += "\"prune\":[";
+      for (size_t i = 0; i < m.prune.size(); ++i) c += std::string(i ? "," : "") + "{\"topic\":" + jstr(tn(m.prune[i])) + "}";
+      c += "]";
+    }
+    o += "\"control\":" + c + "}";
+  }
+  return o + "}";
+}
+
 }  // namespace
 
 extern "C" int gs_trace_encode(const gs_trace_event* ev, int64_t n, int32_t format, int64_t hop_ns,
@@ -166,16 +305,44 @@ extern "C" int gs_trace_encode(const gs_trace_event* ev, int64_t n, int32_t form
     return GS_EINVAL;
   }
   std::string out;
+  auto tn = [&](int t) -> std::string {
+    return t < 0 ? std::string() : (topic_names ? std::string(topic_names[t]) : std::to_string(t));
+  };
   for (int64_t i = 0; i < n; ++i) {
     const gs_trace_event& e = ev[i];
     if (e.type < 0 || e.type > GS_TRACE_PRUNE) {
-      gs_set_error("gs_trace_encode: unknown event type");
+      gs_set_error(e.type == GS_TRACE_RPC_ITEM ? "gs_trace_encode: an RPC item without its RPC event"
+                                               : "gs_trace_encode: unknown event type");
       return GS_EINVAL;
     }
-    const std::string topic =
-        e.topic < 0 ? std::string() : (topic_names ? std::string(topic_names[e.topic]) : std::to_string(e.topic));
+    const std::string topic = tn(e.topic);
     const std::string peer = peer_bytes(e.node);
     const int64_t ts = e.hop * hop_ns;
+    if (e.type == GS_TRACE_RECV_RPC || e.type == GS_TRACE_SEND_RPC || e.type == GS_TRACE_DROP_RPC) {
+      // RecvRPC{receivedFrom=1, meta=2} / SendRPC, DropRPC{sendTo=1, meta=2}
+      int64_t j = i + 1;
+      while (j < n && ev[j].type == GS_TRACE_RPC_ITEM) ++j;
+      const Meta m = collect(ev + i + 1, j - i - 1);
+      const char* who = e.type == GS_TRACE_RECV_RPC ? "receivedFrom" : "sendTo";
+      if (format == GS_TRACE_FORMAT_PB) {
+        std::string body;
+        put_bytes(body, 1, peer_bytes(e.peer));
+        put_bytes(body, 2, meta_pb(m, tn));
+        std::string msg;
+        put_int(msg, 1, e.type);
+        put_bytes(msg, 2, peer);
+        put_int(msg, 3, ts);
+        put_bytes(msg, kSubField[e.type], body);
+        put_varint(out, msg.size());
+        out += msg;
+      } else {
+        out += "{\"type\":" + std::to_string(e.type) + ",\"peerID\":\"" + b64(peer) + "\",\"timestamp\":" +
+               std::to_string(ts) + ",\"" + kSubName[e.type] + "\":{\"" + who + "\":\"" + b64(peer_bytes(e.peer)) +
+               "\",\"meta\":" + meta_json(m, tn) + "}}\n";
+      }
+      i = j - 1;
+      continue;
+    }
     const std::vector<Field> fs = sub_fields(e, topic, proto);
     if (format == GS_TRACE_FORMAT_PB) {
       std::string body;

@@ -101,6 +101,10 @@ TRACE_EVENT_DTYPE = np.dtype([("hop", "<i8"), ("msg", "<i8"), ("type", "<i4"), (
 TRACE_TYPES = ["PUBLISH_MESSAGE", "REJECT_MESSAGE", "DUPLICATE_MESSAGE", "DELIVER_MESSAGE", "ADD_PEER",
                "REMOVE_PEER", "RECV_RPC", "SEND_RPC", "DROP_RPC", "JOIN", "LEAVE", "GRAFT", "PRUNE"]
 GS_TRACE_FORMAT_PB, GS_TRACE_FORMAT_JSON = 0, 1
+# not a pb.TraceEvent type: one RPCMeta entry of the RPC event before it (gossip_engine.h)
+GS_TRACE_RPC_ITEM = 32
+(GS_RPC_ITEM_MSG, GS_RPC_ITEM_SUB, GS_RPC_ITEM_CTL, GS_RPC_ITEM_IHAVE, GS_RPC_ITEM_IWANT, GS_RPC_ITEM_GRAFT,
+ GS_RPC_ITEM_PRUNE) = range(7)
 
 
 class CountersC(C.Structure):
@@ -181,6 +185,7 @@ ABI_FUNCTIONS = [
     ("gs_set_rpc_accounting", C.c_int, [P, C.POINTER(i32), i32, C.POINTER(i32)]),
     ("gs_read_rpc_bytes", C.c_int, [P, C.POINTER(i64), C.POINTER(i64)]),
     ("gs_set_trace", C.c_int, [P, C.POINTER(u8), i64]),
+    ("gs_set_trace_rpc", C.c_int, [P, i32]),
     ("gs_trace_read", C.c_int, [P, P, i64, C.POINTER(i64)]),
     ("gs_trace_encode", C.c_int, [P, i64, i32, i64, C.POINTER(C.c_char_p), C.c_char_p, P, i64, C.POINTER(i64)]),
     ("gs_set_profiling", C.c_int, [P, C.c_int]),

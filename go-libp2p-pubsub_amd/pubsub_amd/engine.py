@@ -98,11 +98,13 @@ def WithRPCAccounting(msg_size, id_len=40, topic_len=None):
     return ("rpc_acct", (msg_size, int(id_len), topic_len))
 
 
-def WithEventTracer(nodes, capacity=1 << 22):
+def WithEventTracer(nodes, capacity=1 << 22, rpc=False):
     """EventTracer (pubsub.go:418, trace.go) for the hosts in `nodes` (indices
     or a bool mask): their PublishMessage / DeliverMessage / DuplicateMessage /
-    AddPeer / Join / Graft / Prune events, read with Engine.trace_events()."""
-    return ("trace", (nodes, int(capacity)))
+    AddPeer / Join / Graft / Prune events, and with rpc=True every RPC they
+    send or receive (SendRPC / RecvRPC with the RPCMeta items), read with
+    Engine.trace_events()."""
+    return ("trace", (nodes, int(capacity), bool(rpc)))
 
 
 def WithPeerGater(params):
@@ -185,11 +187,13 @@ class Engine:
                                                _ptr(ob, C.c_uint8), _ptr(direct, C.c_uint8)))
         tr = opts.get("trace")
         if tr is not None:
-            nodes, cap = tr
+            nodes, cap, rpc = tr
             mask = np.zeros(num_nodes, dtype=np.uint8)
             nodes = np.asarray(nodes)
             mask[np.nonzero(nodes)[0] if nodes.dtype == bool else nodes] = 1
             _check(self.lib, self.lib.gs_set_trace(h, _ptr(mask, C.c_uint8), cap))
+            if rpc:
+                _check(self.lib, self.lib.gs_set_trace_rpc(h, 1))
         acct = opts.get("rpc_acct")
         if acct is not None:
             ms, idl, tl = acct
@@ -210,6 +214,7 @@ class Engine:
         self.edge_range = (int(self.rowptr[b.value]), int(self.rowptr[e.value]))
         subs = np.ascontiguousarray(subscriptions, dtype=np.uint64)
         _check(self.lib, self.lib.gs_set_subscriptions(h, _ptr(subs, C.c_uint64)))
+        self.subs = subs  # the initial subscriptions (topic bit masks per node)
         val = opts.get("validation")
         if val is not None:
             tv = np.zeros(num_topics, dtype=np.uint8)

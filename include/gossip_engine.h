@@ -354,11 +354,12 @@ int gs_read_exchange_stats(gs_engine* eng, double* host_ms, int64_t* bytes_in);
  * every connection at the start and on every reconnect) and announcements.
  * Sizes: a message of topic t is msg_size[t] bytes (its Message.Size()),
  * every message id id_len bytes, topic t's name topic_len[t] bytes.  Before
- * the first step; not on a partitioned engine. */
+ * the first step.  A partitioned rank counts the RPCs its own nodes send. */
 int gs_set_rpc_accounting(gs_engine* eng, const int32_t* msg_size /*[T]*/, int32_t id_len,
                           const int32_t* topic_len /*[T]*/);
 /* bytes[e], rpcs[e]: totals sent by node u to col[e] (rowptr[u] <= e <
- * rowptr[u+1]) since the start (either array may be NULL). */
+ * rowptr[u+1]) since the start (either array may be NULL); a partitioned rank
+ * fills its own edges and zeroes the others. */
 int gs_read_rpc_bytes(gs_engine* eng, int64_t* bytes /*[E]*/, int64_t* rpcs /*[E]*/);
 
 /* ---- readbacks (host arrays sized by the caller) ----------------------- */
@@ -409,14 +410,33 @@ int gs_read_deliveries(gs_engine* eng, int64_t id, int32_t* hop /*[N]*/,
 #define GS_TRACE_LEAVE 10
 #define GS_TRACE_GRAFT 11
 #define GS_TRACE_PRUNE 12
+/* Not a pb.TraceEvent type: one entry of the RPCMeta of the RPC event before
+ * it.  reason = GS_RPC_ITEM_*, msg = the message id (MSG, IHAVE, IWANT; SUB:
+ * 1 = subscribe, 0 = unsubscribe), topic = the topic (-1 for IWANT / CTL). */
+#define GS_TRACE_RPC_ITEM 32
+#define GS_RPC_ITEM_MSG 0   /* RPCMeta.messages[]: MessageMeta{messageID, topic}          */
+#define GS_RPC_ITEM_SUB 1   /* RPCMeta.subscription[]: SubMeta{subscribe, topic}          */
+#define GS_RPC_ITEM_CTL 2   /* the RPC carries a ControlMessage (RPCMeta.control is set)  */
+#define GS_RPC_ITEM_IHAVE 3 /* ControlMeta.ihave[topic].messageIDs[]                     */
+#define GS_RPC_ITEM_IWANT 4 /* ControlMeta.iwant[0].messageIDs[]                         */
+#define GS_RPC_ITEM_GRAFT 5 /* ControlMeta.graft[]: ControlGraftMeta{topic}               */
+#define GS_RPC_ITEM_PRUNE 6 /* ControlMeta.prune[]: ControlPruneMeta{topic} (no PX peers) */
 /* One traced event of host `node` (32 bytes).  Recorded: PUBLISH_MESSAGE
  * (validation.go:217), DELIVER_MESSAGE / DUPLICATE_MESSAGE (pubsub.go:1011,
  * 1057; receivedFrom = peer), ADD_PEER (gossipsub.go:507, floodsub.go:45),
  * JOIN (gossipsub.go:1018, floodsub.go:103), GRAFT / PRUNE (gossipsub.go:790,
- * 817, 1057, 1334, 1343).  The RPC events (RECV/SEND/DROP_RPC) are not
- * recorded.  `phase` orders the events of one (hop, node): 0 connection and
- * Join, 1 local publish, 2 received messages, 3 received control, 4 heartbeat;
- * gs_trace_read returns events in the canonical order of include/gs_trace.h. */
+ * 817, 1057, 1334, 1343), and with gs_set_trace_rpc the RPC events RECV_RPC
+ * (pubsub.go:903) and SEND_RPC (gossipsub.go:1152, floodsub.go:93,
+ * randomsub.go:154, pubsub.go:785).  DROP_RPC is never recorded: outbound
+ * queues never drop in this model (gossipsub.go:1149-1156 takes its send
+ * branch), so the reference's drop path is unreachable.  `phase` orders the
+ * events of one (hop, node): 0 connection and Join, 1 local publish, 2
+ * received messages, 3 received control, 4 heartbeat; gs_trace_read returns
+ * events in the canonical order of include/gs_trace.h.
+ * An RPC event (type RECV_RPC / SEND_RPC) has peer = the sender / the
+ * receiver and msg = the RPC's ordinal (gs_trace_rpc_ordinal); it is followed
+ * by one GS_TRACE_RPC_ITEM event per entry of its traceRPCMeta (trace.go:
+ * 310-383), in the order the encoders write them. */
 typedef struct gs_trace_event {
   int64_t hop;    /* virtual time: timestamp = hop * hop_ns */
   int64_t msg;    /* message id, -1 = none */
@@ -444,6 +464,10 @@ typedef struct gs_trace_event {
  * keeping up to `capacity` events between two gs_trace_read calls (more is a
  * GS_ECAPACITY error of gs_step). */
 int gs_set_trace(gs_engine* eng, const uint8_t* node_mask, int64_t capacity);
+/* Before the first step: also record the RPC events of the traced hosts
+ * (every RPC they send or receive, with its traceRPCMeta items).  The
+ * product library records them on an unpartitioned engine only. */
+int gs_set_trace_rpc(gs_engine* eng, int32_t on);
 /* Moves up to `cap` recorded events, in canonical order, into out; *n = the
  * number written.  Call until *n < cap to drain. */
 int gs_trace_read(gs_engine* eng, gs_trace_event* out, int64_t cap, int64_t* n);

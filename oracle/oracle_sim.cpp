@@ -44,6 +44,9 @@ struct RPC {
   std::vector<int64_t> publish;
   bool hasCtl = false;
   Control ctl;
+  // trace ordinal (include/gs_trace.h): the send phase and its position there
+  int sp = 0;
+  int64_t ord = 0;
 };
 
 // Peer-gater view of one node at hop start (AcceptFrom, peer_gater.go:320-363):
@@ -95,7 +98,7 @@ struct Node {
   void gsPublish(const Msg& m, int from);
   std::vector<int> getPeers(int topic, int count, int site, const std::function<bool(int)>& filter);
   void join(int topic);
-  void handleRPC(int from, const Control& ctl);
+  void handleRPC(int from, const RPC& in);
   std::vector<int64_t> handleIHave(int p, const Control& ctl);
   std::vector<int64_t> handleIWant(int p, const Control& ctl);
   std::vector<PruneEntry> handleGraft(int p, const Control& ctl);
@@ -162,6 +165,12 @@ struct Sim {
   // EventTracer (trace.go:61-499) of the hosts with traced[u] != 0
   std::vector<uint8_t> traced;
   std::vector<gs_trace_event> events;  // drained from the nodes' buffers by gs_trace_read
+  bool traceRpc = false;               // gs_set_trace_rpc: RECV_RPC / SEND_RPC with their items
+  // one RPC event of `node` and its traceRPCMeta items (gossip_engine.h);
+  // subs: the RPC's subscriptions (topic, subscribe)
+  void emitRpc(int type, int node, int peer, int phase, int64_t ord, const RPC* r,
+               const std::vector<std::pair<int, int>>& subs = {});
+  void traceHello(int node, int from);  // RECV of from's hello packet (pubsub.go:495)
   // RPC byte accounting (gs_set_rpc_accounting): RPC.Size() and count of every
   // RPC a host sends, per directed edge (the sender's row)
   bool acct = false;
@@ -204,7 +213,15 @@ struct Sim {
   void start();
   void step();
   void applyEvents(std::vector<std::map<int, std::vector<RPC>>>& inbox);
-  void announce(int a, int topic);
+  // RecvRPC (pubsub.go:903) of every RPC in node u's inbox: before AcceptFrom,
+  // so graylisted and gated RPCs are traced too
+  void traceRecv(int u, const std::map<int, std::vector<RPC>>& in) {
+    if (!traceRpc || traced.empty() || !traced[u]) return;
+    for (auto& kv : in)
+      for (const RPC& r : kv.second)
+        emitRpc(GS_TRACE_RECV_RPC, u, kv.first, r.publish.empty() ? 3 : 2, GS_RPC_ORD(r.sp, r.ord), &r);
+  }
+  void announce(int a, int topic, bool sub);
 };
 
 void Sim::emit(int type, int node, int peer, int topic, int64_t msg, int phase, int reason) {
@@ -213,6 +230,37 @@ void Sim::emit(int type, int node, int peer, int topic, int64_t msg, int phase, 
   e.hop = hop; e.msg = msg; e.type = type; e.node = node; e.peer = peer;
   e.topic = (int16_t)topic; e.phase = (uint8_t)phase; e.reason = (uint8_t)reason;
   if (nodes.empty()) events.push_back(e); else nodes[node].ev.push_back(e);
+}
+
+void Sim::emitRpc(int type, int node, int peer, int phase, int64_t ord, const RPC* r,
+                  const std::vector<std::pair<int, int>>& subs) {
+  if (!traceRpc || traced.empty() || !traced[node]) return;
+  std::vector<gs_trace_event>& buf = nodes.empty() ? events : nodes[node].ev;
+  buf.push_back(gs_trace_event{hop, ord, type, node, peer, -1, (uint8_t)phase, 0});
+  auto item = [&](int kind, int topic, int64_t msg) {
+    buf.push_back(gs_trace_event{hop, msg, GS_TRACE_RPC_ITEM, node, peer, (int16_t)topic, (uint8_t)phase, (uint8_t)kind});
+  };
+  if (r) {  // traceRPCMeta (trace.go:310-383)
+    for (int64_t mid : r->publish) item(GS_RPC_ITEM_MSG, msgs[mid].topic, mid);
+    if (r->hasCtl) {
+      item(GS_RPC_ITEM_CTL, -1, -1);
+      for (const IHaveEntry& ih : r->ctl.ihave)
+        for (int64_t mid : ih.mids) item(GS_RPC_ITEM_IHAVE, ih.topic, mid);
+      for (int64_t mid : r->ctl.iwant) item(GS_RPC_ITEM_IWANT, -1, mid);
+      for (int t : r->ctl.graft) item(GS_RPC_ITEM_GRAFT, t, -1);
+      for (const PruneEntry& pe : r->ctl.prune) item(GS_RPC_ITEM_PRUNE, pe.topic, -1);
+    }
+  }
+  for (auto& st : subs) item(GS_RPC_ITEM_SUB, st.first, st.second);
+}
+
+void Sim::traceHello(int node, int from) {
+  if (!traceRpc || traced.empty() || !traced[node]) return;
+  std::vector<std::pair<int, int>> subs;
+  const uint64_t m = nodes.empty() ? 0 : nodes[from].mySubs;
+  for (int t = 0; t < T; ++t)
+    if ((m >> t) & 1) subs.push_back({t, 1});
+  emitRpc(GS_TRACE_RECV_RPC, node, from, 0, GS_RPC_ORD(0, GS_RPC_O_HELLO), nullptr, subs);
 }
 
 gs_counters Sim::total() const {
@@ -265,6 +313,7 @@ void Node::sendRPC(int p, RPC rpc) {
     gossip.erase(g);
   }
   sim->account(id, p, sim->acct ? sim->rpcSize(rpc) : 0);
+  sim->emitRpc(GS_TRACE_SEND_RPC, id, p, rpc.sp, GS_RPC_ORD(rpc.sp, rpc.ord), &rpc);  // gossipsub.go:1152
   ctr.grafts_sent += (int64_t)rpc.ctl.graft.size();
   ctr.prunes_sent += (int64_t)rpc.ctl.prune.size();
   ctr.ihave_sent += (int64_t)rpc.ctl.ihave.size();
@@ -317,6 +366,7 @@ void Node::join(int topic) {
     sim->emit(GS_TRACE_GRAFT, id, p, topic, -1, 0);        // tracer.Graft gossipsub.go:1057
     if (sim->scoring) score.Graft(p, topic, sim->now());  // tracer.Graft
     RPC r; r.hasCtl = true; r.ctl.graft.push_back(topic);  // sendGraft gossipsub.go:1080
+    r.sp = 0; r.ord = topic;
     sendRPC(p, std::move(r));
   }
 }
@@ -426,6 +476,7 @@ void Node::routerPublish(const Msg& m, int from) {
     for (int pid : tm->second) {
       if (pid == from || pid == m.from) continue;
       RPC r; r.publish.push_back(m.id);
+      r.sp = from == id ? 1 : 2; r.ord = m.id;
       sendRPC(pid, std::move(r));
     }
     return;
@@ -455,6 +506,7 @@ void Node::routerPublish(const Msg& m, int from) {
     }
     for (int p : tosend) {
       RPC r; r.publish.push_back(m.id);
+      r.sp = from == id ? 1 : 2; r.ord = m.id;
       sendRPC(p, std::move(r));
     }
     return;
@@ -499,12 +551,14 @@ void Node::gsPublish(const Msg& m, int from) {
   for (int pid : tosend) {
     if (pid == from || pid == m.from) continue;
     RPC r; r.publish.push_back(m.id);
+    r.sp = from == id ? 1 : 2; r.ord = m.id;
     sendRPC(pid, std::move(r));
   }
 }
 
 // HandleRPC — gossipsub.go:591-608 (one call per control-carrying RPC).
-void Node::handleRPC(int from, const Control& ctl) {
+void Node::handleRPC(int from, const RPC& in) {
+  const Control& ctl = in.ctl;
   auto iwant = handleIHave(from, ctl);
   auto ihave = handleIWant(from, ctl);
   auto prune = handleGraft(from, ctl);
@@ -516,6 +570,9 @@ void Node::handleRPC(int from, const Control& ctl) {
   if (!iwant.empty()) r.ctl.iwant = iwant;
   r.ctl.prune = prune;
   ctr.iwant_served += (int64_t)ihave.size();
+  // the reply's ordinal names the RPC it answers (include/gs_trace.h)
+  r.sp = 3;
+  r.ord = in.sp == 0 ? in.ord : in.sp == 2 ? GS_RPC_O_ANS_SPAM : in.sp == 3 ? GS_RPC_O_ANS_REPLY : GS_RPC_O_ANS_HB;
   sendRPC(from, std::move(r));
 }
 
@@ -874,12 +931,14 @@ void Node::heartbeat() {
       for (int topic : pr->second) r.ctl.prune.push_back(makePrune(p, topic));
       toprune.erase(pr);
     }
+    r.sp = 4;
     sendRPC(p, std::move(r));
   }
   for (auto& kv : toprune) {
     RPC r;
     r.hasCtl = true;
     for (int topic : kv.second) r.ctl.prune.push_back(makePrune(kv.first, topic));
+    r.sp = 4;
     sendRPC(kv.first, std::move(r));
   }
   // flush — gossipsub.go:1714-1728
@@ -888,6 +947,7 @@ void Node::heartbeat() {
   for (int p : gpeers) {
     RPC r;
     r.hasCtl = true;
+    r.sp = 4;
     sendRPC(p, std::move(r));  // sendRPC piggybacks the pending IHAVE
   }
   mcache.Shift();
@@ -947,6 +1007,7 @@ void Node::leaveTopic(int topic) {
     RPC r;  // sendPrune (gossipsub.go:1093-1097)
     r.hasCtl = true;
     r.ctl.prune.push_back(makePrune(p, topic));
+    r.sp = 0; r.ord = GS_RPC_O_LEAVE + topic;
     sendRPC(p, std::move(r));
   }
 }
@@ -967,10 +1028,13 @@ void Node::joinTopic(int topic) {
 // join (canonical order); disconnects and connects in schedule order, leaves
 // and joins by (node, topic).  A lost connection drops what was in flight.
 // announce (pubsub.go:775-792): one SubOpts RPC to every connected peer
-void Sim::announce(int a, int topic) {
-  if (!acct) return;
+void Sim::announce(int a, int topic, bool sub) {
   for (int p : nodes[a].nbrs)
-    if (!nodes[a].dead.count(p)) account(a, p, gs_pb_field(gs_pb_subopts(acctTl[topic])));
+    if (!nodes[a].dead.count(p)) {
+      if (acct) account(a, p, gs_pb_field(gs_pb_subopts(acctTl[topic])));
+      emitRpc(GS_TRACE_SEND_RPC, a, p, 0, GS_RPC_ORD(0, GS_RPC_O_ANNOUNCE + topic), nullptr,
+              {{topic, sub ? 1 : 0}});  // pubsub.go:785
+    }
 }
 
 void Sim::applyEvents(std::vector<std::map<int, std::vector<RPC>>>& inbox) {
@@ -979,6 +1043,8 @@ void Sim::applyEvents(std::vector<std::map<int, std::vector<RPC>>>& inbox) {
       Node& np = nodes[p];
       if (np.dead.count(an.node)) continue;
       if (an.sub) np.topics[an.topic].insert(an.node); else np.topics[an.topic].erase(an.node);
+      emitRpc(GS_TRACE_RECV_RPC, p, an.node, 0, GS_RPC_ORD(0, GS_RPC_O_ANNOUNCE + an.topic), nullptr,
+              {{an.topic, an.sub ? 1 : 0}});
     }
   pendingAnn.clear();
   // one hop's events in four passes (disconnects, connects, leaves, joins),
@@ -1006,18 +1072,20 @@ void Sim::applyEvents(std::vector<std::map<int, std::vector<RPC>>>& inbox) {
         if (!nodes[ev.a].dead.count(ev.b)) break;
         nodes[ev.a].addPeer(ev.b);
         nodes[ev.b].addPeer(ev.a);
+        traceHello(ev.a, ev.b);
+        traceHello(ev.b, ev.a);
         account(ev.a, ev.b, acct ? helloSize(nodes[ev.a].mySubs) : 0);  // hello packets (pubsub.go:534)
         account(ev.b, ev.a, acct ? helloSize(nodes[ev.b].mySubs) : 0);
         break;
       case GS_EV_LEAVE:
         if (!((nodes[ev.a].mySubs >> ev.b) & 1)) break;
-        announce(ev.a, ev.b);
+        announce(ev.a, ev.b, false);
         nodes[ev.a].leaveTopic(ev.b);
         pendingAnn.push_back({ev.a, ev.b, false});
         break;
       case GS_EV_JOIN:
         if ((nodes[ev.a].mySubs >> ev.b) & 1) break;
-        announce(ev.a, ev.b);
+        announce(ev.a, ev.b, true);
         nodes[ev.a].joinTopic(ev.b);
         pendingAnn.push_back({ev.a, ev.b, true});
         break;
@@ -1061,6 +1129,8 @@ void Sim::start() {
         if (!subs.empty() && ((subs[v] >> t) & 1)) nd.topics[t].insert(v);
     }
   }
+  for (int u = 0; u < N; ++u)  // the hello packet of every connection (pubsub.go:495)
+    for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) traceHello(u, col[e]);
   if (acct) {  // the hello packet of every connection (pubsub.go:495)
     rpcBytes.assign(E, 0);
     rpcCount.assign(E, 0);
@@ -1126,6 +1196,7 @@ void Sim::step() {
     for (int u = 0; u < N; ++u) {
       Node& nd = nodes[u];
       nd.valUsed = 0;
+      traceRecv(u, inbox[u]);
       for (auto& kv : inbox[nd.id]) {
         const int s = kv.first;
         std::vector<int64_t> got;  // accepted payload (the IWANT spammer re-requests it)
@@ -1140,13 +1211,14 @@ void Sim::step() {
             for (int64_t mid : r.publish) nd.handleMessage(s, msgs[mid]);
             got.insert(got.end(), r.publish.begin(), r.publish.end());
           }
-          if (r.hasCtl && cfg.router == GS_ROUTER_GOSSIPSUB) nd.handleRPC(s, r.ctl);  // pubsub.go:969
+          if (r.hasCtl && cfg.router == GS_ROUTER_GOSSIPSUB) nd.handleRPC(s, r);  // pubsub.go:969
         }
         if ((nd.behave & GS_BEHAVE_IWANT_SPAM) && !got.empty() && cfg.router == GS_ROUTER_GOSSIPSUB) {
           std::sort(got.begin(), got.end());
           RPC r;
           r.hasCtl = true;
           r.ctl.iwant = got;
+          r.sp = 2; r.ord = GS_RPC_O_SPAM;
           nd.sendRPC(s, std::move(r));
         }
       }
@@ -1159,6 +1231,7 @@ void Sim::step() {
     Node& nd = nodes[u];
     nd.acceptStatus.clear();
     nd.valUsed = 0;
+    traceRecv(u, inbox[u]);
     for (auto& kv : inbox[nd.id]) {
       int s = kv.first;
       bool anyCtl = false;
@@ -1191,6 +1264,7 @@ void Sim::step() {
         RPC r;
         r.hasCtl = true;
         r.ctl.iwant = mids;
+        r.sp = 2; r.ord = GS_RPC_O_SPAM;
         nd.sendRPC(s, std::move(r));
       }
     }
@@ -1204,7 +1278,7 @@ void Sim::step() {
         int s = kv.first;
         if (nd.acceptStatus[s] == PeerGater::AcceptNone) continue;
         for (const RPC& r : kv.second)
-          if (r.hasCtl) nd.handleRPC(s, r.ctl);
+          if (r.hasCtl) nd.handleRPC(s, r);
       }
     }
   }
@@ -1621,6 +1695,11 @@ int gs_set_trace(gs_engine* g, const uint8_t* node_mask, int64_t capacity) {
   else g->sim.traced.clear();
   return GS_OK;
 }
+int gs_set_trace_rpc(gs_engine* g, int32_t on) {
+  if (g->sim.started) { set_error("tracing must be set before the first step"); return GS_ESTATE; }
+  g->sim.traceRpc = on != 0;
+  return GS_OK;
+}
 int gs_trace_read(gs_engine* g, gs_trace_event* out, int64_t cap, int64_t* n) {
   Sim& s = g->sim;
   if (s.traceRead == 0) {
@@ -1628,7 +1707,7 @@ int gs_trace_read(gs_engine* g, gs_trace_event* out, int64_t cap, int64_t* n) {
       s.events.insert(s.events.end(), nd.ev.begin(), nd.ev.end());
       nd.ev.clear();
     }
-    std::stable_sort(s.events.begin(), s.events.end(), gs_trace_less);
+    gs_trace_canonical(s.events, s.cfg.seed, s.gp.MaxIHaveLength);
   }
   const int64_t k = std::min<int64_t>(cap, (int64_t)(s.events.size() - s.traceRead));
   for (int64_t i = 0; i < k; ++i) out[i] = s.events[s.traceRead + i];
