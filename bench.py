@@ -212,9 +212,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="partition", choices=["partition", "replicas"])
     ap.add_argument("--peers", type=int, default=0, help="override the workload's peer count (rehearsals)")
-    ap.add_argument("--transport", default="rccl", choices=["rccl", "torch"],
-                    help="partitioned ranks' exchange: the product library's native RCCL transport "
-                         "(include/gs_transport.h) or torch.distributed collectives")
+    ap.add_argument("--transport", default="torch", choices=["rccl", "torch"],
+                    help="partitioned ranks' exchange: torch.distributed collectives (RCCL under the "
+                         "nccl backend; the default, whose multi-rank path the tests run over gloo) or "
+                         "the product library's native RCCL transport (include/gs_transport.h), which "
+                         "has run at world 1 only")
     ap.add_argument("--rpc-accounting", action="store_true",
                     help="also sum RPC bytes per edge (gs_set_rpc_accounting; 1 KB messages, 40-byte ids)")
     ap.add_argument("--lib", default=None, help="timing experiments only: another build of the product library "
