@@ -235,7 +235,16 @@ struct Dev {
   int64_t* cIwant[2];  // IWANT request list: arena record (off << 24 | count), -1 = none
   int64_t* cIresp[2];  // messages served for an IWANT: arena record, -1 = none;
                        // indexed by the receiver's in-edge (rev of the sender's edge)
-  int32_t* pool[2];    // slot-id arena for IWANT lists / responses
+  int32_t* pool[2];    // slot-id arena for IWANT lists / responses (and PX lists)
+  // peer exchange (GS_FLAG_PEER_EXCHANGE, unscored engines): a PRUNE's peer
+  // list per (edge, topic) as arena entries topic << 26 | peer node, one record
+  // per edge and hop parity; the dial requests of the hop (v << 32 | peer)
+  int32_t doPX, PrunePeers;
+  int64_t* cPx[2];
+  unsigned long long* pxq;
+  unsigned long long* pxqN;
+  int64_t pxqCap;
+  double acceptPX;
   unsigned long long* poolCnt;  // [2] bump pointers
   int64_t poolCap;     // ids per arena
   // message slots

@@ -10,6 +10,7 @@
 #include <array>
 #include "../../include/gs_rpcsize.h"
 #include <map>
+#include <set>
 #include <tuple>
 #include <chrono>
 #include <cmath>
@@ -153,6 +154,12 @@ struct gs_engine {
   // RPC events (gs_set_trace_rpc): RECV blocks of hops not run yet, and the
   // connections closed at the start of a hop (their in-flight RPCs are lost)
   bool traceRpc = false;
+  // peer exchange (GS_FLAG_PEER_EXCHANGE) and connections down at the start
+  bool doPX = false;
+  std::set<std::pair<int, int>> dormant;       // gs_set_dormant (a < b)
+  std::vector<std::pair<int, int>> pxPend;     // dials of the previous hop (connected at this hop's start)
+  std::vector<unsigned long long> pxqH;
+  int readPx();
   std::vector<gs_trace_event> traceFuture;
   std::vector<std::array<int64_t, 3>> rpcDowns;  // (hop, receiver, sender)
   // an RPC block recorded on the host: hello packets and announcements
@@ -315,6 +322,14 @@ static void score_rows(const Dev& d, int64_t nEdges, int T, double* out, hipStre
   } while (0)
 
 int gs_engine::start() {
+  if (doPX && (scoring || gaterOn || behaveAll != 0 || world > 1 || acctOn)) {
+    gs_set_error("peer exchange is supported by an unscored, honest, unpartitioned engine without RPC accounting");
+    return GS_EUNSUPPORTED;
+  }
+  if (!dormant.empty() && (scoring || acctOn || world > 1)) {
+    gs_set_error("dormant connections are supported by an unscored, unpartitioned engine without RPC accounting");
+    return GS_EUNSUPPORTED;
+  }
   HIPCHECK(hipSetDevice(cfg.device));
   HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   // reverse edges, edge sources, P6
@@ -539,6 +554,18 @@ int gs_engine::start() {
   x.poolCap = (int64_t)(rank + 1) * poolSeg;
   for (int k = 0; k < 2; ++k) { x.pool[k] = dalloc<int32_t>((size_t)poolSeg * world); chk(x.pool[k]); }
   x.poolCnt = dalloc<unsigned long long>(2); chk(x.poolCnt);
+  x.doPX = doPX ? 1 : 0;
+  x.PrunePeers = gp.PrunePeers;
+  x.acceptPX = thr.AcceptPXThreshold;
+  x.cPx[0] = x.cPx[1] = nullptr;
+  x.pxq = x.pxqN = nullptr;
+  x.pxqCap = 0;
+  if (doPX) {
+    for (int k = 0; k < 2; ++k) { x.cPx[k] = dalloc<int64_t>(E, 0xFF); chk(x.cPx[k]); }
+    x.pxqCap = std::max<int64_t>(1 << 16, 4 * (int64_t)N);
+    x.pxq = dalloc<unsigned long long>((size_t)x.pxqCap); x.pxqN = dalloc<unsigned long long>(1);
+    chk(x.pxq); chk(x.pxqN);
+  }
   x.slotSrc = dalloc<int32_t>(S, 0xFF); x.slotPubHop = dalloc<int64_t>(S); x.slotMid = dalloc<int64_t>(S, 0xFF);
   chk(x.slotSrc); chk(x.slotPubHop); chk(x.slotMid);
   // adversarial model
@@ -642,13 +669,14 @@ int gs_engine::start() {
     // floodsub.go:103) of the traced hosts at time 0, recorded on the host
     for (int u = n0; u < n1; ++u) {
       if (!traceMask[u]) continue;
+      auto up = [&](int64_t e) { return !dormant.count({std::min(u, col[e]), std::max(u, col[e])}); };
       for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e)
-        tracePending.push_back(gs_trace_event{0, -1, GS_TRACE_ADD_PEER, u, col[e], -1, 0, 0});
+        if (up(e)) tracePending.push_back(gs_trace_event{0, -1, GS_TRACE_ADD_PEER, u, col[e], -1, 0, 0});
       for (int t = 0; t < T; ++t)
         if ((sub[u] >> t) & 1) tracePending.push_back(gs_trace_event{0, -1, GS_TRACE_JOIN, u, -1, (int16_t)t, 0, 0});
       // the hello packet of every peer (pubsub.go:495; its RecvRPC at time 0)
       for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e)
-        hostRpc(GS_TRACE_RECV_RPC, u, col[e], 0, GS_RPC_ORD(0, GS_RPC_O_HELLO), -1, sub[col[e]], 1);
+        if (up(e)) hostRpc(GS_TRACE_RECV_RPC, u, col[e], 0, GS_RPC_ORD(0, GS_RPC_O_HELLO), -1, sub[col[e]], 1);
     }
     if (traceRpc && world > 1) {
       gs_set_error("RPC trace events need an unpartitioned engine");
@@ -679,9 +707,17 @@ int gs_engine::start() {
     HIPCHECK(hipMemcpyAsync(x.lastpub, lp.data(), lp.size() * 8, hipMemcpyHostToDevice, stream));
     HIPCHECK(hipStreamSynchronize(stream));
   }
-  if (!events.empty()) {
+  if (!events.empty() || doPX || !dormant.empty()) {
     const int rc = enableChurn();
     if (rc) return rc;
+  }
+  if (!dormant.empty()) {  // gs_set_dormant: these connections start down
+    std::vector<uint8_t> al((size_t)E, 1);
+    for (int u = 0; u < N; ++u)
+      for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e)
+        if (dormant.count({std::min(u, col[e]), std::max(u, col[e])})) al[e] = aliveH[e] = 0;
+    HIPCHECK(hipMemcpyAsync(d.alive, al.data(), (size_t)E, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipStreamSynchronize(stream));  // al is pageable
   }
   x.rpcB = x.rpcN = nullptr;
   x.acc = nullptr;
@@ -814,6 +850,26 @@ int gs_engine::enableChurn() {
   return GS_OK;
 }
 
+// The peer-exchange dial requests of this hop (v << 32 | peer), for the next
+// hop's applyEvents.
+int gs_engine::readPx() {
+  unsigned long long n = 0;
+  HIPCHECK(hipMemcpyAsync(&n, d.pxqN, 8, hipMemcpyDeviceToHost, stream));
+  HIPCHECK(hipStreamSynchronize(stream));
+  n = std::min<unsigned long long>(n, (unsigned long long)d.pxqCap);
+  if (n) {
+    pxqH.resize(n);
+    HIPCHECK(hipMemcpyAsync(pxqH.data(), d.pxq, n * 8, hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipMemsetAsync(d.pxqN, 0, 8, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
+    for (unsigned long long x : pxqH) {
+      const int a = (int)(x >> 32), b = (int)(x & 0xFFFFFFFFu);
+      pxPend.push_back({std::min(a, b), std::max(a, b)});
+    }
+  }
+  return GS_OK;
+}
+
 int gs_engine::uploadList(const std::vector<int32_t>& v) {
   if ((int64_t)v.size() > evCap) {
     int32_t* p = nullptr;
@@ -855,7 +911,25 @@ int gs_engine::applyEvents(int64_t h) {
     auto it = std::lower_bound(bgn, fin, b);
     return (int64_t)(it - col.begin());
   };
-  for (int pass = GS_EV_DISCONNECT; pass <= GS_EV_JOIN; ++pass)
+  for (int pass = GS_EV_DISCONNECT; pass <= GS_EV_JOIN; ++pass) {
+    if (pass == GS_EV_LEAVE && doPX) {
+      // the peer-exchange dials of the previous hop complete, after this hop's
+      // scheduled disconnects and connects: each pair once, ascending
+      std::sort(pxPend.begin(), pxPend.end());
+      pxPend.erase(std::unique(pxPend.begin(), pxPend.end()), pxPend.end());
+      for (auto& pr : pxPend) {
+        const int64_t ab = edgeOf(pr.first, pr.second), ba = edgeOf(pr.second, pr.first);
+        if (aliveH[ab]) continue;
+        aliveH[ab] = aliveH[ba] = 1;
+        up.push_back((int32_t)ab);
+        up.push_back((int32_t)ba);
+        if (traceRpc) {
+          hostRpc(GS_TRACE_RECV_RPC, pr.first, pr.second, h, GS_RPC_ORD(0, GS_RPC_O_HELLO), -1, sub[pr.second], 1);
+          hostRpc(GS_TRACE_RECV_RPC, pr.second, pr.first, h, GS_RPC_ORD(0, GS_RPC_O_HELLO), -1, sub[pr.first], 1);
+        }
+      }
+      pxPend.clear();
+    }
     for (size_t k = nextEv; k < end; ++k) {
       const Event& ev = events[k];
       if (ev.kind != pass) continue;
@@ -900,6 +974,7 @@ int gs_engine::applyEvents(int64_t h) {
         (joinEv ? joinM : leaveM)[ev.a] |= bit;
       }
     }
+  }
   nextEv = end;
   // one item per node: node, topic mask (lo, hi) — its topics run in one wave
   // (a partitioned rank: its own nodes)
@@ -1167,6 +1242,10 @@ int gs_engine::stepOne() {
   // RPC accounting: this hop's forwarded and published messages, one RPC each
   if (acctOn && nOwn) k_acct_payload<<<nOwn, 64, 0, stream>>>(d, cur);
   if (traceRpc && nOwn) k_trace_payload<<<nOwn, 64, 0, stream>>>(d, cur, h);
+  if (doPX) {
+    const int rc = readPx();
+    if (rc) return rc;
+  }
   HIPCHECK(hipGetLastError());
   if (world > 1) {
     const int rc = exchange(cur, heartbeatDue(now));
@@ -1533,6 +1612,7 @@ int gs_engine_create(const gs_config* cfg, const gs_gossipsub_params* gsp, const
   if (gsp) g->gp = *gsp; else gs_default_gossipsub_params(&g->gp);
   g->scoring = (cfg->flags & GS_FLAG_SCORING) != 0 && cfg->router == GS_ROUTER_GOSSIPSUB;
   g->floodPublish = (cfg->flags & GS_FLAG_FLOOD_PUBLISH) != 0;
+  g->doPX = (cfg->flags & GS_FLAG_PEER_EXCHANGE) != 0 && cfg->router == GS_ROUTER_GOSSIPSUB;
   g->record = (cfg->flags & GS_FLAG_RECORD_DELIVERIES) != 0;
   g->tps.assign(g->T, gs_topic_score_params{});
   g->tscored.assign(g->T, 0);
@@ -1873,6 +1953,23 @@ int gs_set_trace(gs_engine* g, const uint8_t* node_mask, int64_t capacity) {
   if (node_mask) g->traceMask.assign(node_mask, node_mask + g->N);
   else g->traceMask.clear();
   g->traceCap = capacity;
+  return GS_OK;
+}
+
+int gs_set_dormant(gs_engine* g, int32_t n, const int32_t* a, const int32_t* b) {
+  if (g->started) { gs_set_error("gs_set_dormant: before the first step"); return GS_ESTATE; }
+  if (!g->graphSet) { gs_set_error("graph not set"); return GS_ESTATE; }
+  if (n < 0 || (n > 0 && (!a || !b))) { gs_set_error("gs_set_dormant: bad arguments"); return GS_EINVAL; }
+  for (int32_t i = 0; i < n; ++i) {
+    bool ok = a[i] >= 0 && a[i] < g->N && b[i] >= 0 && b[i] < g->N;
+    if (ok) {
+      auto bgn = g->col.begin() + g->rowptr[a[i]], fin = g->col.begin() + g->rowptr[a[i] + 1];
+      auto it = std::lower_bound(bgn, fin, b[i]);
+      ok = it != fin && *it == b[i];
+    }
+    if (!ok) { gs_set_error("gs_set_dormant: not an edge of the graph"); return GS_EINVAL; }
+    g->dormant.insert({std::min(a[i], b[i]), std::max(a[i], b[i])});
+  }
   return GS_OK;
 }
 

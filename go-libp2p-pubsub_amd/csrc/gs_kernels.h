@@ -348,7 +348,7 @@ __global__ __launch_bounds__(64) void k_join(Dev d, int64_t hop, int64_t now, in
   const uint64_t joined = d.sub[u];
   for (int t = 0; t < d.T; ++t) {
     if (!((joined >> t) & 1)) continue;
-    const bool cand = valid && ((subv >> t) & 1) && !dir && s >= 0;
+    const bool cand = valid && edge_up(d, e) && ((subv >> t) & 1) && !dir && s >= 0;
     const uint64_t key = gs_key64(d.seed, GS_SITE_GP_JOIN, u, (uint32_t)hop, v, t);
     const bool sel = select_k(cand, key, d.D);
     if (sel) {

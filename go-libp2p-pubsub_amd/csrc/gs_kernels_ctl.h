@@ -8,14 +8,24 @@
 // handleGraft for one topic from sender edge e (gossipsub.go:713-792).
 // Scalar (wave-uniform) code; meshcnt is held by lane t.  Returns true when a
 // PRUNE for t must be sent back.
+// noPX: set when this GRAFT takes the peer exchange off the RPC's PRUNEs
+// (unknown topic, direct peer, backoff, negative score: gossipsub.go:716-775).
 __device__ __forceinline__ bool graft_one(const Dev& d, int64_t e, int v, int t, double sc, int64_t now,
-                                          int& meshcnt_lane, uint64_t& meshE, bool& dirty, bool& dirtyUp) {
-  if (!((d.sub[v] >> t) & 1)) return false;  // unknown topic: ignore
+                                          int& meshcnt_lane, uint64_t& meshE, bool& dirty, bool& dirtyUp,
+                                          bool& noPX) {
+  if (!((d.sub[v] >> t) & 1)) {  // unknown topic: ignore
+    noPX = true;
+    return false;
+  }
   if ((meshE >> t) & 1) return false;         // already in mesh
-  if (d.direct[e]) return true;
+  if (d.direct[e]) {
+    noPX = true;
+    return true;
+  }
   const int64_t bi = tix(d, t, e);
   const int64_t be = d.backoff[bi];
   if (be != 0 && now < be) {
+    noPX = true;
     if (d.scoring) {
       d.bp[e] += 1.0;
       const int64_t floodCutoff = be + (d.GraftFloodThreshold - d.PruneBackoff);
@@ -27,6 +37,7 @@ __device__ __forceinline__ bool graft_one(const Dev& d, int64_t e, int v, int t,
     return true;
   }
   if (sc < 0) {
+    noPX = true;
     add_backoff(d, e, t, now, d.PruneBackoff);
     return true;
   }
@@ -61,6 +72,80 @@ __device__ __forceinline__ void prune_topics(const Dev& d, int64_t e, int v, uin
     }
     add_backoff(d, e, t, now, d.PruneRecv);
   }
+}
+
+// ---- peer exchange (GS_FLAG_PEER_EXCHANGE; the engine supports it unscored)
+// makePrune's peer list (gossipsub.go:1811-1836) for the PRUNE of topic t to
+// v's peer on lane p: getPeers(topic, PrunePeers, xp != p && Score(xp) >= 0) —
+// unscored every connected peer of v subscribed to t passes — with its own
+// shuffle (GS_SITE_PX keyed by the pruned peer too).  Wave-uniform; returns
+// the lane mask of the list.
+__device__ __forceinline__ uint64_t px_sel(const Dev& d, int v, int64_t base, int deg, int t, int64_t hop, int p) {
+  const int lane = lane_id();
+  const bool valid = lane < deg;
+  const int64_t e = base + lane;
+  const int u = valid ? d.col[e] : 0;
+  const bool cand = valid && lane != p && edge_up(d, e) && ((d.subA[u] >> t) & 1);
+  const uint32_t pp = (uint32_t)d.col[base + p];
+  const uint64_t key = gs_key64(d.seed, GS_SITE_PX, v, (uint32_t)hop, u, (pp << 6) | (uint32_t)t);
+  return __ballot(select_k(cand, key, d.PrunePeers));
+}
+// Appends the list (lane mask of v's edges) of topic t to the PX record of the
+// receiver's in-edge re.  One lane; the record is rewritten into a new arena
+// segment (the entries of earlier PRUNEs to the same peer in this hop first).
+__device__ __forceinline__ void px_append(const Dev& d, int cur, int64_t re, int t, uint64_t list, int64_t base) {
+  const int k = __popcll(list);
+  if (!k) return;
+  const int64_t old = d.cPx[cur][re];
+  const int on = old >= 0 ? (int)(old & 0xFFFFFF) : 0;
+  const int64_t oo = old >= 0 ? (old >> 24) : 0;
+  const unsigned long long off = atomicAdd(&d.poolCnt[cur], (unsigned long long)(on + k));
+  if ((int64_t)(off + on + k) > d.poolCap) {
+    set_err(d, E_POOL);
+    return;
+  }
+  for (int q = 0; q < on; ++q) d.pool[cur][off + q] = d.pool[cur][oo + q];
+  int w = on;
+  for (uint64_t m = list; m; m &= m - 1)
+    d.pool[cur][off + w++] = (int32_t)(((uint32_t)t << 26) | (uint32_t)d.col[base + __ffsll((long long)m) - 1]);
+  d.cPx[cur][re] = ((int64_t)off << 24) | (int64_t)(on + k);
+}
+// The PX entries of record rec whose topic is in `topics`: fn(topic, peer).
+template <class F>
+__device__ __forceinline__ void px_each(const Dev& d, int buf, int64_t rec, uint64_t topics, F&& fn) {
+  if (rec < 0) return;
+  const int64_t off = rec >> 24;
+  const int n = (int)(rec & 0xFFFFFF);
+  for (int q = 0; q < n; ++q) {
+    const uint32_t x = (uint32_t)d.pool[buf][off + q];
+    const int t = (int)(x >> 26);
+    if ((topics >> t) & 1) fn(t, (int)(x & 0x3FFFFFF));
+  }
+}
+__device__ __forceinline__ int px_count(const Dev& d, int buf, int64_t rec, uint64_t topics) {
+  int n = 0;
+  px_each(d, buf, rec, topics, [&](int, int) { ++n; });
+  return n;
+}
+// pxConnect (gossipsub.go:856-905) for the PX records of node v's in-edge
+// with the pruned topics `topics`: every suggested peer that v has a slot for
+// (an edge of the graph) and is not connected to is dialled (a request for the
+// host, connected at the next hop's start).  Wave-uniform.
+__device__ __forceinline__ void px_connect(const Dev& d, int v, int64_t base, int deg, int buf, int64_t rec,
+                                           uint64_t topics) {
+  const int lane = lane_id();
+  const int myCol = lane < deg ? d.col[base + lane] : -1;
+  px_each(d, buf, rec, topics, [&](int, int xp) {
+    const unsigned long long f = __ballot(myCol == xp);
+    if (!f || xp == v) return;  // no slot for this connection
+    const int j = __ffsll((long long)f) - 1;
+    if (edge_up(d, base + j)) return;  // connected already
+    if (lane == 0) {
+      const unsigned long long k = atomicAdd(d.pxqN, 1ull);
+      if ((int64_t)k < d.pxqCap) d.pxq[k] = ((unsigned long long)(uint32_t)v << 32) | (uint32_t)xp;
+      else set_err(d, E_POOL);
+    }
+  });
 }
 
 #define GS_PTXH 1024  // LDS hash slots for a node's mcache.peertx table (>= 2 * GS_PTX)
@@ -288,6 +373,15 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
       };
       uint64_t pOut = 0;
       int nR = 0;
+      const int64_t reI = d.doPX ? d.rev[ei] : 0;  // the sender's in-edge: our PX record for it
+      // makePrune with PX for the rejected topics of one RPC
+      auto pxPrunes = [&](uint64_t topics) {
+        for (uint64_t mm = topics; mm; mm &= mm - 1) {
+          const int t = __ffsll((long long)mm) - 1;
+          const uint64_t list = px_sel(d, v, base, deg, t, h, i);
+          if (lane == 0) px_append(d, cur, reI, t, list, base);
+        }
+      };
       // (1) Join RPCs: one GRAFT each (gossipsub.go:1080-1084)
       uint64_t gj = gJoin_i;
       while (gj) {
@@ -295,11 +389,12 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
         gj &= gj - 1;
         fresh();
         if (sc_i >= d.gossipThr) ph_i++;  // handleIHave's counter (no IHAVE entries)
-        bool pr;
-        pr = graft_one(d, ei, v, t, sc_i, now, meshcnt, mE, dirty, dirtyUp);
+        bool pr, noPX = false;
+        pr = graft_one(d, ei, v, t, sc_i, now, meshcnt, mE, dirty, dirtyUp, noPX);
         if (pr) {
           pOut |= 1ull << t;
           nR++;
+          if (d.doPX && !noPX) pxPrunes(1ull << t);  // this RPC's PRUNE reply carries PX
         }
       }
       // (2) reply RPCs: IWANT requests and PRUNEs answering our own control
@@ -312,6 +407,9 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
         gIW = gossipOK && iwRec_i >= 0;  // handleIWant (gossipsub.go:674-711): step 2
         gSP = gossipOK && spRec_i >= 0;
         prune_topics(d, ei, v, pRep_i, now, meshcnt, mE, dirty);
+        // PX of these PRUNEs (unscored: Score(p) = 0 against AcceptPXThreshold)
+        if (d.doPX && !(0.0 < d.acceptPX))
+          px_connect(d, v, base, deg, prv, d.cPx[prv][ei], pRep_i & d.sub[v]);
       }
       // (3) heartbeat RPC: IHAVE (step 3), GRAFT, PRUNE
       bool gIH = false;
@@ -324,14 +422,18 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
           gIH = ph_i <= d.MaxIHaveMessages && ia_i < d.MaxIHaveLength && (ihaveT_i & sv) != 0;
         }
         uint64_t g = gHb_i;
+        bool noPX = false;  // one doPX for the whole heartbeat RPC (gossipsub.go:716)
         while (g) {
           const int t = __ffsll((long long)g) - 1;
           g &= g - 1;
           bool pr;
-          pr = graft_one(d, ei, v, t, sc_i, now, meshcnt, mE, dirty, dirtyUp);
+          pr = graft_one(d, ei, v, t, sc_i, now, meshcnt, mE, dirty, dirtyUp, noPX);
           if (pr) prunes |= 1ull << t;
         }
+        if (d.doPX && !noPX) pxPrunes(prunes);
         prune_topics(d, ei, v, pHb_i, now, meshcnt, mE, dirty);
+        if (d.doPX && !(0.0 < d.acceptPX))
+          px_connect(d, v, base, deg, prv, d.cPx[prv][ei], pHb_i & d.sub[v]);
       }
       const uint64_t jrej = pOut;
       pOut |= prunes;
@@ -866,6 +968,7 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
     d.cIhave[prv][e] = 0;
     d.cIwant[prv][e] = -1;
     d.cIresp[prv][e] = -1;
+    if (d.doPX) d.cPx[prv][e] = -1;
     if (ADV && d.cSpam[prv] != nullptr) {
       d.cSpam[prv][e] = -1;
       d.cNSrv[prv][e] = 0;
@@ -905,9 +1008,11 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
           // the heartbeat RPC
           for (uint64_t m = joinRej; m; m &= m - 1) {
             const int t = __ffsll((long long)m) - 1;
-            rpc_trace(d, h, v, u, 3, 3, GS_RPC_ORD(3, t), 2, [&](auto put) {
+            const int64_t pxr = d.doPX ? d.cPx[cur][r] : -1;
+            rpc_trace(d, h, v, u, 3, 3, GS_RPC_ORD(3, t), 2 + px_count(d, cur, pxr, 1ull << t), [&](auto put) {
               put(GS_RPC_ITEM_CTL, -1, -1);
               put(GS_RPC_ITEM_PRUNE, t, -1);
+              px_each(d, cur, pxr, 1ull << t, [&](int tt, int q) { put(GS_RPC_ITEM_PX, tt, q); });
             });
           }
           // the served ids of one request list: by each request's verdict
@@ -943,10 +1048,13 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
             });
           if (iwantAny || prunesHb) {
             const int nIw = iwantAny ? (int)(iwantRec & 0xFFFFFF) : 0;
-            rpc_trace(d, h, v, u, 3, 3, GS_RPC_ORD(3, GS_RPC_O_ANS_HB), 1 + nIw + __popcll(hbPr), [&](auto put) {
+            const int64_t pxr = d.doPX ? d.cPx[cur][r] : -1;
+            rpc_trace(d, h, v, u, 3, 3, GS_RPC_ORD(3, GS_RPC_O_ANS_HB), 1 + nIw + __popcll(hbPr) + px_count(d, cur, pxr, hbPr),
+                      [&](auto put) {
               put(GS_RPC_ITEM_CTL, -1, -1);
               for (int q = 0; q < nIw; ++q) put(GS_RPC_ITEM_IWANT, -1, d.slotMid[d.pool[cur][(iwantRec >> 24) + q]]);
               for (uint64_t m = hbPr; m; m &= m - 1) put(GS_RPC_ITEM_PRUNE, __ffsll((long long)m) - 1, -1);
+              px_each(d, cur, pxr, hbPr, [&](int tt, int q) { put(GS_RPC_ITEM_PX, tt, q); });
             });
           }
         }
@@ -1625,6 +1733,22 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
     cyMesh += c1 - c0;
     cyEmit += GS_CLK() - c1;
   }
+  if (d.doPX) {
+    // makePrune with PX for every PRUNE of this heartbeat (sendGraftPrune,
+    // gossipsub.go:1636-1647; unscored: no negative-score prunes, so no noPX)
+    uint64_t any = 0;
+    for (int o = 0; o < 64; ++o) any |= lane_get64(valid ? toprune : 0ull, o);
+    for (uint64_t mm = any; mm; mm &= mm - 1) {
+      const int t = __ffsll((long long)mm) - 1;
+      unsigned long long pl = __ballot(valid && ((toprune >> t) & 1));
+      while (pl) {  // one list per pruned peer
+        const int p = __ffsll((long long)pl) - 1;
+        pl &= pl - 1;
+        const uint64_t list = px_sel(d, v, base, deg, t, hop, p);
+        if (lane == p) px_append(d, cur, d.rev[e], t, list, base);
+      }
+    }
+  }
   GS_STAMPH(3, GS_CLK());
   GS_STAMPH(6, cyMesh);
   GS_STAMPH(7, cyEmit);
@@ -1707,11 +1831,14 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
           const int t = __ffsll((long long)m) - 1;
           for (int w = t * d.Wt; w < (t + 1) * d.Wt; ++w) nIh += __popcll(gwWord(w));
         }
-        rpc_trace(d, hop, v, vcol, 4, 3, GS_RPC_ORD(4, 0), 1 + __popcll(tograft) + __popcll(toprune) + nIh,
+        const int64_t pxr = d.doPX ? d.cPx[cur][re] : -1;
+        rpc_trace(d, hop, v, vcol, 4, 3, GS_RPC_ORD(4, 0),
+                  1 + __popcll(tograft) + __popcll(toprune) + nIh + px_count(d, cur, pxr, toprune),
                   [&](auto put) {
                     put(GS_RPC_ITEM_CTL, -1, -1);
                     for (uint64_t m = tograft; m; m &= m - 1) put(GS_RPC_ITEM_GRAFT, __ffsll((long long)m) - 1, -1);
                     for (uint64_t m = toprune; m; m &= m - 1) put(GS_RPC_ITEM_PRUNE, __ffsll((long long)m) - 1, -1);
+                    px_each(d, cur, pxr, toprune, [&](int tt, int q) { put(GS_RPC_ITEM_PX, tt, q); });
                     for (uint64_t m = ihave; m; m &= m - 1) {
                       const int t = __ffsll((long long)m) - 1;
                       for (int w = t * d.Wt; w < (t + 1) * d.Wt; ++w)
@@ -1810,6 +1937,7 @@ __global__ __launch_bounds__(64) void k_edge_down(Dev d, const int32_t* __restri
     d.cPruneReply[prv][re] = 0; d.cPruneHb[prv][re] = 0; d.cIhave[prv][re] = 0;
     d.cIwant[prv][re] = -1; d.cIresp[prv][re] = -1;
     if (d.cSpam[prv] != nullptr) { d.cSpam[prv][re] = -1; d.cNSrv[prv][re] = 0; }
+    if (d.doPX) d.cPx[prv][re] = -1;
     d.fwdIn[prv][re] = make_ulonglong2(0ull, 0ull);
   }
   if (!ownE) return;
@@ -1926,6 +2054,15 @@ __global__ __launch_bounds__(64) void k_leave(Dev d, const int32_t* __restrict__
       stats_prune(d, e, t);
       if (traced) trace_emit(d, hop, GS_TRACE_PRUNE, v, d.col[e], t, -1, 0);
     }
+    if (d.doPX && !silent) {  // sendPrune's makePrune(p, topic, gs.doPX) (:1087)
+      unsigned long long pl = __ballot(m);
+      while (pl) {
+        const int p = __ffsll((long long)pl) - 1;
+        pl &= pl - 1;
+        const uint64_t list = px_sel(d, v, base, deg, t, hop, p);
+        if (lane == p) px_append(d, cur, d.rev[e], t, list, base);
+      }
+    }
     np += __popcll(__ballot(m));
   }
   if (valid && pruned) {
@@ -1942,9 +2079,12 @@ __global__ __launch_bounds__(64) void k_leave(Dev d, const int32_t* __restrict__
       if (rpc_traced(d, v, d.col[e]))
         for (uint64_t m = pruned; m; m &= m - 1) {
           const int t = __ffsll((long long)m) - 1;
-          rpc_trace(d, hop, v, d.col[e], 0, 3, GS_RPC_ORD(0, GS_RPC_O_LEAVE + t), 2, [&](auto put) {
+          const int64_t pxr = d.doPX ? d.cPx[cur][d.rev[e]] : -1;
+          rpc_trace(d, hop, v, d.col[e], 0, 3, GS_RPC_ORD(0, GS_RPC_O_LEAVE + t), 2 + px_count(d, cur, pxr, 1ull << t),
+                    [&](auto put) {
             put(GS_RPC_ITEM_CTL, -1, -1);
             put(GS_RPC_ITEM_PRUNE, t, -1);
+            px_each(d, cur, pxr, 1ull << t, [&](int tt, int q) { put(GS_RPC_ITEM_PX, tt, q); });
           });
         }
     }

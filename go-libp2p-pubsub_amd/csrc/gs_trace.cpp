@@ -167,7 +167,8 @@ struct Meta {
   bool ctl = false;
   std::vector<std::pair<int, std::vector<int64_t>>> ihave;
   std::vector<int64_t> iwant;
-  std::vector<int> graft, prune;
+  std::vector<int> graft;
+  std::vector<std::pair<int, std::vector<int>>> prune;  // (topic, PX peers)
 };
 Meta collect(const gs_trace_event* it, int64_t n) {
   Meta m;
@@ -183,7 +184,11 @@ Meta collect(const gs_trace_event* it, int64_t n) {
         break;
       case GS_RPC_ITEM_IWANT: m.iwant.push_back(x.msg); break;
       case GS_RPC_ITEM_GRAFT: m.graft.push_back(x.topic); break;
-      case GS_RPC_ITEM_PRUNE: m.prune.push_back(x.topic); break;
+      case GS_RPC_ITEM_PRUNE: m.prune.push_back({x.topic, {}}); break;
+      case GS_RPC_ITEM_PX:
+        for (auto& pr : m.prune)
+          if (pr.first == x.topic) pr.second.push_back((int)x.msg);
+        break;
       default: break;
     }
   }
@@ -221,9 +226,10 @@ std::string meta_pb(const Meta& m, const std::function<std::string(int)>& tn) {
       put_bytes(b, 1, tn(t));
       put_bytes(c, 3, b);
     }
-    for (int t : m.prune) {  // peers: none (no PX records), an empty repeated field
+    for (auto& pr : m.prune) {  // ControlPruneMeta{topic=1, peers=2}
       std::string b;
-      put_bytes(b, 1, tn(t));
+      put_bytes(b, 1, tn(pr.first));
+      for (int q : pr.second) put_bytes(b, 2, peer_bytes(q));
       put_bytes(c, 4, b);
     }
     put_bytes(o, 3, c);
@@ -287,7 +293,16 @@ std::string meta_json(const Meta& m, const std::function<std::string(int)>& tn) 
     if (!m.prune.empty()) {
       csep();
       c += "\"prune\":[";
-      for (size_t i = 0; i < m.prune.size(); ++i) c += std::string(i ? "," : "") + "{\"topic\":" + jstr(tn(m.prune[i])) + "}";
+      for (size_t i = 0; i < m.prune.size(); ++i) {
+        c += std::string(i ? "," : "") + "{\"topic\":" + jstr(tn(m.prune[i].first));
+        if (!m.prune[i].second.empty()) {
+          c += ",\"peers\":[";
+          for (size_t k = 0; k < m.prune[i].second.size(); ++k)
+            c += std::string(k ? "," : "") + "\"" + b64(peer_bytes(m.prune[i].second[k])) + "\"";
+          c += "]";
+        }
+        c += "}";
+      }
       c += "]";
     }
     o += "\"control\":" + c + "}";

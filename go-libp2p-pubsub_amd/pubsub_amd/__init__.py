@@ -15,4 +15,5 @@ from .params import (DefaultGossipSubParams, DefaultPeerGaterParams, GossipSubPa
 from .engine import (PRODUCT_LIB, Engine, GossipEngineError, NewFloodSub, NewGossipSub,  # noqa: F401
                      NewRandomSub, PROTOCOLS, WithDevice, WithEventTracer, encode_trace, WithDirectPeers, WithFloodPublish, WithGossipSubParams,
                      WithHop, WithMessageWindow, WithPartition, WithPeerScore, WithRecordDeliveries, WithSeed,
-                     WithBehaviour, WithPeerGater, WithRPCAccounting, WithValidation, load)
+                     WithBehaviour, WithPeerGater, WithRPCAccounting, WithValidation, WithPeerExchange, WithDormant,
+                     load)

@@ -24,6 +24,7 @@ GS_ROUTER_GOSSIPSUB = 2
 GS_FLAG_SCORING = 1 << 0
 GS_FLAG_FLOOD_PUBLISH = 1 << 1
 GS_FLAG_RECORD_DELIVERIES = 1 << 2
+GS_FLAG_PEER_EXCHANGE = 1 << 3
 
 GS_MSG_VALID, GS_MSG_REJECT, GS_MSG_IGNORE, GS_MSG_PHANTOM = 0, 1, 2, 3
 GS_BEHAVE_NO_FORWARD, GS_BEHAVE_IWANT_SPAM, GS_BEHAVE_GRAFT_SPAM, GS_BEHAVE_IHAVE_SPAM = 1, 2, 4, 8
@@ -104,7 +105,7 @@ GS_TRACE_FORMAT_PB, GS_TRACE_FORMAT_JSON = 0, 1
 # not a pb.TraceEvent type: one RPCMeta entry of the RPC event before it (gossip_engine.h)
 GS_TRACE_RPC_ITEM = 32
 (GS_RPC_ITEM_MSG, GS_RPC_ITEM_SUB, GS_RPC_ITEM_CTL, GS_RPC_ITEM_IHAVE, GS_RPC_ITEM_IWANT, GS_RPC_ITEM_GRAFT,
- GS_RPC_ITEM_PRUNE) = range(7)
+ GS_RPC_ITEM_PRUNE, GS_RPC_ITEM_PX) = range(8)
 
 
 class CountersC(C.Structure):
@@ -186,6 +187,7 @@ ABI_FUNCTIONS = [
     ("gs_read_rpc_bytes", C.c_int, [P, C.POINTER(i64), C.POINTER(i64)]),
     ("gs_set_trace", C.c_int, [P, C.POINTER(u8), i64]),
     ("gs_set_trace_rpc", C.c_int, [P, i32]),
+    ("gs_set_dormant", C.c_int, [P, i32, C.POINTER(i32), C.POINTER(i32)]),
     ("gs_trace_read", C.c_int, [P, P, i64, C.POINTER(i64)]),
     ("gs_trace_encode", C.c_int, [P, i64, i32, i64, C.POINTER(C.c_char_p), C.c_char_p, P, i64, C.POINTER(i64)]),
     ("gs_set_profiling", C.c_int, [P, C.c_int]),

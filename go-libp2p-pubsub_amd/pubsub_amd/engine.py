@@ -63,6 +63,18 @@ def WithFloodPublish(flood):
     return ("flood_publish", bool(flood))
 
 
+def WithPeerExchange(do_px=True):
+    """WithPeerExchange (gossipsub.go:320): PRUNEs carry peer suggestions and a
+    pruned host dials them (needs connection slots: WithDormant)."""
+    return ("px", bool(do_px))
+
+
+def WithDormant(pairs):
+    """Connections (a, b) of the graph that start down (gs_set_dormant): slots
+    a peer-exchange dial or a GS_EV_CONNECT event can bring up."""
+    return ("dormant", [(int(a), int(b)) for a, b in pairs])
+
+
 def WithDirectPeers(direct_edges):
     """direct_edges: uint8[E] flags in CSR order (WithDirectPeers, gossipsub.go:338)."""
     return ("direct", direct_edges)
@@ -155,6 +167,8 @@ class Engine:
             flags |= _abi.GS_FLAG_SCORING
         if opts.get("flood_publish"):
             flags |= _abi.GS_FLAG_FLOOD_PUBLISH
+        if opts.get("px"):
+            flags |= _abi.GS_FLAG_PEER_EXCHANGE
         if opts.get("record"):
             flags |= _abi.GS_FLAG_RECORD_DELIVERIES
         cfg.flags = flags
@@ -185,6 +199,11 @@ class Engine:
         direct = np.ascontiguousarray(direct, dtype=np.uint8) if direct is not None else None
         _check(self.lib, self.lib.gs_set_graph(h, _ptr(self.rowptr, C.c_int64), _ptr(self.col, C.c_int32),
                                                _ptr(ob, C.c_uint8), _ptr(direct, C.c_uint8)))
+        dormant = opts.get("dormant")
+        if dormant:
+            da = np.array([a for a, _ in dormant], dtype=np.int32)
+            db = np.array([b for _, b in dormant], dtype=np.int32)
+            _check(self.lib, self.lib.gs_set_dormant(h, len(da), _ptr(da, C.c_int32), _ptr(db, C.c_int32)))
         tr = opts.get("trace")
         if tr is not None:
             nodes, cap, rpc = tr

@@ -59,6 +59,12 @@ extern "C" {
 /* ---- engine flags ------------------------------------------------------ */
 #define GS_FLAG_SCORING (1u << 0)       /* WithPeerScore (gossipsub.go:258)    */
 #define GS_FLAG_FLOOD_PUBLISH (1u << 1) /* WithFloodPublish (gossipsub.go:304) */
+#define GS_FLAG_PEER_EXCHANGE (1u << 3) /* WithPeerExchange (gossipsub.go:320): PRUNEs carry
+                                           up to PrunePeers peers (makePrune :1803-1839); a
+                                           pruned host connects to them (pxConnect :856-905)
+                                           when the pruner's score is >= AcceptPXThreshold.
+                                           A connection needs a slot in the graph: an edge of
+                                           gs_set_graph that is down (gs_set_dormant, churn) */
 #define GS_FLAG_RECORD_DELIVERIES (1u << 2) /* keep per-(node,message) first
                                                delivery hop/sender for readback */
 
@@ -296,6 +302,12 @@ int gs_set_behaviour(gs_engine* eng, const uint8_t* behaviour /*[N]*/);
  * An event that finds its state already (a connection down twice, a topic
  * left twice) does nothing.  Not supported together with a partitioned engine
  * or the peer gater (GS_EUNSUPPORTED). */
+/* Before the first step: the connections a[i]-b[i] (edges of the graph, both
+ * directions) start down: no AddPeer, no hello, no score record.  A
+ * GS_EV_CONNECT or a peer-exchange connect (GS_FLAG_PEER_EXCHANGE) brings one
+ * up.  A PX-suggested peer without such a slot cannot be dialled (the
+ * reference's connector dials any peer; the simulated graph is fixed). */
+int gs_set_dormant(gs_engine* eng, int32_t n, const int32_t* a, const int32_t* b);
 #define GS_EV_DISCONNECT 0
 #define GS_EV_CONNECT 1
 #define GS_EV_LEAVE 2
@@ -420,7 +432,8 @@ int gs_read_deliveries(gs_engine* eng, int64_t id, int32_t* hop /*[N]*/,
 #define GS_RPC_ITEM_IHAVE 3 /* ControlMeta.ihave[topic].messageIDs[]                     */
 #define GS_RPC_ITEM_IWANT 4 /* ControlMeta.iwant[0].messageIDs[]                         */
 #define GS_RPC_ITEM_GRAFT 5 /* ControlMeta.graft[]: ControlGraftMeta{topic}               */
-#define GS_RPC_ITEM_PRUNE 6 /* ControlMeta.prune[]: ControlPruneMeta{topic} (no PX peers) */
+#define GS_RPC_ITEM_PRUNE 6 /* ControlMeta.prune[]: ControlPruneMeta{topic}              */
+#define GS_RPC_ITEM_PX 7    /* ControlPruneMeta.peers[] of the PRUNE of `topic` (msg = the peer) */
 /* One traced event of host `node` (32 bytes).  Recorded: PUBLISH_MESSAGE
  * (validation.go:217), DELIVER_MESSAGE / DUPLICATE_MESSAGE (pubsub.go:1011,
  * 1057; receivedFrom = peer), ADD_PEER (gossipsub.go:507, floodsub.go:45),

@@ -42,7 +42,10 @@ enum {
   GS_SITE_EMIT_PEERS = 10,     /* {node, hop, peer, topic}  gossipsub.go:1695 */
   GS_SITE_EMIT_MIDS = 11,      /* {node, peer, msg_id, hop} gossipsub.go:1707 */
   GS_SITE_IWANT = 12,          /* {node, peer, msg_id, hop} gossipsub.go:663, gossip_tracer.go:53 */
-  GS_SITE_GATER = 13           /* {node, peer, hop, 0}      peer_gater.go:357 */
+  GS_SITE_GATER = 13,          /* {node, peer, hop, 0}      peer_gater.go:357 */
+  GS_SITE_PX = 14,             /* {node, hop, peer, pruned << 6 | topic}  gossipsub.go:1813 makePrune's
+                                  getPeers (a fresh shuffle per PRUNE: keyed by the pruned peer too) */
+  GS_SITE_PX_CONNECT = 15      /* {node, hop, peer, 0}      gossipsub.go:858 pxConnect's shufflePeerInfo */
 };
 
 GS_HD void gs_mulhilo32(uint32_t a, uint32_t b, uint32_t* hi, uint32_t* lo) {

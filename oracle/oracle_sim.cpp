@@ -33,7 +33,7 @@ static thread_local std::string g_err;
 void set_error(const std::string& s) { g_err = s; }
 
 struct IHaveEntry { int topic; std::vector<int64_t> mids; };
-struct PruneEntry { int topic; uint64_t backoff; bool hasBackoff; };
+struct PruneEntry { int topic; uint64_t backoff; bool hasBackoff; std::vector<int> px; };
 struct Control {
   std::vector<IHaveEntry> ihave;
   std::vector<int64_t> iwant;
@@ -105,7 +105,9 @@ struct Node {
   void handlePrune(int p, const Control& ctl);
   void addBackoff(int p, int topic);
   void doAddBackoff(int p, int topic, int64_t interval);
-  PruneEntry makePrune(int p, int topic);
+  PruneEntry makePrune(int p, int topic, bool doPX);
+  void pxConnect(std::vector<int> px);   // gossipsub.go:856-905
+  std::vector<int> pxReq;                // peers to dial (connected at the next hop's start)
   void heartbeat();
   void emitGossip(int topic, const std::set<int>& exclude);
   void removePeer(int p);                // handleDeadPeers + RemovePeer
@@ -124,6 +126,8 @@ struct Sim {
   std::vector<uint8_t> tscored;
   gs_peer_score_thresholds thr{};
   bool scoring = false, floodPublish = false, record = false;
+  bool doPX = false;                                    // WithPeerExchange
+  std::set<std::pair<int, int>> dormant;               // gs_set_dormant: connections down at the start
   bool gaterOn = false;
   // Reference order (gs_oracle_reference_order): each RPC is
   // handled whole, in arrival order — AcceptFrom on the live score and gater,
@@ -248,7 +252,10 @@ void Sim::emitRpc(int type, int node, int peer, int phase, int64_t ord, const RP
         for (int64_t mid : ih.mids) item(GS_RPC_ITEM_IHAVE, ih.topic, mid);
       for (int64_t mid : r->ctl.iwant) item(GS_RPC_ITEM_IWANT, -1, mid);
       for (int t : r->ctl.graft) item(GS_RPC_ITEM_GRAFT, t, -1);
-      for (const PruneEntry& pe : r->ctl.prune) item(GS_RPC_ITEM_PRUNE, pe.topic, -1);
+      for (const PruneEntry& pe : r->ctl.prune) {
+        item(GS_RPC_ITEM_PRUNE, pe.topic, -1);
+        for (int q : pe.px) item(GS_RPC_ITEM_PX, pe.topic, q);
+      }
     }
   }
   for (auto& st : subs) item(GS_RPC_ITEM_SUB, st.first, st.second);
@@ -628,17 +635,19 @@ std::vector<PruneEntry> Node::handleGraft(int p, const Control& ctl) {
   std::vector<int> prune;
   double sc = Score(p);
   int64_t now = sim->now();
+  bool doPX = sim->doPX;  // cleared by any GRAFT of the RPC that must not leak peers (:716-775)
   for (int topic : ctl.graft) {
     auto pm = mesh.find(topic);
-    if (pm == mesh.end()) continue;
+    if (pm == mesh.end()) { doPX = false; continue; }
     std::set<int>& peers = pm->second;
     if (peers.count(p)) continue;
-    if (direct.count(p)) { prune.push_back(topic); continue; }
+    if (direct.count(p)) { prune.push_back(topic); doPX = false; continue; }
     auto bt = backoff.find(topic);
     if (bt != backoff.end()) {
       auto be = bt->second.find(p);
       if (be != bt->second.end() && now < be->second) {
         if (sim->scoring) score.AddPenalty(p, 1);
+        doPX = false;
         int64_t floodCutoff = be->second + (sim->gp.GraftFloodThreshold - sim->gp.PruneBackoff);
         if (now < floodCutoff && sim->scoring) score.AddPenalty(p, 1);
         addBackoff(p, topic);
@@ -646,7 +655,7 @@ std::vector<PruneEntry> Node::handleGraft(int p, const Control& ctl) {
         continue;
       }
     }
-    if (sc < 0) { prune.push_back(topic); addBackoff(p, topic); continue; }
+    if (sc < 0) { prune.push_back(topic); doPX = false; addBackoff(p, topic); continue; }
     if ((int)peers.size() >= sim->gp.Dhi && !outbound[p]) {
       prune.push_back(topic);
       addBackoff(p, topic);
@@ -657,12 +666,14 @@ std::vector<PruneEntry> Node::handleGraft(int p, const Control& ctl) {
     peers.insert(p);
   }
   std::vector<PruneEntry> res;
-  for (int t : prune) res.push_back(makePrune(p, t));
+  for (int t : prune) res.push_back(makePrune(p, t, doPX));
   return res;
 }
 
 // handlePrune — gossipsub.go:806-838 (PX ignored: no peer records).
 void Node::handlePrune(int p, const Control& ctl) {
+  if (ctl.prune.empty()) return;
+  const double sc = Score(p);  // :807, before any of the RPC's prunes
   for (const PruneEntry& pr : ctl.prune) {
     auto pm = mesh.find(pr.topic);
     if (pm == mesh.end()) continue;
@@ -673,6 +684,27 @@ void Node::handlePrune(int p, const Control& ctl) {
       doAddBackoff(p, pr.topic, (int64_t)pr.backoff * kSecond);
     else
       addBackoff(p, pr.topic);
+    // PX from peers with insufficient score is ignored (:827-836)
+    if (!pr.px.empty() && !(sc < sim->thr.AcceptPXThreshold)) pxConnect(pr.px);
+  }
+}
+
+// pxConnect — gossipsub.go:856-905: at most PrunePeers suggestions (shuffled
+// then truncated), the ones not connected yet are dialled.  A dial needs a slot
+// in the simulated graph (a connection that is down); it completes at the
+// start of the next hop (the connector goroutine, :907-937).
+void Node::pxConnect(std::vector<int> px) {
+  if ((int)px.size() > sim->gp.PrunePeers) {
+    std::vector<std::pair<uint64_t, int>> keyed;
+    for (int q : px) keyed.push_back({gs_key64(sim->cfg.seed, GS_SITE_PX_CONNECT, id, (uint32_t)sim->hop, q, 0), q});
+    std::sort(keyed.begin(), keyed.end());
+    px.clear();
+    for (int i = 0; i < sim->gp.PrunePeers; ++i) px.push_back(keyed[i].second);
+  }
+  for (int q : px) {
+    if (q == id || sim->edgeIndex(id, q) < 0) continue;  // no slot for this connection
+    if (!dead.count(q)) continue;                        // connected already
+    pxReq.push_back(q);
   }
 }
 
@@ -684,13 +716,24 @@ void Node::doAddBackoff(int p, int topic, int64_t interval) {  // :844-854
   int64_t cur = it == b.end() ? kTimeZero : it->second;
   if (cur < expire) b[p] = expire;
 }
-// makePrune — gossipsub.go:1803-1839 (v1.1 peers: backoff in whole seconds)
-PruneEntry Node::makePrune(int p, int topic) {
-  (void)p;
+// makePrune — gossipsub.go:1803-1839 (v1.1 peers: backoff in whole seconds;
+// with PX, up to PrunePeers other topic peers of non-negative score)
+PruneEntry Node::makePrune(int p, int topic, bool doPX) {
   PruneEntry e;
   e.topic = topic;
   e.hasBackoff = true;
   e.backoff = (uint64_t)(sim->gp.PruneBackoff / kSecond);
+  if (doPX) {  // getPeers(topic, PrunePeers, xp != p && Score(xp) >= 0), its own shuffle per PRUNE
+    auto tm = topics.find(topic);
+    std::vector<std::pair<uint64_t, int>> keyed;
+    if (tm != topics.end())
+      for (int xp : tm->second)
+        if (xp != p && Score(xp) >= 0)
+          keyed.push_back({gs_key64(sim->cfg.seed, GS_SITE_PX, id, (uint32_t)sim->hop, xp,
+                                    ((uint32_t)p << 6) | (uint32_t)topic), xp});
+    std::sort(keyed.begin(), keyed.end());
+    for (size_t i = 0; i < keyed.size() && (int)i < sim->gp.PrunePeers; ++i) e.px.push_back(keyed[i].second);
+  }
   return e;
 }
 
@@ -928,7 +971,7 @@ void Node::heartbeat() {
     r.ctl.graft = kv.second;
     auto pr = toprune.find(p);
     if (pr != toprune.end()) {
-      for (int topic : pr->second) r.ctl.prune.push_back(makePrune(p, topic));
+      for (int topic : pr->second) r.ctl.prune.push_back(makePrune(p, topic, sim->doPX && !noPX[p]));
       toprune.erase(pr);
     }
     r.sp = 4;
@@ -937,7 +980,7 @@ void Node::heartbeat() {
   for (auto& kv : toprune) {
     RPC r;
     r.hasCtl = true;
-    for (int topic : kv.second) r.ctl.prune.push_back(makePrune(kv.first, topic));
+    for (int topic : kv.second) r.ctl.prune.push_back(makePrune(kv.first, topic, sim->doPX && !noPX[kv.first]));
     r.sp = 4;
     sendRPC(kv.first, std::move(r));
   }
@@ -1006,7 +1049,7 @@ void Node::leaveTopic(int topic) {
     if (sim->scoring) score.Prune(p, topic);
     RPC r;  // sendPrune (gossipsub.go:1093-1097)
     r.hasCtl = true;
-    r.ctl.prune.push_back(makePrune(p, topic));
+    r.ctl.prune.push_back(makePrune(p, topic, sim->doPX));  // sendPrune: gs.doPX (:1087)
     r.sp = 0; r.ord = GS_RPC_O_LEAVE + topic;
     sendRPC(p, std::move(r));
   }
@@ -1052,6 +1095,22 @@ void Sim::applyEvents(std::vector<std::map<int, std::vector<RPC>>>& inbox) {
   size_t end = nextEvent;
   while (end < sched.size() && sched[end].hop == hop) end++;
   for (int pass = GS_EV_DISCONNECT; pass <= GS_EV_JOIN; ++pass) {
+  if (pass == GS_EV_LEAVE && doPX) {
+    // the peer-exchange dials of the previous hop complete (after this hop's
+    // scheduled disconnects and connects): each pair once, ascending
+    std::set<std::pair<int, int>> px;
+    for (Node& nd : nodes) {
+      for (int q : nd.pxReq) px.insert({std::min(nd.id, q), std::max(nd.id, q)});
+      nd.pxReq.clear();
+    }
+    for (auto& pr : px) {
+      if (!nodes[pr.first].dead.count(pr.second)) continue;
+      nodes[pr.first].addPeer(pr.second);
+      nodes[pr.second].addPeer(pr.first);
+      traceHello(pr.first, pr.second);
+      traceHello(pr.second, pr.first);
+    }
+  }
   std::vector<Event> evs;
   for (size_t k = nextEvent; k < end; ++k)
     if (sched[k].kind == pass) evs.push_back(sched[k]);
@@ -1117,8 +1176,14 @@ void Sim::start() {
     }
     for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) {
       int v = col[e];
-      emit(GS_TRACE_ADD_PEER, u, v, -1, -1, 0);  // AddPeer gossipsub.go:507, floodsub.go:45
       nd.nbrs.push_back(v);
+      if (dormant.count({std::min(u, v), std::max(u, v)})) {  // gs_set_dormant: not connected yet
+        nd.dead.insert(v);
+        nd.outbound[v] = outboundE.empty() ? false : outboundE[e] != 0;
+        if (!directE.empty() && directE[e]) nd.direct.insert(v);
+        continue;
+      }
+      emit(GS_TRACE_ADD_PEER, u, v, -1, -1, 0);  // AddPeer gossipsub.go:507, floodsub.go:45
       nd.outbound[v] = outboundE.empty() ? false : outboundE[e] != 0;  // AddPeer gossipsub.go:505-532
       if (!directE.empty() && directE[e]) nd.direct.insert(v);
       std::vector<uint32_t> ips;
@@ -1129,13 +1194,16 @@ void Sim::start() {
         if (!subs.empty() && ((subs[v] >> t) & 1)) nd.topics[t].insert(v);
     }
   }
+  auto up = [&](int u, int v) { return !dormant.count({std::min(u, v), std::max(u, v)}); };
   for (int u = 0; u < N; ++u)  // the hello packet of every connection (pubsub.go:495)
-    for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) traceHello(u, col[e]);
+    for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e)
+      if (up(u, col[e])) traceHello(u, col[e]);
   if (acct) {  // the hello packet of every connection (pubsub.go:495)
     rpcBytes.assign(E, 0);
     rpcCount.assign(E, 0);
     for (int u = 0; u < N; ++u)
       for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) {
+        if (!up(u, col[e])) continue;
         rpcBytes[e] += helloSize(subs.empty() ? 0 : subs[u]);
         rpcCount[e] += 1;
       }
@@ -1346,6 +1414,7 @@ int gs_engine_create(const gs_config* cfg, const gs_gossipsub_params* gsp, const
   if (gsp) s.gp = *gsp; else defaultGossipSubParams(&s.gp);
   s.scoring = (cfg->flags & GS_FLAG_SCORING) != 0 && cfg->router == GS_ROUTER_GOSSIPSUB;
   s.floodPublish = (cfg->flags & GS_FLAG_FLOOD_PUBLISH) != 0;
+  s.doPX = (cfg->flags & GS_FLAG_PEER_EXCHANGE) != 0 && cfg->router == GS_ROUTER_GOSSIPSUB;
   s.record = (cfg->flags & GS_FLAG_RECORD_DELIVERIES) != 0;
   s.tparams.assign(s.T, gs_topic_score_params{});
   s.tscored.assign(s.T, 0);
@@ -1665,9 +1734,25 @@ int gs_partition_range(const gs_engine* g, int32_t* node_begin, int32_t* node_en
   *node_end = g->sim.N;
   return GS_OK;
 }
+int gs_set_dormant(gs_engine* g, int32_t n, const int32_t* a, const int32_t* b) {
+  Sim& s = g->sim;
+  if (s.started) { set_error("gs_set_dormant: before the first step"); return GS_ESTATE; }
+  if (!s.graphSet) { set_error("graph not set"); return GS_ESTATE; }
+  if (n < 0 || (n > 0 && (!a || !b))) { set_error("gs_set_dormant: bad arguments"); return GS_EINVAL; }
+  for (int32_t i = 0; i < n; ++i) {
+    if (a[i] < 0 || a[i] >= s.N || b[i] < 0 || b[i] >= s.N || s.edgeIndex(a[i], b[i]) < 0) {
+      set_error("gs_set_dormant: not an edge of the graph");
+      return GS_EINVAL;
+    }
+    s.dormant.insert({std::min(a[i], b[i]), std::max(a[i], b[i])});
+  }
+  return GS_OK;
+}
+
 int gs_set_rpc_accounting(gs_engine* g, const int32_t* msg_size, int32_t id_len, const int32_t* topic_len) {
   Sim& sim = g->sim;
   if (sim.started) { set_error("gs_set_rpc_accounting: before the first step"); return GS_ESTATE; }
+  if (sim.doPX) { set_error("RPC byte accounting does not size peer-exchange records"); return GS_EUNSUPPORTED; }
   if (!msg_size || !topic_len || id_len < 0) { set_error("gs_set_rpc_accounting: bad arguments"); return GS_EINVAL; }
   for (int t = 0; t < sim.T; ++t)
     if (msg_size[t] < 0 || topic_len[t] < 0) { set_error("gs_set_rpc_accounting: negative size"); return GS_EINVAL; }

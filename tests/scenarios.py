@@ -533,3 +533,63 @@ ACCT = {
     "acct_churn": lambda lib, x=(): churn_scored(lib, extra=(_acct(2),) + tuple(x)),
 }
 SCENARIOS.update(ACCT)
+
+
+# ---------------------------------------------------------------- peer exchange
+# PRUNE peer exchange (WithPeerExchange, gossipsub.go:806-937, 1803-1839).
+from pubsub_amd import WithDormant, WithPeerExchange  # noqa: E402
+
+
+def px_star(lib, n=20, seed=71, extra=()):
+    """TestGossipsubStarTopology (gossipsub_test.go:945-1024) restated: host 0
+    dials hosts 1..n-1 (a star); every other pair is a connection slot that
+    starts down.  D = 4, Dlo = 3, Dhi = 5, Dscore = 3, flood publish, PX on.
+    The leaves' GRAFTs fill the centre's mesh (it dialled them: outbound peers
+    pass the Dhi check), its heartbeat prunes the excess with PX, the pruned
+    leaves dial the suggested peers and graft each other; then every host
+    publishes a message that every host must receive."""
+    rowptr = np.arange(0, n * (n - 1) + 1, n - 1, dtype=np.int64)
+    col = np.array([v for u in range(n) for v in range(n) if v != u], dtype=np.int32)
+    # the centre dials the leaves; a leaf pair is dialled by its lower index
+    src = np.repeat(np.arange(n), n - 1)
+    outbound = ((src == 0) | ((col != 0) & (src < col) & (src != 0))).astype(np.uint8)
+    dormant = [(a, b) for a in range(1, n) for b in range(a + 1, n)]
+    gp = GossipSubParams(D=4, Dlo=3, Dhi=5, Dscore=3)
+    e = NewGossipSub(n, 1, (rowptr, col, outbound), graphs.all_subscribed(n, 1), WithGossipSubParams(gp),
+                     WithPeerExchange(True), WithFloodPublish(True), WithDormant(dormant), WithRecordDeliveries(),
+                     WithSeed(seed), WithHop(HOP), WithMessageWindow(64), *extra, lib=lib)
+    e.publish(np.arange(n, dtype=np.int32), np.zeros(n, np.int32), 100 + np.arange(n))
+    return e, 100 + n + 30
+
+
+def px_scored(lib, extra=()):
+    """PX in a scored random graph with connection slots: 15% of every node's
+    connections start down, negative app scores (noPX for negative-score
+    prunes, AcceptPXThreshold), Dhi pruning of degree-24 nodes."""
+    n, k, seed = 200, 24, 72
+    g = graphs.random_regular(n, k, seed)
+    rowptr, col, _ = g
+    rng = np.random.default_rng(seed)
+    pairs = [(u, int(v)) for u in range(n) for v in col[rowptr[u]:rowptr[u + 1]] if u < v]
+    dormant = [pairs[i] for i in np.flatnonzero(rng.random(len(pairs)) < 0.15)]
+    sp = eth2_peer_score_params(1)
+    app = np.where(rng.random(n) < 0.15, -150.0, 0.0)
+    thr = eth2_thresholds()
+    thr.AcceptPXThreshold = 0.0
+    e = NewGossipSub(n, 1, g, graphs.all_subscribed(n, 1), WithPeerScore(sp, thr), WithPeerExchange(True),
+                     WithDormant(dormant), WithRecordDeliveries(), WithSeed(seed), WithHop(HOP),
+                     WithMessageWindow(512), *extra, app_score=app, lib=lib)
+    e.app_score = app  # for the test's checks
+    src, top, hops = _publish_schedule(n, 1, 200, 20, 1, seed)
+    e.publish(src, top, hops)
+    return e, int(hops[-1]) + 40
+
+
+PX = {
+    "px_star": lambda lib, x=(): px_star(lib, extra=x),
+}
+SCENARIOS.update(PX)
+# oracle only: the engine's peer exchange is unscored (GS_EUNSUPPORTED with scoring)
+ORACLE_ONLY = {
+    "px_scored": lambda lib, x=(): px_scored(lib, extra=x),
+}
