@@ -160,6 +160,17 @@ struct gs_engine {
   std::vector<std::pair<int, int>> pxPend;     // dials of the previous hop (connected at this hop's start)
   std::vector<unsigned long long> pxqH;
   int readPx();
+  // direct peers (gossipsub.go:492-502, 1594-1616): the (host, direct peer)
+  // edges, dialled by the connector when down
+  std::vector<std::pair<int, int>> directPairs;
+  int64_t directInitHop = 0;
+  void directConnect() {
+    for (auto& pr : directPairs) {
+      const auto bgn = col.begin() + rowptr[pr.first], fin = col.begin() + rowptr[pr.first + 1];
+      if (!aliveH.empty() && !aliveH[std::lower_bound(bgn, fin, pr.second) - col.begin()])
+        pxPend.push_back({std::min(pr.first, pr.second), std::max(pr.first, pr.second)});
+    }
+  }
   std::vector<gs_trace_event> traceFuture;
   std::vector<std::array<int64_t, 3>> rpcDowns;  // (hop, receiver, sender)
   // an RPC block recorded on the host: hello packets and announcements
@@ -326,8 +337,8 @@ int gs_engine::start() {
     gs_set_error("peer exchange is supported by an unscored, honest, unpartitioned engine without RPC accounting");
     return GS_EUNSUPPORTED;
   }
-  if (!dormant.empty() && (scoring || acctOn || world > 1)) {
-    gs_set_error("dormant connections are supported by an unscored, unpartitioned engine without RPC accounting");
+  if (!dormant.empty() && world > 1) {
+    gs_set_error("dormant connections are supported by an unpartitioned engine");
     return GS_EUNSUPPORTED;
   }
   HIPCHECK(hipSetDevice(cfg.device));
@@ -367,6 +378,15 @@ int gs_engine::start() {
     gs_set_error("a partitioned engine supports floodsub and gossipsub (randomsub target masks are not exchanged)");
     return GS_EUNSUPPORTED;
   }
+  // connections down at the start (gs_set_dormant): no score record, no IP
+  std::vector<uint8_t> downH;
+  if (!dormant.empty()) {
+    downH.assign((size_t)E, 0);
+    for (int u = 0; u < N; ++u)
+      for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e)
+        downH[e] = dormant.count({std::min(u, col[e]), std::max(u, col[e])}) ? 1 : 0;
+  }
+  auto isDown = [&](int64_t e) { return !downH.empty() && downH[e]; };
   std::vector<double> p6(E, 0.0);
   if (scoring && sp.IPColocationFactorWeight != 0 && !ipv4.empty()) {
     // ipColocationFactor (score.go:335-379): peers per IP among the observer's peers
@@ -374,10 +394,10 @@ int gs_engine::start() {
     for (int u = 0; u < N; ++u) {
       cnt.clear();
       for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e)
-        if (ipv4[col[e]] != 0) cnt[ipv4[col[e]]]++;
+        if (ipv4[col[e]] != 0 && !isDown(e)) cnt[ipv4[col[e]]]++;
       for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) {
         const uint32_t ip = ipv4[col[e]];
-        if (ip == 0) continue;
+        if (ip == 0 || isDown(e)) continue;
         bool wl = false;
         for (auto& nm : whitelist)
           if ((ip & nm.second) == (nm.first & nm.second)) { wl = true; break; }
@@ -394,6 +414,12 @@ int gs_engine::start() {
   if (sub.empty()) sub.assign(N, 0);
   if (outbound.empty()) outbound.assign(E, 0);
   if (direct.empty()) direct.assign(E, 0);
+  directPairs.clear();
+  if (cfg.router == GS_ROUTER_GOSSIPSUB)
+    for (int u = 0; u < N; ++u)
+      for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e)
+        if (direct[e]) directPairs.push_back({u, col[e]});
+  directInitHop = gp.DirectConnectInitialDelay <= 0 ? 0 : (gp.DirectConnectInitialDelay + cfg.hop_ns - 1) / cfg.hop_ns;
 
   Dev& x = d;
   x.N = N; x.T = T; x.Wt = Wt; x.W = W; x.St = St; x.S = S; x.R = R;
@@ -711,12 +737,12 @@ int gs_engine::start() {
     const int rc = enableChurn();
     if (rc) return rc;
   }
-  if (!dormant.empty()) {  // gs_set_dormant: these connections start down
+  if (!dormant.empty()) {  // gs_set_dormant: these connections start down, without a score record
     std::vector<uint8_t> al((size_t)E, 1);
-    for (int u = 0; u < N; ++u)
-      for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e)
-        if (dormant.count({std::min(u, col[e]), std::max(u, col[e])})) al[e] = aliveH[e] = 0;
+    for (int64_t e = 0; e < E; ++e)
+      if (downH[e]) al[e] = aliveH[e] = 0;
     HIPCHECK(hipMemcpyAsync(d.alive, al.data(), (size_t)E, hipMemcpyHostToDevice, stream));
+    if (d.rstate) HIPCHECK(hipMemcpyAsync(d.rstate, al.data(), (size_t)E, hipMemcpyHostToDevice, stream));
     HIPCHECK(hipStreamSynchronize(stream));  // al is pageable
   }
   x.rpcB = x.rpcN = nullptr;
@@ -740,7 +766,10 @@ int gs_engine::start() {
     // the hello packet of every connection present at the start (pubsub.go:495)
     std::vector<unsigned long long> hb((size_t)E), hn((size_t)E, 1ull);
     for (int u = 0; u < N; ++u)
-      for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) hb[e] = (unsigned long long)helloBytes(sub[u]);
+      for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) {
+        hb[e] = isDown(e) ? 0ull : (unsigned long long)helloBytes(sub[u]);
+        hn[e] = isDown(e) ? 0ull : 1ull;
+      }
     HIPCHECK(hipMemcpyAsync(ac, ah.data(), (size_t)T * sizeof(AcctT), hipMemcpyHostToDevice, stream));
     HIPCHECK(hipMemcpyAsync(x.rpcB, hb.data(), (size_t)E * 8, hipMemcpyHostToDevice, stream));
     HIPCHECK(hipMemcpyAsync(x.rpcN, hn.data(), (size_t)E * 8, hipMemcpyHostToDevice, stream));
@@ -912,17 +941,22 @@ int gs_engine::applyEvents(int64_t h) {
     return (int64_t)(it - col.begin());
   };
   for (int pass = GS_EV_DISCONNECT; pass <= GS_EV_JOIN; ++pass) {
-    if (pass == GS_EV_LEAVE && doPX) {
-      // the peer-exchange dials of the previous hop complete, after this hop's
-      // scheduled disconnects and connects: each pair once, ascending
+    if (pass == GS_EV_LEAVE && (doPX || !directPairs.empty())) {
+      // the connector's dials of the previous hop (peer exchange, direct
+      // peers) complete after this hop's scheduled disconnects and connects:
+      // each pair once, ascending
       std::sort(pxPend.begin(), pxPend.end());
       pxPend.erase(std::unique(pxPend.begin(), pxPend.end()), pxPend.end());
       for (auto& pr : pxPend) {
         const int64_t ab = edgeOf(pr.first, pr.second), ba = edgeOf(pr.second, pr.first);
         if (aliveH[ab]) continue;
         aliveH[ab] = aliveH[ba] = 1;
-        up.push_back((int32_t)ab);
-        up.push_back((int32_t)ba);
+        if (world == 1 || (ab >= e0 && ab < e1) || (ba >= e0 && ba < e1)) {
+          up.push_back((int32_t)ab);
+          up.push_back((int32_t)ba);
+        }
+        if (acctOn)  // hello packets both ways (pubsub.go:534)
+          acctPend.insert(acctPend.end(), {ab, helloBytes(sub[pr.first]), ba, helloBytes(sub[pr.second])});
         if (traceRpc) {
           hostRpc(GS_TRACE_RECV_RPC, pr.first, pr.second, h, GS_RPC_ORD(0, GS_RPC_O_HELLO), -1, sub[pr.second], 1);
           hostRpc(GS_TRACE_RECV_RPC, pr.second, pr.first, h, GS_RPC_ORD(0, GS_RPC_O_HELLO), -1, sub[pr.first], 1);
@@ -1028,6 +1062,7 @@ int gs_engine::stepOne() {
   if (churnOn) {
     const int rc = applyEvents(h);
     if (rc) return rc;
+    if (h == directInitHop) directConnect();  // after DirectConnectInitialDelay (gossipsub.go:492-502)
   }
   const bool gossip = cfg.router == GS_ROUTER_GOSSIPSUB;
   // this hop's local publishes [b, e)
@@ -1214,6 +1249,7 @@ int gs_engine::stepOne() {
   }
   if (heartbeatDue(now)) {
     ticks++;
+    if (!directPairs.empty() && ticks % gp.DirectConnectTicks == 0) directConnect();  // gossipsub.go:1318
     if (nOwn) TIMED(this, GS_K_HB_PRE, (k_hb_pre<<<nOwn, 64, 0, stream>>>(d, now, ticks)));
     // right after a refresh S0 holds exact scores: recompute only what hb_pre
     // dirtied; opportunistic grafting (every OGT ticks) ranks every mesh
@@ -1627,6 +1663,10 @@ int gs_engine_create(const gs_config* cfg, const gs_gossipsub_params* gsp, const
       gs_set_error("HeartbeatInterval must be a multiple of hop_ns and >= 2 hops; "
                    "HeartbeatInitialDelay a multiple of hop_ns and >= 1 hop");
       return GS_EUNSUPPORTED;
+    }
+    if (p.DirectConnectTicks == 0) {  // heartbeatTicks % DirectConnectTicks (gossipsub.go:1597)
+      gs_set_error("DirectConnectTicks must be > 0");
+      return GS_EINVAL;
     }
     if (p.GossipRetransmission < 0 || p.MaxIHaveMessages < 0 || p.D < 0 || p.Dhi < 0 || p.Dscore < 0 ||
         p.Dscore > p.D || p.D > p.Dhi) {

@@ -300,13 +300,23 @@ int gs_set_behaviour(gs_engine* eng, const uint8_t* behaviour /*[N]*/);
  *   GS_EV_JOIN (a, topic b): node a subscribes (handleAddSubscription
  *     pubsub.go:692-713): announce, then Join (gossipsub.go:1011-1060).
  * An event that finds its state already (a connection down twice, a topic
- * left twice) does nothing.  Not supported together with a partitioned engine
- * or the peer gater (GS_EUNSUPPORTED). */
+ * left twice) does nothing.  Not supported together with the peer gater
+ * (GS_EUNSUPPORTED); a partitioned engine applies every event on every rank,
+ * each rank launching the side of a connection it owns.
+ * Direct peers (gs_set_graph's direct flags) that are not connected are
+ * dialled by the connector at hop ceil(DirectConnectInitialDelay / hop_ns)
+ * (gossipsub.go:492-502) and at every heartbeat whose tick count is a
+ * multiple of DirectConnectTicks (directConnect, gossipsub.go:1594-1616); a
+ * dial made during hop h connects at the start of hop h + 1, after that hop's
+ * scheduled disconnects and connects (AddPeer both ways, hellos).
+ * DirectConnectTicks = 0 is GS_EINVAL at creation (the reference divides by
+ * it). */
 /* Before the first step: the connections a[i]-b[i] (edges of the graph, both
  * directions) start down: no AddPeer, no hello, no score record.  A
- * GS_EV_CONNECT or a peer-exchange connect (GS_FLAG_PEER_EXCHANGE) brings one
- * up.  A PX-suggested peer without such a slot cannot be dialled (the
- * reference's connector dials any peer; the simulated graph is fixed). */
+ * GS_EV_CONNECT, a peer-exchange connect (GS_FLAG_PEER_EXCHANGE) or a direct
+ * peer's dial brings one up.  A PX-suggested peer without such a slot cannot
+ * be dialled (the reference's connector dials any peer; the simulated graph
+ * is fixed). */
 int gs_set_dormant(gs_engine* eng, int32_t n, const int32_t* a, const int32_t* b);
 #define GS_EV_DISCONNECT 0
 #define GS_EV_CONNECT 1

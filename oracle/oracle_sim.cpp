@@ -108,6 +108,7 @@ struct Node {
   PruneEntry makePrune(int p, int topic, bool doPX);
   void pxConnect(std::vector<int> px);   // gossipsub.go:856-905
   std::vector<int> pxReq;                // peers to dial (connected at the next hop's start)
+  void directConnect();
   void heartbeat();
   void emitGossip(int topic, const std::set<int>& exclude);
   void removePeer(int p);                // handleDeadPeers + RemovePeer
@@ -127,6 +128,8 @@ struct Sim {
   gs_peer_score_thresholds thr{};
   bool scoring = false, floodPublish = false, record = false;
   bool doPX = false;                                    // WithPeerExchange
+  bool hasDirect = false;                               // some host has direct peers (the connector dials them)
+  int64_t directInitHop = 0;                            // DirectConnectInitialDelay in hops
   std::set<std::pair<int, int>> dormant;               // gs_set_dormant: connections down at the start
   bool gaterOn = false;
   // Reference order (gs_oracle_reference_order): each RPC is
@@ -801,6 +804,14 @@ void Node::emitGossip(int topic, const std::set<int>& exclude) {
   }
 }
 
+// directConnect — gossipsub.go:1594-1616 (and the initial dial of :492-502):
+// every direct peer that is not connected is dialled; the connector's dials
+// complete at the next hop's start (Sim::applyEvents).
+void Node::directConnect() {
+  for (int p : direct)
+    if (dead.count(p)) pxReq.push_back(p);
+}
+
 // heartbeat — gossipsub.go:1299-1552
 void Node::heartbeat() {
   const gs_gossipsub_params& gp = sim->gp;
@@ -813,6 +824,7 @@ void Node::heartbeat() {
   peerhave.clear();  // clearIHaveCounters
   iasked.clear();
   applyIwantPenalties();
+  if (heartbeatTicks % gp.DirectConnectTicks == 0) directConnect();
   std::map<int, double> scores;  // score memo
   auto score = [&](int p) {
     auto it = scores.find(p);
@@ -1095,9 +1107,10 @@ void Sim::applyEvents(std::vector<std::map<int, std::vector<RPC>>>& inbox) {
   size_t end = nextEvent;
   while (end < sched.size() && sched[end].hop == hop) end++;
   for (int pass = GS_EV_DISCONNECT; pass <= GS_EV_JOIN; ++pass) {
-  if (pass == GS_EV_LEAVE && doPX) {
-    // the peer-exchange dials of the previous hop complete (after this hop's
-    // scheduled disconnects and connects): each pair once, ascending
+  if (pass == GS_EV_LEAVE && (doPX || hasDirect)) {
+    // the connector's dials of the previous hop (peer exchange, direct peers)
+    // complete after this hop's scheduled disconnects and connects: each pair
+    // once, ascending
     std::set<std::pair<int, int>> px;
     for (Node& nd : nodes) {
       for (int q : nd.pxReq) px.insert({std::min(nd.id, q), std::max(nd.id, q)});
@@ -1109,6 +1122,8 @@ void Sim::applyEvents(std::vector<std::map<int, std::vector<RPC>>>& inbox) {
       nodes[pr.second].addPeer(pr.first);
       traceHello(pr.first, pr.second);
       traceHello(pr.second, pr.first);
+      account(pr.first, pr.second, acct ? helloSize(nodes[pr.first].mySubs) : 0);
+      account(pr.second, pr.first, acct ? helloSize(nodes[pr.second].mySubs) : 0);
     }
   }
   std::vector<Event> evs;
@@ -1194,6 +1209,10 @@ void Sim::start() {
         if (!subs.empty() && ((subs[v] >> t) & 1)) nd.topics[t].insert(v);
     }
   }
+  hasDirect = false;
+  for (const Node& nd : nodes) hasDirect = hasDirect || !nd.direct.empty();
+  hasDirect = hasDirect && cfg.router == GS_ROUTER_GOSSIPSUB;
+  directInitHop = gp.DirectConnectInitialDelay <= 0 ? 0 : (gp.DirectConnectInitialDelay + cfg.hop_ns - 1) / cfg.hop_ns;
   auto up = [&](int u, int v) { return !dormant.count({std::min(u, v), std::max(u, v)}); };
   for (int u = 0; u < N; ++u)  // the hello packet of every connection (pubsub.go:495)
     for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e)
@@ -1223,6 +1242,8 @@ void Sim::step() {
   // maps, peerScore, mcache, outbox, counters and trace buffer) and reads
   // shared immutable data, so nodes run in parallel; the phase order is kept.
   applyEvents(inbox);
+  if (hasDirect && hop == directInitHop)  // connect to direct peers after DirectConnectInitialDelay (:492-502)
+    for (Node& nd : nodes) nd.directConnect();
   if (hop == 0) {  // Join: the GRAFTs it sends arrive in hop 1
 #pragma omp parallel for schedule(dynamic, 64)
     for (int u = 0; u < N; ++u)
@@ -1436,6 +1457,10 @@ int gs_engine_create(const gs_config* cfg, const gs_gossipsub_params* gsp, const
         s.gp.HeartbeatInitialDelay < 0 || s.gp.HeartbeatInitialDelay % cfg->hop_ns != 0) {
       set_error("HeartbeatInterval and HeartbeatInitialDelay must be multiples of hop_ns");
       return GS_EUNSUPPORTED;
+    }
+    if (s.gp.DirectConnectTicks == 0) {  // heartbeatTicks % DirectConnectTicks (gossipsub.go:1597)
+      set_error("DirectConnectTicks must be > 0");
+      return GS_EINVAL;
     }
   }
   if (s.scoring) {

@@ -585,8 +585,67 @@ def px_scored(lib, extra=()):
     return e, int(hops[-1]) + 40
 
 
+def direct_peers(lib, seed=73, extra=()):
+    """TestGossipsubDirectPeers (gossipsub_test.go:1122-1184) restated: hosts 1
+    and 2 are direct peers, DirectConnectTicks = 2; host 0 connects to both, the
+    1-2 connection starts down and the initial direct dial brings it up; the
+    hosts subscribe, publish 3 messages; 1-2 closes, the heartbeat's
+    directConnect redials it, 3 more messages reach everyone."""
+    n = 3
+    rowptr = np.array([0, 2, 4, 6], np.int64)
+    col = np.array([1, 2, 0, 2, 0, 1], np.int32)
+    outbound = np.array([1, 1, 0, 1, 0, 0], np.uint8)
+    direct = np.array([0, 0, 0, 1, 0, 1], np.uint8)
+    gp = GossipSubParams(DirectConnectTicks=2)
+    e = NewGossipSub(n, 1, (rowptr, col, outbound), np.zeros(n, np.uint64), WithGossipSubParams(gp),
+                     WithDirectPeers(direct), WithDormant([(1, 2)]), WithRecordDeliveries(), WithSeed(seed),
+                     WithHop(HOP), WithMessageWindow(64), *extra, lib=lib)
+    e.schedule_events([GS_EV_JOIN] * 3 + [GS_EV_DISCONNECT], [0, 1, 2, 1], [0, 0, 0, 2], [20, 20, 20, 40])
+    e.publish(np.array([0, 1, 2, 0, 1, 2], np.int32), np.zeros(6, np.int32),
+              np.array([30, 31, 32, 90, 91, 92], np.int64))
+    return e, 110
+
+
+def direct_churn(lib, extra=()):
+    """Scored random graph with 5% direct connections: half of them start
+    down (dialled after DirectConnectInitialDelay), the rest close at random
+    hops and are redialled by directConnect every 3 heartbeats; ordinary
+    connections churn beside them."""
+    n, k, seed = 200, 16, 74
+    g = graphs.random_regular(n, k, seed)
+    rowptr, col, _ = g
+    src = np.repeat(np.arange(n), np.diff(rowptr))
+    rng = np.random.default_rng(seed)
+    pairs = sorted({(min(int(a), int(b)), max(int(a), int(b))) for a, b in zip(src, col)})
+    dpairs = [pairs[i] for i in np.flatnonzero(rng.random(len(pairs)) < 0.05)]
+    dset = set(dpairs)
+    direct = np.array([(min(a, b), max(a, b)) in dset for a, b in zip(src, col)], np.uint8)
+    dormant = dpairs[::2]
+    ev = []
+    for h in range(15, 120, 7):
+        a, b = dpairs[1::2][int(rng.integers(0, len(dpairs[1::2])))]
+        ev.append((h, GS_EV_DISCONNECT, a, b))
+        a, b = pairs[int(rng.integers(0, len(pairs)))]
+        ev.append((h, GS_EV_DISCONNECT, a, b))
+        ev.append((h + int(rng.integers(3, 20)), GS_EV_CONNECT, a, b))
+    ev.sort(key=lambda x: x[0])
+    gp = GossipSubParams(DirectConnectTicks=3, DirectConnectInitialDelay=500 * Millisecond)
+    sp = eth2_peer_score_params(1)
+    thr = eth2_thresholds()
+    e = NewGossipSub(n, 1, g, graphs.all_subscribed(n, 1), WithGossipSubParams(gp), WithPeerScore(sp, thr),
+                     WithDirectPeers(direct), WithDormant(dormant), WithRecordDeliveries(), WithSeed(seed),
+                     WithHop(HOP), WithMessageWindow(512), *extra, lib=lib)
+    e.schedule_events([x[1] for x in ev], [x[2] for x in ev], [x[3] for x in ev], [x[0] for x in ev])
+    src_ = rng.integers(0, n, 240).astype(np.int32)
+    e.publish(src_, np.zeros(240, np.int32), (5 + np.arange(240) // 2).astype(np.int64))
+    e.direct_pairs, e.dormant_pairs = dpairs, dormant
+    return e, 150
+
+
 PX = {
     "px_star": lambda lib, x=(): px_star(lib, extra=x),
+    "direct_peers": lambda lib, x=(): direct_peers(lib, extra=x),
+    "direct_churn": lambda lib, x=(): direct_churn(lib, extra=x),
 }
 SCENARIOS.update(PX)
 # oracle only: the engine's peer exchange is unscored (GS_EUNSUPPORTED with scoring)
