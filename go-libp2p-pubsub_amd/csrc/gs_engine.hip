@@ -333,8 +333,8 @@ static void score_rows(const Dev& d, int64_t nEdges, int T, double* out, hipStre
   } while (0)
 
 int gs_engine::start() {
-  if (doPX && (scoring || gaterOn || behaveAll != 0 || world > 1 || acctOn)) {
-    gs_set_error("peer exchange is supported by an unscored, honest, unpartitioned engine without RPC accounting");
+  if (doPX && (gaterOn || behaveAll != 0 || world > 1 || acctOn)) {
+    gs_set_error("peer exchange is supported by an honest, unpartitioned engine without the gater or RPC accounting");
     return GS_EUNSUPPORTED;
   }
   if (!dormant.empty() && world > 1) {

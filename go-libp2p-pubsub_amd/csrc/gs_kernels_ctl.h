@@ -74,18 +74,35 @@ __device__ __forceinline__ void prune_topics(const Dev& d, int64_t e, int v, uin
   }
 }
 
-// ---- peer exchange (GS_FLAG_PEER_EXCHANGE; the engine supports it unscored)
+// ---- peer exchange (GS_FLAG_PEER_EXCHANGE)
+// makePrune's score filter Score(xp) >= 0 (gossipsub.go:1813) for the lane's
+// connected peer: the live score, exact (one wave-wide score per connected
+// peer; PX PRUNEs are rare).  Unscored every peer passes.  Wave-uniform.
+__device__ __forceinline__ bool px_score_ok(const Dev& d, int64_t base, int deg, double* lds) {
+  if (!d.scoring) return true;
+  const int lane = lane_id();
+  double s = 0.0;
+  unsigned long long m = __ballot(lane < deg && edge_up(d, base + lane));
+  while (m) {
+    const int j = __ffsll((long long)m) - 1;
+    m &= m - 1;
+    const double sj = edge_score_wave(d, base + j, lds);
+    if (lane == j) s = sj;
+  }
+  return s >= 0.0;
+}
 // makePrune's peer list (gossipsub.go:1811-1836) for the PRUNE of topic t to
-// v's peer on lane p: getPeers(topic, PrunePeers, xp != p && Score(xp) >= 0) —
-// unscored every connected peer of v subscribed to t passes — with its own
-// shuffle (GS_SITE_PX keyed by the pruned peer too).  Wave-uniform; returns
-// the lane mask of the list.
-__device__ __forceinline__ uint64_t px_sel(const Dev& d, int v, int64_t base, int deg, int t, int64_t hop, int p) {
+// v's peer on lane p: getPeers(topic, PrunePeers, xp != p && Score(xp) >= 0)
+// (ok: the lane passes the score filter, px_score_ok) with its own shuffle
+// (GS_SITE_PX keyed by the pruned peer too).  Wave-uniform; returns the lane
+// mask of the list.
+__device__ __forceinline__ uint64_t px_sel(const Dev& d, int v, int64_t base, int deg, int t, int64_t hop, int p,
+                                           bool ok) {
   const int lane = lane_id();
   const bool valid = lane < deg;
   const int64_t e = base + lane;
   const int u = valid ? d.col[e] : 0;
-  const bool cand = valid && lane != p && edge_up(d, e) && ((d.subA[u] >> t) & 1);
+  const bool cand = ok && valid && lane != p && edge_up(d, e) && ((d.subA[u] >> t) & 1);
   const uint32_t pp = (uint32_t)d.col[base + p];
   const uint64_t key = gs_key64(d.seed, GS_SITE_PX, v, (uint32_t)hop, u, (pp << 6) | (uint32_t)t);
   return __ballot(select_k(cand, key, d.PrunePeers));
@@ -374,13 +391,22 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
       uint64_t pOut = 0;
       int nR = 0;
       const int64_t reI = d.doPX ? d.rev[ei] : 0;  // the sender's in-edge: our PX record for it
-      // makePrune with PX for the rejected topics of one RPC
+      // makePrune with PX for the rejected topics of one RPC (live scores)
       auto pxPrunes = [&](uint64_t topics) {
+        if (!topics) return;
+        const bool ok = px_score_ok(d, base, deg, sterm);
         for (uint64_t mm = topics; mm; mm &= mm - 1) {
           const int t = __ffsll((long long)mm) - 1;
-          const uint64_t list = px_sel(d, v, base, deg, t, h, i);
+          const uint64_t list = px_sel(d, v, base, deg, t, h, i, ok);
           if (lane == 0) px_append(d, cur, reI, t, list, base);
         }
+      };
+      // handlePrune's PX acceptance (gossipsub.go:807, 827-836): the sender's
+      // live score before the RPC's PRUNEs against AcceptPXThreshold
+      auto pxAccept = [&](uint64_t topics) {
+        if (!d.doPX || !topics || d.cPx[prv][ei] < 0) return false;
+        const double sx = d.scoring ? edge_score_wave(d, ei, sterm) : 0.0;
+        return !(sx < d.acceptPX);
       };
       // (1) Join RPCs: one GRAFT each (gossipsub.go:1080-1084)
       uint64_t gj = gJoin_i;
@@ -406,10 +432,9 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
         if (gossipOK) ph_i += nRep;
         gIW = gossipOK && iwRec_i >= 0;  // handleIWant (gossipsub.go:674-711): step 2
         gSP = gossipOK && spRec_i >= 0;
+        const bool acc = pxAccept(pRep_i & d.sub[v]);
         prune_topics(d, ei, v, pRep_i, now, meshcnt, mE, dirty);
-        // PX of these PRUNEs (unscored: Score(p) = 0 against AcceptPXThreshold)
-        if (d.doPX && !(0.0 < d.acceptPX))
-          px_connect(d, v, base, deg, prv, d.cPx[prv][ei], pRep_i & d.sub[v]);
+        if (acc) px_connect(d, v, base, deg, prv, d.cPx[prv][ei], pRep_i & d.sub[v]);  // the PRUNEs' PX
       }
       // (3) heartbeat RPC: IHAVE (step 3), GRAFT, PRUNE
       bool gIH = false;
@@ -431,9 +456,9 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
           if (pr) prunes |= 1ull << t;
         }
         if (d.doPX && !noPX) pxPrunes(prunes);
+        const bool acc = pxAccept(pHb_i & d.sub[v]);
         prune_topics(d, ei, v, pHb_i, now, meshcnt, mE, dirty);
-        if (d.doPX && !(0.0 < d.acceptPX))
-          px_connect(d, v, base, deg, prv, d.cPx[prv][ei], pHb_i & d.sub[v]);
+        if (acc) px_connect(d, v, base, deg, prv, d.cPx[prv][ei], pHb_i & d.sub[v]);
       }
       const uint64_t jrej = pOut;
       pOut |= prunes;
@@ -1548,6 +1573,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
   uint64_t boM = vm ? d.boMask[e] : 0;  // topics in backoff with this peer
   double S = vm ? d.score1[e] : 0.0;
   const uint64_t joined = d.sub[v];
+  const bool hbNoPX = vm && S < 0 && (meshl & joined) != 0;  // pruned for its negative score: noPX
   if (d.scoring && !allExact) {
     // score1 is exact only where k_score_rows<4> recomputed it; the Dhi
     // ranking compares scores as values, so the mesh members of a topic that
@@ -1735,16 +1761,18 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
   }
   if (d.doPX) {
     // makePrune with PX for every PRUNE of this heartbeat (sendGraftPrune,
-    // gossipsub.go:1636-1647; unscored: no negative-score prunes, so no noPX)
+    // gossipsub.go:1636-1647), with the live scores after every mesh change;
+    // none for a peer dropped for its negative score (noPX, :1350-1356)
     uint64_t any = 0;
-    for (int o = 0; o < 64; ++o) any |= lane_get64(valid ? toprune : 0ull, o);
+    for (int o = 0; o < 64; ++o) any |= lane_get64(valid && !hbNoPX ? toprune : 0ull, o);
+    const bool ok = any ? px_score_ok(d, base, deg, sterm) : true;
     for (uint64_t mm = any; mm; mm &= mm - 1) {
       const int t = __ffsll((long long)mm) - 1;
-      unsigned long long pl = __ballot(valid && ((toprune >> t) & 1));
+      unsigned long long pl = __ballot(valid && !hbNoPX && ((toprune >> t) & 1));
       while (pl) {  // one list per pruned peer
         const int p = __ffsll((long long)pl) - 1;
         pl &= pl - 1;
-        const uint64_t list = px_sel(d, v, base, deg, t, hop, p);
+        const uint64_t list = px_sel(d, v, base, deg, t, hop, p, ok);
         if (lane == p) px_append(d, cur, d.rev[e], t, list, base);
       }
     }
@@ -2030,6 +2058,7 @@ __global__ __launch_bounds__(64) void k_p6(Dev d, double* __restrict__ p6) {
 // One wave per node (items: node, topic mask lo, hi), its topics ascending;
 // lane = edge.
 __global__ __launch_bounds__(64) void k_leave(Dev d, const int32_t* __restrict__ items, int64_t hop, int cur) {
+  __shared__ double sterm[64];
   const int v = items[3 * blockIdx.x];
   const uint64_t mask = (uint64_t)(uint32_t)items[3 * blockIdx.x + 1] | ((uint64_t)(uint32_t)items[3 * blockIdx.x + 2] << 32);
   const int lane = lane_id();
@@ -2048,18 +2077,24 @@ __global__ __launch_bounds__(64) void k_leave(Dev d, const int32_t* __restrict__
     if (lane == 0 && traced) trace_emit(d, hop, d.router == 1 ? GS_TRACE_JOIN : GS_TRACE_LEAVE, v, -1, t, -1, 0);
     if (d.router != 2) continue;  // floodsub / randomsub (randomsub.go:166-168 traces a Join)
     const bool m = valid && (meshl & bit);
+    // makePrune's live scores: the mesh peers are pruned one after another
+    // (ascending), each PRUNE's list made right after its peer's Prune — so a
+    // peer's score counts its own Prune once the list is for it or a later peer
+    const bool pxOn = d.doPX && !silent && __ballot(m) != 0;
+    const bool okPre = pxOn ? px_score_ok(d, base, deg, sterm) : true;
     if (m) {
       meshl &= ~bit;
       pruned |= bit;
       stats_prune(d, e, t);
       if (traced) trace_emit(d, hop, GS_TRACE_PRUNE, v, d.col[e], t, -1, 0);
     }
-    if (d.doPX && !silent) {  // sendPrune's makePrune(p, topic, gs.doPX) (:1087)
+    if (pxOn) {  // sendPrune's makePrune(p, topic, gs.doPX) (:1087)
+      const bool okPost = px_score_ok(d, base, deg, sterm);
       unsigned long long pl = __ballot(m);
       while (pl) {
         const int p = __ffsll((long long)pl) - 1;
         pl &= pl - 1;
-        const uint64_t list = px_sel(d, v, base, deg, t, hop, p);
+        const uint64_t list = px_sel(d, v, base, deg, t, hop, p, (m && lane <= p) ? okPost : okPre);
         if (lane == p) px_append(d, cur, d.rev[e], t, list, base);
       }
     }

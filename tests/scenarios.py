@@ -646,9 +646,6 @@ PX = {
     "px_star": lambda lib, x=(): px_star(lib, extra=x),
     "direct_peers": lambda lib, x=(): direct_peers(lib, extra=x),
     "direct_churn": lambda lib, x=(): direct_churn(lib, extra=x),
-}
-SCENARIOS.update(PX)
-# oracle only: the engine's peer exchange is unscored (GS_EUNSUPPORTED with scoring)
-ORACLE_ONLY = {
     "px_scored": lambda lib, x=(): px_scored(lib, extra=x),
 }
+SCENARIOS.update(PX)

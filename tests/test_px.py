@@ -12,8 +12,9 @@ CPU, the oracle:
     gossipsub.go:1350-1356), and PX from a pruner below AcceptPXThreshold is
     not dialled;
   * the encoders write ControlPruneMeta.peers.
-GPU: the engine (its peer exchange is unscored) equals the oracle bit for
-bit on the star, trace included, and refuses PX with scoring."""
+GPU: the engine equals the oracle bit for bit on both scenarios (readbacks in
+test_parity_gpu, the RPC trace with the PX lists here); PX with RPC
+accounting is refused (the accounting does not size PX records)."""
 import base64
 import json
 
@@ -29,8 +30,8 @@ T = _abi.TRACE_TYPES.index
 SEND, RECV, ITEM = T("SEND_RPC"), T("RECV_RPC"), _abi.GS_TRACE_RPC_ITEM
 
 
-def _run(lib, name, nodes, table=scenarios.SCENARIOS):
-    e, hops = table[name](lib, (WithEventTracer(nodes, rpc=True),))
+def _run(lib, name, nodes):
+    e, hops = scenarios.SCENARIOS[name](lib, (WithEventTracer(nodes, rpc=True),))
     e.step(hops)
     return e, hops, e.trace_events()
 
@@ -62,7 +63,7 @@ def test_oracle_star_topology_bootstraps_through_px(oracle_path):
 
 def test_oracle_px_scored_rules(oracle_path):
     nodes = list(range(200))
-    e, hops, ev = _run(oracle_path, "px_scored", nodes, scenarios.ORACLE_ONLY)
+    e, hops, ev = _run(oracle_path, "px_scored", nodes)
     app = e.app_score
     n_px = 0
     offered = set()   # (receiver, suggested peer) of PX from a pruner at or above AcceptPXThreshold (0)
@@ -118,18 +119,18 @@ def test_encode_prune_peers():
 
 
 @pytest.mark.gpu
-def test_gpu_star_equals_oracle(oracle_path):
-    want = scenarios.run(oracle_path, "px_star")
-    got = scenarios.run(PRODUCT_LIB, "px_star")
-    assert scenarios.compare(want, got) == []
-    _, _, ew = _run(oracle_path, "px_star", list(range(20)))
-    _, _, eg = _run(PRODUCT_LIB, "px_star", list(range(20)))
+@pytest.mark.parametrize("name", ["px_star", "px_scored"])
+def test_gpu_px_trace_equals_oracle(name, oracle_path):
+    nodes = list(range(20)) if name == "px_star" else list(range(200))
+    _, _, ew = _run(oracle_path, name, nodes)
+    _, _, eg = _run(PRODUCT_LIB, name, nodes)
     assert len(eg) == len(ew) and np.array_equal(eg, ew)
 
 
 @pytest.mark.gpu
-def test_gpu_refuses_scored_px():
-    e, hops = scenarios.ORACLE_ONLY["px_scored"](PRODUCT_LIB)
+def test_gpu_refuses_px_with_accounting():
+    from scenarios import _acct
     with pytest.raises(GossipEngineError) as ei:
+        e, hops = scenarios.SCENARIOS["px_star"](PRODUCT_LIB, (_acct(1),))
         e.step(1)
     assert ei.value.code == _abi.GS_EUNSUPPORTED
