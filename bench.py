@@ -139,15 +139,27 @@ def algorithmic_bytes(kernel, eng, wl, per_hop):
                        bytes_lists=int(list_reads + list_writes), bytes_pending=int(pending),
                        bytes_seen=int(seen), bytes_meta=int(meta))
     if kernel == "refresh":
-        # What the kernel must move (it skips unchanged writes; imd exists only
-        # once a validator rejected something, never in this workload):
-        # reads per (edge, topic) dlt 4, fmd / mmd / mfp 24, graftTime 8,
-        # flags 1; writes per (edge, topic) in the mesh: meshTime 8 and the
-        # decayed fmd / mmd 16 (pairs outside the mesh hold zeros or decay
-        # without fresh credit; counted as unwritten); per edge: bp r+w 16,
-        # score0 w 8, sdirty w 1
-        mesh_pairs = per_hop.get("mesh_pairs", 0)
-        return E * (37.0 * T + 25) + 24.0 * mesh_pairs, dict(E=E, T=T, mesh_pairs=mesh_pairs)
+        # 80 B per (edge, topic) (the four f64 counters read
+        # and written 64, meshTime written 8, graft time read, flags r+w,
+        # padded to 80) + 16 B per edge (P7 read and written).  The engine
+        # moves less (PMC `traffic`): unchanged counters (zeros staying zero)
+        # are not written back and its pending word is 4 B.
+        return E * (80.0 * T + 16), dict(E=E, T=T, per_pair=80, per_edge=16)
+    if kernel == "heartbeat":
+        # 14 B per candidate edge per (node, topic) (score 8,
+        # backoff 4, outbound and mesh bits 2) over the joined topics, plus the
+        # gossip windows (HistoryGossip mcache windows of W words read per
+        # node, the node's gw row written) and the per-edge masks (mesh and
+        # fanout read and written, backoff mask read: 40 B)
+        deg = np.diff(eng.rowptr)[n0:n1].astype(np.int64)
+        subs = np.asarray(eng.subs, dtype=np.uint64)[n0:n1]
+        joined = np.array([bin(int(x)).count("1") for x in subs], dtype=np.int64) if len(subs) < 4096 else \
+            np.unpackbits(subs.view(np.uint8).reshape(-1, 8), axis=1).sum(axis=1).astype(np.int64)
+        cand = int((deg * joined).sum())
+        W = T * wl["slots"] // 64
+        hg = 5
+        b = 14.0 * cand + 8.0 * N * W * (hg + 1) + 40.0 * E
+        return b, dict(candidates=cand, W=W)
     if kernel == "score":
         # full pass: per (edge, topic) flags 1 + fmd/mfp/imd 24 + pending 4 (+ mmd, meshTime when
         # active); per edge col 4 + app 8 + p6 8 + bp 8 + out 8
@@ -360,7 +372,7 @@ def main():
     # the score kernels' rooflines too (north-star target: >= 50% of HBM on
     # score / propagation): refreshScores streams every (edge, topic) record
     rooflines = {}
-    for k in ("refresh",):
+    for k in ("refresh", "heartbeat"):
         if k in kstats and kstats[k][1]:
             b_k, _ = algorithmic_bytes(k, eng, wl, per_hop)
             ms_k = kstats[k][0] / kstats[k][1]

@@ -16,6 +16,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstring>
 #include <memory>
 #include <string>
 #include <unordered_map>
@@ -211,7 +212,43 @@ struct gs_engine {
     evUsed = 0;
   }
 
+  // Pinned staging ring for the per-hop host-to-device uploads: the copy is
+  // asynchronous on the engine stream and the host goes on preparing the next
+  // hop; a slot is refilled only after the copy that used it has completed.
+  struct Stage {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+    bool used = false;
+  };
+  static constexpr int kStages = 8;
+  Stage stages[kStages];
+  int stageNext = 0;
+  int upload(void* dst, const void* src, size_t bytes) {
+    if (!bytes) return GS_OK;
+    Stage& st = stages[stageNext];
+    stageNext = (stageNext + 1) % kStages;
+    if (st.used) HIPCHECK(hipEventSynchronize(st.ev));
+    if (st.cap < bytes) {
+      if (st.p) HIPCHECK(hipHostFree(st.p));
+      st.p = nullptr;
+      st.cap = std::max<size_t>(bytes, (size_t)1 << 16);
+      HIPCHECK(hipHostMalloc(&st.p, st.cap, hipHostMallocDefault));
+    }
+    if (!st.ev) HIPCHECK(hipEventCreateWithFlags(&st.ev, hipEventDisableTiming));
+    std::memcpy(st.p, src, bytes);
+    HIPCHECK(hipMemcpyAsync(dst, st.p, bytes, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipEventRecord(st.ev, stream));
+    st.used = true;
+    return GS_OK;
+  }
+
   ~gs_engine() {
+    if (stream) (void)hipStreamSynchronize(stream);  // staged uploads in flight
+    for (Stage& st : stages) {
+      if (st.ev) (void)hipEventDestroy(st.ev);
+      if (st.p) (void)hipHostFree(st.p);
+    }
     for (hipEvent_t ev : evPool) (void)hipEventDestroy(ev);
     for (uint8_t* p : {xSend, xRecv, xSendE, xRecvE}) if (p) (void)hipFree(p);
     if (xHost) (void)hipHostFree(xHost);
@@ -623,7 +660,10 @@ int gs_engine::start() {
         if (behaveH[v] & GS_BEHAVE_IWANT_SPAM) row[v] = nsp++;
       x.pmaskRow = dalloc<int32_t>(N); chk(x.pmaskRow);
       x.pmask = dalloc<uint64_t>((size_t)nsp * S); chk(x.pmask);
-      if (ok) HIPCHECK(hipMemcpyAsync(x.pmaskRow, row.data(), (size_t)N * 4, hipMemcpyHostToDevice, stream));
+      if (ok) {
+        HIPCHECK(hipMemcpyAsync(x.pmaskRow, row.data(), (size_t)N * 4, hipMemcpyHostToDevice, stream));
+        HIPCHECK(hipStreamSynchronize(stream));  // row is pageable and dies with this block
+      }
       // peertx counts of the owned edges whose peer is an IWANT spammer
       spamRowH.assign((size_t)E, -1);
       int64_t nrow = 0;
@@ -908,9 +948,7 @@ int gs_engine::uploadList(const std::vector<int32_t>& v) {
     dEv = p;
     evCap = cap;
   }
-  HIPCHECK(hipMemcpyAsync(dEv, v.data(), v.size() * 4, hipMemcpyHostToDevice, stream));
-  HIPCHECK(hipStreamSynchronize(stream));  // v is pageable
-  return GS_OK;
+  return upload(dEv, v.data(), v.size() * 4);
 }
 
 // The events of hop h, at its start (the oracle's Sim::applyEvents): the
@@ -1025,9 +1063,14 @@ int gs_engine::applyEvents(int64_t h) {
     const int rc = flushAcct();
     if (rc) return rc;
   }
-  if (subAChanged) HIPCHECK(hipMemcpyAsync(dSubA, subA.data(), (size_t)N * 8, hipMemcpyHostToDevice, stream));
-  if (subChanged) HIPCHECK(hipMemcpyAsync(dSubOwn, sub.data(), (size_t)N * 8, hipMemcpyHostToDevice, stream));
-  if (subAChanged || subChanged) HIPCHECK(hipStreamSynchronize(stream));  // pageable sources
+  if (subAChanged) {
+    const int rc = upload(dSubA, subA.data(), (size_t)N * 8);
+    if (rc) return rc;
+  }
+  if (subChanged) {
+    const int rc = upload(dSubOwn, sub.data(), (size_t)N * 8);
+    if (rc) return rc;
+  }
   if (!down.empty()) {
     int rc = uploadList(down);
     if (rc) return rc;
@@ -1099,8 +1142,8 @@ int gs_engine::stepOne() {
       ++rk;
     }
     if (rk) {
-      HIPCHECK(hipMemcpyAsync(d.yTab, yTabH.data(), yTabH.size() * 8, hipMemcpyHostToDevice, stream));
-      HIPCHECK(hipStreamSynchronize(stream));  // yTabH is pageable host memory
+      const int rc = upload(d.yTab, yTabH.data(), yTabH.size() * 8);
+      if (rc) return rc;
     }
   }
   std::vector<int32_t> retireWords;
@@ -1139,9 +1182,9 @@ int gs_engine::stepOne() {
         dPairs = p;
         pairCap = np * 2;
       }
-      HIPCHECK(hipMemcpyAsync(dPairs, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, stream));
+      const int rc = upload(dPairs, pairs.data(), pairs.size() * 4);
+      if (rc) return rc;
       TIMED(this, GS_K_FANOUT, (k_fanout_pub<<<np, 64, 0, stream>>>(d, dPairs, np, h, now)));
-      HIPCHECK(hipStreamSynchronize(stream));  // `pairs` is pageable host memory
     }
   }
   if (eOwn) TIMED(this, GS_K_FWD, (k_fwd<<<eb, 256, 0, stream>>>(d, cur)));
@@ -1191,10 +1234,10 @@ int gs_engine::stepOne() {
       dRetire = p;
       retireCap = (int)retireWords.size() * 2;
     }
-    HIPCHECK(hipMemcpyAsync(dRetire, retireWords.data(), retireWords.size() * 4, hipMemcpyHostToDevice, stream));
+    const int rc = upload(dRetire, retireWords.data(), retireWords.size() * 4);
+    if (rc) return rc;
     const int nw = (int)retireWords.size();
     if (nOwn) k_retire<<<nblk((int64_t)nOwn * nw, 256), 256, 0, stream>>>(d, cur, dRetire, nw);
-    HIPCHECK(hipStreamSynchronize(stream));  // retireWords is pageable host memory
   }
   if (n > 0) {
     TIMED(this, GS_K_PUBLISH, (k_publish<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, h, cur, head)));
