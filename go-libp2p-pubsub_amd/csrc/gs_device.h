@@ -176,7 +176,7 @@ struct Dev {
   uint64_t* pmask;       // [spammers][S] drec.peers: in-edges whose duplicate was counted
   uint8_t* pflag[2];     // IWANT-spam runs: per arena entry, the served verdict of that request
   int32_t* spamRow;      // [E] row of in-edge e in spamCnt when col[e] is an IWANT spammer, else -1
-  uint32_t* spamCnt;     // [rows][S / 4] mcache.peertx counts of those requesters, one byte per slot
+  uint32_t* spamCnt;     // [rows][S / 8] mcache.peertx counts of those requesters, a nibble per slot
   uint8_t* cNSrv[2];     // [E] reply RPCs carrying served messages (0..2)
   // peer gater (peer_gater.go), one per node; stats per (observer, IP) kept on
   // the observer's first edge to a peer of that IP (gGrp = its in-row index)
@@ -276,27 +276,28 @@ __device__ __forceinline__ bool is_traced(const Dev& d, int v) { return d.traced
 __device__ __forceinline__ bool edge_up(const Dev& d, int64_t e) { return d.alive == nullptr || d.alive[e] != 0; }
 // Score(p) of an observer without a record of p is 0 (score.go:246-249)
 // mcache.peertx (mcache.go:66-80) of a requester that is an IWANT spammer: a
-// byte per (in-edge, slot) in HBM instead of the node's LDS hash, which would
+// nibble per (in-edge, slot) in HBM instead of the node's LDS hash, which would
 // need an entry per (message, spammer).  A count only matters while its
 // message is cached (GetForPeer), so it is cleared when the slot is recycled
-// (k_retire) rather than at mcache.Shift.  Saturates at 255 (> GossipRetransmission).
+// (k_retire) rather than at mcache.Shift.  Saturates at 15: handleIWant only
+// compares it with GossipRetransmission, which the host requires to be < 15.
 __device__ __forceinline__ uint32_t* spam_word(const Dev& d, int row, int slot) {
-  return d.spamCnt + (int64_t)row * (d.S >> 2) + (slot >> 2);
+  return d.spamCnt + (int64_t)row * (d.S >> 3) + (slot >> 3);
 }
 __device__ __forceinline__ int spam_incr(const Dev& d, int row, int slot) {
   uint32_t* w = spam_word(d, row, slot);
-  const int sh = (slot & 3) * 8;
+  const int sh = (slot & 7) * 4;
   uint32_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), assumed;
   do {
     assumed = old;
-    if (((assumed >> sh) & 0xFF) == 0xFF) return 0xFF;
+    if (((assumed >> sh) & 0xF) == 0xF) return 0xF;
     old = atomicCAS(w, assumed, assumed + (1u << sh));
   } while (old != assumed);
-  return (int)((assumed >> sh) & 0xFF) + 1;
+  return (int)((assumed >> sh) & 0xF) + 1;
 }
 __device__ __forceinline__ int spam_count(const Dev& d, int row, int slot) {
   const uint32_t x = __hip_atomic_load(spam_word(d, row, slot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return (int)((x >> ((slot & 3) * 8)) & 0xFF);
+  return (int)((x >> ((slot & 7) * 4)) & 0xF);
 }
 // count one or more RPCs of `bytes` in total sent over the sender's edge e
 __device__ __forceinline__ void acct_send(const Dev& d, int64_t e, int64_t bytes, int n) {
@@ -332,7 +333,7 @@ __device__ __forceinline__ void trace_emit(const Dev& d, int64_t hop, int type, 
 // A block is the RPC event and its nItems items, contiguous in the buffer;
 // gen(put) must call put(kind, topic, msg) exactly nItems times.  One lane.
 template <class G>
-__device__ void rpc_trace(const Dev& d, int64_t hop, int snd, int rcv, int sPhase, int rPhase, int64_t ord, int nItems,
+__device__ __forceinline__ void rpc_trace(const Dev& d, int64_t hop, int snd, int rcv, int sPhase, int rPhase, int64_t ord, int nItems,
                           G&& gen) {
   for (int dir = 0; dir < 2; ++dir) {
     const int node = dir ? rcv : snd, peer = dir ? snd : rcv;

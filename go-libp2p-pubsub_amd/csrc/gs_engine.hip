@@ -221,7 +221,8 @@ struct gs_engine {
     hipEvent_t ev = nullptr;
     bool used = false;
   };
-  static constexpr int kStages = 8;
+  static constexpr int kStages = 16;
+  Dev* dDev = nullptr;  // device copy of d for the kernels that take it by pointer (k_phase_a / k_phase_b)
   Stage stages[kStages];
   int stageNext = 0;
   int upload(void* dst, const void* src, size_t bytes) {
@@ -459,6 +460,8 @@ int gs_engine::start() {
   directInitHop = gp.DirectConnectInitialDelay <= 0 ? 0 : (gp.DirectConnectInitialDelay + cfg.hop_ns - 1) / cfg.hop_ns;
 
   Dev& x = d;
+  dDev = dalloc<Dev>(1);
+  if (!dDev) { gs_set_error("device allocation failed (Dev record)"); return GS_ENOMEM; }
   x.N = N; x.T = T; x.Wt = Wt; x.W = W; x.St = St; x.S = S; x.R = R;
   x.HL = gp.HistoryLength; x.HG = gp.HistoryGossip; x.E = E;
   x.router = cfg.router; x.scoring = scoring; x.floodPublish = floodPublish;
@@ -660,10 +663,7 @@ int gs_engine::start() {
         if (behaveH[v] & GS_BEHAVE_IWANT_SPAM) row[v] = nsp++;
       x.pmaskRow = dalloc<int32_t>(N); chk(x.pmaskRow);
       x.pmask = dalloc<uint64_t>((size_t)nsp * S); chk(x.pmask);
-      if (ok) {
-        HIPCHECK(hipMemcpyAsync(x.pmaskRow, row.data(), (size_t)N * 4, hipMemcpyHostToDevice, stream));
-        HIPCHECK(hipStreamSynchronize(stream));  // row is pageable and dies with this block
-      }
+      if (ok) HIPCHECK(hipMemcpyAsync(x.pmaskRow, row.data(), (size_t)N * 4, hipMemcpyHostToDevice, stream));
       // peertx counts of the owned edges whose peer is an IWANT spammer
       spamRowH.assign((size_t)E, -1);
       int64_t nrow = 0;
@@ -672,7 +672,11 @@ int gs_engine::start() {
       if (nrow > INT32_MAX) { gs_set_error("too many IWANT-spammer edges"); return GS_ECAPACITY; }
       x.spamRow = dalloc<int32_t>(E); chk(x.spamRow);
       for (int k = 0; k < 2; ++k) { x.pflag[k] = dalloc<uint8_t>((size_t)poolSeg * world); chk(x.pflag[k]); }
-      x.spamCnt = dalloc<uint32_t>((size_t)std::max<int64_t>(nrow, 1) * (S / 4)); chk(x.spamCnt);
+      if (gp.GossipRetransmission >= 15) {  // spam_incr's nibble saturates at 15
+        gs_set_error("IWANT spammers need GossipRetransmission < 15 in this build");
+        return GS_EUNSUPPORTED;
+      }
+      x.spamCnt = dalloc<uint32_t>((size_t)std::max<int64_t>(nrow, 1) * (S / 8)); chk(x.spamCnt);
       if (ok) HIPCHECK(hipMemcpyAsync(x.spamRow, spamRowH.data(), (size_t)E * 4, hipMemcpyHostToDevice, stream));
       // `row` is pageable and dies with this block: the copy must have read it
       HIPCHECK(hipStreamSynchronize(stream));
@@ -1211,14 +1215,18 @@ int gs_engine::stepOne() {
     const bool hasUnc = d.needAge || (adv && d.pmaskRow != nullptr);
     size_t lds = (narrow ? 2 : 4) * nCnt + 16 * (size_t)nR + (size_t)nYp + (hasUnc ? 4 * nCnt : 0);
     if (adv) lds += 4 * nCnt + 4 * 64 * 4 + 8 * 64 + 8 * (size_t)nR;
+    if (nOwn) {
+      const int rc = upload(dDev, &d, sizeof(Dev));
+      if (rc) return rc;
+    }
     TIMED(this, GS_K_PHASE_A, launch_wpl(W, [&](auto w) {
             if (!nOwn) return;
             constexpr int WV = decltype(w)::value;
             if (adv) {
               if (narrow)
-                k_phase_a<WV, true, true><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR, nYp);
+                k_phase_a<WV, true, true><<<nOwn, 64, lds, stream>>>(dDev, h, cur, head, amR, amW, nR, nYp);
               else
-                k_phase_a<WV, false, true><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR, nYp);
+                k_phase_a<WV, false, true><<<nOwn, 64, lds, stream>>>(dDev, h, cur, head, amR, amW, nR, nYp);
             } else if (narrow) {
               k_phase_a<WV, true, false><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR, nYp);
             } else {
@@ -1257,14 +1265,18 @@ int gs_engine::stepOne() {
       cutMode = (int64_t)(b2 - a) > (int64_t)gp.MaxIHaveLength ? 1 : 0;
     }
     const size_t ldsB = d.ptxCap > GS_PTX ? GS_CUTLDS + 4 * ((size_t)1 << d.ptxHBits) : (cutMode ? GS_CUTLDS : 0);
+    if (nOwn) {
+      const int rc = upload(dDev, &d, sizeof(Dev));
+      if (rc) return rc;
+    }
     TIMED(this, GS_K_PHASE_B,
           launch_wpl(W, [&](auto wpl) {
             constexpr int WV = decltype(wpl)::value;
             if (!nOwn) return;
             if (topicVal != 0 || gaterOn || behaveAll != 0 || anyPhantom || cutMode)
-              k_phase_b<WV, true><<<nOwn, 64, ldsB, stream>>>(d, h, now, cur, head, cutMode);
+              k_phase_b<WV, true><<<nOwn, 64, ldsB, stream>>>(dDev, h, now, cur, head, cutMode);
             else
-              k_phase_b<WV, false><<<nOwn, 64, ldsB, stream>>>(d, h, now, cur, head, 0);
+              k_phase_b<WV, false><<<nOwn, 64, ldsB, stream>>>(dDev, h, now, cur, head, 0);
           }));
   }
   if (refreshDue(now)) {

@@ -595,9 +595,18 @@ __device__ __forceinline__ int wave_min_int(int x) {
 //     deliverer, then message id) are validated, the copies of the rest are
 //     RejectValidationQueueFull (not seen; the gater's throttle counter);
 //   * an IWANT spammer re-requests every message it received, per sender.
+// ADV takes the Dev record from device memory (the engine uploads it before
+// the launch): as a by-value argument the compiler copied all 1.5 KB of it to
+// every lane's scratch in the adversarial instantiations.  The honest path
+// keeps the kernel-argument copy (a little faster there).
+template <bool ADV>
+using PhaseADev = std::conditional_t<ADV, const Dev*, Dev>;
+__device__ __forceinline__ const Dev& dev_of(const Dev& d) { return d; }
+__device__ __forceinline__ const Dev& dev_of(const Dev* d) { return *d; }
 template <int WPL, bool NARROW, bool ADV>
-__global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int cur, int head, WMask amR, WMask amW,
-                                                int nR, int nY) {
+__global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, int64_t h, int cur, int head,
+                                                WMask amR, WMask amW, int nR, int nY) {
+  const Dev& d = dev_of(dArg);
   extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
   const int nCnt = (d.T * d.maxDeg + 7) & ~7;
   const int nCntW = NARROW ? nCnt / 2 : nCnt;             // LDS words of the counter table
@@ -934,7 +943,38 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
     }
     __syncthreads();
   };
-  walk([&](int i, int slot) { deliver(i, slot, true); }, true);
+  long long nValidated = 0, nRejected = 0, nThrottledCopies = 0;
+  // ADV: a copy of a message dropped by a full validation queue (the second
+  // walk below): RejectValidationQueueFull, neither a delivery nor a duplicate
+  bool dropPass = false;
+  auto drop = [&](int i, int slot, bool payloadRpc) {
+    const int rk = sRk[slot >> 6];
+    if (rk == 0xFFFF || !((sDrop[rk] >> (slot & 63)) & 1)) return;
+    if (payloadRpc && gated(i, slot)) return;
+    const int t = (int)__umulhi((unsigned)slot, d.stMagic);
+    const int kind = kindOf(slot, t);
+    atomicSub(&sPer[i], 1u);
+    if (kind == GS_MSG_REJECT) atomicSub(&sInv[i * T + t], 1u);
+    if (kind == GS_MSG_VALID) {
+      if (NARROW) {
+        const int pl = i * T + t;
+        atomicSub(&scnt[pl >> 1], 1u << (16 * (pl & 1)));
+      } else {
+        atomicSub(&scnt[i * T + t], 1u);
+      }
+    }
+    ++nThrottledCopies;
+    --nCopies;
+    if (trv)  // validation.go:240
+      trace_emit(d, h, GS_TRACE_REJECT_MESSAGE, v, d.col[base + i], t, d.slotMid[slot], 2, GS_REJECT_QUEUE_FULL);
+  };
+  // one walk instantiation for both passes (a second one made the compiler
+  // copy the kernel arguments to scratch)
+  auto onCopy = [&](int i, int slot) {
+    if (ADV && dropPass) drop(i, slot, true);
+    else deliver(i, slot, true);
+  };
+  walk(onCopy, true);
   if (__ballot(((relayAll | pubAll) & ~sv) != 0)) {
     // copies of topics v is not subscribed to: transmitted, then ignored
     // (churn runs only: a mesh or announced peer that has just left)
@@ -1009,7 +1049,6 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
       }
     }
   }
-  long long nValidated = 0, nRejected = 0, nThrottledCopies = 0;
   bool anyDrop = false;
   if constexpr (ADV) {
     // ---- the validation queue: the first valQueue fresh messages of topics
@@ -1131,28 +1170,8 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(Dev d, int64_t h, int 
       // ---- second walk: every copy of a dropped message is RejectValidation-
       // QueueFull: neither a delivery nor a duplicate (its counts leave the
       // tables), the gater's throttle, and it fulfils promises (gossip_tracer.go:133)
-      auto drop = [&](int i, int slot, bool payloadRpc) {
-        const int rk = sRk[slot >> 6];
-        if (rk == 0xFFFF || !((sDrop[rk] >> (slot & 63)) & 1)) return;
-        if (payloadRpc && gated(i, slot)) return;
-        const int t = (int)__umulhi((unsigned)slot, d.stMagic);
-        const int kind = kindOf(slot, t);
-        atomicSub(&sPer[i], 1u);
-        if (kind == GS_MSG_REJECT) atomicSub(&sInv[i * T + t], 1u);
-        if (kind == GS_MSG_VALID) {
-          if (NARROW) {
-            const int pl = i * T + t;
-            atomicSub(&scnt[pl >> 1], 1u << (16 * (pl & 1)));
-          } else {
-            atomicSub(&scnt[i * T + t], 1u);
-          }
-        }
-        ++nThrottledCopies;
-        --nCopies;
-        if (trv)  // validation.go:240
-          trace_emit(d, h, GS_TRACE_REJECT_MESSAGE, v, d.col[base + i], t, d.slotMid[slot], 2, GS_REJECT_QUEUE_FULL);
-      };
-      walk([&](int i, int slot) { drop(i, slot, true); }, false);
+      dropPass = true;
+      walk(onCopy, false);
       if (!gray && !ctlGated)
         for (int k = 0; k < irN; ++k) drop(lane, d.pool[prv][irOff + k], false);
       __syncthreads();
@@ -1462,13 +1481,13 @@ __global__ void k_retire(Dev d, int cur, const int32_t* __restrict__ words, int 
     for (int64_t e = d.rowptr[v]; e < d.rowptr[v + 1]; ++e) {
       const int row = d.spamRow[e];
       if (row < 0) continue;
-      uint32_t* c = d.spamCnt + (int64_t)row * (d.S >> 2) + w * 16;
-      for (int q = 0; q < 16; ++q) {
-        const uint32_t b = (uint32_t)(pm >> (4 * q)) & 0xFu;
+      uint32_t* c = d.spamCnt + (int64_t)row * (d.S >> 3) + w * 8;
+      for (int q = 0; q < 8; ++q) {
+        const uint32_t b = (uint32_t)(pm >> (8 * q)) & 0xFFu;
         if (!b) continue;
         uint32_t m = 0;
-        for (int j = 0; j < 4; ++j)
-          if ((b >> j) & 1) m |= 0xFFu << (8 * j);
+        for (int j = 0; j < 8; ++j)
+          if ((b >> j) & 1) m |= 0xFu << (4 * j);
         c[q] &= ~m;
       }
     }

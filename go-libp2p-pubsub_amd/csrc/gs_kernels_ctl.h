@@ -248,6 +248,21 @@ __device__ __forceinline__ int lane_prefix(int x, int* total) {
   return incl - x;
 }
 
+// The served message ids of request record rec (off << 24 | n) for the RPC
+// trace: every id, or with flags (IWANT-spam runs) those whose request was
+// served.  put(kind, topic, msg) per id.
+template <class P>
+__device__ __forceinline__ void put_served(const Dev& d, const int32_t* pool, const uint8_t* flags, int64_t rec,
+                                           P& put) {
+  const int64_t off = rec >> 24;
+  const int n = (int)(rec & 0xFFFFFF);
+  for (int q = 0; q < n; ++q)
+    if (flags == nullptr || flags[off + q]) {
+      const int slot = pool[off + q];
+      put(GS_RPC_ITEM_MSG, (int)__umulhi((unsigned)slot, d.stMagic), d.slotMid[slot]);
+    }
+}
+
 // Phase B — HandleRPC for every control RPC sent to node v in the previous
 // hop (gossipsub.go:591-838), one wave per node.
 //   step 1 (serial, senders ascending, RPCs in send order: join GRAFTs, reply
@@ -270,7 +285,9 @@ __device__ __forceinline__ int lane_prefix(int x, int* total) {
 // squatters, the dynamic peertx hash, phantom ids and the cuts; the honest
 // instantiation carries none of them.
 template <int WPL, bool ADV>
-__global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int64_t now, int cur, int head, int cutModeArg) {
+__global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict__ dp, int64_t h, int64_t now, int cur,
+                                                int head, int cutModeArg) {
+  const Dev& d = *dp;  // from device memory, as k_phase_a
   const int cutMode = ADV ? cutModeArg : 0;
   __shared__ uint64_t scache[64 * WPL];  // v's mcache windows (handleIWant, step 2)
   uint64_t* const sseen = scache;        // then v's seen row (handleIHave, step 3)
@@ -1042,34 +1059,19 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(Dev d, int64_t h, int6
           }
           // the served ids of one request list: by each request's verdict
           // (pflag) when spam lists exist, else the whole served record
-          auto served = [&](int64_t reqRec, bool useFlags, auto put) {
-            if (useFlags) {
-              const int64_t off = reqRec >> 24;
-              const int n = (int)(reqRec & 0xFFFFFF);
-              for (int q = 0; q < n; ++q)
-                if (d.pflag[prv][off + q]) {
-                  const int slot = d.pool[prv][off + q];
-                  put(GS_RPC_ITEM_MSG, (int)__umulhi((unsigned)slot, d.stMagic), d.slotMid[slot]);
-                }
-            } else {
-              const int64_t off = respRec >> 24;
-              const int n = (int)(respRec & 0xFFFFFF);
-              for (int q = 0; q < n; ++q) {
-                const int slot = d.pool[cur][off + q];
-                put(GS_RPC_ITEM_MSG, (int)__umulhi((unsigned)slot, d.stMagic), d.slotMid[slot]);
-              }
-            }
-          };
-          const bool useFlags = ADV && d.pflag[0] != nullptr;
+          const int32_t* const poolPrv = prv ? d.pool[1] : d.pool[0];
+          const int32_t* const poolCur = cur ? d.pool[1] : d.pool[0];
+          const uint8_t* const flagPrv = (ADV && d.pflag[0] != nullptr) ? (prv ? d.pflag[1] : d.pflag[0]) : nullptr;
           if (srvS > 0 && respRec >= 0)
             rpc_trace(d, h, v, u, 3, 2, GS_RPC_ORD(3, GS_RPC_O_ANS_SPAM), 1 + srvS, [&](auto put) {
               put(GS_RPC_ITEM_CTL, -1, -1);
-              served(spRec, true, put);
+              put_served(d, poolPrv, flagPrv, spRec, put);
             });
           if (srvR > 0 && respRec >= 0)
             rpc_trace(d, h, v, u, 3, 2, GS_RPC_ORD(3, GS_RPC_O_ANS_REPLY), 1 + srvR, [&](auto put) {
               put(GS_RPC_ITEM_CTL, -1, -1);
-              served(iwRec, useFlags, put);
+              if (flagPrv != nullptr) put_served(d, poolPrv, flagPrv, iwRec, put);
+              else put_served(d, poolCur, nullptr, respRec, put);
             });
           if (iwantAny || prunesHb) {
             const int nIw = iwantAny ? (int)(iwantRec & 0xFFFFFF) : 0;
