@@ -284,9 +284,19 @@ def main():
     if args.rpc_accounting:
         from pubsub_amd import WithRPCAccounting
         extra = tuple(extra) + (WithRPCAccounting(1000, id_len=40),)
+    def dev_free():
+        try:
+            import torch
+            return torch.cuda.mem_get_info(local)[0]
+        except Exception:  # noqa: BLE001 — a report field only
+            return None
+    free0 = dev_free()
     eng, g = build_engine(wl, rounds, 3 if partitioned else 3 + rank, local, extra=extra, lib=args.lib)
     # hop 0 (Join) + warm-up rounds: meshes form, the message window fills
     eng.step(1 + args.warmup * HOPS_PER_ROUND)
+    eng.sync()
+    free1 = dev_free()
+    device_gb = round((free0 - free1) / 2**30, 2) if free0 is not None and free1 is not None else None
     setup_s = time.perf_counter() - t_setup
 
     def barrier():
@@ -409,6 +419,7 @@ def main():
         "events_per_step": {k: v // args.steps for k, v in events.items()},
         "roofline": roofline,
         "rooflines_other": rooflines,
+        "device_gib": device_gb,  # device memory the engine holds (free memory before / after its start)
         "setup_s": round(setup_s, 1),
     }
     if args.lib:

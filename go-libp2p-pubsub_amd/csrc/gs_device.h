@@ -190,7 +190,8 @@ struct Dev {
   uint8_t* gGrp;         // [E] in-row index of the edge holding this peer's IP stats
   int64_t* lastpub;        // [N][T], INT64_MIN = none
   uint64_t* fanoutPresent; // [N]
-  int64_t* promMid;  // [N][64]
+  int32_t nOwnH;      // owned nodes n1 - n0: the mcache ring is [R][nOwnH][W] (v - n0)
+  int64_t* promMid;  // [N][64] (owned rows only: the pointer is shifted by n0 rows)
   int64_t* promExp;
   int32_t* promSlot;
   uint8_t* promEdge;

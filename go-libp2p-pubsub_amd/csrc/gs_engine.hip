@@ -536,8 +536,16 @@ int gs_engine::start() {
   x.alive = nullptr; x.rstate = nullptr; x.rexpire = nullptr; x.ipv4 = nullptr; x.ipWL = nullptr;
   x.RetainScore = sp.RetainScore; x.IPThr = sp.IPColocationFactorThreshold;
 
-  x.seen = dalloc<uint64_t>(NW); chk(x.seen);
-  x.hist = dalloc<uint64_t>((size_t)R * NW); chk(x.hist);
+  // Per-node state only the node's own wave touches (seen, the mcache ring,
+  // first-delivery ages / senders, promises, peertx, drec.peers) is allocated
+  // for the owned nodes [n0, n1) only: seen / age / ffrom / promises / peertx
+  // through a base pointer shifted by n0 rows, the mcache ring [R][nOwn][W]
+  // indexed by v - n0 (hist_row).  A partitioned rank holds 1/world of it.
+  const int64_t nOwnN = n1 - n0;
+  const size_t NWo = (size_t)nOwnN * W, NSo = (size_t)nOwnN * S;
+  x.nOwnH = (int32_t)nOwnN;
+  x.seen = dalloc<uint64_t>(NWo); chk(x.seen);
+  x.hist = dalloc<uint64_t>((size_t)R * NWo); chk(x.hist);
   x.gw = cfg.router == GS_ROUTER_GOSSIPSUB ? dalloc<uint64_t>(NW) : nullptr;
   if (cfg.router == GS_ROUTER_GOSSIPSUB) chk(x.gw);
   // per-slot first-delivery hops only when read back or when the P3 window
@@ -546,10 +554,14 @@ int gs_engine::start() {
   // that long always credits it (score.go:955)
   x.record = record ? 1 : 0;
   x.needAge = (x.record || (scoring && ageWindowNeeded())) ? 1 : 0;
-  x.age = x.needAge ? dalloc<int16_t>(NS) : nullptr;
-  x.ffrom = x.record ? dalloc<uint8_t>(NS) : nullptr;
+  x.age = x.needAge ? dalloc<int16_t>(NSo) : nullptr;
+  x.ffrom = x.record ? dalloc<uint8_t>(NSo) : nullptr;
   if (x.needAge) chk(x.age);
   if (x.record) chk(x.ffrom);
+  if (!ok) { gs_set_error("device allocation failed (per-node state)"); return GS_ENOMEM; }
+  x.seen -= (size_t)n0 * W;
+  if (x.age) x.age -= (size_t)n0 * S;
+  if (x.ffrom) x.ffrom -= (size_t)n0 * S;
   // frontier lists: per node FC entries of 4 bytes (a node's first deliveries
   // of one hop plus its own publishes), at most 8 GiB per parity
   {
@@ -572,18 +584,22 @@ int gs_engine::start() {
   if (cfg.router == GS_ROUTER_RANDOMSUB) chk(x.sel);
   x.lastpub = dalloc<int64_t>((size_t)N * T); chk(x.lastpub);
   x.fanoutPresent = dalloc<uint64_t>(N); chk(x.fanoutPresent);
-  const size_t NQ = (size_t)N * GS_TABLE;
+  const size_t NQ = (size_t)nOwnN * GS_TABLE;
   x.promMid = dalloc<int64_t>(NQ); x.promExp = dalloc<int64_t>(NQ); x.promSlot = dalloc<int32_t>(NQ);
-  x.promEdge = dalloc<uint8_t>(NQ); x.promN = dalloc<int32_t>(N);
+  x.promEdge = dalloc<uint8_t>(NQ); x.promN = dalloc<int32_t>(nOwnN);
   // mcache.peertx: 512 entries per node.  With IWANT spammers present the
   // honest requests grow too (messages dropped by validation queues come back
   // through gossip), so those runs get 4096; the spammers' own requests, one
   // per (message, spammer), are counted in spamCnt instead
   x.ptxCap = (behaveAll & GS_BEHAVE_IWANT_SPAM) ? 4096 : GS_PTX;
   x.ptxHBits = 13;  // the dynamic hash of the 4096-entry table: 8192 slots (32 KiB)
-  x.ptx = dalloc<uint64_t>((size_t)N * x.ptxCap); x.ptxN = dalloc<int32_t>(N);
+  x.ptx = dalloc<uint64_t>((size_t)nOwnN * x.ptxCap); x.ptxN = dalloc<int32_t>(nOwnN);
   chk(x.promMid); chk(x.promExp); chk(x.promSlot); chk(x.promEdge); chk(x.promN);
   chk(x.ptx); chk(x.ptxN);
+  if (!ok) { gs_set_error("device allocation failed (promises / peertx)"); return GS_ENOMEM; }
+  x.promMid -= (size_t)n0 * GS_TABLE; x.promExp -= (size_t)n0 * GS_TABLE;
+  x.promSlot -= (size_t)n0 * GS_TABLE; x.promEdge -= (size_t)n0 * GS_TABLE; x.promN -= n0;
+  x.ptx -= (size_t)n0 * x.ptxCap; x.ptxN -= n0;
   x.mesh = dalloc<uint64_t>(E); x.fanout = dalloc<uint64_t>(E);
   chk(x.mesh); chk(x.fanout);
   for (int k = 0; k < 2; ++k) {
@@ -659,7 +675,7 @@ int gs_engine::start() {
       }
       std::vector<int32_t> row(N, -1);
       int nsp = 0;
-      for (int v = 0; v < N; ++v)
+      for (int v = n0; v < n1; ++v)  // drec.peers rows of the owned spammers
         if (behaveH[v] & GS_BEHAVE_IWANT_SPAM) row[v] = nsp++;
       x.pmaskRow = dalloc<int32_t>(N); chk(x.pmaskRow);
       x.pmask = dalloc<uint64_t>((size_t)nsp * S); chk(x.pmask);

@@ -1045,7 +1045,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
         Sw[j] = d.seen[(int64_t)v * W + w];
         Uw[j] = D;  // & ~seen below
         Ow[j] = d.oldm[w];
-        if (d.router == 2) Hw[j] = d.hist[((int64_t)head * d.N + v) * W + w];
+        if (d.router == 2) Hw[j] = d.hist[((int64_t)head * d.nOwnH + (v - d.n0)) * W + w];
       }
     }
   }
@@ -1391,7 +1391,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
     if (U) {
       if ((U & Ow[j]) || !wm_has(amW, w)) set_err(d, E_LATE);
       d.seen[(int64_t)v * W + w] = Sw[j] | U;
-      if (d.router == 2 && Ud) d.hist[((int64_t)head * d.N + v) * W + w] = Hw[j] | Ud;
+      if (d.router == 2 && Ud) d.hist[((int64_t)head * d.nOwnH + (v - d.n0)) * W + w] = Hw[j] | Ud;
       nDeliv += k;
       uint64_t y = Ud;
       while (y) {
@@ -1526,7 +1526,7 @@ __global__ void k_publish(Dev d, int b, int n, int64_t h, int cur, int head) {
     const int w = slot >> 6;
     const unsigned long long bit = 1ull << (slot & 63);
     atomicOr((unsigned long long*)&d.seen[(int64_t)src * d.W + w], bit);
-    if (d.router == 2) atomicOr((unsigned long long*)&d.hist[((int64_t)head * d.N + src) * d.W + w], bit);
+    if (d.router == 2) atomicOr((unsigned long long*)&d.hist[((int64_t)head * d.nOwnH + (src - d.n0)) * d.W + w], bit);
     if (d.needAge) d.age[(int64_t)src * d.S + slot] = 0;
     if (d.record) d.ffrom[(int64_t)src * d.S + slot] = 255;
     return;
@@ -1538,7 +1538,7 @@ __global__ void k_publish(Dev d, int b, int n, int64_t h, int cur, int head) {
   const int w = slot >> 6;
   const unsigned long long bit = 1ull << (slot & 63);
   atomicOr((unsigned long long*)&d.seen[(int64_t)src * d.W + w], bit);
-  if (d.router == 2) atomicOr((unsigned long long*)&d.hist[((int64_t)head * d.N + src) * d.W + w], bit);
+  if (d.router == 2) atomicOr((unsigned long long*)&d.hist[((int64_t)head * d.nOwnH + (src - d.n0)) * d.W + w], bit);
   if (d.needAge) d.age[(int64_t)src * d.S + slot] = 0;
   if (d.record) d.ffrom[(int64_t)src * d.S + slot] = 255;
   ctr_add(d, C_PUBLISHED, 1ull);

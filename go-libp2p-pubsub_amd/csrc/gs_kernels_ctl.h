@@ -530,7 +530,7 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
     const int hN = 1 << hbits;
     for (int w = lane; w < W; w += 64) {
       uint64_t x = 0;
-      for (int k = 0; k < d.HL; ++k) x |= d.hist[((int64_t)((head + k) % d.R) * d.N + v) * W + w];
+      for (int k = 0; k < d.HL; ++k) x |= d.hist[((int64_t)((head + k) % d.R) * d.nOwnH + (v - d.n0)) * W + w];
       scache[w] = x;
     }
     for (int k = lane; k < hN; k += 64) hT[k] = 0u;
@@ -1542,7 +1542,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
       uint64_t y[2][GS_MAX_WPL];
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
-        const uint64_t* src = d.hist + ((int64_t)((head + k0 + k) % d.R) * d.N + v) * d.W;
+        const uint64_t* src = d.hist + ((int64_t)((head + k0 + k) % d.R) * d.nOwnH + (v - d.n0)) * d.W;
 #pragma unroll
         for (int j = 0; j < GS_MAX_WPL; ++j) {
           const int w = lane + 64 * j;
@@ -1853,7 +1853,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
         // applies emitGossip's MaxIHaveLength cut, include/gs_trace.h)
         auto gwWord = [&](int w) {
           uint64_t x = 0;
-          for (int k = 0; k < d.HG; ++k) x |= d.hist[((int64_t)((head + k) % d.R) * d.N + v) * d.W + w];
+          for (int k = 0; k < d.HG; ++k) x |= d.hist[((int64_t)((head + k) % d.R) * d.nOwnH + (v - d.n0)) * d.W + w];
           return x;
         };
         int nIh = 0;
@@ -1895,7 +1895,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
   const int n = d.ptxN[v];
   if (n > 0) {
     const int last = (head + d.HL - 1) % d.R;
-    const uint64_t* lastw = d.hist + ((int64_t)last * d.N + v) * d.W;
+    const uint64_t* lastw = d.hist + ((int64_t)last * d.nOwnH + (v - d.n0)) * d.W;
     int kept = 0;
     for (int base = 0; base < n; base += 64) {
       const int q = base + lane;
@@ -1913,7 +1913,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
     }
     if (lane == 0) d.ptxN[v] = kept;
   }
-  for (int w = lane; w < d.W; w += 64) d.hist[((int64_t)newhead * d.N + v) * d.W + w] = 0;
+  for (int w = lane; w < d.W; w += 64) d.hist[((int64_t)newhead * d.nOwnH + (v - d.n0)) * d.W + w] = 0;
   GS_STAMPH(5, GS_CLK());
 }
 

@@ -59,7 +59,7 @@ def test_reference_order_distance(oracle_path, name):
     ca, cb = a["counters"], b["counters"]
     assert np.array_equal(a["mesh"], b["mesh"]), "meshes differ"
     if not any(k in name for k in ("gossipsub", "churn", "sinkhole", "squatters", "adversarial", "spam_invalid",
-                                  "acct_multitopic", "acct_graylist")):
+                                  "acct_multitopic", "acct_graylist", "px_", "direct_")):
         # floodsub / randomsub carry no control; the spam pairs handle one RPC kind per hop
         assert scenarios.compare(a, b) == []
         return
