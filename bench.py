@@ -417,6 +417,10 @@ def main():
         "hops_per_sec": rounds_per_s * HOPS_PER_ROUND,
         "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kstats.items() if v[1]},
         "events_per_step": {k: v // args.steps for k, v in events.items()},
+        # the control counters depend on the canonical schedule: each
+        # hop handles every payload RPC before any control RPC; the per-RPC order of
+        # the oracle's reference mode roughly doubles iwant_sent on gossipsub_scored
+        "schedule": "phase split: payload before control per hop (DESIGN.md 3a; per-RPC order ~2x iwant_sent)",
         "roofline": roofline,
         "rooflines_other": rooflines,
         "device_gib": device_gb,  # device memory the engine holds (free memory before / after its start)
