@@ -16,6 +16,7 @@
 #include "../../include/gs_rng.h"
 #include "../../include/gs_rpcsize.h"
 #include "../../include/gs_trace.h"
+#include "../../include/gs_fp.h"
 
 #define GS_WAVE 64
 // Occupancy hints (waves per SIMD the register allocator must allow) of the
@@ -451,13 +452,10 @@ __device__ __forceinline__ bool select_k(bool cand, uint64_t key, int k) {
 
 // "+1, cap" applied n times — markFirstMessageDelivery / markDuplicate-
 // MessageDelivery (score.go:915-928, 960-963) one message at a time, since
-// (x+1)+1 != x+2 for fractional decayed counters.
+// (x+1)+1 != x+2 for fractional decayed counters: gs_add_ones_capped
+// (include/gs_fp.h) takes one exact add per binade, same result.
 __device__ __forceinline__ double add_ones_capped(double x, int n, double cap) {
-  for (int i = 0; i < n; ++i) {
-    x += 1.0;
-    if (x > cap) { x = cap; break; }
-  }
-  return x;
+  return gs_add_ones_capped(x, n, cap);
 }
 
 // One topic's contribution topicScore * TopicWeight (score.go:265-311) for

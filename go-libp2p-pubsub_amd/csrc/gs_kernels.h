@@ -1285,7 +1285,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
         const uint32_t n = ((scoredT >> t) & 1) ? sInv[pl] : 0u;
         if (!n) continue;
         double x = d.imd[base * T + pl];
-        for (uint32_t k = 0; k < n; ++k) x += 1.0;
+        x = gs_add_ones(x, n);  // +1 steps (include/gs_fp.h)
         d.imd[base * T + pl] = x;
         d.sdirty[base + pl / T] = 1;  // a score-lowering change
       }
@@ -1316,7 +1316,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
           const uint32_t n = sPer[k * 64 + lane];
           if (!n) continue;
           double x = d.gSt[k * d.E + base + lane];
-          for (uint32_t c = 0; c < n; ++c) x += 1.0;
+          x = gs_add_ones(x, n);
           d.gSt[k * d.E + base + lane] = x;
         }
       }
@@ -1324,12 +1324,12 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
       if (lane == 0) {
         if (nValidated) {
           double x = d.gValidate[v];
-          for (long long c = 0; c < nValidated; ++c) x += 1.0;
+          x = gs_add_ones(x, nValidated);
           d.gValidate[v] = x;
         }
         if (thc) {
           double x = d.gThrottle[v];
-          for (long long c = 0; c < thc; ++c) x += 1.0;
+          x = gs_add_ones(x, thc);
           d.gThrottle[v] = x;
           d.gLast[v] = h * d.hop_ns;
         }
