@@ -40,7 +40,11 @@ HOPS_PER_ROUND = 10
 MSGS_PER_ROUND = 1000
 
 WORKLOADS = {
-    "config4": dict(n=1_000_000, k=32, topics=64, slots=256),
+    # slots per topic: a message holds its slot for retireHops = 100 hops (3
+    # heartbeats of delivery horizon + HistoryLength + 2 heartbeats), i.e. 10
+    # rounds x 1000 / 64 = 157 messages per topic; 192 (3 words) is the least
+    # multiple of 64 that covers it (W = 192 words: phase A's 3-word variant)
+    "config4": dict(n=1_000_000, k=32, topics=64, slots=192),
     "config3": dict(n=1_000_000, k=32, topics=1, slots=10048),
     # BASELINE configs[4] (the adversarial run) on ONE GPU: 1M peers (the
     # 10M-peer figure is the 8-GPU node's; --peers raises it), 20% Sybils split
@@ -224,6 +228,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="partition", choices=["partition", "replicas"])
     ap.add_argument("--peers", type=int, default=0, help="override the workload's peer count (rehearsals)")
+    ap.add_argument("--slots", type=int, default=0,
+                    help="override the engine's message slots per topic (a capacity, not the workload)")
     ap.add_argument("--transport", default="torch", choices=["rccl", "torch"],
                     help="partitioned ranks' exchange: torch.distributed collectives (RCCL under the "
                          "nccl backend; the default, whose multi-rank path the tests run over gloo) or "
@@ -278,6 +284,8 @@ def main():
     wl = dict(WORKLOADS[args.workload])
     if args.peers:
         wl["n"] = args.peers
+    if args.slots:
+        wl["slots"] = args.slots
     rounds = args.warmup + args.steps + 1
     t_setup = time.perf_counter()
     # partitioned ranks simulate ONE graph and schedule (same seed); replicas differ
