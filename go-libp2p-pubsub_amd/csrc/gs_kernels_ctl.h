@@ -528,11 +528,8 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
       while (hbits < d.ptxHBits && (1 << hbits) < need) ++hbits;
     }
     const int hN = 1 << hbits;
-    for (int w = lane; w < W; w += 64) {
-      uint64_t x = 0;
-      for (int k = 0; k < d.HL; ++k) x |= d.hist[((int64_t)((head + k) % d.R) * d.nOwnH + (v - d.n0)) * W + w];
-      scache[w] = x;
-    }
+    __shared__ uint64_t sNeedW[GS_MAX_WPL];  // the mcache words the requests name (bit per word)
+    if (lane < GS_MAX_WPL) sNeedW[lane] = 0ull;
     for (int k = lane; k < hN; k += 64) hT[k] = 0u;
     const int itI = (nI + 15) >> 4, itS = (nS + 15) >> 4;
     int totalItems;
@@ -575,6 +572,25 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
     auto cached = [&](int slot) {
       return ((scache[slot >> 6] >> (slot & 63)) & 1) && !(ADV && d.slotKind[slot] == GS_MSG_PHANTOM);
     };
+    // v's mcache windows (HistoryLength windows ORed) for the words the
+    // requests name only: a node serves a few dozen ids, not W words' worth
+    for (int b = lane; b < totalItems; b += 64) {
+      int i, off, cnt;
+      bool sp;
+      item(b, i, off, cnt, sp);
+      for (int q = 0; q < cnt; ++q) {
+        const int w = d.pool[prv][off + q] >> 6;
+        atomicOr((unsigned long long*)&sNeedW[w >> 6], 1ull << (w & 63));
+      }
+    }
+    __syncthreads();
+    for (int w = lane; w < W; w += 64) {
+      if (!((sNeedW[w >> 6] >> (w & 63)) & 1)) continue;
+      uint64_t x = 0;
+      for (int k = 0; k < d.HL; ++k) x |= d.hist[((int64_t)((head + k) % d.R) * d.nOwnH + (v - d.n0)) * W + w];
+      scache[w] = x;
+    }
+    __syncthreads();
     // pass a: increments and per-sender served counts.  A spammer's two lists
     // may name the same message (a copy dropped by the validation queue stays
     // unseen, so it is asked for again after the IHAVE): its re-request RPC was
