@@ -101,6 +101,8 @@ def build_engine(wl, rounds, seed, device, lib=None, n=None, msgs_per_round=None
     eng = NewGossipSub(n, T, g, subs, *opts, *extra, lib=lib, **kw)
     eng.publish(src, top, hops, kind=kind)
     eng.schedule = (top, hops)
+    eng.kinds = kind  # GS_MSG_* per published message (None: all valid)
+    eng.ipv4 = kw.get("ipv4")
     return eng, g
 
 

@@ -24,6 +24,7 @@
 
 #include "../../include/gossip_engine.h"
 #include "../../include/gs_trace.h"
+#include "../../include/gs_proto.h"
 #include "gs_host.h"
 #include "gs_kernels.h"
 #include "gs_kernels_ctl.h"
@@ -64,6 +65,15 @@ struct gs_engine {
   std::vector<int64_t> rowptr;
   std::vector<int32_t> col, rev, esrc;
   std::vector<uint8_t> outbound, direct;
+  // mixed networks (gs_set_routers / gs_set_graph_ex): the router of every
+  // host and the protocol of every connection (empty: cfg.router's own)
+  std::vector<uint8_t> routerH, protoH;
+  bool mixed = false;
+  int validateMixed();
+  int routerOf(int u) const {  // GS_ROUTER_* with the v1.0 variant folded into gossipsub
+    const int r = routerH.empty() ? cfg.router : (int)routerH[u];
+    return r == GS_ROUTER_GOSSIPSUB_V10 ? GS_ROUTER_GOSSIPSUB : r;
+  }
   std::vector<uint64_t> sub;
   std::vector<double> app;
   std::vector<uint32_t> ipv4;
@@ -370,7 +380,56 @@ static void score_rows(const Dev& d, int64_t nEdges, int T, double* out, hipStre
     }                                                         \
   } while (0)
 
+// The rules of gs_set_routers / gs_set_graph_ex (gossip_engine.h): protocols
+// both hosts speak, equal on both directions; the negotiated one by default.
+int gs_engine::validateMixed() {
+  auto rt = [&](int u) { return routerH.empty() ? cfg.router : (int)routerH[u]; };
+  mixed = !routerH.empty() || !protoH.empty();
+  const bool given = !protoH.empty();
+  if (!given) protoH.assign((size_t)E, 0);
+  auto edgeOf = [&](int a, int b) -> int64_t {
+    return (int64_t)(std::lower_bound(col.begin() + rowptr[a], col.begin() + rowptr[a + 1], b) - col.begin());
+  };
+  for (int u = 0; u < N; ++u) {
+    const int ru = rt(u);
+    const bool gsHost = ru == GS_ROUTER_GOSSIPSUB || ru == GS_ROUTER_GOSSIPSUB_V10;
+    if (gsHost && cfg.router != GS_ROUTER_GOSSIPSUB) {
+      gs_set_error("gossipsub hosts need cfg.router == GS_ROUTER_GOSSIPSUB (their params come from the engine)");
+      return GS_EINVAL;
+    }
+    if (!behaveH.empty() && behaveH[u] && !gsHost) { gs_set_error("attacker behaviours need gossipsub hosts"); return GS_EINVAL; }
+    for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) {
+      const int v = col[e], rv = rt(v);
+      if (!gsHost && !direct.empty() && direct[e]) { gs_set_error("direct peers need a gossipsub host"); return GS_EINVAL; }
+      if (!given) {
+        protoH[e] = (uint8_t)gs_negotiate(ru, rv);
+        continue;
+      }
+      const int64_t r = edgeOf(v, u);
+      const int pr = protoH[e] == GS_PROTO_DEFAULT ? gs_negotiate(ru, rv) : protoH[e];
+      const int pb = protoH[r] == GS_PROTO_DEFAULT ? gs_negotiate(rv, ru) : protoH[r];
+      if (pr != pb || !gs_router_speaks(ru, pr) || !gs_router_speaks(rv, pr)) {
+        gs_set_error("proto[e] must be a protocol both hosts speak, equal on both directions of the connection");
+        return GS_EINVAL;
+      }
+    }
+  }
+  if (given)
+    for (int u = 0; u < N; ++u)
+      for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e)
+        if (protoH[e] == GS_PROTO_DEFAULT) protoH[e] = (uint8_t)gs_negotiate(rt(u), rt(col[e]));
+  return GS_OK;
+}
+
 int gs_engine::start() {
+  {
+    const int rc = validateMixed();
+    if (rc) return rc;
+    if (mixed) {
+      gs_set_error("mixed router networks are not built in this library yet");
+      return GS_EUNSUPPORTED;
+    }
+  }
   if (doPX && (gaterOn || behaveAll != 0 || world > 1 || acctOn)) {
     gs_set_error("peer exchange is supported by an honest, unpartitioned engine without the gater or RPC accounting");
     return GS_EUNSUPPORTED;
@@ -1783,6 +1842,22 @@ int gs_engine_destroy(gs_engine* eng) {
 
 int gs_set_graph(gs_engine* g, const int64_t* rowptr, const int32_t* col, const uint8_t* outbound,
                  const uint8_t* direct) {
+  return gs_set_graph_ex(g, rowptr, col, outbound, direct, nullptr);
+}
+
+int gs_set_routers(gs_engine* g, const uint8_t* router) {
+  if (g->started) { gs_set_error("routers must be set before the first step"); return GS_ESTATE; }
+  g->routerH.clear();
+  if (router) {
+    for (int u = 0; u < g->N; ++u)
+      if (router[u] > GS_ROUTER_GOSSIPSUB_V10) { gs_set_error("unknown router"); return GS_EINVAL; }
+    g->routerH.assign(router, router + g->N);
+  }
+  return GS_OK;
+}
+
+int gs_set_graph_ex(gs_engine* g, const int64_t* rowptr, const int32_t* col, const uint8_t* outbound,
+                    const uint8_t* direct, const uint8_t* proto) {
   if (g->started) { gs_set_error("graph must be set before the first step"); return GS_ESTATE; }
   g->rowptr.assign(rowptr, rowptr + g->N + 1);
   g->E = g->rowptr[g->N];
@@ -1799,6 +1874,12 @@ int gs_set_graph(gs_engine* g, const int64_t* rowptr, const int32_t* col, const 
   g->direct.assign(g->E, 0);
   if (outbound) g->outbound.assign(outbound, outbound + g->E);
   if (direct) g->direct.assign(direct, direct + g->E);
+  g->protoH.clear();
+  if (proto) {
+    for (int64_t e = 0; e < g->E; ++e)
+      if (proto[e] > GS_PROTO_GOSSIPSUB_V11) { gs_set_error("unknown protocol"); return GS_EINVAL; }
+    g->protoH.assign(proto, proto + g->E);
+  }
   g->graphSet = true;
   return GS_OK;
 }
@@ -2188,6 +2269,46 @@ int gs_read_topic_stats(gs_engine* g, double* fmd, double* mmd, double* mfp, dou
   return copy_back_pairs(g, flags, (const uint8_t*)g->d.flags);
 }
 int gs_read_behaviour_penalty(gs_engine* g, double* bp) { return copy_back(g, bp, g->d.bp, g->E * 8); }
+
+// PubSubRouter.EnoughPeers of every owned host (gossip_engine.h), on the host
+// from the mesh readback and the host mirrors of the announced subscriptions
+// (subA), the connection states (aliveH) and the protocols.  A topic no peer
+// announced counts as empty (the reference's missing p.topics entry).
+int gs_enough_peers(gs_engine* g, int32_t topic, int32_t suggested, uint8_t* out) {
+  if (topic < 0 || topic >= g->T || suggested < 0 || !out) { gs_set_error("gs_enough_peers: bad arguments"); return GS_EINVAL; }
+  if (!g->started) { gs_set_error("gs_enough_peers: no state before the first step"); return GS_ESTATE; }
+  std::vector<uint64_t> mesh((size_t)g->E);
+  int rc = copy_back(g, mesh.data(), g->d.mesh, g->E * 8);
+  if (rc) return rc;
+  const uint64_t bit = 1ull << topic;
+  std::memset(out, 0, (size_t)g->N);
+  for (int u = g->n0; u < g->n1; ++u) {
+    int fs = 0, rs = 0, gsn = 0, any = 0;
+    for (int64_t e = g->rowptr[u]; e < g->rowptr[u + 1]; ++e) {
+      if (!g->aliveH.empty() && !g->aliveH[e]) continue;
+      if (!(g->subA[g->col[e]] & bit)) continue;
+      const int pr = g->protoH[e];
+      any++;
+      fs += pr == GS_PROTO_FLOODSUB;
+      rs += pr == GS_PROTO_RANDOMSUB;
+      gsn += (mesh[e] & bit) != 0;
+    }
+    bool ok;
+    switch (g->routerOf(u)) {
+      case GS_ROUTER_GOSSIPSUB:  // gossipsub.go:549-576: floodsub peers = not mesh-capable
+        ok = (fs + rs) + gsn >= (suggested ? suggested : g->gp.Dlo) || gsn >= g->gp.Dhi;
+        break;
+      case GS_ROUTER_RANDOMSUB:  // randomsub.go:59-89 (RandomSubD = 6)
+        ok = fs + rs >= (suggested ? suggested : 6) || rs >= 6;
+        break;
+      default:  // floodsub.go:52-66 (FloodSubTopicSearchSize = 5)
+        ok = any >= (suggested ? suggested : 5);
+        break;
+    }
+    out[u] = ok ? 1 : 0;
+  }
+  return GS_OK;
+}
 
 int gs_read_topic_stats_edges(gs_engine* g, int64_t n, const int64_t* edges, double* fmd, double* mmd,
                               double* mfp, double* imd, int64_t* mesh_time, int64_t* graft_time,

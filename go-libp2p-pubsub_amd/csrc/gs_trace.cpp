@@ -147,7 +147,13 @@ std::vector<Field> sub_fields(const gs_trace_event& e, const std::string& topic,
       return {{1, "messageID", msg_bytes(e.msg), true}, {2, "topic", topic, false},
               {3, "receivedFrom", peer_bytes(e.peer), true}};
     case GS_TRACE_ADD_PEER:  // {peerID=1, proto=2}
-      return {{1, "peerID", peer_bytes(e.peer), true}, {2, "proto", proto ? proto : "", false}};
+    {
+      // the connection's protocol.ID (reason = GS_PROTO_*); 0: the caller's default
+      static const char* const kProto[] = {nullptr, "/floodsub/1.0.0", "/randomsub/1.0.0", "/meshsub/1.0.0",
+                                           "/meshsub/1.1.0"};
+      const char* pr = e.reason >= 1 && e.reason <= 4 ? kProto[e.reason] : proto;
+      return {{1, "peerID", peer_bytes(e.peer), true}, {2, "proto", pr ? pr : "", false}};
+    }
     case GS_TRACE_JOIN:  // {topic=1}
       return {{1, "topic", topic, false}};
     case GS_TRACE_GRAFT:

@@ -6,7 +6,8 @@ build/libgossip_engine.so (gfx950).
 """
 from ._abi import (GS_BEHAVE_GRAFT_SPAM, GS_BEHAVE_IHAVE_SPAM, GS_BEHAVE_IWANT_SPAM, GS_BEHAVE_NO_FORWARD, GS_MSG_IGNORE,  # noqa: F401
                    GS_EV_CONNECT, GS_EV_DISCONNECT, GS_EV_JOIN, GS_EV_LEAVE, GS_MSG_PHANTOM, GS_MSG_REJECT, GS_MSG_VALID, GS_ROUTER_FLOODSUB, GS_ROUTER_GOSSIPSUB,
-                   GS_ROUTER_RANDOMSUB)
+                   GS_ROUTER_RANDOMSUB, GS_ROUTER_GOSSIPSUB_V10, GS_PROTO_DEFAULT, GS_PROTO_FLOODSUB,
+                   GS_PROTO_RANDOMSUB, GS_PROTO_GOSSIPSUB_V10, GS_PROTO_GOSSIPSUB_V11)
 from .params import (DefaultGossipSubParams, DefaultPeerGaterParams, GossipSubParams,  # noqa: F401
                      Hour, Microsecond, Millisecond, Minute, NewPeerGaterParams, PeerGaterParams,
                      PeerScoreParams, PeerScoreThresholds, ScoreParameterDecay,
@@ -16,4 +17,5 @@ from .engine import (PRODUCT_LIB, Engine, GossipEngineError, NewFloodSub, NewGos
                      NewRandomSub, PROTOCOLS, WithDevice, WithEventTracer, encode_trace, WithDirectPeers, WithFloodPublish, WithGossipSubParams,
                      WithHop, WithMessageWindow, WithPartition, WithPeerScore, WithRecordDeliveries, WithSeed,
                      WithBehaviour, WithPeerGater, WithRPCAccounting, WithValidation, WithPeerExchange, WithDormant,
+                     WithRouters, WithProtocols,
                      load)

@@ -20,6 +20,10 @@ GS_EUNSUPPORTED = -6
 GS_ROUTER_FLOODSUB = 0
 GS_ROUTER_RANDOMSUB = 1
 GS_ROUTER_GOSSIPSUB = 2
+GS_ROUTER_GOSSIPSUB_V10 = 3  # gs_set_routers only: a gossipsub host speaking v1.0 + floodsub
+
+# protocol.ID of a connection (gs_set_graph_ex)
+GS_PROTO_DEFAULT, GS_PROTO_FLOODSUB, GS_PROTO_RANDOMSUB, GS_PROTO_GOSSIPSUB_V10, GS_PROTO_GOSSIPSUB_V11 = 0, 1, 2, 3, 4
 
 GS_FLAG_SCORING = 1 << 0
 GS_FLAG_FLOOD_PUBLISH = 1 << 1
@@ -153,6 +157,9 @@ ABI_FUNCTIONS = [
       C.POINTER(PeerGaterParamsC), C.POINTER(P)]),
     ("gs_engine_destroy", C.c_int, [P]),
     ("gs_set_graph", C.c_int, [P, C.POINTER(i64), C.POINTER(i32), C.POINTER(u8), C.POINTER(u8)]),
+    ("gs_set_graph_ex", C.c_int, [P, C.POINTER(i64), C.POINTER(i32), C.POINTER(u8), C.POINTER(u8), C.POINTER(u8)]),
+    ("gs_set_routers", C.c_int, [P, C.POINTER(u8)]),
+    ("gs_enough_peers", C.c_int, [P, i32, i32, C.POINTER(u8)]),
     ("gs_set_subscriptions", C.c_int, [P, C.POINTER(u64)]),
     ("gs_set_peer_attrs", C.c_int, [P, C.POINTER(f64), C.POINTER(u32)]),
     ("gs_set_ip_whitelist", C.c_int, [P, i32, C.POINTER(u32), C.POINTER(u32)]),

@@ -138,6 +138,20 @@ def WithBehaviour(bits):
     return ("behaviour", bits)
 
 
+def WithRouters(routers):
+    """The router each host runs (gs_set_routers): GS_ROUTER_FLOODSUB /
+    RANDOMSUB / GOSSIPSUB / GOSSIPSUB_V10 per node -- a mixed network
+    (TestMixedGossipsub, gossipsub_test.go:810-851)."""
+    return ("routers", np.ascontiguousarray(routers, dtype=np.uint8))
+
+
+def WithProtocols(proto):
+    """The protocol.ID of every connection (GS_PROTO_* per CSR edge, the
+    `proto` of PubSubRouter.AddPeer, pubsub.go:165); default: negotiated from
+    the hosts' routers."""
+    return ("protocols", np.ascontiguousarray(proto, dtype=np.uint8))
+
+
 def WithPartition(rank, world, transport):
     """Simulate only this rank's node range; exchange RPCs with the other
     ranks through `transport` (a pubsub_amd.transport.TorchTransport) once per
@@ -197,8 +211,18 @@ class Engine:
         ob = np.ascontiguousarray(outbound, dtype=np.uint8) if outbound is not None else None
         direct = opts.get("direct")
         direct = np.ascontiguousarray(direct, dtype=np.uint8) if direct is not None else None
-        _check(self.lib, self.lib.gs_set_graph(h, _ptr(self.rowptr, C.c_int64), _ptr(self.col, C.c_int32),
-                                               _ptr(ob, C.c_uint8), _ptr(direct, C.c_uint8)))
+        proto = opts.get("protocols")
+        if proto is None:
+            _check(self.lib, self.lib.gs_set_graph(h, _ptr(self.rowptr, C.c_int64), _ptr(self.col, C.c_int32),
+                                                   _ptr(ob, C.c_uint8), _ptr(direct, C.c_uint8)))
+        else:
+            _check(self.lib, self.lib.gs_set_graph_ex(h, _ptr(self.rowptr, C.c_int64), _ptr(self.col, C.c_int32),
+                                                      _ptr(ob, C.c_uint8), _ptr(direct, C.c_uint8),
+                                                      _ptr(proto, C.c_uint8)))
+        routers = opts.get("routers")
+        if routers is not None:
+            _check(self.lib, self.lib.gs_set_routers(h, _ptr(routers, C.c_uint8)))
+        self.routers = routers
         dormant = opts.get("dormant")
         if dormant:
             da = np.array([a for a, _ in dormant], dtype=np.int32)
@@ -245,6 +269,7 @@ class Engine:
             _check(self.lib, self.lib.gs_set_behaviour(h, _ptr(beh, C.c_uint8)))
         app = np.ascontiguousarray(app_score, dtype=np.float64) if app_score is not None else None
         ips = np.ascontiguousarray(ipv4, dtype=np.uint32) if ipv4 is not None else None
+        self.app_attr, self.ipv4_attr = app, ips  # gs_set_peer_attrs inputs (None: zeros)
         if app is not None or ips is not None:
             _check(self.lib, self.lib.gs_set_peer_attrs(h, _ptr(app, C.c_double), _ptr(ips, C.c_uint32)))
 
@@ -357,6 +382,12 @@ class Engine:
         sh = (len(edges), self.T)
         return dict(fmd=fmd.reshape(sh), mmd=mmd.reshape(sh), mfp=mfp.reshape(sh), imd=imd.reshape(sh),
                     mesh_time=mt.reshape(sh), graft_time=gt.reshape(sh), flags=fl.reshape(sh))
+
+    def enough_peers(self, topic, suggested=0):
+        """PubSubRouter.EnoughPeers(topic, suggested) of every host (bool [N])."""
+        out = np.zeros(self.N, dtype=np.uint8)
+        _check(self.lib, self.lib.gs_enough_peers(self.h, int(topic), int(suggested), _ptr(out, C.c_uint8)))
+        return out.astype(bool)
 
     def behaviour_penalty(self):
         a = np.empty(self.E, dtype=np.float64)

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 2
+#define GS_ABI_VERSION 3
 
 /* ---- error codes ------------------------------------------------------- */
 #define GS_OK 0
@@ -227,6 +227,46 @@ int gs_engine_destroy(gs_engine* eng);
  * direct[e]   != 0: col[e] is a direct peer of u (WithDirectPeers).  NULL = 0. */
 int gs_set_graph(gs_engine* eng, const int64_t* rowptr, const int32_t* col,
                  const uint8_t* outbound, const uint8_t* direct);
+
+/* ---- mixed networks: routers per host, protocols per connection -------- */
+/* The protocol.ID a connection runs, as PubSubRouter.AddPeer(peer.ID,
+ * protocol.ID) receives it (pubsub.go:165; gossipsub.go:505, randomsub.go:49,
+ * floodsub.go:44).  Both hosts of a connection run the same protocol (the one
+ * multistream-select negotiated: the first of the dialer's Protocols() the
+ * listener supports, gossipsub.go:29-30 GossipSubDefaultProtocols). */
+#define GS_PROTO_DEFAULT 0       /* the engine's own: the router of cfg.router     */
+#define GS_PROTO_FLOODSUB 1      /* /floodsub/1.0.0   floodsub.go:12              */
+#define GS_PROTO_RANDOMSUB 2     /* /randomsub/1.0.0  randomsub.go:13             */
+#define GS_PROTO_GOSSIPSUB_V10 3 /* /meshsub/1.0.0    gossipsub.go:23: mesh, no PX */
+#define GS_PROTO_GOSSIPSUB_V11 4 /* /meshsub/1.1.0    gossipsub.go:26: mesh + PX   */
+/* gs_set_graph plus proto[e] (GS_PROTO_*, NULL: negotiated from the hosts'
+ * routers, gs_set_routers).  proto[e] must be one both hosts speak and equal
+ * on both directions of the connection (checked at the first step).  A
+ * gossipsub host sends to a FLOODSUB / RANDOMSUB-protocol peer as to a
+ * floodsub peer: it forwards every message of the peer's topics when the
+ * peer's score >= PublishThreshold (gossipsub.go:969-975), never grafts it or
+ * gossips to it (GossipSubFeatureMesh, gossipsub_feat.go:27-38, getPeers
+ * :1849, emitGossip :1681) and counts it in EnoughPeers (:557-562); to a
+ * GOSSIPSUB_V10 peer its PRUNEs carry neither PX nor a backoff (makePrune
+ * :1804-1807).  A randomsub host always forwards to its FLOODSUB-protocol
+ * peers and samples only its RANDOMSUB-protocol ones (randomsub.go:117-150). */
+int gs_set_graph_ex(gs_engine* eng, const int64_t* rowptr, const int32_t* col,
+                    const uint8_t* outbound, const uint8_t* direct, const uint8_t* proto);
+/* The router each host runs (NewFloodSub / NewRandomSub / NewGossipSub):
+ * router[u] = GS_ROUTER_FLOODSUB, GS_ROUTER_RANDOMSUB (NewRandomSub with
+ * cfg.randomsub_size), GS_ROUTER_GOSSIPSUB (protocols v1.1, v1.0, floodsub)
+ * or GS_ROUTER_GOSSIPSUB_V10 (a gossipsub host speaking only v1.0 and
+ * floodsub: WithGossipSubProtocols, gossipsub_feat.go:41-56).  NULL: every
+ * host runs cfg.router.  Gossipsub hosts need cfg.router == GS_ROUTER_GOSSIPSUB
+ * (their params, scoring, peer gater and options come from the engine);
+ * attacker behaviours (gs_set_behaviour) need gossipsub hosts.  Before the
+ * first step. */
+#define GS_ROUTER_GOSSIPSUB_V10 3
+int gs_set_routers(gs_engine* eng, const uint8_t* router /*[N]*/);
+/* PubSubRouter.EnoughPeers(topic, suggested) of every host (gossipsub.go:
+ * 549-576, randomsub.go:59-89, floodsub.go:52-66) at the current state:
+ * out[u] = 1 / 0 (a partitioned engine fills its own nodes, 0 elsewhere). */
+int gs_enough_peers(gs_engine* eng, int32_t topic, int32_t suggested, uint8_t* out /*[N]*/);
 /* Topic subscriptions (bit t of sub_mask[u]): Join(t) at hop 0. */
 int gs_set_subscriptions(gs_engine* eng, const uint64_t* sub_mask);
 /* Per-node attributes: app_score[N] (P5, AppSpecificScore), ipv4[N] (P6),
@@ -468,7 +508,8 @@ typedef struct gs_trace_event {
   int32_t peer;   /* peer / receivedFrom, -1 = none */
   int16_t topic;  /* -1 = none */
   uint8_t phase;
-  uint8_t reason; /* REJECT_MESSAGE: GS_REJECT_* */
+  uint8_t reason; /* REJECT_MESSAGE: GS_REJECT_*; ADD_PEER: the connection's GS_PROTO_*
+                     (0 on a single-router engine: gs_trace_encode's `proto`) */
 } gs_trace_event;
 /* RejectMessage reasons, in the order of tracer.go:27-38 (their strings are
  * what the encoders write). */

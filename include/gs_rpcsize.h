@@ -54,4 +54,8 @@ GS_PBFN int64_t gs_pb_prune(int64_t topic_len, uint64_t backoff_s) {
   return gs_pb_field(topic_len) + 1 + gs_pb_vlen(backoff_s);
 }
 
+/* ControlPrune body for a gossipsub v1.0 peer: topicID only (makePrune
+ * gossipsub.go:1804-1807 sends neither PX nor a backoff to it) */
+GS_PBFN int64_t gs_pb_prune_v10(int64_t topic_len) { return gs_pb_field(topic_len); }
+
 #endif

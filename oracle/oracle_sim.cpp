@@ -26,6 +26,7 @@
 #include "oracle_core.hpp"
 #include "../include/gs_trace.h"
 #include "../include/gs_rpcsize.h"
+#include "../include/gs_proto.h"
 
 namespace oracle {
 
@@ -87,6 +88,17 @@ struct Node {
   GateSnap gsnap;
   int valUsed = 0;                       // validation-queue entries used this hop
   uint8_t behave = 0;                    // GS_BEHAVE_* bits
+  // mixed networks (gs_set_routers / gs_set_graph_ex): this host's router and
+  // the protocol.ID of each of its connections (gs.peers / rs.peers,
+  // gossipsub.go:505-508, randomsub.go:48-51)
+  int router = GS_ROUTER_GOSSIPSUB;
+  std::map<int, int> proto;
+  bool isGossip() const { return router == GS_ROUTER_GOSSIPSUB; }
+  // gs.feature(GossipSubFeatureMesh / GossipSubFeaturePX, gs.peers[p]) (gossipsub_feat.go:27-38)
+  bool meshCap(int p) const;
+  bool pxCap(int p) const;
+  bool scored() const;                   // a peerScore exists (WithPeerScore on a gossipsub host)
+  bool gatered() const;                  // a peerGater exists (WithPeerGater on a gossipsub host)
   int acceptFrom(int s, uint32_t draw);  // AcceptFrom incl. the gater, per RPC
   std::vector<gs_trace_event> ev;        // this node's trace events (it is the tracing host)
 
@@ -143,6 +155,11 @@ struct Sim {
   std::vector<uint8_t> topicVal;   // RegisterTopicValidator per topic
   int32_t valQueue = 0;            // validation queue entries per node per hop (0 = unlimited)
   std::vector<uint8_t> behave;     // GS_BEHAVE_* per node
+  // mixed networks: router per host (gs_set_routers, empty: cfg.router) and
+  // protocol per connection (gs_set_graph_ex, empty: negotiated at start)
+  std::vector<uint8_t> nodeRouter, protoE;
+  bool mixed = false;              // some host or connection differs from cfg.router's own
+  int validateMixed();             // the gs_set_routers / gs_set_graph_ex rules (gossip_engine.h)
   std::vector<uint8_t> msgKind;    // GS_MSG_* per message id
   // churn / subscription events (gs_schedule_events), by hop
   struct Event { int64_t hop; int32_t kind, a, b; };
@@ -296,7 +313,8 @@ int64_t Sim::rpcSize(const RPC& r) const {
     for (const IHaveEntry& ih : r.ctl.ihave) c += gs_pb_field(gs_pb_ihave(acctTl[ih.topic], (int64_t)ih.mids.size(), acctId));
     if (!r.ctl.iwant.empty()) c += gs_pb_field(gs_pb_iwant((int64_t)r.ctl.iwant.size(), acctId));
     for (int t : r.ctl.graft) c += gs_pb_field(gs_pb_graft(acctTl[t]));
-    for (const PruneEntry& pe : r.ctl.prune) c += gs_pb_field(gs_pb_prune(acctTl[pe.topic], pe.backoff));
+    for (const PruneEntry& pe : r.ctl.prune)
+      c += gs_pb_field(pe.hasBackoff ? gs_pb_prune(acctTl[pe.topic], pe.backoff) : gs_pb_prune_v10(acctTl[pe.topic]));
     s += gs_pb_field(c);
   }
   return s;
@@ -309,7 +327,20 @@ int64_t Sim::helloSize(uint64_t subs) const {
   return s;
 }
 
-double Node::Score(int p) { return sim->scoring ? score.score(p) : 0.0; }
+bool Node::scored() const { return sim->scoring && isGossip(); }
+// a single-router engine's connections all run the router's own protocol
+bool Node::meshCap(int p) const {
+  if (!sim->mixed) return true;
+  auto it = proto.find(p);
+  return it != proto.end() && it->second >= GS_PROTO_GOSSIPSUB_V10;
+}
+bool Node::pxCap(int p) const {
+  if (!sim->mixed) return true;
+  auto it = proto.find(p);
+  return it != proto.end() && it->second == GS_PROTO_GOSSIPSUB_V11;
+}
+bool Node::gatered() const { return sim->gaterOn && isGossip(); }
+double Node::Score(int p) { return scored() ? score.score(p) : 0.0; }
 
 // sendRPC / doSendRPC — gossipsub.go:1092-1156 (queues never drop in the
 // simulator; pending gossip is piggybacked exactly as sendRPC does).
@@ -336,8 +367,8 @@ std::vector<int> Node::getPeers(int topic, int count, int site, const std::funct
   auto tm = topics.find(topic);
   if (tm == topics.end()) return {};
   std::vector<std::pair<uint64_t, int>> peers;
-  for (int p : tm->second)  // all peers speak gossipsub (GossipSubFeatureMesh)
-    if (filter(p))
+  for (int p : tm->second)  // mesh-capable peers only (gossipsub.go:1849)
+    if (meshCap(p) && filter(p))
       peers.push_back({gs_key64(sim->cfg.seed, site, id, (uint32_t)sim->hop, p, topic), p});
   std::sort(peers.begin(), peers.end());
   std::vector<int> res;
@@ -348,7 +379,7 @@ std::vector<int> Node::getPeers(int topic, int count, int site, const std::funct
 
 // Join — gossipsub.go:1011-1060 (router); floodsub/randomsub Join only trace.
 void Node::join(int topic) {
-  if (sim->cfg.router != GS_ROUTER_GOSSIPSUB) return;
+  if (!isGossip()) return;
   if (mesh.count(topic)) return;
   std::set<int> gmap;
   auto fo = fanout.find(topic);
@@ -389,7 +420,7 @@ void Node::localPublish(const Msg& m) {
     // an advertised-only id: in the author's mcache (so emitGossip lists it)
     // and seen set, never sent (IHAVE spam, gossipsub_spam_test.go:196-203)
     seen.insert(m.id);
-    if (sim->cfg.router == GS_ROUTER_GOSSIPSUB) mcache.Put(m);
+    if (isGossip()) mcache.Put(m);
     return;
   }
   sim->emit(GS_TRACE_PUBLISH_MESSAGE, id, -1, m.topic, m.id, 1);  // validation.go:217
@@ -409,15 +440,15 @@ void Node::handleMessage(int from, const Msg& m) {
   if (!((mySubs >> m.topic) & 1)) return;  // subscribedToMsg / canRelayMsg (pubsub.go:959)
   const int64_t now = sim->now();
   if (m.from == id && from != id) {         // self-origin rejection (pubsub.go:1001-1006)
-    if (sim->scoring) score.RejectMessage(m, from, RejectSelfOrigin, now);
-    if (sim->gaterOn) gater.RejectMessage(from, RejectSelfOrigin, now);
+    if (scored()) score.RejectMessage(m, from, RejectSelfOrigin, now);
+    if (gatered()) gater.RejectMessage(from, RejectSelfOrigin, now);
     return;
   }
   if (seen.count(m.id)) {                   // duplicate (pubsub.go:1010-1013)
     sim->emit(GS_TRACE_DUPLICATE_MESSAGE, id, from, m.topic, m.id, 2);
     ctr.duplicates++;
-    if (sim->scoring) score.DuplicateMessage(m, from, now);
-    if (sim->gaterOn) gater.DuplicateMessage(from);
+    if (scored()) score.DuplicateMessage(m, from, now);
+    if (gatered()) gater.DuplicateMessage(from);
     return;
   }
   if (sim->topicVal[m.topic]) {             // val.Push: a validator applies (validation.go:230-243)
@@ -425,22 +456,22 @@ void Node::handleMessage(int from, const Msg& m) {
       // RejectValidationQueueFull: not marked seen, a later copy may validate
       sim->emit(GS_TRACE_REJECT_MESSAGE, id, from, m.topic, m.id, 2, GS_REJECT_QUEUE_FULL);
       ctr.throttled++;
-      if (sim->scoring) gtracer.RejectMessage(m.id, RejectValidationQueueFull);  // peerScore ignores it
-      if (sim->gaterOn) gater.RejectMessage(from, RejectValidationQueueFull, now);
+      if (scored()) gtracer.RejectMessage(m.id, RejectValidationQueueFull);  // peerScore ignores it
+      if (gatered()) gater.RejectMessage(from, RejectValidationQueueFull, now);
       return;
     }
     valUsed++;
     seen.insert(m.id);                      // validate(): markSeen, then ValidateMessage
-    if (sim->scoring) { score.ValidateMessage(m, now); gtracer.ValidateMessage(m.id); }
-    if (sim->gaterOn) gater.ValidateMessage();
+    if (scored()) { score.ValidateMessage(m, now); gtracer.ValidateMessage(m.id); }
+    if (gatered()) gater.ValidateMessage();
     const int kind = sim->kindOf(m);
     if (kind == GS_MSG_REJECT || kind == GS_MSG_IGNORE) {  // validation.go:331-336, 349-352
       const int reason = kind == GS_MSG_REJECT ? RejectValidationFailed : RejectValidationIgnored;
       sim->emit(GS_TRACE_REJECT_MESSAGE, id, from, m.topic, m.id, 2,
                 kind == GS_MSG_REJECT ? GS_REJECT_VALIDATION_FAILED : GS_REJECT_VALIDATION_IGNORED);
       ctr.rejected++;
-      if (sim->scoring) { score.RejectMessage(m, from, reason, now); gtracer.RejectMessage(m.id, reason); }
-      if (sim->gaterOn) gater.RejectMessage(from, reason, now);
+      if (scored()) { score.RejectMessage(m, from, reason, now); gtracer.RejectMessage(m.id, reason); }
+      if (gatered()) gater.RejectMessage(from, reason, now);
       return;
     }
   } else {
@@ -449,11 +480,11 @@ void Node::handleMessage(int from, const Msg& m) {
   sim->emit(GS_TRACE_DELIVER_MESSAGE, id, from, m.topic, m.id, 2);
   ctr.deliveries++;
   if (sim->record) sim->deliv[id][m.id] = {(int32_t)sim->hop, from};
-  if (sim->scoring) {                       // tracer.DeliverMessage -> raw tracers
+  if (scored()) {                       // tracer.DeliverMessage -> raw tracers
     score.DeliverMessage(m, from, now);
     gtracer.DeliverMessage(m.id);
   }
-  if (sim->gaterOn) gater.DeliverMessage(from);
+  if (gatered()) gater.DeliverMessage(from);
   if (behave & GS_BEHAVE_NO_FORWARD) return;  // a squatter relays nothing
   routerPublish(m, from);
 }
@@ -462,16 +493,16 @@ void Node::handleMessage(int from, const Msg& m) {
 // 320-363) on the hop-start snapshot; `draw` names the RPC (the message id of a
 // payload RPC, 0xFFFFFFFF for the sender's control RPCs of this hop).
 int Node::acceptFrom(int s, uint32_t draw) {
-  if (sim->cfg.router != GS_ROUTER_GOSSIPSUB) return PeerGater::AcceptAll;
+  if (!isGossip()) return PeerGater::AcceptAll;  // floodsub.go:68, randomsub.go:91
   if (direct.count(s)) return PeerGater::AcceptAll;
   if (sim->liveScore) {  // gossipsub.go:578-589 on the live score, then peer_gater.go:320-363 live
-    if (sim->scoring && Score(s) < sim->thr.GraylistThreshold) return PeerGater::AcceptNone;
-    if (!sim->gaterOn) return PeerGater::AcceptAll;
+    if (scored() && Score(s) < sim->thr.GraylistThreshold) return PeerGater::AcceptNone;
+    if (!gatered()) return PeerGater::AcceptAll;
     const double u = gs_key_to_unit(gs_key64(sim->cfg.seed, GS_SITE_GATER, id, s, (uint32_t)sim->hop, draw));
     return gater.AcceptFrom(s, sim->now(), u);
   }
-  if (sim->scoring && memo[s] < sim->thr.GraylistThreshold) return PeerGater::AcceptNone;
-  if (!sim->gaterOn || !gsnap.active) return PeerGater::AcceptAll;
+  if (scored() && memo[s] < sim->thr.GraylistThreshold) return PeerGater::AcceptNone;
+  if (!gatered() || !gsnap.active) return PeerGater::AcceptAll;
   auto it = gsnap.thr.find(s);
   if (it == gsnap.thr.end()) return PeerGater::AcceptAll;  // total == 0
   const double u = gs_key_to_unit(gs_key64(sim->cfg.seed, GS_SITE_GATER, id, s, (uint32_t)sim->hop, draw));
@@ -479,7 +510,6 @@ int Node::acceptFrom(int s, uint32_t draw) {
 }
 
 void Node::routerPublish(const Msg& m, int from) {
-  const int router = sim->cfg.router;
   if (router == GS_ROUTER_FLOODSUB) {  // FloodSubRouter.Publish floodsub.go:76-100
     auto tm = topics.find(m.topic);
     if (tm == topics.end()) return;
@@ -495,10 +525,11 @@ void Node::routerPublish(const Msg& m, int from) {
     auto tm = topics.find(m.topic);
     if (tm == topics.end()) return;
     std::set<int> tosend;
-    std::vector<int> rspeers;  // every peer speaks randomsub in this engine
+    std::vector<int> rspeers;
     for (int p : tm->second) {
       if (p == from || p == m.from) continue;
-      rspeers.push_back(p);
+      if (sim->mixed && proto[p] == GS_PROTO_FLOODSUB) tosend.insert(p);  // floodsub peers: always (randomsub.go:117-118)
+      else rspeers.push_back(p);
     }
     const int RandomSubD = 6;  // randomsub.go:17
     if ((int)rspeers.size() > RandomSubD) {
@@ -532,14 +563,16 @@ void Node::gsPublish(const Msg& m, int from) {
   std::set<int> tosend;
   auto tm = topics.find(topic);
   if (tm == topics.end()) return;
-  auto s0 = [&](int p) { return sim->scoring ? (sim->liveScore ? Score(p) : memo[p]) : 0.0; };
+  auto s0 = [&](int p) { return scored() ? (sim->liveScore ? Score(p) : memo[p]) : 0.0; };
   if (sim->floodPublish && from == id) {
     for (int p : tm->second)
       if (direct.count(p) || s0(p) >= sim->thr.PublishThreshold) tosend.insert(p);
   } else {
     for (int p : direct)
       if (tm->second.count(p)) tosend.insert(p);
-    // floodsub peers: none (every peer speaks gossipsub in this engine)
+    // floodsub peers (gossipsub.go:969-975): not mesh-capable, score >= publishThreshold
+    for (int p : tm->second)
+      if (!meshCap(p) && s0(p) >= sim->thr.PublishThreshold) tosend.insert(p);
     auto gm = mesh.find(topic);
     std::set<int> gmap;
     if (gm == mesh.end()) {
@@ -724,6 +757,11 @@ void Node::doAddBackoff(int p, int topic, int64_t interval) {  // :844-854
 PruneEntry Node::makePrune(int p, int topic, bool doPX) {
   PruneEntry e;
   e.topic = topic;
+  if (!pxCap(p)) {  // gossipsub v1.0 peer: neither PX nor a backoff (gossipsub.go:1804-1807)
+    e.hasBackoff = false;
+    e.backoff = 0;
+    return e;
+  }
   e.hasBackoff = true;
   e.backoff = (uint64_t)(sim->gp.PruneBackoff / kSecond);
   if (doPX) {  // getPeers(topic, PrunePeers, xp != p && Score(xp) >= 0), its own shuffle per PRUNE
@@ -731,7 +769,7 @@ PruneEntry Node::makePrune(int p, int topic, bool doPX) {
     std::vector<std::pair<uint64_t, int>> keyed;
     if (tm != topics.end())
       for (int xp : tm->second)
-        if (xp != p && Score(xp) >= 0)
+        if (meshCap(xp) && xp != p && Score(xp) >= 0)  // getPeers' mesh filter (:1849)
           keyed.push_back({gs_key64(sim->cfg.seed, GS_SITE_PX, id, (uint32_t)sim->hop, xp,
                                     ((uint32_t)p << 6) | (uint32_t)topic), xp});
     std::sort(keyed.begin(), keyed.end());
@@ -771,7 +809,8 @@ void Node::emitGossip(int topic, const std::set<int>& exclude) {
   auto tm = topics.find(topic);
   if (tm != topics.end())
     for (int p : tm->second)
-      if (spam || (!exclude.count(p) && !direct.count(p) && Score(p) >= sim->thr.GossipThreshold)) peers.push_back(p);
+      if (meshCap(p) && (spam || (!exclude.count(p) && !direct.count(p) && Score(p) >= sim->thr.GossipThreshold)))
+        peers.push_back(p);
   int target = sim->gp.Dlazy;
   int factor = (int)(sim->gp.GossipFactor * (double)peers.size());
   if (factor > target) target = factor;
@@ -1019,8 +1058,8 @@ void Node::removePeer(int p) {
   for (auto& kv : mesh) kv.second.erase(p);
   for (auto& kv : fanout) kv.second.erase(p);
   gossip.erase(p);
-  if (sim->scoring) score.RemovePeer(p, sim->now());
-  if (sim->gaterOn) gater.RemovePeer(p, sim->now());
+  if (scored()) score.RemovePeer(p, sim->now());
+  if (gatered()) gater.RemovePeer(p, sim->now());
 }
 
 // A new stream from p (pubsub.go:499-515): AddPeer (gossipsub.go:505-532,
@@ -1029,15 +1068,15 @@ void Node::removePeer(int p) {
 void Node::addPeer(int p) {
   if (!dead.count(p)) return;
   dead.erase(p);
-  sim->emit(GS_TRACE_ADD_PEER, id, p, -1, -1, 0);
+  sim->emit(GS_TRACE_ADD_PEER, id, p, -1, -1, 0, sim->mixed ? proto[p] : 0);
   const int64_t e = sim->edgeIndex(id, p);
   outbound[p] = sim->outboundE.empty() ? false : sim->outboundE[e] != 0;
-  if (sim->scoring) {
+  if (scored()) {
     std::vector<uint32_t> ips;
     if (!sim->ipv4.empty() && sim->ipv4[p] != 0) ips.push_back(sim->ipv4[p]);
     score.AddPeer(p, ips);
   }
-  if (sim->gaterOn) gater.AddPeer(p);
+  if (gatered()) gater.AddPeer(p);
   for (int t = 0; t < sim->T; ++t)
     if ((sim->nodes[p].mySubs >> t) & 1) topics[t].insert(p);
 }
@@ -1049,8 +1088,8 @@ void Node::leaveTopic(int topic) {
   const uint64_t bit = 1ull << topic;
   if (!(mySubs & bit)) return;
   mySubs &= ~bit;
-  if (sim->cfg.router == GS_ROUTER_RANDOMSUB) { sim->emit(GS_TRACE_JOIN, id, -1, topic, -1, 0); return; }
-  if (sim->cfg.router == GS_ROUTER_FLOODSUB) { sim->emit(GS_TRACE_LEAVE, id, -1, topic, -1, 0); return; }
+  if (router == GS_ROUTER_RANDOMSUB) { sim->emit(GS_TRACE_JOIN, id, -1, topic, -1, 0); return; }
+  if (router == GS_ROUTER_FLOODSUB) { sim->emit(GS_TRACE_LEAVE, id, -1, topic, -1, 0); return; }
   auto gm = mesh.find(topic);
   if (gm == mesh.end()) return;
   sim->emit(GS_TRACE_LEAVE, id, -1, topic, -1, 0);
@@ -1058,7 +1097,7 @@ void Node::leaveTopic(int topic) {
   mesh.erase(gm);
   for (int p : gmap) {
     sim->emit(GS_TRACE_PRUNE, id, p, topic, -1, 0);  // tracer.Prune (gossipsub.go:1075)
-    if (sim->scoring) score.Prune(p, topic);
+    if (scored()) score.Prune(p, topic);
     RPC r;  // sendPrune (gossipsub.go:1093-1097)
     r.hasCtl = true;
     r.ctl.prune.push_back(makePrune(p, topic, sim->doPX));  // sendPrune: gs.doPX (:1087)
@@ -1169,6 +1208,45 @@ void Sim::applyEvents(std::vector<std::map<int, std::vector<RPC>>>& inbox) {
   nextEvent = end;
 }
 
+// protocol negotiation: include/gs_proto.h (shared with the product)
+static int negotiate(int ra, int rb) { return gs_negotiate(ra, rb); }
+static bool speaks(int r, int proto) { return gs_router_speaks(r, proto) != 0; }
+
+int Sim::validateMixed() {
+  auto rt = [&](int u) { return nodeRouter.empty() ? cfg.router : (int)nodeRouter[u]; };
+  mixed = !nodeRouter.empty() || !protoE.empty();
+  const bool given = !protoE.empty();
+  if (!given) protoE.assign((size_t)E, 0);
+  for (int u = 0; u < N; ++u) {
+    const int ru = rt(u);
+    if ((ru == GS_ROUTER_GOSSIPSUB || ru == GS_ROUTER_GOSSIPSUB_V10) && cfg.router != GS_ROUTER_GOSSIPSUB) {
+      set_error("gossipsub hosts need cfg.router == GS_ROUTER_GOSSIPSUB (their params come from the engine)");
+      return GS_EINVAL;
+    }
+    const bool gsHost = ru == GS_ROUTER_GOSSIPSUB || ru == GS_ROUTER_GOSSIPSUB_V10;
+    if (!behave.empty() && behave[u] && !gsHost) { set_error("attacker behaviours need gossipsub hosts"); return GS_EINVAL; }
+    for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) {
+      const int v = col[e], rv = rt(v);
+      if (!gsHost && !directE.empty() && directE[e]) { set_error("direct peers need a gossipsub host"); return GS_EINVAL; }
+      if (!given) {
+        protoE[e] = (uint8_t)negotiate(ru, rv);
+      } else {
+        const int pr = protoE[e] == GS_PROTO_DEFAULT ? negotiate(ru, rv) : protoE[e];
+        const int pb = protoE[edgeIndex(v, u)] == GS_PROTO_DEFAULT ? negotiate(rv, ru) : protoE[edgeIndex(v, u)];
+        if (pr != pb || !speaks(ru, pr) || !speaks(rv, pr)) {
+          set_error("proto[e] must be a protocol both hosts speak, equal on both directions of the connection");
+          return GS_EINVAL;
+        }
+      }
+    }
+  }
+  if (given)
+    for (int u = 0; u < N; ++u)
+      for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e)
+        if (protoE[e] == GS_PROTO_DEFAULT) protoE[e] = (uint8_t)negotiate(rt(u), rt(col[e]));
+  return GS_OK;
+}
+
 void Sim::start() {
   nodes.assign(N, Node());
   if (record) deliv.assign(N, {});
@@ -1185,6 +1263,8 @@ void Sim::start() {
     nd.score.whitelist = whitelist;
     nd.gtracer.followUpTime = gp.IWantFollowupTime;
     nd.behave = behave.empty() ? 0 : behave[u];
+    nd.router = nodeRouter.empty() ? cfg.router
+                : nodeRouter[u] == GS_ROUTER_GOSSIPSUB_V10 ? GS_ROUTER_GOSSIPSUB : nodeRouter[u];
     if (gaterOn) {
       nd.gater.params = gaterParams;
       nd.gater.getIP = [this](int p) { return ipv4.empty() ? 0u : ipv4[p]; };  // 0 = "<unknown>"
@@ -1192,25 +1272,26 @@ void Sim::start() {
     for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) {
       int v = col[e];
       nd.nbrs.push_back(v);
+      nd.proto[v] = protoE[e];
       if (dormant.count({std::min(u, v), std::max(u, v)})) {  // gs_set_dormant: not connected yet
         nd.dead.insert(v);
         nd.outbound[v] = outboundE.empty() ? false : outboundE[e] != 0;
         if (!directE.empty() && directE[e]) nd.direct.insert(v);
         continue;
       }
-      emit(GS_TRACE_ADD_PEER, u, v, -1, -1, 0);  // AddPeer gossipsub.go:507, floodsub.go:45
+      emit(GS_TRACE_ADD_PEER, u, v, -1, -1, 0, mixed ? protoE[e] : 0);  // AddPeer gossipsub.go:507, floodsub.go:45
       nd.outbound[v] = outboundE.empty() ? false : outboundE[e] != 0;  // AddPeer gossipsub.go:505-532
       if (!directE.empty() && directE[e]) nd.direct.insert(v);
       std::vector<uint32_t> ips;
       if (!ipv4.empty() && ipv4[v] != 0) ips.push_back(ipv4[v]);
-      if (scoring) nd.score.AddPeer(v, ips);
-      if (gaterOn) nd.gater.AddPeer(v);  // tracer.AddPeer -> peerGater.AddPeer (peer_gater.go:366-372)
+      if (nd.scored()) nd.score.AddPeer(v, ips);
+      if (nd.gatered()) nd.gater.AddPeer(v);  // tracer.AddPeer -> peerGater.AddPeer (peer_gater.go:366-372)
       for (int t = 0; t < T; ++t)
         if (!subs.empty() && ((subs[v] >> t) & 1)) nd.topics[t].insert(v);
     }
   }
   hasDirect = false;
-  for (const Node& nd : nodes) hasDirect = hasDirect || !nd.direct.empty();
+  for (const Node& nd : nodes) hasDirect = hasDirect || (nd.isGossip() && !nd.direct.empty());
   hasDirect = hasDirect && cfg.router == GS_ROUTER_GOSSIPSUB;
   directInitHop = gp.DirectConnectInitialDelay <= 0 ? 0 : (gp.DirectConnectInitialDelay + cfg.hop_ns - 1) / cfg.hop_ns;
   auto up = [&](int u, int v) { return !dormant.count({std::min(u, v), std::max(u, v)}); };
@@ -1259,9 +1340,9 @@ void Sim::step() {
     for (int u = 0; u < N; ++u) {
       Node& nd = nodes[u];
       nd.memo.clear();
-      if (scoring)
+      if (nd.scored())
         for (int v : nd.nbrs) nd.memo[v] = nd.score.score(v);
-      if (gaterOn) {
+      if (nd.gatered()) {
         PeerGater& g = nd.gater;
         nd.gsnap.thr.clear();
         nd.gsnap.active = !(g.lastThrottle == kTimeZero || t - g.lastThrottle > g.params.Quiet) &&
@@ -1295,14 +1376,14 @@ void Sim::step() {
           if (st == PeerGater::AcceptNone) { nd.ctr.graylisted++; continue; }  // pubsub.go:947-949
           if (st == PeerGater::AcceptControl) {                                // pubsub.go:951-955
             if (!r.publish.empty()) nd.ctr.gated++;
-            if (scoring) nd.gtracer.ThrottlePeer(s);
+            if (nd.scored()) nd.gtracer.ThrottlePeer(s);
           } else {
             for (int64_t mid : r.publish) nd.handleMessage(s, msgs[mid]);
             got.insert(got.end(), r.publish.begin(), r.publish.end());
           }
-          if (r.hasCtl && cfg.router == GS_ROUTER_GOSSIPSUB) nd.handleRPC(s, r);  // pubsub.go:969
+          if (r.hasCtl && nd.isGossip()) nd.handleRPC(s, r);  // pubsub.go:969
         }
-        if ((nd.behave & GS_BEHAVE_IWANT_SPAM) && !got.empty() && cfg.router == GS_ROUTER_GOSSIPSUB) {
+        if ((nd.behave & GS_BEHAVE_IWANT_SPAM) && !got.empty() && nd.isGossip() && nd.meshCap(s)) {
           std::sort(got.begin(), got.end());
           RPC r;
           r.hasCtl = true;
@@ -1345,10 +1426,10 @@ void Sim::step() {
       nd.ctr.graylisted += gray;
       if (gray) continue;  // AcceptNone is per sender and hop (the S0 memo)
       // tracer.ThrottlePeer -> gossipTracer.ThrottlePeer (gossip_tracer.go:163-181)
-      if (throttledPeer && scoring) nd.gtracer.ThrottlePeer(s);
+      if (throttledPeer && nd.scored()) nd.gtracer.ThrottlePeer(s);
       std::sort(mids.begin(), mids.end());
       for (int64_t mid : mids) nd.handleMessage(s, msgs[mid]);
-      if ((nd.behave & GS_BEHAVE_IWANT_SPAM) && !mids.empty() && cfg.router == GS_ROUTER_GOSSIPSUB) {
+      if ((nd.behave & GS_BEHAVE_IWANT_SPAM) && !mids.empty() && nd.isGossip() && nd.meshCap(s)) {
         // re-request every message received from s (gossipsub_spam_test.go:113-128)
         RPC r;
         r.hasCtl = true;
@@ -1363,6 +1444,7 @@ void Sim::step() {
 #pragma omp parallel for schedule(dynamic, 64)
     for (int u = 0; u < N; ++u) {
       Node& nd = nodes[u];
+      if (!nd.isGossip()) continue;  // FloodSubRouter / RandomSubRouter.HandleRPC: no-ops
       for (auto& kv : inbox[nd.id]) {
         int s = kv.first;
         if (nd.acceptStatus[s] == PeerGater::AcceptNone) continue;
@@ -1385,7 +1467,8 @@ void Sim::step() {
   }
   if (heartbeatDue(t)) {
 #pragma omp parallel for schedule(dynamic, 64)
-    for (int u = 0; u < N; ++u) nodes[u].heartbeat();
+    for (int u = 0; u < N; ++u)
+      if (nodes[u].isGossip()) nodes[u].heartbeat();
     ctr.heartbeats++;
   }
   ctr.hops++;
@@ -1491,6 +1574,11 @@ int gs_oracle_reference_order(gs_engine* eng, int32_t on) {
 
 int gs_set_graph(gs_engine* eng, const int64_t* rowptr, const int32_t* col, const uint8_t* outbound,
                  const uint8_t* direct) {
+  return gs_set_graph_ex(eng, rowptr, col, outbound, direct, nullptr);
+}
+
+int gs_set_graph_ex(gs_engine* eng, const int64_t* rowptr, const int32_t* col, const uint8_t* outbound,
+                    const uint8_t* direct, const uint8_t* proto) {
   Sim& s = eng->sim;
   if (s.started) { set_error("graph must be set before the first step"); return GS_ESTATE; }
   s.rowptr.assign(rowptr, rowptr + s.N + 1);
@@ -1509,7 +1597,61 @@ int gs_set_graph(gs_engine* eng, const int64_t* rowptr, const int32_t* col, cons
   s.directE.assign(s.E, 0);
   if (outbound) s.outboundE.assign(outbound, outbound + s.E);
   if (direct) s.directE.assign(direct, direct + s.E);
+  s.protoE.clear();
+  if (proto) {
+    for (int64_t e = 0; e < s.E; ++e)
+      if (proto[e] > GS_PROTO_GOSSIPSUB_V11) { set_error("unknown protocol"); return GS_EINVAL; }
+    s.protoE.assign(proto, proto + s.E);
+  }
   s.graphSet = true;
+  return GS_OK;
+}
+
+int gs_set_routers(gs_engine* eng, const uint8_t* router) {
+  Sim& s = eng->sim;
+  if (s.started) { set_error("routers must be set before the first step"); return GS_ESTATE; }
+  s.nodeRouter.clear();
+  if (router) {
+    for (int u = 0; u < s.N; ++u)
+      if (router[u] > GS_ROUTER_GOSSIPSUB_V10) { set_error("unknown router"); return GS_EINVAL; }
+    s.nodeRouter.assign(router, router + s.N);
+  }
+  return GS_OK;
+}
+
+// PubSubRouter.EnoughPeers per host (gossip_engine.h).  A topic no peer of the
+// host announced counts as an empty one.
+int gs_enough_peers(gs_engine* eng, int32_t topic, int32_t suggested, uint8_t* out) {
+  Sim& s = eng->sim;
+  if (topic < 0 || topic >= s.T || suggested < 0 || !out) { set_error("gs_enough_peers: bad arguments"); return GS_EINVAL; }
+  if (!s.started) { set_error("gs_enough_peers: no state before the first step"); return GS_ESTATE; }
+  for (int u = 0; u < s.N; ++u) {
+    Node& nd = s.nodes[u];
+    auto tm = nd.topics.find(topic);
+    const std::set<int> none;
+    const std::set<int>& tmap = tm == nd.topics.end() ? none : tm->second;
+    bool ok = false;
+    if (nd.router == GS_ROUTER_GOSSIPSUB) {  // gossipsub.go:549-576
+      int fs = 0;
+      for (int p : tmap) fs += nd.meshCap(p) ? 0 : 1;
+      auto gm = nd.mesh.find(topic);
+      const int gsn = gm == nd.mesh.end() ? 0 : (int)gm->second.size();
+      const int sg = suggested == 0 ? s.gp.Dlo : suggested;
+      ok = fs + gsn >= sg || gsn >= s.gp.Dhi;
+    } else if (nd.router == GS_ROUTER_RANDOMSUB) {  // randomsub.go:59-89
+      int fs = 0, rs = 0;
+      for (int p : tmap) {
+        fs += nd.proto[p] == GS_PROTO_FLOODSUB;
+        rs += nd.proto[p] == GS_PROTO_RANDOMSUB;
+      }
+      const int sg = suggested == 0 ? 6 : suggested;  // RandomSubD
+      ok = fs + rs >= sg || rs >= 6;
+    } else {  // floodsub.go:52-66
+      const int sg = suggested == 0 ? 5 : suggested;  // FloodSubTopicSearchSize
+      ok = (int)tmap.size() >= sg;
+    }
+    out[u] = ok ? 1 : 0;
+  }
   return GS_OK;
 }
 
@@ -1601,7 +1743,11 @@ int gs_schedule_events(gs_engine* eng, int32_t n, const int32_t* kind, const int
 int gs_step(gs_engine* eng, int64_t hops) {
   Sim& s = eng->sim;
   if (!s.graphSet) { set_error("graph not set"); return GS_ESTATE; }
-  if (!s.started) s.start();
+  if (!s.started) {
+    const int rc = s.validateMixed();
+    if (rc) return rc;
+    s.start();
+  }
   for (int64_t i = 0; i < hops; ++i) s.step();
   return GS_OK;
 }

@@ -649,3 +649,99 @@ PX = {
     "px_scored": lambda lib, x=(): px_scored(lib, extra=x),
 }
 SCENARIOS.update(PX)
+
+
+# ---------------------------------------------------------------- mixed networks
+# Hosts running different routers and connections running different protocols
+# (gs_set_routers / gs_set_graph_ex; PubSubRouter.AddPeer(peer.ID, protocol.ID),
+# pubsub.go:165; gossipsub_feat.go:18-56).
+from pubsub_amd import (GS_ROUTER_FLOODSUB, GS_ROUTER_GOSSIPSUB, GS_ROUTER_GOSSIPSUB_V10,  # noqa: E402
+                        GS_ROUTER_RANDOMSUB, WithRouters)
+
+
+def mixed_gossip_flood(lib, seed=81, extra=()):
+    """TestMixedGossipsub (gossipsub_test.go:810-851): 30 hosts, 20 run
+    gossipsub and 10 floodsub, sparseConnect, one topic, 2 s of heartbeats, then
+    100 messages from random owners; every host must get every message."""
+    n = 30
+    g = graphs.sparse_connect(n, seed)
+    routers = np.array([GS_ROUTER_GOSSIPSUB] * 20 + [GS_ROUTER_FLOODSUB] * 10, np.uint8)
+    e = NewGossipSub(n, 1, g, graphs.all_subscribed(n, 1), WithRouters(routers), WithRecordDeliveries(),
+                     WithSeed(seed), WithHop(HOP), WithMessageWindow(256), *extra, lib=lib)
+    src, top, hops = _publish_schedule(n, 1, 100, 20, 1, seed)
+    e.publish(src, top, hops)
+    return e, int(hops[-1]) + 40
+
+
+def mixed_routers(n, seed, flood=0.15, v10=0.15, rs=0.10):
+    """Per-host routers: the given fractions run floodsub, gossipsub v1.0 and
+    randomsub, the rest gossipsub v1.1."""
+    r = np.random.default_rng(seed + 31).random(n)
+    routers = np.full(n, GS_ROUTER_GOSSIPSUB, np.uint8)
+    routers[r < flood + v10 + rs] = GS_ROUTER_RANDOMSUB
+    routers[r < flood + v10] = GS_ROUTER_GOSSIPSUB_V10
+    routers[r < flood] = GS_ROUTER_FLOODSUB
+    return routers
+
+
+def mixed_scored(lib, n=300, k=20, topics=3, seed=82, msgs=300, hb=12, px=True, extra=()):
+    """A scored mixed network: 15% floodsub, 15% gossipsub-v1.0-only and 10%
+    randomsub (size 50) hosts among gossipsub v1.1 ones, 3 topics with 70%
+    subscription (publishes to unjoined topics use fanout), negative app
+    scores around PublishThreshold (-200): a gossipsub host forwards to its
+    non-mesh peers only at score >= PublishThreshold (gossipsub.go:969-975).
+    PX on with 10% of the connections starting down: v1.0 peers get PRUNEs
+    without PX and backoff (gossipsub.go:1804-1807), PX lists hold
+    mesh-capable peers only (getPeers, :1849)."""
+    rng = np.random.default_rng(seed)
+    g = graphs.random_regular(n, k, seed)
+    rowptr, col, _ = g
+    routers = mixed_routers(n, seed)
+    subs = np.zeros(n, dtype=np.uint64)
+    for t in range(topics):
+        subs |= (rng.random(n) < 0.7).astype(np.uint64) << np.uint64(t)
+    sp = eth2_peer_score_params(topics)
+    thr = eth2_thresholds()
+    thr.AcceptPXThreshold = 0.0
+    app = np.zeros(n)
+    neg = rng.random(n)
+    app[neg < 0.08] = -250.0   # below PublishThreshold, above GraylistThreshold
+    app[(neg >= 0.08) & (neg < 0.15)] = -150.0
+    opts = [WithPeerScore(sp, thr), WithRouters(routers), WithRecordDeliveries(), WithSeed(seed), WithHop(HOP),
+            WithMessageWindow(512)]
+    if px:
+        pairs = [(u, int(v)) for u in range(n) for v in col[rowptr[u]:rowptr[u + 1]] if u < v]
+        dormant = [pairs[i] for i in np.flatnonzero(rng.random(len(pairs)) < 0.10)]
+        opts += [WithPeerExchange(True), WithDormant(dormant)]
+    e = NewGossipSub(n, topics, g, subs, *opts, *extra, app_score=app, randomsub_size=50, lib=lib)
+    rng2 = np.random.default_rng(seed + 100)
+    src = rng2.integers(0, n, msgs).astype(np.int32)
+    top = rng2.integers(0, topics, msgs).astype(np.int32)
+    hops = (5 + (np.arange(msgs) * (hb * 10 - 20)) // msgs).astype(np.int64)
+    e.publish(src, top, hops)
+    e.routers_h = routers
+    return e, hb * 10 + 5
+
+
+def mixed_randomsub(lib, n=200, k=16, seed=83, msgs=60, extra=()):
+    """randomsub.go:99-160 in a network where 30% of the hosts run floodsub:
+    a randomsub host always forwards to its floodsub-protocol topic peers and
+    samples max(6, ceil(sqrt(100))) = 10 of its randomsub-protocol ones."""
+    g = graphs.random_regular(n, k, seed)
+    routers = np.where(np.random.default_rng(seed).random(n) < 0.3, GS_ROUTER_FLOODSUB,
+                       GS_ROUTER_RANDOMSUB).astype(np.uint8)
+    e = NewRandomSub(n, 1, g, graphs.all_subscribed(n, 1), 100, WithRouters(routers), WithRecordDeliveries(),
+                     WithSeed(seed), WithMessageWindow(128), *extra, lib=lib)
+    src, top, hops = _publish_schedule(n, 1, msgs, 0, 1, seed)
+    e.publish(src, top, hops)
+    e.routers_h = routers
+    return e, int(hops[-1]) + 20
+
+
+MIXED = {
+    "mixed_gossip_flood": lambda lib, x=(): mixed_gossip_flood(lib, extra=x),
+    "mixed_scored": lambda lib, x=(): mixed_scored(lib, extra=x),
+    "mixed_randomsub": lambda lib, x=(): mixed_randomsub(lib, extra=x),
+    "acct_mixed": lambda lib, x=(): mixed_scored(lib, px=False, seed=84, extra=(_acct(3),) + tuple(x)),
+}
+SCENARIOS.update(MIXED)

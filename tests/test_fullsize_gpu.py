@@ -94,6 +94,51 @@ def test_config3_full_size_with_ihave_cuts(olib):
     _score_check(olib, e)
 
 
+def test_config5_full_size_steady_state(olib):
+    """BASELINE configs[4]'s adversarial mix on one GPU at 1M peers (bench.py
+    --workload config5), past its broken-promise regime: the first IWANT
+    promise can break at hop 50 (IWantFollowupTime = 3 s after the hop-11
+    IWANTs), so 7 rounds (hop 71) reach P7 penalties, graylisting, validation
+    rejections, queue-full throttling and gater drops all at once
+    (gossip_tracer.go:79-117, gossipsub.go:1566-1571, peer_gater.go:320-363).
+    Checked: no device error (step raises on one), every adversarial counter
+    active after round 5, the copy accounting (every copy on the wire is a
+    delivery, a duplicate, a rejection, a queue drop, or inside a graylisted or
+    gated RPC), and 3,000 sampled scores -- P4 invalid deliveries, P6 shared
+    IPs and the P7 behaviour penalty included -- recomputed bit for bit by the
+    oracle's score() from the engine's counters."""
+    from pubsub_amd import GS_MSG_VALID
+    wl = bench.WORKLOADS["config5"]
+    rounds = 7
+    e, g = bench.build_engine(wl, rounds, 3, 0)
+    e.step(1 + 5 * H)
+    c5 = e.counters()
+    for k in ("promises_broken", "graylisted", "rejected", "throttled", "gated"):
+        assert c5[k] > 0, (k, c5)
+    e.step(2 * H + 1)
+    c = e.counters()
+    assert c["promises_broken"] > c5["promises_broken"], c
+    handled = c["deliveries"] + c["duplicates"] + c["rejected"] + c["throttled"]
+    # graylisted / gated count RPCs, each carrying at least one copy
+    assert handled + c["graylisted"] + c["gated"] <= c["transmissions"], c
+    valid = int((e.kinds == GS_MSG_VALID).sum())
+    assert c["deliveries"] <= valid * (e.N - 1)
+    assert c["deliveries"] > 0.9 * valid * (e.N - 1), (c["deliveries"], valid)
+    bp = e.behaviour_penalty()
+    rng = np.random.default_rng(5)
+    pen = np.flatnonzero(bp > 0)
+    assert len(pen) > 0
+    edges = np.unique(np.concatenate([sample_edges(e.E, 2000, 7, must=[0, e.E - 1]),
+                                      rng.choice(pen, min(1000, len(pen)), replace=False)]))
+    got, st = oracle_scores(olib, e.score_params, e, edges, ipv4=e.ipv4)
+    want = e.scores()[edges]
+    bad = np.flatnonzero(got.view(np.uint64) != want.view(np.uint64))
+    assert len(bad) == 0, f"{len(bad)} of {len(edges)} scores differ, first edge {edges[bad[0]]}: " \
+                          f"engine {want[bad[0]]!r} oracle {got[bad[0]]!r}"
+    assert (st["imd"] > 0).any() and (bp[edges] > 0).sum() >= min(1000, len(pen))
+    assert (want < 0).any()  # penalised peers are in the sample
+
+
 @pytest.mark.parametrize("size", ["100", "N"])
 def test_config2_randomsub_100k(size):
     """BASELINE configs[1], the randomsub leg: 100k peers, random 32-regular
