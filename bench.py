@@ -102,6 +102,7 @@ def build_engine(wl, rounds, seed, device, lib=None, n=None, msgs_per_round=None
     eng.publish(src, top, hops, kind=kind)
     eng.schedule = (top, hops)
     eng.kinds = kind  # GS_MSG_* per published message (None: all valid)
+    eng.srcs = src
     eng.ipv4 = kw.get("ipv4")
     return eng, g
 

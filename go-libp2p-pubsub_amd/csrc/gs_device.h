@@ -90,6 +90,7 @@ struct AcctT {
   int32_t msgF;       // RPC.publish entry of a message of the topic
   int32_t graftEnt;   // ControlMessage.graft entry
   int32_t pruneEnt;   // ControlMessage.prune entry (makePrune: topic + backoff)
+  int32_t pruneEnt10; // the same to a gossipsub v1.0 peer (topic only, gossipsub.go:1804-1807)
   int32_t ihaveHead;  // ControlIHave topicID field (the ids add acctIdF each)
 };
 
@@ -98,6 +99,12 @@ struct Dev {
   int32_t N, T, Wt, W, St, S, R, HL, HG;
   int64_t E;
   int32_t router, scoring, floodPublish, rsTarget, maxAge;
+  // mixed networks (gs_set_routers / gs_set_graph_ex): the router of every host
+  // (GS_ROUTER_*, the v1.0 variant folded into gossipsub) and the protocol of
+  // every connection (GS_PROTO_*); nullptr: every host runs `router` and every
+  // connection its own protocol
+  const uint8_t* nrouter;
+  const uint8_t* proto;
   // partition (gs_set_partition): this rank owns nodes [n0, n1) and their CSR
   // rows, i.e. edges [e0, e1).  Node kernels run one wave per owned node, edge
   // kernels one lane per owned edge; per-(edge, topic) state is allocated for
@@ -189,6 +196,11 @@ struct Dev {
   int64_t* gLast;        // [N] lastThrottle, INT64_MIN = never
   double* gSt;           // [4][E] deliver, duplicate, ignore, reject (at group edges)
   uint8_t* gGrp;         // [E] in-row index of the edge holding this peer's IP stats
+  // the stats object's lifecycle (peer_gater.go:366-383, 219-259), at group
+  // edges: connected peers of the IP, and the expiry set by the last RemovePeer
+  int32_t* gConn;        // [E]
+  int64_t* gExp;         // [E]
+  int64_t gRetain;       // RetainStats
   int64_t* lastpub;        // [N][T], INT64_MIN = none
   uint64_t* fanoutPresent; // [N]
   int32_t nOwnH;      // owned nodes n1 - n0: the mcache ring is [R][nOwnH][W] (v - n0)
@@ -267,6 +279,23 @@ struct Dev {
 };
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+// ---- mixed networks (gossip_engine.h gs_set_routers / gs_set_graph_ex)
+__device__ __forceinline__ int router_of(const Dev& d, int u) { return d.nrouter ? (int)d.nrouter[u] : d.router; }
+__device__ __forceinline__ bool gossip_host(const Dev& d, int u) { return router_of(d, u) == GS_ROUTER_GOSSIPSUB; }
+// a randomsub host (its per-message target masks live in d.sel)
+__device__ __forceinline__ bool rs_host(const Dev& d, int u) {
+  return d.sel != nullptr && router_of(d, u) == GS_ROUTER_RANDOMSUB;
+}
+// gs.feature(GossipSubFeatureMesh / GossipSubFeaturePX, gs.peers[p]) of the
+// connection of edge e (gossipsub_feat.go:27-38); symmetric in e
+__device__ __forceinline__ bool mesh_peer(const Dev& d, int64_t e) {
+  return d.proto == nullptr || d.proto[e] >= GS_PROTO_GOSSIPSUB_V10;
+}
+__device__ __forceinline__ bool px_peer(const Dev& d, int64_t e) {
+  return d.proto == nullptr || d.proto[e] == GS_PROTO_GOSSIPSUB_V11;
+}
+// makePrune's ControlPrune entry size for the peer of edge e (RPC accounting)
+__device__ __forceinline__ int64_t prune_entry(const Dev& d, int64_t e, int t);
 __device__ __forceinline__ bool behaves(const Dev& d, int v, unsigned bit) {
   return d.behave != nullptr && (d.behave[v] & bit) != 0;
 }
@@ -307,6 +336,9 @@ __device__ __forceinline__ void acct_send(const Dev& d, int64_t e, int64_t bytes
   d.rpcN[e] += (unsigned long long)n;
 }
 __device__ __forceinline__ bool has_record(const Dev& d, int64_t e) { return d.rstate == nullptr || d.rstate[e] != 0; }
+__device__ __forceinline__ int64_t prune_entry(const Dev& d, int64_t e, int t) {
+  return px_peer(d, e) ? d.acc[t].pruneEnt : d.acc[t].pruneEnt10;
+}
 __device__ __forceinline__ void set_err(const Dev& d, int code);
 __device__ __forceinline__ void trace_emit(const Dev& d, int64_t hop, int type, int node, int peer, int topic,
                                            int64_t msg, int phase, int reason = 0) {

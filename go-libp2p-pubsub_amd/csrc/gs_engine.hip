@@ -425,10 +425,11 @@ int gs_engine::start() {
   {
     const int rc = validateMixed();
     if (rc) return rc;
-    if (mixed) {
-      gs_set_error("mixed router networks are not built in this library yet");
-      return GS_EUNSUPPORTED;
-    }
+  }
+  bool anyRandom = cfg.router == GS_ROUTER_RANDOMSUB;  // some host runs randomsub (d.sel)
+  if (!routerH.empty()) {
+    anyRandom = false;
+    for (uint8_t r : routerH) anyRandom = anyRandom || r == GS_ROUTER_RANDOMSUB;
   }
   if (doPX && (gaterOn || behaveAll != 0 || world > 1 || acctOn)) {
     gs_set_error("peer exchange is supported by an honest, unpartitioned engine without the gater or RPC accounting");
@@ -471,7 +472,7 @@ int gs_engine::start() {
   n1 = part[rank + 1];
   e0 = rowptr[n0];
   e1 = rowptr[n1];
-  if (world > 1 && cfg.router == GS_ROUTER_RANDOMSUB) {
+  if (world > 1 && anyRandom) {
     gs_set_error("a partitioned engine supports floodsub and gossipsub (randomsub target masks are not exchanged)");
     return GS_EUNSUPPORTED;
   }
@@ -524,8 +525,10 @@ int gs_engine::start() {
   x.N = N; x.T = T; x.Wt = Wt; x.W = W; x.St = St; x.S = S; x.R = R;
   x.HL = gp.HistoryLength; x.HG = gp.HistoryGossip; x.E = E;
   x.router = cfg.router; x.scoring = scoring; x.floodPublish = floodPublish;
+  x.nrouter = nullptr;
+  x.proto = nullptr;
   x.rsTarget = 6;
-  if (cfg.router == GS_ROUTER_RANDOMSUB) {
+  if (anyRandom) {
     const int sq = (int)std::ceil(std::sqrt((double)cfg.randomsub_size));
     x.rsTarget = std::max(6, sq);
   }
@@ -639,8 +642,23 @@ int gs_engine::start() {
   x.oldm = dalloc<uint64_t>(W); chk(x.oldm);
   x.yTab = dalloc<uint64_t>(2 * (size_t)W); chk(x.yTab);
   x.nAuth = dalloc<int32_t>(N); chk(x.nAuth);
-  x.sel = cfg.router == GS_ROUTER_RANDOMSUB ? dalloc<uint64_t>(NS) : nullptr;
-  if (cfg.router == GS_ROUTER_RANDOMSUB) chk(x.sel);
+  x.sel = anyRandom ? dalloc<uint64_t>(NS) : nullptr;
+  if (anyRandom) chk(x.sel);
+  if (mixed) {
+    // the hosts' routers (v1.0 folded into gossipsub) and the connections' protocols
+    uint8_t* nr = dalloc<uint8_t>(N);
+    uint8_t* pr = dalloc<uint8_t>(E);
+    chk(nr); chk(pr);
+    if (ok) {
+      std::vector<uint8_t> rh((size_t)N);
+      for (int u = 0; u < N; ++u) rh[u] = (uint8_t)routerOf(u);
+      HIPCHECK(hipMemcpyAsync(nr, rh.data(), (size_t)N, hipMemcpyHostToDevice, stream));
+      HIPCHECK(hipMemcpyAsync(pr, protoH.data(), (size_t)E, hipMemcpyHostToDevice, stream));
+      HIPCHECK(hipStreamSynchronize(stream));  // rh is pageable
+    }
+    x.nrouter = nr;
+    x.proto = pr;
+  }
   x.lastpub = dalloc<int64_t>((size_t)N * T); chk(x.lastpub);
   x.fanoutPresent = dalloc<uint64_t>(N); chk(x.fanoutPresent);
   const size_t NQ = (size_t)nOwnN * GS_TABLE;
@@ -762,13 +780,17 @@ int gs_engine::start() {
   x.gLast = nullptr;
   x.gSt = nullptr;
   x.gGrp = nullptr;
+  x.gConn = nullptr;
+  x.gExp = nullptr;
+  x.gRetain = gaterP.RetainStats;
   if (gaterOn) {
     x.gThreshold = gaterP.Threshold; x.gGlobalDecay = gaterP.GlobalDecay; x.gSourceDecay = gaterP.SourceDecay;
     x.gDecayToZero = gaterP.DecayToZero; x.gDupW = gaterP.DuplicateWeight; x.gIgnW = gaterP.IgnoreWeight;
     x.gRejW = gaterP.RejectWeight; x.gQuiet = gaterP.Quiet;
     x.gValidate = dalloc<double>(N); x.gThrottle = dalloc<double>(N); x.gLast = dalloc<int64_t>(N);
     x.gSt = dalloc<double>(4 * (size_t)E); x.gGrp = dalloc<uint8_t>(E);
-    chk(x.gValidate); chk(x.gThrottle); chk(x.gLast); chk(x.gSt); chk(x.gGrp);
+    x.gConn = dalloc<int32_t>(E); x.gExp = dalloc<int64_t>(E);
+    chk(x.gValidate); chk(x.gThrottle); chk(x.gLast); chk(x.gSt); chk(x.gGrp); chk(x.gConn); chk(x.gExp);
     if (ok) {
       // peers of one IP share a stats object (peer_gater.go:262-280); getIP = ipv4, 0 = "<unknown>"
       std::vector<uint8_t> grp(E);
@@ -780,6 +802,12 @@ int gs_engine::start() {
           grp[e] = (uint8_t)(f - rowptr[u]);
         }
       std::vector<int64_t> never(N, INT64_MIN);
+      // connected peers per stats object (AddPeer of every connection up at the start)
+      std::vector<int32_t> conn((size_t)E, 0);
+      for (int u = 0; u < N; ++u)
+        for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e)
+          if (!isDown(e)) conn[rowptr[u] + grp[e]]++;
+      HIPCHECK(hipMemcpyAsync(x.gConn, conn.data(), (size_t)E * 4, hipMemcpyHostToDevice, stream));
       HIPCHECK(hipMemcpyAsync(x.gGrp, grp.data(), E, hipMemcpyHostToDevice, stream));
       HIPCHECK(hipMemcpyAsync(x.gLast, never.data(), (size_t)N * 8, hipMemcpyHostToDevice, stream));
       HIPCHECK(hipStreamSynchronize(stream));
@@ -816,7 +844,8 @@ int gs_engine::start() {
       if (!traceMask[u]) continue;
       auto up = [&](int64_t e) { return !dormant.count({std::min(u, col[e]), std::max(u, col[e])}); };
       for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e)
-        if (up(e)) tracePending.push_back(gs_trace_event{0, -1, GS_TRACE_ADD_PEER, u, col[e], -1, 0, 0});
+        if (up(e))  // the connection's protocol in `reason` on a mixed network
+          tracePending.push_back(gs_trace_event{0, -1, GS_TRACE_ADD_PEER, u, col[e], -1, 0, mixed ? protoH[e] : (uint8_t)0});
       for (int t = 0; t < T; ++t)
         if ((sub[u] >> t) & 1) tracePending.push_back(gs_trace_event{0, -1, GS_TRACE_JOIN, u, -1, (int16_t)t, 0, 0});
       // the hello packet of every peer (pubsub.go:495; its RecvRPC at time 0)
@@ -879,6 +908,7 @@ int gs_engine::start() {
       ah[t].msgF = (int32_t)gs_pb_field(acctMsg[t]);
       ah[t].graftEnt = (int32_t)gs_pb_field(gs_pb_graft(acctTl[t]));
       ah[t].pruneEnt = (int32_t)gs_pb_field(gs_pb_prune(acctTl[t], bo));
+      ah[t].pruneEnt10 = (int32_t)gs_pb_field(gs_pb_prune_v10(acctTl[t]));
       ah[t].ihaveHead = (int32_t)gs_pb_field(acctTl[t]);
     }
     x.acctIdF = (int32_t)gs_pb_field(acctIdLen);
@@ -1245,6 +1275,7 @@ int gs_engine::stepOne() {
     for (size_t i = b; i < e; ++i) {
       const int src = mSrc[i], t = mTopic[i];
       if (src < n0 || src >= n1) continue;  // another rank's publisher
+      if (routerOf(src) != GS_ROUTER_GOSSIPSUB) continue;  // floodsub / randomsub hosts keep no fanout
       if ((sub[src] >> t) & 1) continue;
       const uint64_t key = ((uint64_t)src << 6) | (uint64_t)t;
       if (std::find(seenPair.begin(), seenPair.end(), key) != seenPair.end()) continue;
@@ -1325,7 +1356,7 @@ int gs_engine::stepOne() {
   if (n > 0) {
     TIMED(this, GS_K_PUBLISH, (k_publish<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, h, cur, head)));
     k_publist<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, cur);
-    if (cfg.router == GS_ROUTER_RANDOMSUB) k_publish_rs<<<n, 64, 0, stream>>>(d, (int)b);
+    if (d.sel) k_publish_rs<<<n, 64, 0, stream>>>(d, (int)b);
   }
   if (gossip) {
     if (scoring) TIMED(this, GS_K_SCORE, (score_rows<2>(d, eOwn, T, nullptr, stream)));
@@ -1375,7 +1406,7 @@ int gs_engine::stepOne() {
   }
   if (gaterDecayDue(now)) {  // peerGater.background ticker (peer_gater.go:204-217)
     const int64_t nth = std::max<int64_t>(nOwn, eOwn);
-    if (nth) k_gater_decay<<<nblk(nth, 256), 256, 0, stream>>>(d);
+    if (nth) k_gater_decay<<<nblk(nth, 256), 256, 0, stream>>>(d, now);
   }
   if (heartbeatDue(now)) {
     ticks++;
@@ -1971,7 +2002,6 @@ int gs_schedule_events(gs_engine* g, int32_t n, const int32_t* kind, const int32
                        const int64_t* hop) {
   if (n < 0 || (n > 0 && (!kind || !a || !b || !hop))) { gs_set_error("gs_schedule_events: bad arguments"); return GS_EINVAL; }
   if (!g->graphSet) { gs_set_error("graph not set"); return GS_ESTATE; }
-  if (g->gaterOn) { gs_set_error("connection churn with the peer gater is not supported"); return GS_EUNSUPPORTED; }
   if (n > 0 && !g->churnWindow && !g->mId.empty()) {
     // late joiners catch up through gossip: the wide message window is chosen
     // when the first churn is scheduled, and it cannot change once messages
@@ -2240,6 +2270,10 @@ int gs_read_scores(gs_engine* g, double* score) {
   score_rows<0>(g->d, g->E, g->d.T, g->dScoreTmp, g->stream);
   HIPCHECK(hipMemcpyAsync(score, g->dScoreTmp, g->E * 8, hipMemcpyDeviceToHost, g->stream));
   HIPCHECK(hipStreamSynchronize(g->stream));
+  if (g->mixed)  // only gossipsub hosts keep a peerScore (floodsub / randomsub: none, score 0)
+    for (int u = 0; u < g->N; ++u)
+      if (g->routerOf(u) != GS_ROUTER_GOSSIPSUB)
+        for (int64_t e = g->rowptr[u]; e < g->rowptr[u + 1]; ++e) score[e] = 0.0;
   return GS_OK;
 }
 

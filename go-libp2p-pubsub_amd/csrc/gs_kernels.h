@@ -335,6 +335,7 @@ __global__ void k_recap(Dev d, int t, double fmdCap, double mmdCap) {
 // At hop 0 no fanout exists, so Join takes getPeers(D, !direct && score >= 0).
 __global__ __launch_bounds__(64) void k_join(Dev d, int64_t hop, int64_t now, int cur) {
   const int u = d.n0 + blockIdx.x;
+  if (!gossip_host(d, u)) return;  // floodsub.go:102-104, randomsub.go:162-164: Join only traces
   const int lane = lane_id();
   const int64_t base = d.rowptr[u];
   const int deg = (int)(d.rowptr[u + 1] - base);
@@ -348,7 +349,7 @@ __global__ __launch_bounds__(64) void k_join(Dev d, int64_t hop, int64_t now, in
   const uint64_t joined = d.sub[u];
   for (int t = 0; t < d.T; ++t) {
     if (!((joined >> t) & 1)) continue;
-    const bool cand = valid && edge_up(d, e) && ((subv >> t) & 1) && !dir && s >= 0;
+    const bool cand = valid && edge_up(d, e) && mesh_peer(d, e) && ((subv >> t) & 1) && !dir && s >= 0;
     const uint64_t key = gs_key64(d.seed, GS_SITE_GP_JOIN, u, (uint32_t)hop, v, t);
     const bool sel = select_k(cand, key, d.D);
     if (sel) {
@@ -402,7 +403,8 @@ __global__ __launch_bounds__(64) void k_fanout_pub(Dev d, const int32_t* __restr
   const bool present = (d.fanoutPresent[u] >> t) & 1;
   const int have = __popcll(__ballot((fo >> t) & 1));
   if (!present || have == 0) {
-    const bool cand = valid && edge_up(d, e) && ((d.subA[v] >> t) & 1) && !d.direct[e] && d.score0[e] >= d.publishThr;
+    const bool cand = valid && edge_up(d, e) && mesh_peer(d, e) && ((d.subA[v] >> t) & 1) && !d.direct[e] &&
+                      d.score0[e] >= d.publishThr;
     const uint64_t key = gs_key64(d.seed, GS_SITE_GP_FANOUT_PUB, u, (uint32_t)hop, v, t);
     const bool sel = select_k(cand, key, d.D);
     const unsigned long long any = __ballot(sel);
@@ -423,19 +425,22 @@ __global__ void k_fwd(Dev d, int cur) {
   const int u = d.esrc[e];
   const uint64_t sv = d.subA[d.col[e]];  // the peer's subscriptions as u knows them
   uint64_t relay, pub;
-  if (d.router != 2) {  // floodsub.go:85-99 / randomsub.go:115-150: every topic peer
+  if (!gossip_host(d, u)) {  // floodsub.go:85-99 / randomsub.go:115-150: every topic peer
     relay = sv;
     pub = sv;
   } else {
     const uint64_t joined = d.sub[u];
     const uint64_t m = d.mesh[e];
     const bool dir = d.direct[e];
-    relay = joined & (m | (dir ? sv : 0));
+    // a floodsub-protocol peer gets every message of its topics at score >=
+    // PublishThreshold (gossipsub.go:969-975)
+    const uint64_t fs = (!mesh_peer(d, e) && d.score0[e] >= d.publishThr) ? sv : 0;
+    relay = joined & (m | (dir ? sv : 0) | fs);
     if (behaves(d, u, GS_BEHAVE_NO_FORWARD)) relay = 0;  // a squatter relays nothing
     if (d.floodPublish) {
       pub = (dir || d.score0[e] >= d.publishThr) ? sv : 0;
     } else {
-      pub = (dir ? sv : 0) | (m & joined) | (d.fanout[e] & ~joined);
+      pub = (dir ? sv : 0) | (m & joined) | (d.fanout[e] & ~joined) | fs;
     }
   }
   if (!edge_up(d, e)) relay = pub = 0;  // no connection: nothing is sent
@@ -461,18 +466,23 @@ __global__ void k_pubmask(Dev d, int b, int n, int cur) {
 // publish): every topic peer except ReceivedFrom and the author, and if more
 // than RandomSubD (6) remain, the keyed-shuffle prefix of max(6, ceil(sqrt(size))).
 // Wave-cooperative, lanes = u's neighbours; stores the chosen neighbour mask.
-__device__ __forceinline__ void rs_select(const Dev& d, int u, int deg, int p, uint64_t subp, int slot, int ff) {
+// Floodsub-protocol peers are always sent to (randomsub.go:117-118); only the
+// randomsub-protocol candidates are sampled.
+__device__ __forceinline__ void rs_select(const Dev& d, int u, int64_t base, int deg, int p, uint64_t subp, int slot,
+                                          int ff) {
   const int lane = lane_id();
   const int t = slot / d.St;
   const int origin = d.slotSrc[slot];
   const bool cand = lane < deg && ((subp >> t) & 1) && lane != ff && p != origin;
-  const int n = __popcll(__ballot(cand));
+  const bool fs = cand && d.proto != nullptr && d.proto[base + lane] == GS_PROTO_FLOODSUB;
+  const bool rc = cand && !fs;
+  const int n = __popcll(__ballot(rc));
   bool sel = cand;
   if (n > 6) {
     int target = d.rsTarget < n ? d.rsTarget : n;
     if (target < n) {
       const uint64_t key = gs_key64(d.seed, GS_SITE_RANDOMSUB, u, (uint32_t)d.slotMid[slot], p, 0);
-      sel = select_k(cand, key, target);
+      sel = fs || select_k(rc, key, target);
     }
   }
   const unsigned long long m = __ballot(sel);
@@ -648,7 +658,8 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   const int deg = (int)(d.rowptr[v + 1] - base);
   const uint64_t sv = d.sub[v];
   const bool valid = lane < deg;
-  const bool scoring = d.scoring != 0;
+  const bool gossipV = gossip_host(d, v);  // peerScore, gater and mcache exist on gossipsub hosts only
+  const bool scoring = d.scoring != 0 && gossipV;
   // in-edge metadata (lane = in-edge)
   int u = 0, jr = -1, Ln = 0;
   uint64_t relay = 0, pub = 0, relayAll = 0, pubAll = 0;
@@ -671,7 +682,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
       irOff = (int)(ir >> 24);
       irN = (int)(ir & 0xFFFFFF);
     }
-    gray = d.router == 2 && scoring && !d.direct[e] && d.score0[e] < d.graylistThr;
+    gray = scoring && !d.direct[e] && d.score0[e] < d.graylistThr;
     if (relayAll | pubAll) Ln = d.fln[prv][u];
   }
   GS_STAMP(0);
@@ -704,7 +715,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
     for (int k = lane; k < 4 * 64; k += 64) sPer[k] = 0;
     for (int k = lane; k < nR; k += 64) sDrop[k] = 0;
     double thr = -1.0;
-    if (d.gater && valid && !gray && !d.direct[base + lane]) {
+    if (d.gater && gossipV && valid && !gray && !d.direct[base + lane]) {
       // AcceptFrom's circuit breaker on this node's hop-start counters (:329-342)
       const int64_t last = d.gLast[v];
       const double gv = d.gValidate[v], gt = d.gThrottle[v];
@@ -743,7 +754,8 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   }
   sRelay[lane] = relay;
   sPub[lane] = pub;
-  sSnd[lane] = valid ? (u | (jr << 24) | (gray ? (1 << 31) : 0)) : 0;
+  // sender node | jr << 24 | randomsub sender << 30 | graylisted << 31
+  sSnd[lane] = valid ? (u | (jr << 24) | (rs_host(d, u) ? (1 << 30) : 0) | (gray ? (1 << 31) : 0)) : 0;
   sLn[lane] = Ln;
   const uint64_t scoredT = __ballot(lane < T && scoring && d.tp[lane].scored);  // scored topics
   __syncthreads();
@@ -890,7 +902,8 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
           const int i = si[rr] < 0 ? 0 : si[rr];
           const int snd = sSnd[i];
           const int uu = snd & 0xFFFFFF;
-          const int jri = (snd >> 24) & 0x7F;
+          const int jri = (snd >> 24) & 0x3F;
+          const bool rsS = (snd >> 30) & 1;
           const bool isGray = snd < 0;
           const uint64_t rl = sRelay[i], pb = sPub[i];
           const int n = si[rr] < 0 ? 0 : min(4, sLn[i] - 4 * kb[rr]);
@@ -902,7 +915,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
             const int t = (int)__umulhi((unsigned)slot, d.stMagic);
             bool sent = c < n && (tag == 255 ? ((pb >> t) & 1) : ((rl >> t) & 1));
             sent = sent && tag != jri;  // ReceivedFrom exclusion (gossipsub.go:1003)
-            if (sent && d.router == 1) sent = (d.sel[(int64_t)uu * d.S + slot] >> jri) & 1;
+            if (sent && rsS) sent = (d.sel[(int64_t)uu * d.S + slot] >> jri) & 1;
             if (sent && authV && d.slotSrc[slot] == v) sent = false;  // never to the author
             if (count) {
               nSent += sent;
@@ -987,7 +1000,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
         const int t = (int)__umulhi((unsigned)slot, d.stMagic);
         bool sent = tag == 255 ? ((pu >> t) & 1) : ((ru >> t) & 1);
         sent = sent && tag != jr;
-        if (sent && d.router == 1) sent = (d.sel[(int64_t)u * d.S + slot] >> jr) & 1;
+        if (sent && rs_host(d, u)) sent = (d.sel[(int64_t)u * d.S + slot] >> jr) & 1;
         if (sent && authV && d.slotSrc[slot] == v) sent = false;
         if (sent) {
           ++nSent;
@@ -1045,7 +1058,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
         Sw[j] = d.seen[(int64_t)v * W + w];
         Uw[j] = D;  // & ~seen below
         Ow[j] = d.oldm[w];
-        if (d.router == 2) Hw[j] = d.hist[((int64_t)head * d.nOwnH + (v - d.n0)) * W + w];
+        if (gossipV) Hw[j] = d.hist[((int64_t)head * d.nOwnH + (v - d.n0)) * W + w];
       }
     }
   }
@@ -1293,7 +1306,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   }
   if constexpr (ADV) {
     __syncthreads();
-    if (d.gater) {
+    if (d.gater && gossipV) {
       // peerGater counters (peer_gater.go:390-440): per IP group (+1 steps)
       // and per node; lane = in-edge, its group's stats edge gets the sums
       const int cp = valid ? (int)sPer[lane] : 0;
@@ -1335,7 +1348,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
         }
       }
     }
-    if (d.cSpam[cur] != nullptr && valid && !gray && behaves(d, v, GS_BEHAVE_IWANT_SPAM)) {
+    if (d.cSpam[cur] != nullptr && valid && !gray && behaves(d, v, GS_BEHAVE_IWANT_SPAM) && mesh_peer(d, base + lane)) {
       // IWANT spam (gossipsub_spam_test.go:113-128): one request per message
       // received from this sender (its accepted copies), in an extra RPC
       auto each = [&](auto&& fn) {
@@ -1391,7 +1404,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
     if (U) {
       if ((U & Ow[j]) || !wm_has(amW, w)) set_err(d, E_LATE);
       d.seen[(int64_t)v * W + w] = Sw[j] | U;
-      if (d.router == 2 && Ud) d.hist[((int64_t)head * d.nOwnH + (v - d.n0)) * W + w] = Hw[j] | Ud;
+      if (gossipV && Ud) d.hist[((int64_t)head * d.nOwnH + (v - d.n0)) * W + w] = Hw[j] | Ud;
       nDeliv += k;
       uint64_t y = Ud;
       while (y) {
@@ -1416,7 +1429,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
         }
       }
     }
-    if (d.router == 1) {  // randomsub: targets of every message first delivered here
+    if (rs_host(d, v)) {  // randomsub: targets of every message first delivered here
       unsigned long long lanesWith = __ballot(Ud != 0);
       while (lanesWith) {
         const int src = __ffsll((long long)lanesWith) - 1;
@@ -1427,7 +1440,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
         while (y) {
           const int b = __ffsll((long long)y) - 1;
           y &= y - 1;
-          rs_select(d, v, deg, valid ? u : -1, valid && edge_up(d, base + lane) ? d.subA[u] : 0, wsrc * 64 + b,
+          rs_select(d, v, base, deg, valid ? u : -1, valid && edge_up(d, base + lane) ? d.subA[u] : 0, wsrc * 64 + b,
                     sFirst[fidx(rks, b)]);
         }
       }
@@ -1526,7 +1539,7 @@ __global__ void k_publish(Dev d, int b, int n, int64_t h, int cur, int head) {
     const int w = slot >> 6;
     const unsigned long long bit = 1ull << (slot & 63);
     atomicOr((unsigned long long*)&d.seen[(int64_t)src * d.W + w], bit);
-    if (d.router == 2) atomicOr((unsigned long long*)&d.hist[((int64_t)head * d.nOwnH + (src - d.n0)) * d.W + w], bit);
+    if (gossip_host(d, src)) atomicOr((unsigned long long*)&d.hist[((int64_t)head * d.nOwnH + (src - d.n0)) * d.W + w], bit);
     if (d.needAge) d.age[(int64_t)src * d.S + slot] = 0;
     if (d.record) d.ffrom[(int64_t)src * d.S + slot] = 255;
     return;
@@ -1538,7 +1551,7 @@ __global__ void k_publish(Dev d, int b, int n, int64_t h, int cur, int head) {
   const int w = slot >> 6;
   const unsigned long long bit = 1ull << (slot & 63);
   atomicOr((unsigned long long*)&d.seen[(int64_t)src * d.W + w], bit);
-  if (d.router == 2) atomicOr((unsigned long long*)&d.hist[((int64_t)head * d.nOwnH + (src - d.n0)) * d.W + w], bit);
+  if (gossip_host(d, src)) atomicOr((unsigned long long*)&d.hist[((int64_t)head * d.nOwnH + (src - d.n0)) * d.W + w], bit);
   if (d.needAge) d.age[(int64_t)src * d.S + slot] = 0;
   if (d.record) d.ffrom[(int64_t)src * d.S + slot] = 255;
   ctr_add(d, C_PUBLISHED, 1ull);
@@ -1580,19 +1593,21 @@ __global__ __launch_bounds__(64) void k_publish_rs(Dev d, int b) {
   const int i = blockIdx.x;
   const int slot = d.mSlot[b + i];
   const int u = d.mSrc[b + i];
+  if (!rs_host(d, u)) return;  // another router's publish (mixed networks)
   const int lane = lane_id();
   const int64_t base = d.rowptr[u];
   const int deg = (int)(d.rowptr[u + 1] - base);
   const int p = lane < deg ? d.col[base + lane] : -1;
   const uint64_t subp = p >= 0 && edge_up(d, base + lane) ? d.subA[p] : 0;
-  rs_select(d, u, deg, p, subp, slot, 255);
+  rs_select(d, u, base, deg, p, subp, slot, 255);
 }
 
 // ---------------------------------------------------------------- peer gater decay
 // peerGater.decayStats (peer_gater.go:219-259) every gater DecayInterval: the
 // node counters (thread per node) and the per-IP stats held on group edges
-// (thread per edge).  Every peer stays connected (static graph), so no stats
-// object expires.
+// (thread per edge).  A stats object with a connected peer decays; one whose
+// peers all disconnected is frozen until its expiry (RemovePeer + RetainStats,
+// :374-383), then deleted — its counters restart from zero.
 __device__ __forceinline__ double gdecay(double x, double f, double z) {
   x *= f;
   return x < z ? 0.0 : x;
@@ -1616,6 +1631,7 @@ __global__ __launch_bounds__(64) void k_acct_payload(Dev d, int p) {
   const bool authW = valid && (d.world > 1 || d.nAuth[w] > 0);
   const int Ln = d.fln[p][u];
   const uint32_t* L = d.fl[p] + (int64_t)u * d.FC;
+  const bool rsU = rs_host(d, u);
   unsigned long long b = 0, n = 0;
   for (int k0 = 0; k0 < Ln; k0 += 64) {
     const uint32_t mine = k0 + lane < Ln ? L[k0 + lane] : 0u;
@@ -1626,7 +1642,7 @@ __global__ __launch_bounds__(64) void k_acct_payload(Dev d, int p) {
       const int t = (int)__umulhi((unsigned)slot, d.stMagic);
       bool sent = tag == 255 ? ((pu >> t) & 1) : ((ru >> t) & 1);
       sent = sent && tag != lane;  // not back to the deliverer (gossipsub.go:1003)
-      if (sent && d.router == 1) sent = (d.sel[(int64_t)u * d.S + slot] >> lane) & 1;
+      if (sent && rsU) sent = (d.sel[(int64_t)u * d.S + slot] >> lane) & 1;
       if (sent && authW && d.slotSrc[slot] == w) sent = false;  // never to the author
       if (sent) {
         b += (unsigned long long)d.acc[t].msgF;
@@ -1663,7 +1679,7 @@ __global__ __launch_bounds__(64) void k_trace_payload(Dev d, int p, int64_t hop)
       const int t = (int)__umulhi((unsigned)slot, d.stMagic);
       bool sent = tr && (tag == 255 ? ((pu >> t) & 1) : ((ru >> t) & 1));
       sent = sent && tag != lane;  // not back to the deliverer (gossipsub.go:1003)
-      if (sent && d.router == 1) sent = (d.sel[(int64_t)u * d.S + slot] >> lane) & 1;
+      if (sent && rs_host(d, u)) sent = (d.sel[(int64_t)u * d.S + slot] >> lane) & 1;
       if (sent && d.slotSrc[slot] == w) sent = false;  // never to the author
       if (sent) {
         const int sp = tag == 255 ? 1 : 2;  // local publish / forward
@@ -1682,7 +1698,7 @@ __global__ void k_acct_add(Dev d, const int64_t* __restrict__ pairs, int n) {
   atomicAdd(&d.rpcN[pairs[2 * k]], 1ull);
 }
 
-__global__ void k_gater_decay(Dev d) {
+__global__ void k_gater_decay(Dev d, int64_t now) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < d.n1 - d.n0) {
     const int v = d.n0 + (int)i;
@@ -1692,5 +1708,9 @@ __global__ void k_gater_decay(Dev d) {
   const int64_t e = d.e0 + i;
   if (e >= d.e1) return;
   if (d.rowptr[d.esrc[e]] + d.gGrp[e] != e) return;  // not a group's stats edge
-  for (int k = 0; k < 4; ++k) d.gSt[k * d.E + e] = gdecay(d.gSt[k * d.E + e], d.gSourceDecay, d.gDecayToZero);
+  if (d.gConn[e] > 0) {
+    for (int k = 0; k < 4; ++k) d.gSt[k * d.E + e] = gdecay(d.gSt[k * d.E + e], d.gSourceDecay, d.gDecayToZero);
+  } else if (d.gExp[e] < now) {
+    for (int k = 0; k < 4; ++k) d.gSt[k * d.E + e] = 0.0;  // delete(pg.ipStats, ip)
+  }
 }

@@ -70,7 +70,9 @@ __device__ __forceinline__ void prune_topics(const Dev& d, int64_t e, int v, uin
       meshE &= ~(1ull << t);
       if (lane_id() == t) meshcnt_lane--;
     }
-    add_backoff(d, e, t, now, d.PruneRecv);
+    // a v1.1 PRUNE carries the sender's backoff in whole seconds; a v1.0 one
+    // none, so the receiver's own PruneBackoff applies (handlePrune :819-825)
+    add_backoff(d, e, t, now, px_peer(d, e) ? d.PruneRecv : d.PruneBackoff);
   }
 }
 
@@ -102,7 +104,8 @@ __device__ __forceinline__ uint64_t px_sel(const Dev& d, int v, int64_t base, in
   const bool valid = lane < deg;
   const int64_t e = base + lane;
   const int u = valid ? d.col[e] : 0;
-  const bool cand = ok && valid && lane != p && edge_up(d, e) && ((d.subA[u] >> t) & 1);
+  // getPeers: mesh-capable topic peers only (gossipsub.go:1849)
+  const bool cand = ok && valid && lane != p && edge_up(d, e) && mesh_peer(d, e) && ((d.subA[u] >> t) & 1);
   const uint32_t pp = (uint32_t)d.col[base + p];
   const uint64_t key = gs_key64(d.seed, GS_SITE_PX, v, (uint32_t)hop, u, (pp << 6) | (uint32_t)t);
   return __ballot(select_k(cand, key, d.PrunePeers));
@@ -289,6 +292,7 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
                                                 int head, int cutModeArg) {
   const Dev& d = *dp;  // from device memory, as k_phase_a
   const int cutMode = ADV ? cutModeArg : 0;
+  if (!gossip_host(d, d.n0 + (int)blockIdx.x)) return;  // FloodSubRouter / RandomSubRouter.HandleRPC: no-ops
   __shared__ uint64_t scache[64 * WPL];  // v's mcache windows (handleIWant, step 2)
   uint64_t* const sseen = scache;        // then v's seen row (handleIHave, step 3)
   // step 2's peertx hash; the step-3 arrays below live in the same LDS once
@@ -437,7 +441,7 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
         if (pr) {
           pOut |= 1ull << t;
           nR++;
-          if (d.doPX && !noPX) pxPrunes(1ull << t);  // this RPC's PRUNE reply carries PX
+          if (d.doPX && !noPX && px_peer(d, ei)) pxPrunes(1ull << t);  // this RPC's PRUNE reply carries PX
         }
       }
       // (2) reply RPCs: IWANT requests and PRUNEs answering our own control
@@ -472,7 +476,7 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
           pr = graft_one(d, ei, v, t, sc_i, now, meshcnt, mE, dirty, dirtyUp, noPX);
           if (pr) prunes |= 1ull << t;
         }
-        if (d.doPX && !noPX) pxPrunes(prunes);
+        if (d.doPX && !noPX && px_peer(d, ei)) pxPrunes(prunes);
         const bool acc = pxAccept(pHb_i & d.sub[v]);
         prune_topics(d, ei, v, pHb_i, now, meshcnt, mE, dirty);
         if (acc) px_connect(d, v, base, deg, prv, d.cPx[prv][ei], pHb_i & d.sub[v]);
@@ -1049,12 +1053,12 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
           // with an empty control message (2 bytes); IWANT + PRUNEs for the
           // heartbeat RPC
           int64_t b = 0;
-          for (uint64_t m = joinRej; m; m &= m - 1) b += gs_pb_field(d.acc[__ffsll((long long)m) - 1].pruneEnt);
+          for (uint64_t m = joinRej; m; m &= m - 1) b += gs_pb_field(prune_entry(d, e, __ffsll((long long)m) - 1));
           if (srvB) b += (int64_t)srvB + 2;
           if (srvBS) b += (int64_t)srvBS + 2;
           if (iwantAny || prunesHb) {
             int64_t body = iwantAny ? gs_pb_field((int64_t)(iwantRec & 0xFFFFFF) * d.acctIdF) : 0;
-            for (uint64_t m = hbPr; m; m &= m - 1) body += d.acc[__ffsll((long long)m) - 1].pruneEnt;
+            for (uint64_t m = hbPr; m; m &= m - 1) body += prune_entry(d, e, __ffsll((long long)m) - 1);
             b += gs_pb_field(body);
           }
           acct_send(d, e, b, nReplies);
@@ -1540,6 +1544,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
   __shared__ double sterm[64];
   __shared__ uint64_t sgw[64 * GS_MAX_WPL];
   const int v = d.n0 + blockIdx.x;
+  if (!gossip_host(d, v)) return;  // only gossipsub hosts run a heartbeat
   const int lane = lane_id();
   const int64_t base = d.rowptr[v];
   const int deg = (int)(d.rowptr[v + 1] - base);
@@ -1586,6 +1591,10 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
   if (lane < d.T)
     for (int w = lane * d.Wt; w < (lane + 1) * d.Wt; ++w) nmT += __popcll(sgw[w]);
   const uint64_t subv = vm && edge_up(d, e) ? d.subA[vcol] : 0;  // topic peers: connected, announced
+  // the candidates of getPeers and emitGossip: mesh-capable topic peers
+  // (GossipSubFeatureMesh, gossipsub.go:1681, 1849)
+  const bool mc = vm && mesh_peer(d, e);
+  const uint64_t subvM = mc ? subv : 0;
   uint64_t meshl = vm ? d.mesh[e] : 0;
   uint64_t fanl = valid ? d.fanout[e] : 0;
   uint64_t boM = vm ? d.boMask[e] : 0;  // topics in backoff with this peer
@@ -1619,7 +1628,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
   const bool graftSpam = behaves(d, v, GS_BEHAVE_GRAFT_SPAM);
   uint64_t spamGraft = 0;  // GRAFTs without a mesh change (not traced as Graft)
   if constexpr (PAIR) {
-    hb_pair(d, v, base, deg, vm, e, vcol, hop, now, ticks, head, joined, subv, S, dir, ob, graftSpam, nmT, meshl, boM,
+    hb_pair(d, v, base, deg, vm, e, vcol, hop, now, ticks, head, joined, subvM, S, dir, ob, graftSpam, nmT, meshl, boM,
             Slive, dirty, dirtyUp, tograft, toprune, ihave, spamGraft, plst, obs, posOf, (double*)sgw, cyMesh, cyEmit,
             cySel);
     if (!valid) tograft = toprune = ihave = spamGraft = 0;  // the mirror half is done
@@ -1628,7 +1637,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
     if (!((joined >> t) & 1)) continue;
     const unsigned long long c0 = GS_CLK();
     const uint64_t bit = 1ull << t;
-    const bool inTopic = valid && ((subv >> t) & 1);
+    const bool inTopic = valid && ((subvM >> t) & 1);
     bool m = valid && (meshl & bit);
     // drop all peers with negative score, without PX; a GRAFT spammer first
     // leaves its whole mesh (gossipsub_spam_test.go:428-446)
@@ -1782,11 +1791,13 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
     // gossipsub.go:1636-1647), with the live scores after every mesh change;
     // none for a peer dropped for its negative score (noPX, :1350-1356)
     uint64_t any = 0;
-    for (int o = 0; o < 64; ++o) any |= lane_get64(valid && !hbNoPX ? toprune : 0ull, o);
+    // v1.0 peers get no PX (makePrune gossipsub.go:1804-1807)
+    const bool pxTo = valid && !hbNoPX && px_peer(d, e);
+    for (int o = 0; o < 64; ++o) any |= lane_get64(pxTo ? toprune : 0ull, o);
     const bool ok = any ? px_score_ok(d, base, deg, sterm) : true;
     for (uint64_t mm = any; mm; mm &= mm - 1) {
       const int t = __ffsll((long long)mm) - 1;
-      unsigned long long pl = __ballot(valid && !hbNoPX && ((toprune >> t) & 1));
+      unsigned long long pl = __ballot(pxTo && ((toprune >> t) & 1));
       while (pl) {  // one list per pruned peer
         const int p = __ffsll((long long)pl) - 1;
         pl &= pl - 1;
@@ -1821,15 +1832,15 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
     }
     const int cnt = __popcll(__ballot(f));
     if (cnt < d.D) {
-      const bool cand = inTopic && !f && !dir && S >= d.publishThr;
+      const bool cand = inTopic && mc && !f && !dir && S >= d.publishThr;
       const uint64_t key = gs_key64(d.seed, GS_SITE_GP_FANOUT_HB, v, hw, vcol, t);
       if (select_k_lds(cand, key, d.D - cnt, (uint64_t*)sterm)) {
         fanl |= bit;
         f = true;
       }
     }
-    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic, f, dir, Slive, dirty, dirtyUp, base, (double*)sgw,
-                         lane_get(nmT, t));
+    ihave |= emit_gossip(d, v, t, hop, head, valid, vcol, inTopic && mc, f, dir, Slive, dirty, dirtyUp, base,
+                         (double*)sgw, lane_get(nmT, t));
   }
   // sendGraftPrune + flush: one heartbeat RPC per peer with any control
   if (valid && is_traced(d, v)) {  // prunePeer / graftPeer, gossipsub.go:1334, 1343
@@ -1850,7 +1861,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
         body += gs_pb_field(d.acc[t].ihaveHead + (int64_t)sterm[t] * d.acctIdF);
       }
       for (uint64_t m = tograft; m; m &= m - 1) body += d.acc[__ffsll((long long)m) - 1].graftEnt;
-      for (uint64_t m = toprune; m; m &= m - 1) body += d.acc[__ffsll((long long)m) - 1].pruneEnt;
+      for (uint64_t m = toprune; m; m &= m - 1) body += prune_entry(d, e, __ffsll((long long)m) - 1);
       acct_send(d, e, gs_pb_field(body), 1);
     }
   }
@@ -1995,6 +2006,11 @@ __global__ __launch_bounds__(64) void k_edge_down(Dev d, const int32_t* __restri
     d.fwdPub[prv][e] = 0;
     d.sdirty[e] = 1;
     if (is_traced(d, u)) trace_emit(d, hop, GS_TRACE_REMOVE_PEER, u, v, -1, -1, 0);  // trace.go:215
+    if (d.gater) {  // peerGater.RemovePeer (peer_gater.go:374-383) on the IP's stats object
+      const int64_t g = d.rowptr[u] + d.gGrp[e];
+      atomicSub(&d.gConn[g], 1);
+      d.gExp[g] = now + d.gRetain;  // every removal of this hop writes the same expiry
+    }
   }
   if (!d.scoring || d.rstate == nullptr || d.rstate[e] != 1) return;
   const bool drop = s > 0;
@@ -2040,7 +2056,9 @@ __global__ void k_edge_up(Dev d, const int32_t* __restrict__ edges, int n, int64
   d.alive[e] = 1;
   if (d.rstate != nullptr) d.rstate[e] = 1;
   d.sdirty[e] = 1;
-  if (is_traced(d, d.esrc[e])) trace_emit(d, hop, GS_TRACE_ADD_PEER, d.esrc[e], d.col[e], -1, -1, 0);
+  if (d.gater) atomicAdd(&d.gConn[d.rowptr[d.esrc[e]] + d.gGrp[e]], 1);  // peerGater.AddPeer (:366-372)
+  if (is_traced(d, d.esrc[e]))  // the connection's protocol in `reason` (mixed networks)
+    trace_emit(d, hop, GS_TRACE_ADD_PEER, d.esrc[e], d.col[e], -1, -1, 0, d.proto ? d.proto[e] : 0);
 }
 
 // ipColocationFactor (score.go:335-379) after the record set changed: per
@@ -2092,8 +2110,9 @@ __global__ __launch_bounds__(64) void k_leave(Dev d, const int32_t* __restrict__
   for (uint64_t mm = mask; mm; mm &= mm - 1) {
     const int t = __ffsll((long long)mm) - 1;
     const uint64_t bit = 1ull << t;
-    if (lane == 0 && traced) trace_emit(d, hop, d.router == 1 ? GS_TRACE_JOIN : GS_TRACE_LEAVE, v, -1, t, -1, 0);
-    if (d.router != 2) continue;  // floodsub / randomsub (randomsub.go:166-168 traces a Join)
+    const int rv = router_of(d, v);
+    if (lane == 0 && traced) trace_emit(d, hop, rv == GS_ROUTER_RANDOMSUB ? GS_TRACE_JOIN : GS_TRACE_LEAVE, v, -1, t, -1, 0);
+    if (rv != GS_ROUTER_GOSSIPSUB) continue;  // floodsub / randomsub (randomsub.go:166-168 traces a Join)
     const bool m = valid && (meshl & bit);
     // makePrune's live scores: the mesh peers are pruned one after another
     // (ascending), each PRUNE's list made right after its peer's Prune — so a
@@ -2108,7 +2127,7 @@ __global__ __launch_bounds__(64) void k_leave(Dev d, const int32_t* __restrict__
     }
     if (pxOn) {  // sendPrune's makePrune(p, topic, gs.doPX) (:1087)
       const bool okPost = px_score_ok(d, base, deg, sterm);
-      unsigned long long pl = __ballot(m);
+      unsigned long long pl = __ballot(m && px_peer(d, e));  // no PX to v1.0 peers (:1804-1807)
       while (pl) {
         const int p = __ffsll((long long)pl) - 1;
         pl &= pl - 1;
@@ -2126,7 +2145,7 @@ __global__ __launch_bounds__(64) void k_leave(Dev d, const int32_t* __restrict__
       d.cPre[cur][re] = (uint8_t)(d.cPre[cur][re] + __popcll(pruned));  // one sendPrune RPC per topic
       if (d.rpcB != nullptr) {
         int64_t b = 0;
-        for (uint64_t m = pruned; m; m &= m - 1) b += gs_pb_field(d.acc[__ffsll((long long)m) - 1].pruneEnt);
+        for (uint64_t m = pruned; m; m &= m - 1) b += gs_pb_field(prune_entry(d, e, __ffsll((long long)m) - 1));
         acct_send(d, e, b, __popcll(pruned));
       }
       if (rpc_traced(d, v, d.col[e]))
@@ -2175,7 +2194,7 @@ __global__ __launch_bounds__(64) void k_join_pairs(Dev d, const int32_t* __restr
     const int t = __ffsll((long long)mm) - 1;
     const uint64_t bit = 1ull << t;
     if (lane == 0 && traced) trace_emit(d, hop, GS_TRACE_JOIN, v, -1, t, -1, 0);
-    if (d.router != 2) continue;
+    if (!gossip_host(d, v)) continue;
     unsigned long long xm = __ballot(stale);
     while (xm) {  // exact Score(p) where the memo may be off
       const int j = __ffsll((long long)xm) - 1;
@@ -2186,7 +2205,7 @@ __global__ __launch_bounds__(64) void k_join_pairs(Dev d, const int32_t* __restr
         stale = false;
       }
     }
-    const bool inTopic = valid && edge_up(d, e) && ((d.subA[vcol] >> t) & 1);
+    const bool inTopic = valid && edge_up(d, e) && mesh_peer(d, e) && ((d.subA[vcol] >> t) & 1);
     const uint64_t key = gs_key64(d.seed, GS_SITE_GP_JOIN, v, (uint32_t)hop, vcol, t);
     bool g;
     if ((fpres >> t) & 1) {

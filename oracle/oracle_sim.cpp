@@ -1726,7 +1726,6 @@ int gs_schedule_events(gs_engine* eng, int32_t n, const int32_t* kind, const int
   Sim& s = eng->sim;
   if (n < 0 || (n > 0 && (!kind || !a || !b || !hop))) { set_error("gs_schedule_events: bad arguments"); return GS_EINVAL; }
   if (!s.graphSet) { set_error("graph not set"); return GS_ESTATE; }
-  if (s.gaterOn) { set_error("connection churn with the peer gater is not supported"); return GS_EUNSUPPORTED; }
   int64_t last = s.sched.empty() ? std::max<int64_t>(1, s.hop) : std::max(s.hop, s.sched.back().hop);
   for (int32_t i = 0; i < n; ++i) {
     bool ok = hop[i] >= last && hop[i] >= 1 && kind[i] >= GS_EV_DISCONNECT && kind[i] <= GS_EV_JOIN &&

@@ -3,7 +3,7 @@ oracle's counters and a SHA-256 digest of every readback array (float64 on
 their bit patterns).  The oracle is the CPU restatement pinned by the
 reference's known-answer tests; these vectors pin the
 simulator-level results so any change to the oracle or the engine that alters
-a single bit is caught.  Usage: python tests/golden/make_golden.py"""
+a single bit is caught.  Usage: python tests/golden/make_golden.py [name ...]"""
 import hashlib
 import json
 import os
@@ -39,8 +39,12 @@ def digest(snapshot):
 
 
 def main():
-    res = {name: digest(scenarios.run(ORACLE, name)) for name in sorted(scenarios.SCENARIOS)}
+    """Every scenario, or only the names given (merged into the file)."""
     path = os.path.join(HERE, "scenarios.json")
+    names = sys.argv[1:]
+    res = json.load(open(path)) if names and os.path.exists(path) else {}
+    for name in names or sorted(scenarios.SCENARIOS):
+        res[name] = digest(scenarios.run(ORACLE, name))
     with open(path, "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
     print("wrote", path)

@@ -339,11 +339,12 @@ def sinkhole(lib, extra=()):
 
 
 def adversarial_mix(lib, n=400, k=16, seed=51, sybil_frac=0.2, queue=6, msgs=600, hb=10, gater=True,
-                    window=2048, extra=()):
+                    window=2048, churn=0, retain=None, extra=()):
     """A config-5-like mix: 20% Sybils split over IWANT spam,
     GRAFT spam, phantom-IHAVE spam and invalid-message publishing, 20 Sybils
     per shared IP (P6), the peer gater, topic validator with a bounded queue,
-    Eth2 scoring."""
+    Eth2 scoring.  churn: connections going down per 3 hops (each back after
+    5-40 hops); retain: the gater's RetainStats."""
     rng = np.random.default_rng(seed)
     g = graphs.random_regular(n, k, seed)
     sybil = rng.random(n) < sybil_frac
@@ -360,8 +361,22 @@ def adversarial_mix(lib, n=400, k=16, seed=51, sybil_frac=0.2, queue=6, msgs=600
     opts = [WithPeerScore(sp, thr), WithHop(HOP), WithMessageWindow(window), WithSeed(seed), WithBehaviour(beh),
             WithValidation([1], queue), WithRecordDeliveries()]
     if gater:
-        opts.append(WithPeerGater(DefaultPeerGaterParams()))
+        gpar = DefaultPeerGaterParams()
+        if retain is not None:
+            gpar.RetainStats = retain
+        opts.append(WithPeerGater(gpar))
     e = NewGossipSub(n, 1, g, graphs.all_subscribed(n, 1), *opts, *extra, ipv4=ipv4, lib=lib)
+    if churn:
+        crng = np.random.default_rng(seed + 77)
+        pairs = _pairs_of(g, range(n))
+        ev = []
+        for h in range(12, hb * 10 - 10, 3):
+            for i in crng.choice(len(pairs), churn, replace=False):
+                a, b = pairs[i]
+                ev.append((h, GS_EV_DISCONNECT, a, b))
+                ev.append((h + int(crng.integers(5, 40)), GS_EV_CONNECT, a, b))
+        ev.sort(key=lambda x: x[0])
+        e.schedule_events([x[1] for x in ev], [x[2] for x in ev], [x[3] for x in ev], [x[0] for x in ev])
     honest_ids = np.flatnonzero(~sybil)
     hops = (5 + (np.arange(msgs) * (hb * 10 - 20)) // msgs).astype(np.int64)
     src = rng.choice(honest_ids, msgs).astype(np.int32)
@@ -500,6 +515,10 @@ def churn_scored(lib, n=240, k=16, topics=2, seed=65, msgs=400, hb=14, extra=())
 
 
 CHURN = {
+    # the peer gater under churn: peerGater.AddPeer / RemovePeer with a 2 s
+    # RetainStats, so stats objects of disconnected IPs freeze, expire and
+    # restart from zero (peer_gater.go:219-259, 366-383)
+    "churn_gater": lambda lib, x=(): adversarial_mix(lib, n=300, seed=66, churn=6, retain=2 * Second, hb=12, extra=x),
     "churn_remove_peer": lambda lib, x=(): churn_remove_peer(lib, extra=x),
     "churn_prune": lambda lib, x=(): churn_prune(lib, extra=x),
     "churn_graft": lambda lib, x=(): churn_graft(lib, extra=x),

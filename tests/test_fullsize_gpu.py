@@ -128,8 +128,13 @@ def test_config5_full_size_steady_state(olib):
     rng = np.random.default_rng(5)
     pen = np.flatnonzero(bp > 0)
     assert len(pen) > 0
+    # edges towards invalid-message authors carry P4 (imd)
+    from pubsub_amd import GS_MSG_REJECT
+    inv = np.unique(e.srcs[e.kinds == GS_MSG_REJECT])
+    to_inv = np.flatnonzero(np.isin(e.col, inv))
     edges = np.unique(np.concatenate([sample_edges(e.E, 2000, 7, must=[0, e.E - 1]),
-                                      rng.choice(pen, min(1000, len(pen)), replace=False)]))
+                                      rng.choice(pen, min(1000, len(pen)), replace=False),
+                                      rng.choice(to_inv, min(500, len(to_inv)), replace=False)]))
     got, st = oracle_scores(olib, e.score_params, e, edges, ipv4=e.ipv4)
     want = e.scores()[edges]
     bad = np.flatnonzero(got.view(np.uint64) != want.view(np.uint64))

@@ -101,3 +101,14 @@ def test_bad_events(oracle_path):
         e.schedule_events([GS_EV_LEAVE], [0], [5], [30])        # no topic 5
     with pytest.raises(GossipEngineError):
         e.schedule_events([GS_EV_CONNECT], [0], [1], [1])       # before the last scheduled hop
+
+
+def test_churn_with_the_peer_gater(oracle_path):
+    """Connection churn with the peer gater (peer_gater.go:366-383 AddPeer /
+    RemovePeer, decayStats :219-259 with a 2 s RetainStats): the adversarial
+    mix keeps throttling and gating while connections come and go."""
+    e, hops = scenarios.SCENARIOS["churn_gater"](oracle_path)
+    e.step(hops)
+    c = e.counters()
+    assert c["throttled"] > 0 and c["gated"] > 0 and c["graylisted"] > 0, c
+    assert c["deliveries"] > 0

@@ -235,3 +235,20 @@ def test_protocol_validation(oracle_path):
     e = NewRandomSub(10, 1, g, graphs.all_subscribed(10, 1), 10, WithRouters(routers), lib=oracle_path)
     with pytest.raises(GossipEngineError):
         e.step(1)
+
+
+def test_add_peer_trace_carries_the_protocol(oracle_path):
+    """tracer.AddPeer(p, proto) (gossipsub.go:507, randomsub.go:49,
+    floodsub.go:45): on a mixed network each AddPeer event names the
+    connection's protocol, and the encoders write its protocol.ID."""
+    from pubsub_amd import _abi, encode_trace
+    e, hops = scenarios.mixed_scored(oracle_path, extra=(WithEventTracer(list(range(40))),))
+    e.step(3)
+    ev = e.trace_events()
+    add = ev[ev["type"] == _abi.GS_TRACE_ADD_PEER] if hasattr(_abi, "GS_TRACE_ADD_PEER") else ev[ev["type"] == 4]
+    assert len(add) > 0
+    proto = negotiated(e.routers_h, e.rowptr, e.col)
+    for x in add:
+        k = int(np.searchsorted(e.col[e.rowptr[x["node"]]:e.rowptr[x["node"] + 1]], x["peer"])) + int(e.rowptr[x["node"]])
+        assert int(x["reason"]) == int(proto[k])
+    assert set(int(r) for r in add["reason"]) >= {GS_PROTO_FLOODSUB, GS_PROTO_GOSSIPSUB_V10, GS_PROTO_GOSSIPSUB_V11}

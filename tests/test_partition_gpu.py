@@ -118,6 +118,8 @@ def run_partitioned(world, name, oracle):
     (3, "churn_graft"),
     (2, "churn_scored"),
     (3, "acct_churn"),
+    # a mixed network (TestMixedGossipsub): floodsub hosts beside gossipsub ones
+    (2, "mixed_gossip_flood"),
 ])
 def test_partitioned_engine_matches_oracle(world, name, oracle_path):
     res = run_partitioned(world, name, oracle_path)

@@ -213,7 +213,7 @@ def test_encode_round_trip_sizes(oracle_path):
 # ---------------------------------------------------------------- GPU parity
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["gossipsub_scored", "gossipsub_multitopic", "floodsub_dense",
-                                  "gossipsub_dense_dhi", "gossipsub_negative_app", "gossipsub_flood_publish"])
+                                  "gossipsub_dense_dhi", "gossipsub_negative_app", "gossipsub_flood_publish", "mixed_scored"])
 def test_gpu_trace_equals_oracle(oracle_path, name):
     nodes = [u for u in TRACED if u < 20] if name == "floodsub_dense" else [u for u in TRACED if u < 120]
     _, ref = traced_run(oracle_path, name, nodes)

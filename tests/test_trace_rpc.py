@@ -243,7 +243,7 @@ def test_encode_rpc_meta_json():
 
 # ---------------------------------------------------------------- GPU
 GPU_CASES = ["gossipsub_scored", "gossipsub_multitopic", "floodsub_dense", "randomsub_100", "adversarial_mix",
-             "churn_scored", "spam_ihave", "c3shape"]
+             "churn_scored", "spam_ihave", "c3shape", "mixed_scored", "mixed_randomsub"]
 
 
 @pytest.mark.gpu
