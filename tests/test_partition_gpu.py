@@ -120,6 +120,8 @@ def run_partitioned(world, name, oracle):
     (3, "acct_churn"),
     # a mixed network (TestMixedGossipsub): floodsub hosts beside gossipsub ones
     (2, "mixed_gossip_flood"),
+    # the peer gater's AddPeer / RemovePeer / RetainStats under churn
+    (2, "churn_gater"),
 ])
 def test_partitioned_engine_matches_oracle(world, name, oracle_path):
     res = run_partitioned(world, name, oracle_path)
