@@ -235,10 +235,15 @@ struct gs_engine {
   Dev* dDev = nullptr;  // device copy of d for the kernels that take it by pointer (k_phase_a / k_phase_b)
   Stage stages[kStages];
   int stageNext = 0;
+  // uploads above kStageMax (the full N x 8 subscription rows of an
+  // announcement hop: 80 MB at 10M peers) share one pinned buffer instead of
+  // growing every ring slot to their size
+  static constexpr size_t kStageMax = (size_t)4 << 20;
+  Stage bigStage;
   int upload(void* dst, const void* src, size_t bytes) {
     if (!bytes) return GS_OK;
-    Stage& st = stages[stageNext];
-    stageNext = (stageNext + 1) % kStages;
+    Stage& st = bytes > kStageMax ? bigStage : stages[stageNext];
+    if (&st != &bigStage) stageNext = (stageNext + 1) % kStages;
     if (st.used) HIPCHECK(hipEventSynchronize(st.ev));
     if (st.cap < bytes) {
       if (st.p) HIPCHECK(hipHostFree(st.p));
@@ -256,6 +261,10 @@ struct gs_engine {
 
   ~gs_engine() {
     if (stream) (void)hipStreamSynchronize(stream);  // staged uploads in flight
+    for (Stage* st : {&bigStage}) {
+      if (st->ev) (void)hipEventDestroy(st->ev);
+      if (st->p) (void)hipHostFree(st->p);
+    }
     for (Stage& st : stages) {
       if (st.ev) (void)hipEventDestroy(st.ev);
       if (st.p) (void)hipHostFree(st.p);
@@ -431,8 +440,12 @@ int gs_engine::start() {
     anyRandom = false;
     for (uint8_t r : routerH) anyRandom = anyRandom || r == GS_ROUTER_RANDOMSUB;
   }
-  if (doPX && (gaterOn || behaveAll != 0 || world > 1 || acctOn)) {
-    gs_set_error("peer exchange is supported by an honest, unpartitioned engine without the gater or RPC accounting");
+  if (doPX && (behaveAll != 0 || world > 1 || acctOn)) {
+    gs_set_error("peer exchange is supported by an honest, unpartitioned engine without RPC accounting");
+    return GS_EUNSUPPORTED;
+  }
+  if (doPX && N >= (1 << 26)) {  // a PX arena entry is topic << 26 | peer (gs_kernels_ctl.h px_append)
+    gs_set_error("peer exchange supports fewer than 2^26 peers in this build");
     return GS_EUNSUPPORTED;
   }
   if (!dormant.empty() && world > 1) {

@@ -151,6 +151,11 @@ __device__ __forceinline__ int px_count(const Dev& d, int buf, int64_t rec, uint
 // with the pruned topics `topics`: every suggested peer that v has a slot for
 // (an edge of the graph) and is not connected to is dialled (a request for the
 // host, connected at the next hop's start).  Wave-uniform.
+// The record of an edge holds the lists of every PRUNE its sender made this
+// hop (reply and heartbeat RPCs); each call filters it by the topics of one
+// RPC.  pxConnect's shuffle-and-truncate to PrunePeers (:857-862) is never
+// needed: every list comes from makePrune, which takes at most PrunePeers
+// peers (an honest sender; PX is refused together with attacker behaviours).
 __device__ __forceinline__ void px_connect(const Dev& d, int v, int64_t base, int deg, int buf, int64_t rec,
                                            uint64_t topics) {
   const int lane = lane_id();

@@ -581,10 +581,12 @@ def px_star(lib, n=20, seed=71, extra=()):
     return e, 100 + n + 30
 
 
-def px_scored(lib, extra=()):
+def px_scored(lib, extra=(), gater=False):
     """PX in a scored random graph with connection slots: 15% of every node's
     connections start down, negative app scores (noPX for negative-score
-    prunes, AcceptPXThreshold), Dhi pruning of degree-24 nodes."""
+    prunes, AcceptPXThreshold), Dhi pruning of degree-24 nodes.  gater: the
+    peer gater with a 2-entry validation queue, so PX dials (AddPeer) reach
+    throttling gaters (peer_gater.go:366-372)."""
     n, k, seed = 200, 24, 72
     g = graphs.random_regular(n, k, seed)
     rowptr, col, _ = g
@@ -595,9 +597,13 @@ def px_scored(lib, extra=()):
     app = np.where(rng.random(n) < 0.15, -150.0, 0.0)
     thr = eth2_thresholds()
     thr.AcceptPXThreshold = 0.0
+    if gater:
+        gpar = DefaultPeerGaterParams()
+        gpar.RetainStats = 2 * Second
+        extra = (WithPeerGater(gpar), WithValidation([1], 2)) + tuple(extra)
     e = NewGossipSub(n, 1, g, graphs.all_subscribed(n, 1), WithPeerScore(sp, thr), WithPeerExchange(True),
                      WithDormant(dormant), WithRecordDeliveries(), WithSeed(seed), WithHop(HOP),
-                     WithMessageWindow(512), *extra, app_score=app, lib=lib)
+                     WithMessageWindow(2048 if gater else 512), *extra, app_score=app, lib=lib)
     e.app_score = app  # for the test's checks
     src, top, hops = _publish_schedule(n, 1, 200, 20, 1, seed)
     e.publish(src, top, hops)
@@ -666,6 +672,7 @@ PX = {
     "direct_peers": lambda lib, x=(): direct_peers(lib, extra=x),
     "direct_churn": lambda lib, x=(): direct_churn(lib, extra=x),
     "px_scored": lambda lib, x=(): px_scored(lib, extra=x),
+    "px_gater": lambda lib, x=(): px_scored(lib, extra=x, gater=True),
 }
 SCENARIOS.update(PX)
 
