@@ -167,6 +167,22 @@ def algorithmic_bytes(kernel, eng, wl, per_hop):
         hg = 5
         b = 14.0 * cand + 8.0 * N * W * (hg + 1) + 40.0 * E
         return b, dict(candidates=cand, W=W)
+    if kernel == "phase_b":
+        # HandleRPC over one round's control, averaged per launch (10 per
+        # round).  Per IHAVE entry (edge, topic): the sender's gossip-window
+        # words of the topic and the receiver's seen words of it, 2 * Wt * 8
+        # (SURVEY.md §8(d) "Gossip", per topic as the engine reads them); per
+        # IWANT id: the id, HistoryLength mcache window words and the peertx
+        # entry (4 + 8 * 5 + 8); per served id its response entry (4); per
+        # GRAFT / PRUNE the edge's control record (64).  Every hop every in-edge's
+        # control-count bytes (cPre, cHb: 2 B per edge).
+        ev = per_hop["events_per_round"]
+        Wt = wl["slots"] // 64
+        b_round = (ev["ihave_sent"] * 2.0 * Wt * 8 + ev["iwant_sent"] * 52.0 + ev["iwant_served"] * 4.0 +
+                   (ev["grafts_sent"] + ev["prunes_sent"]) * 64.0)
+        b = b_round / HOPS_PER_ROUND + 2.0 * E
+        return b, dict(ihave_entries_per_round=ev["ihave_sent"], iwant_ids_per_round=ev["iwant_sent"],
+                       served_per_round=ev["iwant_served"], Wt=Wt, per_ihave_entry=2 * Wt * 8, per_iwant_id=52)
     if kernel == "score":
         # full pass: per (edge, topic) flags 1 + fmd/mfp/imd 24 + pending 4 (+ mmd, meshTime when
         # active); per edge col 4 + app 8 + p6 8 + bp 8 + out 8
@@ -225,8 +241,8 @@ def cpu_baseline(wl, seconds=20.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="config4", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="partition", choices=["partition", "replicas"])
@@ -350,7 +366,8 @@ def main():
         return
 
     nh = args.steps * HOPS_PER_ROUND
-    per_hop = {"deliveries": (c1["deliveries"] - c0["deliveries"]) / nh,
+    per_hop = {"events_per_round": {k: v / args.steps for k, v in events.items()},
+               "deliveries": (c1["deliveries"] - c0["deliveries"]) / nh,
                "published": (c1["published"] - c0["published"]) / nh,
                "active_words": float(np.mean([active_words(eng, wl, hop0 + i) for i in range(nh)])),
                "mesh_pairs": int(np.bitwise_count(eng.mesh()[eng.edge_range[0]:eng.edge_range[1]]).sum(dtype=np.int64))}
@@ -393,7 +410,9 @@ def main():
     # the score kernels' rooflines too (north-star target: >= 50% of HBM on
     # score / propagation): refreshScores streams every (edge, topic) record
     rooflines = {}
-    for k in ("refresh", "heartbeat"):
+    for k in ("refresh", "heartbeat", "phase_b", "phase_a"):
+        if k == dom:
+            continue
         if k in kstats and kstats[k][1]:
             b_k, _ = algorithmic_bytes(k, eng, wl, per_hop)
             ms_k = kstats[k][0] / kstats[k][1]
