@@ -25,7 +25,7 @@ import os
 # minutes); GS_FULL_SCHEDULE=1 sweeps every parity scenario.
 REPRESENTATIVE = ["floodsub_dense", "randomsub_100", "gossipsub_dense", "gossipsub_scored", "gossipsub_multitopic",
                   "adversarial_mix", "spam_ihave", "sinkhole", "churn_scored", "acct_multitopic", "px_scored",
-                  "direct_churn"]
+                  "direct_churn", "mixed_scored"]
 FAST = ([n for n in scenarios.SCENARIOS if n not in scenarios.HEAVY] if os.environ.get("GS_FULL_SCHEDULE")
         else [n for n in REPRESENTATIVE if n in scenarios.SCENARIOS])
 _BASE = {}
@@ -55,7 +55,7 @@ def test_live_scores_equal_hop_start_memo(oracle_path, name):
     a = _run(oracle_path, name, 0)
     b = _run(oracle_path, name, 2)
     bad = scenarios.compare(a, b)
-    if "adversarial" in name:
+    if "adversarial" in name or "gater" in name:
         # the gater's hop-start snapshot vs its live counters: a few percent of
         # the throttled copies, never the mesh
         assert np.array_equal(a["mesh"], b["mesh"])
@@ -73,11 +73,12 @@ def test_reference_order_distance(oracle_path, name):
     ca, cb = a["counters"], b["counters"]
     assert np.array_equal(a["mesh"], b["mesh"]), "meshes differ"
     if not any(k in name for k in ("gossipsub", "churn", "sinkhole", "squatters", "adversarial", "spam_invalid",
-                                  "acct_multitopic", "acct_graylist", "px_", "direct_")):
+                                  "acct_multitopic", "acct_graylist", "px_", "direct_", "mixed_scored",
+                                  "acct_mixed", "mixed_gossip")):
         # floodsub / randomsub carry no control; the spam pairs handle one RPC kind per hop
         assert scenarios.compare(a, b) == []
         return
-    if "adversarial" not in name and name != "spam_invalid":
+    if "adversarial" not in name and "gater" not in name and name != "spam_invalid":
         assert ca["deliveries"] == cb["deliveries"]
         # the race only ever adds IWANTs: a message still unseen when the
         # IHAVE is handled, delivered later in the same hop
