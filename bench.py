@@ -53,6 +53,10 @@ WORKLOADS = {
     # 32-entry queue per hop.  500 msgs/round: the adversarial delivery
     # window keeps 200 hops of messages alive (10240 slots).
     "config5": dict(n=1_000_000, k=32, topics=1, slots=10240, msgs=500, adversarial=True),
+    # SURVEY.md §8(d) config 4's other variant: every peer in topic 0 plus 2
+    # random subnets of the 64 (the Eth2 attestation-subnet shape); the
+    # 1000 msgs/round go round-robin over the 64 topics as in config4
+    "config4sub": dict(n=1_000_000, k=32, topics=64, slots=192, subnets=2),
 }
 
 
@@ -62,6 +66,13 @@ def build_engine(wl, rounds, seed, device, lib=None, n=None, msgs_per_round=None
     msgs_per_round = msgs_per_round or wl.get("msgs", MSGS_PER_ROUND)
     g = graphs.random_regular_fast(n, wl["k"], seed)
     subs = graphs.all_subscribed(n, T)
+    if wl.get("subnets"):
+        # topic 0 + `subnets` distinct random topics of 1..T-1 per peer
+        srng = np.random.default_rng(seed + 13)
+        pick = np.argsort(srng.random((n, T - 1)), axis=1)[:, :wl["subnets"]] + 1
+        subs = np.ones(n, dtype=np.uint64)
+        for j in range(wl["subnets"]):
+            subs |= np.left_shift(np.uint64(1), pick[:, j].astype(np.uint64))
     opts = [WithPeerScore(eth2_peer_score_params(T), eth2_thresholds()), WithHop(100 * Millisecond),
             WithMessageWindow(wl["slots"]), WithSeed(seed)]
     if lib is None or "libgossip_engine" in os.path.basename(lib):
@@ -211,7 +222,7 @@ def cpu_baseline(wl, seconds=20.0):
     lib = os.path.join(REPO, "oracle", "_build", "libgossip_oracle.so")
     if not os.path.exists(lib):
         return None
-    threads = ctypes.CDLL(lib).gs_oracle_threads()
+    threads = ctypes.CDLL(lib).gs_oracle_threads()  # OMP_NUM_THREADS: 16 on the GPU box (its CPU share)
     n = 2000
     swl = dict(wl, n=n)
     rounds = 8
@@ -232,6 +243,8 @@ def cpu_baseline(wl, seconds=20.0):
             "rounds_per_sec_extrapolated_1M": rps * n / wl["n"],
             "extrapolation": f"per-peer linear: rounds/s x {n}/{wl['n']} (labelled estimate, not measured)",
             "cpu_model": cpu_info(), "nproc": os.cpu_count(),
+            "threads_note": "OpenMP threads = OMP_NUM_THREADS, which the GPU box sets to 16 (this job's CPU share "
+                            "of the shared host; nproc shows the whole machine)",
             "sample": f"oracle/ (C++ restatement, OpenMP {threads} threads), {n} peers k={wl['k']}, "
                       f"{wl['topics']} topics, Eth2 scoring, {wl.get('msgs', MSGS_PER_ROUND)} msgs/round"
                       f"{' (config-5 adversarial mix)' if wl.get('adversarial') else ''}, {hops} hops "
@@ -438,6 +451,7 @@ def main():
         "config": {"workload": f"{args.workload}: {wl['n'] / 1e6:g}M peers, {wl['topics']} topic"
                    f"{'s' if wl['topics'] > 1 else ''}, k=32, gossipsub v1.1 + Eth2 scoring, "
                    f"{msgs_round} msgs/round, 10 hops/round" +
+                   (f", each peer in topic 0 + {wl['subnets']} random subnets" if wl.get("subnets") else "") +
                    (", 20% Sybils (IWANT / GRAFT / phantom-IHAVE spam, invalid messages, 20 per IP), "
                     "peer gater, validation queue 32" if wl.get("adversarial") else ""),
                    "peers": wl["n"], "topics": wl["topics"], "degree": wl["k"],

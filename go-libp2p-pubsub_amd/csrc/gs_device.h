@@ -82,7 +82,13 @@ struct TopicP {  // TopicScoreParams (score_params.go:98-148) + scored flag
   double MfpWeight, MfpDecay, ImdWeight, ImdDecay;
   int32_t scored;
   int32_t pad;
+  uint64_t qMagic;  // floor(2^64 / TimeInMeshQuantum) for a quantum >= 2, else 0 (quantum_div)
 };
+
+// meshTime / TimeInMeshQuantum without a 64-bit divide (include/gs_fp.h)
+__device__ __forceinline__ int64_t quantum_div(int64_t mt, const TopicP& tp) {
+  return gs_quantum_div(mt, tp.TimeInMeshQuantum, tp.qMagic);
+}
 
 // RPC byte accounting (gs_set_rpc_accounting): per topic, the sizes of the
 // RPC parts that carry it (include/gs_rpcsize.h)
@@ -529,7 +535,7 @@ __device__ __forceinline__ TermIn term_load(const Dev& d, int64_t i) {
 __device__ __forceinline__ double term_eval(const TopicP& tp, const TermIn& x) {
   double topicScore = 0.0;
   if (x.fl & 1) {
-    double p1 = (double)(x.mt / tp.TimeInMeshQuantum);
+    double p1 = (double)quantum_div(x.mt, tp);
     if (p1 > tp.TimeInMeshCap) p1 = tp.TimeInMeshCap;
     topicScore += p1 * tp.TimeInMeshWeight;
   }

@@ -358,6 +358,8 @@ static TopicP to_dev(const gs_topic_score_params& p, bool scored) {
   t.ImdWeight = p.InvalidMessageDeliveriesWeight;
   t.ImdDecay = p.InvalidMessageDeliveriesDecay;
   t.scored = scored ? 1 : 0;
+  // reciprocal of the quantum for quantum_div: floor(2^64 / q), q >= 2
+  t.qMagic = gs_quantum_magic(t.TimeInMeshQuantum);
   return t;
 }
 

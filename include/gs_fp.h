@@ -52,4 +52,26 @@ GS_HD double gs_add_ones_capped(double x, int64_t n, double cap) {
   return y > cap ? cap : y;
 }
 
+/* floor(2^64 / q) for q >= 2 (else 0): the reciprocal gs_quantum_div uses. */
+GS_HD uint64_t gs_quantum_magic(int64_t q) {
+  return q >= 2 ? (uint64_t)(((unsigned __int128)1 << 64) / (uint64_t)q) : 0;
+}
+/* meshTime / TimeInMeshQuantum (score.go:273: Go int64 division, truncating)
+ * without a 64-bit divide: the high half of mt * magic is floor(mt / q) or one
+ * below it, and the remainder fixes it up.  Negative operands take the plain
+ * division (meshTime is never negative). */
+GS_HD int64_t gs_quantum_div(int64_t mt, int64_t q, uint64_t magic) {
+  if (q == 1) return mt;
+  if (magic == 0 || mt < 0) return mt / q;
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t d = __umul64hi((uint64_t)mt, magic);
+#else
+  uint64_t d = (uint64_t)(((unsigned __int128)(uint64_t)mt * magic) >> 64);
+#endif
+  uint64_t r = (uint64_t)mt - d * (uint64_t)q;
+  if (r >= (uint64_t)q) { ++d; r -= (uint64_t)q; }
+  if (r >= (uint64_t)q) ++d;
+  return (int64_t)d;
+}
+
 #endif /* GS_FP_H */

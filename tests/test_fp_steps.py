@@ -58,3 +58,45 @@ def test_add_ones_equals_serial_steps(tmp_path):
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True, timeout=300).stdout.split()
     cases, bad = int(out[0]), int(out[1])
     assert cases == 400000 and bad == 0
+
+
+QSRC = r"""
+#include <cstdio>
+#include <random>
+#include "gs_fp.h"
+int main() {
+  std::mt19937_64 g(11);
+  long long bad = 0, cases = 0;
+  const long long qs[] = {1, 2, 3, 7, 1000, 1000000000LL, 1000000007LL, 60000000000LL, (1LL << 40) + 3,
+                          (1LL << 62) + 1, 9223372036854775807LL};
+  for (long long q : qs)
+    for (int it = 0; it < 200000; ++it) {
+      long long mt;
+      switch (it % 4) {
+        case 0: mt = (long long)(g() >> 1); break;                 // any int64 >= 0
+        case 1: mt = (long long)(g() % 100000000000000ULL); break; // hours of ns
+        case 2: mt = (long long)(g() % 1000) * q + (long long)(g() % 3) - 1; break;  // around multiples
+        default: mt = (long long)(g() % 4096); break;
+      }
+      if (mt < 0) mt = 0;
+      const long long want = mt / q, got = gs_quantum_div(mt, q, gs_quantum_magic(q));
+      bad += want != got;
+      ++cases;
+    }
+  std::printf("%lld %lld\n", cases, bad);
+  return 0;
+}
+"""
+
+
+def test_quantum_div_equals_integer_division(tmp_path):
+    """gs_quantum_div (the engine's meshTime / TimeInMeshQuantum, score.go:273)
+    equals Go's int64 division on 2.2M cases: quanta from 1 to 2^63 - 1,
+    times anywhere in [0, 2^63) and right around the multiples of q."""
+    src = tmp_path / "q.cpp"
+    src.write_text(QSRC)
+    exe = tmp_path / "q"
+    subprocess.run(["g++", "-O2", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True,
+                   capture_output=True, timeout=120)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True, timeout=300).stdout.split()
+    assert int(out[0]) == 11 * 200000 and int(out[1]) == 0
