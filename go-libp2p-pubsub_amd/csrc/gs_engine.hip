@@ -867,10 +867,6 @@ int gs_engine::start() {
       for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e)
         if (up(e)) hostRpc(GS_TRACE_RECV_RPC, u, col[e], 0, GS_RPC_ORD(0, GS_RPC_O_HELLO), -1, sub[col[e]], 1);
     }
-    if (traceRpc && world > 1) {
-      gs_set_error("RPC trace events need an unpartitioned engine");
-      return GS_EUNSUPPORTED;
-    }
   }
   if (world > 1) {
     x.xmark = dalloc<uint8_t>(E); chk(x.xmark);

@@ -530,7 +530,10 @@ typedef struct gs_trace_event {
 int gs_set_trace(gs_engine* eng, const uint8_t* node_mask, int64_t capacity);
 /* Before the first step: also record the RPC events of the traced hosts
  * (every RPC they send or receive, with its traceRPCMeta items).  The
- * product library records them on an unpartitioned engine only. */
+ * product library records an RPC where it is sent: on a partitioned engine a
+ * rank returns its own traced hosts' events plus the RECV_RPC blocks of the
+ * RPCs its hosts sent to other ranks' traced hosts, so the union of every
+ * rank's stream is the unpartitioned stream (each rank's in canonical order). */
 int gs_set_trace_rpc(gs_engine* eng, int32_t on);
 /* Moves up to `cap` recorded events, in canonical order, into out; *n = the
  * number written.  Call until *n < cap to drain. */

@@ -205,3 +205,66 @@ def test_partitioned_randomsub_is_refused():
     with pytest.raises(GossipEngineError) as ei:
         e.step(1)
     assert ei.value.code == _abi.GS_EUNSUPPORTED
+
+
+def _rpc_worker(rank, world, port, name, q):
+    """RPC trace events on a partitioned engine: this rank's stream."""
+    try:
+        sys.path.insert(0, HERE)
+        sys.path.insert(0, os.path.join(os.path.dirname(HERE), "go-libp2p-pubsub_amd"))
+        import torch
+        import torch.distributed as dist
+
+        import scenarios
+        from pubsub_amd import PRODUCT_LIB, WithEventTracer, WithPartition
+        from pubsub_amd.transport import TorchTransport
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        tr = TorchTransport(memory="device")
+        e, hops = scenarios.SCENARIOS[name](PRODUCT_LIB, (WithPartition(rank, world, tr),
+                                                          WithEventTracer(TRACED, rpc=True)))
+        e.step(hops)
+        q.put((rank, e.trace_events().tobytes(), e.node_range))
+        dist.destroy_process_group()
+    except Exception as ex:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, None, f"worker raised: {ex!r}\n{traceback.format_exc()}"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,name", [(2, "gossipsub_scored"), (3, "churn_scored"), (2, "adversarial_mix")])
+def test_partitioned_rpc_trace_union_equals_oracle(world, name, oracle_path):
+    """gs_set_trace_rpc on a partitioned engine: each rank records the RPCs its
+    hosts send (SEND_RPC of its traced hosts, RECV_RPC of any traced receiver)
+    and its hosts' own events; the union of the ranks' streams is the oracle's
+    stream event for event (compared as multisets: one canonical order per
+    rank), and every non-RPC event sits on the rank owning its host."""
+    import numpy as np
+
+    import scenarios
+    from pubsub_amd import WithEventTracer, _abi
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rpc_worker, args=(r, world, port, name, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted((q.get(timeout=240) for _ in range(world)), key=lambda r: r[0])
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    assert all(r[1] is not None for r in res), [r[2] for r in res]
+    eo, hops = scenarios.SCENARIOS[name](oracle_path, (WithEventTracer(TRACED, rpc=True),))
+    eo.step(hops)
+    want = eo.trace_events()
+    streams = [np.frombuffer(r[1], dtype=_abi.TRACE_EVENT_DTYPE) for r in res]
+    for (rank, _, (n0, n1)), ev in zip(res, streams):
+        plain = ev[(ev["type"] != _abi.TRACE_TYPES.index("RECV_RPC")) & (ev["type"] != 32)]
+        assert ((plain["node"] >= n0) & (plain["node"] < n1)).all(), rank
+    got = np.concatenate(streams)
+    assert (got["type"] == _abi.TRACE_TYPES.index("RECV_RPC")).any() and len(got) == len(want)
+    key = lambda a: np.sort(a.view(np.dtype((np.void, a.dtype.itemsize))))  # noqa: E731
+    assert np.array_equal(key(got), key(want))
