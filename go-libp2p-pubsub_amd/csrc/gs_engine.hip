@@ -442,16 +442,12 @@ int gs_engine::start() {
     anyRandom = false;
     for (uint8_t r : routerH) anyRandom = anyRandom || r == GS_ROUTER_RANDOMSUB;
   }
-  if (doPX && (behaveAll != 0 || world > 1 || acctOn)) {
-    gs_set_error("peer exchange is supported by an honest, unpartitioned engine without RPC accounting");
+  if (doPX && (behaveAll != 0 || acctOn)) {
+    gs_set_error("peer exchange is supported by an honest engine without RPC accounting");
     return GS_EUNSUPPORTED;
   }
   if (doPX && N >= (1 << 26)) {  // a PX arena entry is topic << 26 | peer (gs_kernels_ctl.h px_append)
     gs_set_error("peer exchange supports fewer than 2^26 peers in this build");
-    return GS_EUNSUPPORTED;
-  }
-  if (!dormant.empty() && world > 1) {
-    gs_set_error("dormant connections are supported by an unpartitioned engine");
     return GS_EUNSUPPORTED;
   }
   HIPCHECK(hipSetDevice(cfg.device));
@@ -1613,8 +1609,11 @@ int gs_engine::exchange(int cur, bool hb) {
   HIPCHECK(hipStreamSynchronize(stream));  // sendOff is pageable; the transport reads the buffers
   // 3. sizes of every rank: [bcast bytes, list entries, arena ids, gw rows?,
   //    records to rank 0..world-1, device error word]
-  const int nS = 5 + world;
+  // the connector's dials of this hop (peer exchange): every rank applies all
+  // of them at the next hop's start (each launching the sides it owns)
+  const int nS = 6 + world;
   std::vector<int64_t> mine(nS), all((size_t)nS * world);
+  mine[5 + world] = (int64_t)pxPend.size();
   mine[0] = (int64_t)bcast; mine[1] = nEnt; mine[2] = nPool; mine[3] = hb ? 1 : 0;
   for (int r = 0; r < world; ++r) mine[4 + r] = sendRec[r];
   mine[4 + world] = myErr;
@@ -1645,6 +1644,22 @@ int gs_engine::exchange(int cur, bool hb) {
   if (tr.allgather(tr.user, xSend, xRecv, chunk) != 0) {
     gs_set_error("transport allgather failed");
     return GS_EDEVICE;
+  }
+  {
+    int64_t maxD = 0;
+    for (int r = 0; r < world; ++r) maxD = std::max<int64_t>(maxD, all[(size_t)r * nS + 5 + world]);
+    if (maxD > 0) {
+      std::vector<int64_t> dm((size_t)maxD, -1), da((size_t)maxD * world);
+      for (size_t i = 0; i < pxPend.size(); ++i)
+        dm[i] = ((int64_t)pxPend[i].first << 32) | (int64_t)(uint32_t)pxPend[i].second;
+      if (tr.allgather_i64(tr.user, dm.data(), (int32_t)maxD, da.data()) != 0) {
+        gs_set_error("transport allgather_i64 failed (dials)");
+        return GS_EDEVICE;
+      }
+      pxPend.clear();
+      for (int64_t x : da)
+        if (x >= 0) pxPend.push_back({(int)(x >> 32), (int)(uint32_t)x});
+    }
   }
   std::vector<int64_t> sendB(world), recvB(world);
   int64_t totIn = 0;

@@ -35,7 +35,7 @@ struct XRec {  // 96 bytes
   uint64_t relay, pub, gj, ghb, prep, phb, ihave;
   int64_t iwant, iresp;
   int64_t spam;  // an IWANT spammer's re-request list (arena record), -1 = none
-  int64_t pad2;
+  int64_t px;    // the PRUNEs' peer-exchange lists (arena record), -1 = none
 };
 static_assert(sizeof(XRec) == 96, "XRec layout");
 
@@ -80,6 +80,8 @@ __global__ void k_x_pack(Dev d, int cur, const int64_t* __restrict__ off, unsign
     x.iresp = d.cIresp[cur][ri];
     x.spam = d.cSpam[cur] != nullptr ? d.cSpam[cur][ri] : -1;
     x.nsrv = d.cNSrv[cur] != nullptr ? d.cNSrv[cur][ri] : 0;
+    x.px = d.doPX ? d.cPx[cur][ri] : -1;
+    if (d.doPX) d.cPx[cur][ri] = -1;
     if (d.cSpam[cur] != nullptr) {
       d.cSpam[cur][ri] = -1;
       d.cNSrv[cur][ri] = 0;
@@ -95,10 +97,9 @@ __global__ void k_x_pack(Dev d, int cur, const int64_t* __restrict__ off, unsign
     d.cIresp[cur][ri] = -1;
   } else {
     x.gj = x.ghb = x.prep = x.phb = x.ihave = 0;
-    x.iwant = x.iresp = x.spam = -1;
+    x.iwant = x.iresp = x.spam = x.px = -1;
     x.nsrv = 0;
   }
-  x.pad2 = 0;
   d.xmark[e] = 0;
   out[k] = x;
 }
@@ -125,6 +126,7 @@ __global__ void k_x_unpack(Dev d, int cur, const XRec* __restrict__ in, int64_t 
     d.cSpam[cur][ri] = x.spam;
     d.cNSrv[cur][ri] = x.nsrv;
   }
+  if (d.doPX) d.cPx[cur][ri] = x.px;
 }
 
 // Frontier lists of the owned nodes: one wave per node, entries appended at a

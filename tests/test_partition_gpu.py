@@ -122,6 +122,12 @@ def run_partitioned(world, name, oracle):
     (2, "mixed_gossip_flood"),
     # the peer gater's AddPeer / RemovePeer / RetainStats under churn
     (2, "churn_gater"),
+    # peer exchange and the direct-peer connector: PX lists travel in the edge
+    # records and arena, dials are gathered from every rank
+    (2, "px_scored"),
+    (3, "px_star"),
+    (2, "direct_churn"),
+    (2, "px_gater"),
 ])
 def test_partitioned_engine_matches_oracle(world, name, oracle_path):
     res = run_partitioned(world, name, oracle_path)
