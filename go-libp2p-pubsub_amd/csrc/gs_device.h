@@ -53,7 +53,6 @@
 #endif
 #define GS_QCAP 320    // phase A delivery queue (>= 63 pending + 256 appended per sub-round)
 #define GS_BMAP 32     // phase A: list blocks mapped to senders without a search (64 per entry)
-#define GS_TABLE 64    // promise table entries per node (one per lane)
 #define GS_PTX 512     // IWANT-retransmission (mcache peertx) entries per node
 #define GS_CUTS 64     // IHAVE entries above MaxIHaveLength one node can cut per hop
 // phase B dynamic LDS: the MaxIHaveLength-cut tables (cut mode), then the big
@@ -210,7 +209,8 @@ struct Dev {
   int64_t* lastpub;        // [N][T], INT64_MIN = none
   uint64_t* fanoutPresent; // [N]
   int32_t nOwnH;      // owned nodes n1 - n0: the mcache ring is [R][nOwnH][W] (v - n0)
-  int64_t* promMid;  // [N][64] (owned rows only: the pointer is shifted by n0 rows)
+  int32_t promCap;   // promise-table entries per node: a multiple of 64 (banks of one wave)
+  int64_t* promMid;  // [N][promCap] (owned rows only: the pointer is shifted by n0 rows)
   int64_t* promExp;
   int32_t* promSlot;
   uint8_t* promEdge;

@@ -672,7 +672,20 @@ int gs_engine::start() {
   }
   x.lastpub = dalloc<int64_t>((size_t)N * T); chk(x.lastpub);
   x.fanoutPresent = dalloc<uint64_t>(N); chk(x.fanoutPresent);
-  const size_t NQ = (size_t)nOwnN * GS_TABLE;
+  // gossipTracer promises (gossip_tracer.go:48-77): at most one per IWANT,
+  // i.e. per peer per heartbeat (the IHAVE rides the heartbeat RPC); a
+  // promise lives until its message arrives or the first heartbeat after its
+  // expiry (applyIwantPenalties), so a node holds at most
+  // degree x (ceil(IWantFollowupTime / HeartbeatInterval) + 2) of them.  The
+  // table is sized to that bound (banks of 64, at most 8); beyond it E_PROMISES.
+  {
+    int64_t live = 1;
+    if (cfg.router == GS_ROUTER_GOSSIPSUB && gp.HeartbeatInterval > 0)
+      live = (gp.IWantFollowupTime + gp.HeartbeatInterval - 1) / gp.HeartbeatInterval + 2;
+    const int64_t bound = std::max<int64_t>(1, (int64_t)maxdeg * live);
+    x.promCap = (int32_t)(64 * std::min<int64_t>(8, (bound + 63) / 64));
+  }
+  const size_t NQ = (size_t)nOwnN * x.promCap;
   x.promMid = dalloc<int64_t>(NQ); x.promExp = dalloc<int64_t>(NQ); x.promSlot = dalloc<int32_t>(NQ);
   x.promEdge = dalloc<uint8_t>(NQ); x.promN = dalloc<int32_t>(nOwnN);
   // mcache.peertx: 512 entries per node.  With IWANT spammers present the
@@ -685,8 +698,8 @@ int gs_engine::start() {
   chk(x.promMid); chk(x.promExp); chk(x.promSlot); chk(x.promEdge); chk(x.promN);
   chk(x.ptx); chk(x.ptxN);
   if (!ok) { gs_set_error("device allocation failed (promises / peertx)"); return GS_ENOMEM; }
-  x.promMid -= (size_t)n0 * GS_TABLE; x.promExp -= (size_t)n0 * GS_TABLE;
-  x.promSlot -= (size_t)n0 * GS_TABLE; x.promEdge -= (size_t)n0 * GS_TABLE; x.promN -= n0;
+  x.promMid -= (size_t)n0 * x.promCap; x.promExp -= (size_t)n0 * x.promCap;
+  x.promSlot -= (size_t)n0 * x.promCap; x.promEdge -= (size_t)n0 * x.promCap; x.promN -= n0;
   x.ptx -= (size_t)n0 * x.ptxCap; x.ptxN -= n0;
   x.mesh = dalloc<uint64_t>(E); x.fanout = dalloc<uint64_t>(E);
   chk(x.mesh); chk(x.fanout);
@@ -1491,7 +1504,10 @@ int gs_engine::deviceErrorCode(int32_t err) {
   switch (err) {
     case E_NONE: return GS_OK;
     case E_POOL: gs_set_error("IWANT payload arena overflow (4 ids per edge per hop)"); return GS_ECAPACITY;
-    case E_PROMISES: gs_set_error("per-node promise table overflow (64 entries)"); return GS_ECAPACITY;
+    case E_PROMISES:
+      gs_set_error("per-node promise table overflow (degree x (IWantFollowupTime / HeartbeatInterval + 2) entries, "
+                   "at most 512)");
+      return GS_ECAPACITY;
     case E_PEERTX:
       gs_set_error("per-node IWANT retransmission table overflow (512 entries; 4096 with IWANT spammers)");
       return GS_ECAPACITY;

@@ -1194,30 +1194,34 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
       // loses its own (gossip_tracer.go:119-126, 163-181); lane = table entry
       const int n = d.promN[v];
       if (n > 0) {
-        const int64_t ti = (int64_t)v * GS_TABLE + lane;
-        int64_t pm = -1, pe = 0;
-        int ps = 0, pg = 0;
-        bool live = lane < n;
-        if (live) {
-          pm = d.promMid[ti];
-          pe = d.promExp[ti];
-          ps = d.promSlot[ti];
-          pg = d.promEdge[ti];
-          if ((throttled >> pg) & 1) live = false;
-          const int rk = sRk[ps >> 6];
-          if (anyDrop && rk != 0xFFFF && ((sDrop[rk] >> (ps & 63)) & 1)) live = false;
+        int kept = 0;  // the table in banks of 64 (lane = entry), compacted in place
+        for (int b0 = 0; b0 < n; b0 += 64) {
+          const int64_t ti = (int64_t)v * d.promCap + b0 + lane;
+          int64_t pm = -1, pe = 0;
+          int ps = 0, pg = 0;
+          bool live = b0 + lane < n;
+          if (live) {
+            pm = d.promMid[ti];
+            pe = d.promExp[ti];
+            ps = d.promSlot[ti];
+            pg = d.promEdge[ti];
+            if ((throttled >> pg) & 1) live = false;
+            const int rk = sRk[ps >> 6];
+            if (anyDrop && rk != 0xFFFF && ((sDrop[rk] >> (ps & 63)) & 1)) live = false;
+          }
+          const unsigned long long lm = __ballot(live);
+          const int pos = kept + __popcll(lm & ((1ull << lane) - 1));
+          __syncthreads();
+          if (live) {  // pos <= b0 + lane: never past an entry not yet read
+            const int64_t to = (int64_t)v * d.promCap + pos;
+            d.promMid[to] = pm;
+            d.promExp[to] = pe;
+            d.promSlot[to] = ps;
+            d.promEdge[to] = (uint8_t)pg;
+          }
+          kept += __popcll(lm);
         }
-        const unsigned long long lm = __ballot(live);
-        const int pos = __popcll(lm & ((1ull << lane) - 1));
-        __syncthreads();
-        if (live) {
-          const int64_t to = (int64_t)v * GS_TABLE + pos;
-          d.promMid[to] = pm;
-          d.promExp[to] = pe;
-          d.promSlot[to] = ps;
-          d.promEdge[to] = (uint8_t)pg;
-        }
-        if (lane == 0) d.promN[v] = __popcll(lm);
+        if (lane == 0) d.promN[v] = kept;
       }
     }
     if (scoring) sRelay[lane] = valid ? d.mesh[base + lane] : 0ull;

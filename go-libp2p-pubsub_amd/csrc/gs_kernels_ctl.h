@@ -988,38 +988,56 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
   if (d.scoring) {
     const unsigned long long pm = __ballot(iwantAny);
     if (pm) {
-      int promN = d.promN[v];
-      int64_t pMid = lane < promN ? d.promMid[(int64_t)v * GS_TABLE + lane] : -1;
-      int64_t pExp = lane < promN ? d.promExp[(int64_t)v * GS_TABLE + lane] : 0;
-      int32_t pSlot = lane < promN ? d.promSlot[(int64_t)v * GS_TABLE + lane] : 0;
-      int pEdge = lane < promN ? d.promEdge[(int64_t)v * GS_TABLE + lane] : 0;
+      // the table's first bank of 64 in registers (lane = entry); entries past
+      // it (promCap > 64: a node with many peers, each promise alive up to
+      // IWantFollowupTime plus a heartbeat) read and appended in memory.  A
+      // sender appears once below, so only the entries present before this
+      // call can repeat (mid, peer) (AddPromise keeps the first expiry, :66-71).
+      const int n0p = d.promN[v];
+      int promN = n0p;
+      const int64_t row = (int64_t)v * d.promCap;
+      int64_t pMid = lane < promN ? d.promMid[row + lane] : -1;
+      int64_t pExp = lane < promN ? d.promExp[row + lane] : 0;
+      int32_t pSlot = lane < promN ? d.promSlot[row + lane] : 0;
+      int pEdge = lane < promN ? d.promEdge[row + lane] : 0;
       unsigned long long m = pm;
       while (m) {
         const int i = __ffsll((long long)m) - 1;
         m &= m - 1;
         const int64_t bm = sMid[i];
         const int bs = sSlot[i];
-        const unsigned long long ex = __ballot(lane < promN && pMid == bm && pEdge == i);
+        unsigned long long ex = __ballot(lane < promN && pMid == bm && pEdge == i);
+        for (int b0 = 64; !ex && b0 < n0p; b0 += 64) {
+          const bool in = b0 + lane < n0p;
+          ex = __ballot(in && d.promMid[row + b0 + lane] == bm && d.promEdge[row + b0 + lane] == i);
+        }
         if (ex) continue;
-        if (promN >= GS_TABLE) {
+        if (promN >= d.promCap) {
           if (lane == 0) set_err(d, E_PROMISES);
           continue;
         }
-        if (lane == promN) {
-          pMid = bm;
-          pSlot = bs;
-          pEdge = i;
-          pExp = now + d.IWantFollowupTime;
+        if (promN < 64) {
+          if (lane == promN) {
+            pMid = bm;
+            pSlot = bs;
+            pEdge = i;
+            pExp = now + d.IWantFollowupTime;
+          }
+        } else if (lane == 0) {
+          d.promMid[row + promN] = bm;
+          d.promExp[row + promN] = now + d.IWantFollowupTime;
+          d.promSlot[row + promN] = bs;
+          d.promEdge[row + promN] = (uint8_t)i;
         }
         promN++;
       }
-      if (lane < promN && lane < GS_TABLE) {
-        d.promMid[(int64_t)v * GS_TABLE + lane] = pMid;
-        d.promExp[(int64_t)v * GS_TABLE + lane] = pExp;
-        d.promSlot[(int64_t)v * GS_TABLE + lane] = pSlot;
-        d.promEdge[(int64_t)v * GS_TABLE + lane] = (uint8_t)pEdge;
+      if (lane < promN && lane < 64) {
+        d.promMid[row + lane] = pMid;
+        d.promExp[row + lane] = pExp;
+        d.promSlot[row + lane] = pSlot;
+        d.promEdge[row + lane] = (uint8_t)pEdge;
       }
-      if (lane == 0) d.promN[v] = promN < GS_TABLE ? promN : GS_TABLE;
+      if (lane == 0) d.promN[v] = promN;
     }
   }
 
@@ -1156,46 +1174,48 @@ __global__ __launch_bounds__(64) void k_hb_pre(Dev d, int64_t now, uint64_t tick
   if (!d.scoring) return;
   const int n = d.promN[v];
   if (n == 0) return;
-  const int64_t ti = (int64_t)v * GS_TABLE + lane;
-  int64_t mid = -1, exp = 0;
-  int slot = 0, edge = 0;
-  if (lane < n) {
-    mid = d.promMid[ti];
-    exp = d.promExp[ti];
-    slot = d.promSlot[ti];
-    edge = d.promEdge[ti];
-  }
-  bool live = lane < n, broken = false;
-  if (live) {
-    const bool seen = (d.seen[(int64_t)v * d.W + (slot >> 6)] >> (slot & 63)) & 1;
-    if (seen) live = false;
-    else if (exp < now) { live = false; broken = true; }
-  }
-  // per-peer broken counts -> AddPenalty(p, count) once per peer
-  unsigned long long bm = __ballot(broken);
-  int total = __popcll(bm);
-  while (bm) {
-    const int q = __ffsll((long long)bm) - 1;
-    const int pe = lane_get(edge, q);
-    const unsigned long long same = __ballot(broken && edge == pe);
-    bm &= ~same;
-    if (lane == 0 && has_record(d, base + pe)) {  // AddPenalty needs a record (score.go:681-684)
-      d.bp[base + pe] += (double)__popcll(same);
-      d.sdirty[base + pe] = 1;
+  // the table in banks of 64 (lane = entry): broken promises counted per peer
+  // over every bank, then one AddPenalty(p, count) per peer (GetBrokenPromises
+  // returns a count per peer, gossipsub.go:1566-1571); live entries compacted
+  __shared__ int sBroken[64];
+  sBroken[lane] = 0;
+  __syncthreads();
+  int kept = 0, total = 0;
+  for (int b0 = 0; b0 < n; b0 += 64) {
+    const int64_t ti = (int64_t)v * d.promCap + b0 + lane;
+    int64_t mid = -1, exp = 0;
+    int slot = 0, edge = 0;
+    bool live = b0 + lane < n, broken = false;
+    if (live) {
+      mid = d.promMid[ti];
+      exp = d.promExp[ti];
+      slot = d.promSlot[ti];
+      edge = d.promEdge[ti];
+      const bool seen = (d.seen[(int64_t)v * d.W + (slot >> 6)] >> (slot & 63)) & 1;
+      if (seen) live = false;
+      else if (exp < now) { live = false; broken = true; }
     }
+    if (broken) atomicAdd(&sBroken[edge], 1);
+    total += __popcll(__ballot(broken));
+    const unsigned long long lm = __ballot(live);
+    const int pos = kept + __popcll(lm & ((1ull << lane) - 1));
+    if (live) {  // pos <= b0 + lane: never past an entry not yet read
+      const int64_t to = (int64_t)v * d.promCap + pos;
+      d.promMid[to] = mid;
+      d.promExp[to] = exp;
+      d.promSlot[to] = slot;
+      d.promEdge[to] = (uint8_t)edge;
+    }
+    kept += __popcll(lm);
   }
-  // compact the surviving entries
-  const unsigned long long lm = __ballot(live);
-  const int pos = __popcll(lm & ((1ull << lane) - 1));
-  if (live) {
-    const int64_t to = (int64_t)v * GS_TABLE + pos;
-    d.promMid[to] = mid;
-    d.promExp[to] = exp;
-    d.promSlot[to] = slot;
-    d.promEdge[to] = (uint8_t)edge;
+  __syncthreads();
+  const int nb = sBroken[lane];
+  if (nb && has_record(d, base + lane)) {  // AddPenalty needs a record (score.go:681-684)
+    d.bp[base + lane] += (double)nb;
+    d.sdirty[base + lane] = 1;
   }
   if (lane == 0) {
-    d.promN[v] = __popcll(lm);
+    d.promN[v] = kept;
     if (total) ctr_add(d, C_PROMISES_BROKEN, (unsigned long long)total);
   }
 }
