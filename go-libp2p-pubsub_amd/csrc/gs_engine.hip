@@ -1431,20 +1431,21 @@ int gs_engine::stepOne() {
   if (heartbeatDue(now)) {
     ticks++;
     if (!directPairs.empty() && ticks % gp.DirectConnectTicks == 0) directConnect();  // gossipsub.go:1318
-    if (nOwn) TIMED(this, GS_K_HB_PRE, (k_hb_pre<<<nOwn, 64, 0, stream>>>(d, now, ticks)));
     // right after a refresh S0 holds exact scores: recompute only what hb_pre
     // dirtied; opportunistic grafting (every OGT ticks) ranks every mesh
     // score, so it gets the full exact pass; otherwise the threshold-exact
-    // memo pass (k_score_rows<4>)
+    // memo pass (k_score_rows<4>), with the Dhi ranking's mesh members marked
+    // by hb_pre so it computes their exact scores too
+    const bool exactPass = scoring && (refreshedHop == h || ticks % (uint64_t)d.OGT == 0);
+    if (nOwn)
+      TIMED(this, GS_K_HB_PRE, (k_hb_pre<<<nOwn, 64, 0, stream>>>(d, now, ticks, scoring && !exactPass ? 1 : 0)));
     int allExact = 1;
     if (scoring && refreshedHop == h)
       TIMED(this, GS_K_SCORE, (score_rows<3>(d, eOwn, T, nullptr, stream)));
     else if (scoring && ticks % (uint64_t)d.OGT == 0)
       TIMED(this, GS_K_SCORE, (score_rows<0>(d, eOwn, T, d.score1, stream)));
-    else if (scoring) {
+    else if (scoring)
       TIMED(this, GS_K_SCORE, (score_rows<4>(d, eOwn, T, nullptr, stream)));
-      allExact = 0;
-    }
     const int newhead = (head + R - 1) % R;
     // nodes of degree <= 32: two topics per wave (one per half-wave)
     if (nOwn && d.maxDeg <= 32)

@@ -1147,7 +1147,13 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
 // applyIwantPenalties (:1566-1571 -> gossip_tracer.go:79-115, score.go:382).
 // A promise is fulfilled iff its message has been delivered since (it was
 // unseen when promised), so "fulfilled" == "seen now".
-__global__ __launch_bounds__(64) void k_hb_pre(Dev d, int64_t now, uint64_t ticks) {
+// flagDhi: the heartbeat's memo pass (k_score_rows<4>) is exact only where
+// a score-lowering change happened or S0 < 0, but the Dhi ranking compares the
+// mesh members of an over-full topic by value: those members get sdirty here,
+// so the memo pass computes their exact heartbeat-start scores in its
+// streaming form (every lane busy, a batch of records in flight) instead of the
+// heartbeat wave fetching each 64-topic record on its own.
+__global__ __launch_bounds__(64) void k_hb_pre(Dev d, int64_t now, uint64_t ticks, int flagDhi) {
   const int v = d.n0 + blockIdx.x;
   const int lane = lane_id();
   const int64_t base = d.rowptr[v];
@@ -1157,6 +1163,17 @@ __global__ __launch_bounds__(64) void k_hb_pre(Dev d, int64_t now, uint64_t tick
   if (valid) {
     d.peerhave[e] = 0;
     d.iasked[e] = 0;
+  }
+  if (flagDhi && gossip_host(d, v)) {
+    const uint64_t joined = d.sub[v];
+    const uint64_t meshl = valid ? d.mesh[e] & joined : 0ull;
+    bool needX = false;
+    for (uint64_t jm = joined; jm; jm &= jm - 1) {
+      const int t = __ffsll((long long)jm) - 1;
+      const bool mt = (meshl >> t) & 1;
+      if (__popcll(__ballot(mt)) > d.Dhi) needX |= mt;
+    }
+    if (needX) d.sdirty[e] = 1;
   }
   if (ticks % 15 == 0) {  // v's in-edges own the contiguous pairs [base*T, (base+deg)*T)
     for (int j = 0; j < deg; ++j) {  // one edge's topics per step (lane = topic), its mask rebuilt
