@@ -156,6 +156,16 @@ __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t no
   const int tl = lane < T ? lane : 0;
   const uint64_t scoredT = __ballot(lane < T && d.tp[tl].scored);
   const int tLane = LANE_T ? (lane & (T - 1)) : 0;
+  // the score tail's per-edge inputs (P5 app score through col, P6, P7) of the
+  // lane's edge, loaded with the first batch instead of after the topic sums
+  // (one edge per lane when the wave covers at most 64 edges)
+  double tApp = 0.0, tP6 = 0.0, tBp = 0.0;
+  if (epw <= 64 && lane < ng) {
+    const int64_t e = e0 + lane;
+    tApp = d.app[d.col[e]];
+    tP6 = d.p6[e];
+    tBp = d.bp[e];
+  }
   for (int k0 = 0; 64 * k0 < np; k0 += GS_RB) {
     uint32_t q[GS_RB];
     double fmd[GS_RB], mmd[GS_RB], mfp[GS_RB], imd[GS_RB];
@@ -243,7 +253,8 @@ __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t no
       frozen = st != 1;
       dropped = st == 2 && now > d.rexpire[e];
     }
-    double b = d.bp[e];
+    const bool pre = epw <= 64;  // tail inputs already in registers (lane j == edge j)
+    double b = pre ? tBp : d.bp[e];
     if (dropped) {
       b = 0;
       d.bp[e] = 0;
@@ -257,7 +268,8 @@ __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t no
     if (d.scoring && !dropped && (!CHURN || has_record(d, e))) {
       for (int t = 0; t < T; ++t)
         if ((scoredT >> t) & 1) score += sT[rp_pad(j * T + t)];
-      score = score_tail(d, e, score);
+      // score_tail with the refreshed P7 (d.bp[e] == b after the store above)
+      score = pre ? score_tail_v(d, score, tApp, tP6, b) : score_tail(d, e, score);
     }
     d.score0[e] = score;
     d.sdirty[e] = 0;
