@@ -39,7 +39,8 @@ def check_invariants(e, ev, nodes):
     types = set(ev["type"].tolist())
     want = {T("ADD_PEER"), T("JOIN"), T("PUBLISH_MESSAGE"), T("DELIVER_MESSAGE"), T("DUPLICATE_MESSAGE")}
     if e.router == _abi.GS_ROUTER_GOSSIPSUB:
-        want |= {T("GRAFT"), T("PRUNE")}
+        # a mixed network's few traced gossipsub hosts may never prune
+        want |= {T("GRAFT")} if getattr(e, "routers", None) is not None else {T("GRAFT"), T("PRUNE")}
     assert want <= types, f"missing event types {want - types}"
     deg = np.diff(e.rowptr)
     mesh = e.mesh()
@@ -71,7 +72,7 @@ def check_invariants(e, ev, nodes):
 
 
 @pytest.mark.parametrize("name", ["gossipsub_scored", "gossipsub_multitopic", "floodsub_dense",
-                                  "gossipsub_dense_dhi"])
+                                  "gossipsub_dense_dhi", "acct_mixed"])
 def test_oracle_trace_invariants(oracle_path, name):
     nodes = [u for u in TRACED if u < 20] if name == "floodsub_dense" else [u for u in TRACED if u < 120]
     e, ev = traced_run(oracle_path, name, nodes)
@@ -213,7 +214,7 @@ def test_encode_round_trip_sizes(oracle_path):
 # ---------------------------------------------------------------- GPU parity
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["gossipsub_scored", "gossipsub_multitopic", "floodsub_dense",
-                                  "gossipsub_dense_dhi", "gossipsub_negative_app", "gossipsub_flood_publish", "mixed_scored"])
+                                  "gossipsub_dense_dhi", "gossipsub_negative_app", "gossipsub_flood_publish", "acct_mixed"])
 def test_gpu_trace_equals_oracle(oracle_path, name):
     nodes = [u for u in TRACED if u < 20] if name == "floodsub_dense" else [u for u in TRACED if u < 120]
     _, ref = traced_run(oracle_path, name, nodes)
