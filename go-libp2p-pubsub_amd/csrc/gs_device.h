@@ -53,10 +53,9 @@
 #endif
 #define GS_QCAP 320    // phase A delivery queue (>= 63 pending + 256 appended per sub-round)
 #define GS_BMAP 32     // phase A: list blocks mapped to senders without a search (64 per entry)
-#define GS_PTX 512     // IWANT-retransmission (mcache peertx) entries per node
+#define GS_PTX_BITS 10 // mcache.peertx hash slots per node: 2^10 (2^13 when IWANT spammers run)
 #define GS_CUTS 64     // IHAVE entries above MaxIHaveLength one node can cut per hop
-// phase B dynamic LDS: the MaxIHaveLength-cut tables (cut mode), then the big
-// peertx hash (IWANT-spam runs)
+// phase B dynamic LDS: the MaxIHaveLength-cut tables (cut mode)
 #define GS_CUTLDS (256 * 4 + GS_CUTS * 4 + GS_CUTS * 16 + 64 * 16 + 128 * 4 + 16)
 
 // device counter slots (same order as gs_counters)
@@ -215,10 +214,11 @@ struct Dev {
   int32_t* promSlot;
   uint8_t* promEdge;
   int32_t* promN;
-  uint64_t* ptx;     // [N][ptxCap] packed (slot << 32 | edge << 8 | count)
-  int32_t ptxCap;    // entries per node: GS_PTX, more when IWANT spammers run
-  int32_t ptxHBits;  // log2 of the dynamic LDS hash of a larger table
-  int32_t* ptxN;
+  // mcache.peertx per node: an open-addressing hash in HBM, 2^ptxBits 32-bit
+  // entries slot << 14 | in-edge << 8 | count (0 = empty), linear probing
+  uint32_t* ptxT;    // [N][2^ptxBits] (owned rows only: shifted by n0 rows)
+  int32_t ptxBits;
+  int32_t* ptxN;     // [N] entries in the table
   // per-edge state
   uint64_t* mesh;
   uint64_t* fanout;
@@ -316,21 +316,21 @@ __device__ __forceinline__ bool edge_up(const Dev& d, int64_t e) { return d.aliv
 // nibble per (in-edge, slot) in HBM instead of the node's LDS hash, which would
 // need an entry per (message, spammer).  A count only matters while its
 // message is cached (GetForPeer), so it is cleared when the slot is recycled
-// (k_retire) rather than at mcache.Shift.  Saturates at 15: handleIWant only
-// compares it with GossipRetransmission, which the host requires to be < 15.
+// (k_retire) rather than at mcache.Shift.  handleIWant only compares the count
+// with GossipRetransmission (GR), so a nibble is held at GR + 1: one atomic add
+// per request returns the count, and an add past GR + 1 is taken back (the
+// nibble peaks at GR + 2 < 16, so no carry reaches a neighbour; one request
+// list names a slot once and a spammer's two lists are counted one after the
+// other, so no two adds race on one nibble).  The host requires GR < 14.
 __device__ __forceinline__ uint32_t* spam_word(const Dev& d, int row, int slot) {
   return d.spamCnt + (int64_t)row * (d.S >> 3) + (slot >> 3);
 }
 __device__ __forceinline__ int spam_incr(const Dev& d, int row, int slot) {
   uint32_t* w = spam_word(d, row, slot);
   const int sh = (slot & 7) * 4;
-  uint32_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), assumed;
-  do {
-    assumed = old;
-    if (((assumed >> sh) & 0xF) == 0xF) return 0xF;
-    old = atomicCAS(w, assumed, assumed + (1u << sh));
-  } while (old != assumed);
-  return (int)((assumed >> sh) & 0xF) + 1;
+  const int c = (int)((atomicAdd(w, 1u << sh) >> sh) & 0xF) + 1;
+  if (c > d.GR + 1) atomicSub(w, 1u << sh);
+  return c;
 }
 __device__ __forceinline__ int spam_count(const Dev& d, int row, int slot) {
   const uint32_t x = __hip_atomic_load(spam_word(d, row, slot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

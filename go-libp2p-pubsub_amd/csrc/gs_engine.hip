@@ -688,19 +688,22 @@ int gs_engine::start() {
   const size_t NQ = (size_t)nOwnN * x.promCap;
   x.promMid = dalloc<int64_t>(NQ); x.promExp = dalloc<int64_t>(NQ); x.promSlot = dalloc<int32_t>(NQ);
   x.promEdge = dalloc<uint8_t>(NQ); x.promN = dalloc<int32_t>(nOwnN);
-  // mcache.peertx: 512 entries per node.  With IWANT spammers present the
-  // honest requests grow too (messages dropped by validation queues come back
-  // through gossip), so those runs get 4096; the spammers' own requests, one
-  // per (message, spammer), are counted in spamCnt instead
-  x.ptxCap = (behaveAll & GS_BEHAVE_IWANT_SPAM) ? 4096 : GS_PTX;
-  x.ptxHBits = 13;  // the dynamic hash of the 4096-entry table: 8192 slots (32 KiB)
-  x.ptx = dalloc<uint64_t>((size_t)nOwnN * x.ptxCap); x.ptxN = dalloc<int32_t>(nOwnN);
+  // mcache.peertx: a hash of 1024 entries per node in HBM.  With IWANT
+  // spammers present the honest requests grow too (messages dropped by
+  // validation queues come back through gossip), so those runs get 8192; the
+  // spammers' own requests, one per (message, spammer), are counted in spamCnt
+  x.ptxBits = (behaveAll & GS_BEHAVE_IWANT_SPAM) ? 13 : GS_PTX_BITS;
+  x.ptxT = dalloc<uint32_t>((size_t)nOwnN << x.ptxBits); x.ptxN = dalloc<int32_t>(nOwnN);
   chk(x.promMid); chk(x.promExp); chk(x.promSlot); chk(x.promEdge); chk(x.promN);
-  chk(x.ptx); chk(x.ptxN);
+  chk(x.ptxT); chk(x.ptxN);
   if (!ok) { gs_set_error("device allocation failed (promises / peertx)"); return GS_ENOMEM; }
   x.promMid -= (size_t)n0 * x.promCap; x.promExp -= (size_t)n0 * x.promCap;
   x.promSlot -= (size_t)n0 * x.promCap; x.promEdge -= (size_t)n0 * x.promCap; x.promN -= n0;
-  x.ptx -= (size_t)n0 * x.ptxCap; x.ptxN -= n0;
+  x.ptxT -= (size_t)n0 << x.ptxBits; x.ptxN -= n0;
+  if (gp.GossipRetransmission > 253) {  // a peertx count byte peaks at GossipRetransmission + 2
+    gs_set_error("GossipRetransmission > 253 is not supported");
+    return GS_EUNSUPPORTED;
+  }
   x.mesh = dalloc<uint64_t>(E); x.fanout = dalloc<uint64_t>(E);
   chk(x.mesh); chk(x.fanout);
   for (int k = 0; k < 2; ++k) {
@@ -789,8 +792,8 @@ int gs_engine::start() {
       if (nrow > INT32_MAX) { gs_set_error("too many IWANT-spammer edges"); return GS_ECAPACITY; }
       x.spamRow = dalloc<int32_t>(E); chk(x.spamRow);
       for (int k = 0; k < 2; ++k) { x.pflag[k] = dalloc<uint8_t>((size_t)poolSeg * world); chk(x.pflag[k]); }
-      if (gp.GossipRetransmission >= 15) {  // spam_incr's nibble saturates at 15
-        gs_set_error("IWANT spammers need GossipRetransmission < 15 in this build");
+      if (gp.GossipRetransmission >= 14) {  // spam_incr's nibble peaks at GossipRetransmission + 2
+        gs_set_error("IWANT spammers need GossipRetransmission < 14 in this build");
         return GS_EUNSUPPORTED;
       }
       x.spamCnt = dalloc<uint32_t>((size_t)std::max<int64_t>(nrow, 1) * (S / 8)); chk(x.spamCnt);
@@ -1390,7 +1393,7 @@ int gs_engine::stepOne() {
       const auto b2 = std::upper_bound(mHop.begin(), mHop.end(), h);
       cutMode = (int64_t)(b2 - a) > (int64_t)gp.MaxIHaveLength ? 1 : 0;
     }
-    const size_t ldsB = d.ptxCap > GS_PTX ? GS_CUTLDS + 4 * ((size_t)1 << d.ptxHBits) : (cutMode ? GS_CUTLDS : 0);
+    const size_t ldsB = cutMode ? GS_CUTLDS : 0;
     if (nOwn) {
       const int rc = upload(dDev, &d, sizeof(Dev));
       if (rc) return rc;
@@ -1454,6 +1457,8 @@ int gs_engine::stepOne() {
     else if (nOwn)
       TIMED(this, GS_K_HEARTBEAT,
             (k_heartbeat<false><<<nOwn, 64, 0, stream>>>(d, h, now, ticks, cur, head, newhead, allExact)));
+    // the peertx counters of the window that left the cache (pre-shift HL - 1)
+    if (nOwn && gossip) k_ptx_rebuild<<<nOwn, 64, (size_t)4 << d.ptxBits, stream>>>(d, (head + d.HL - 1) % R);
     head = newhead;
     heartbeats++;
   }
@@ -1510,7 +1515,7 @@ int gs_engine::deviceErrorCode(int32_t err) {
                    "at most 512)");
       return GS_ECAPACITY;
     case E_PEERTX:
-      gs_set_error("per-node IWANT retransmission table overflow (512 entries; 4096 with IWANT spammers)");
+      gs_set_error("per-node IWANT retransmission table overflow (1024 entries; 8192 with IWANT spammers)");
       return GS_ECAPACITY;
     case E_LATE:
       gs_set_error("a message was first delivered later than the message window allows; raise slots_per_topic");
@@ -2460,6 +2465,12 @@ int gs_read_deliveries(gs_engine* g, int64_t id, int32_t* hop, int32_t* from) {
 int gs_debug_stamps(gs_engine* g, unsigned long long* out, int n) {
   HIPCHECK(hipStreamSynchronize(g->stream));
   HIPCHECK(hipMemcpy(out, g->d.stamps, (size_t)n * 8, hipMemcpyDeviceToHost));
+  return GS_OK;
+}
+// Debug build: the peertx entry count of every owned node.
+int gs_debug_ptxn(gs_engine* g, int32_t* out, int n) {
+  HIPCHECK(hipStreamSynchronize(g->stream));
+  HIPCHECK(hipMemcpy(out, g->d.ptxN + g->n0, (size_t)n * 4, hipMemcpyDeviceToHost));
   return GS_OK;
 }
 #endif

@@ -173,23 +173,16 @@ __device__ __forceinline__ void px_connect(const Dev& d, int v, int64_t base, in
   });
 }
 
-#define GS_PTXH 1024  // LDS hash slots for a node's mcache.peertx table (>= 2 * GS_PTX)
-
-// The LDS hash holds 32-bit entries slot << 14 | in-edge << 8 | count (slot <
-// 2^14, in-edge < 64); the node's list in HBM keeps the 64-bit form
-// slot << 32 | in-edge << 8 | count.  Keys (count bits 0) are passed as u64.
+// mcache.peertx entries: slot << 14 | in-edge << 8 | count (slot < 2^14,
+// in-edge < 64); keys (count bits 0) are passed as u64 slot << 32 | in-edge << 8.
 __device__ __forceinline__ uint32_t ptx_key32(uint64_t key) {
   return ((uint32_t)(key >> 32) << 14) | ((uint32_t)((key >> 8) & 0x3F) << 8);
 }
-__device__ __forceinline__ uint32_t ptx_to32(uint64_t ent) { return ptx_key32(ent) | (uint32_t)(ent & 0xFF); }
-__device__ __forceinline__ uint64_t ptx_to64(uint32_t e) {
-  return ((uint64_t)(e >> 14) << 32) | ((uint64_t)((e >> 8) & 0x3F) << 8) | (uint64_t)(e & 0xFF);
-}
-// hbits: log2 of the hash size (GS_PTXH, or the larger dynamic table of an
-// IWANT-spam run)
 __device__ __forceinline__ int ptx_hash(uint32_t key, int hbits) {
   return (int)((key * 0x9E3779B1u) >> (32 - hbits));
 }
+// the node's peertx table in HBM
+__device__ __forceinline__ uint32_t* ptx_row(const Dev& d, int v) { return d.ptxT + ((int64_t)v << d.ptxBits); }
 
 // k-th set bit (0-based) of m
 __device__ __forceinline__ int kth_bit(uint64_t m, int k) {
@@ -197,26 +190,28 @@ __device__ __forceinline__ int kth_bit(uint64_t m, int k) {
   return __ffsll((long long)m) - 1;
 }
 
-// ++peertx[slot][edge] (mcache.GetForPeer, mcache.go:66-80) in the LDS hash;
-// returns the new count, or 0 when the table is full (E_PEERTX raised).
-__device__ __forceinline__ int ptx_incr(const Dev& d, unsigned int* sH, int hbits, uint64_t key64) {
-  const uint32_t key = ptx_key32(key64);
-  const int hmask = (1 << hbits) - 1;
-  int hsl = ptx_hash(key, hbits);
+// ++peertx[slot][edge] (mcache.GetForPeer, mcache.go:66-80) in the node's
+// HBM hash, given the outcome `prev` of a first CAS(0 -> key | 1) at the key's
+// home slot hs; returns the new count (0 with E_PEERTX when the table is full),
+// and sets ins when the key was inserted.  handleIWant only compares the count
+// with GossipRetransmission (GR), so a count is held at GR + 1: an increment
+// past it is taken back (the byte peaks at GR + 2; one request list names an
+// id once and a requester's two lists are counted one after the other, so no
+// two increments of one key race).  Entries are never moved during a hop
+// (k_ptx_rebuild compacts the table at the heartbeat), so a key found stays.
+__device__ __forceinline__ int ptx_settle(const Dev& d, uint32_t* row, uint32_t key, int hs, uint32_t prev, bool& ins) {
+  const int hmask = (1 << d.ptxBits) - 1;
+  int hsl = hs;
   for (int probe = 0; probe <= hmask; ++probe) {
-    unsigned int cur = sH[hsl];
-    while (true) {
-      if (cur == 0) {
-        const unsigned int prev = atomicCAS(&sH[hsl], 0u, key | 1u);
-        if (prev == 0) return 1;
-        cur = prev;
-      }
-      if ((cur & ~0xFFu) != key) break;  // another key: probe on
-      const unsigned int c = cur & 0xFF;
-      const unsigned int nw = key | (c < 255 ? c + 1 : 255);
-      const unsigned int prev = atomicCAS(&sH[hsl], cur, nw);
-      if (prev == cur) return (int)(nw & 0xFF);
-      cur = prev;
+    if (probe > 0) prev = atomicCAS(&row[hsl], 0u, key | 1u);
+    if (prev == 0u) {
+      ins = true;
+      return 1;
+    }
+    if ((prev & ~0xFFu) == key) {
+      const int c = (int)(atomicAdd(&row[hsl], 1u) & 0xFFu) + 1;
+      if (c > d.GR + 1) atomicSub(&row[hsl], 1u);
+      return c;
     }
     hsl = (hsl + 1) & hmask;
   }
@@ -224,14 +219,14 @@ __device__ __forceinline__ int ptx_incr(const Dev& d, unsigned int* sH, int hbit
   return 0;
 }
 
-__device__ __forceinline__ int ptx_count(const unsigned int* sH, int hbits, uint64_t key64) {
-  const uint32_t key = ptx_key32(key64);
-  const int hmask = (1 << hbits) - 1;
-  int hsl = ptx_hash(key, hbits);
+// the count of key in the node's HBM hash (0 = absent)
+__device__ __forceinline__ int ptx_count_g(const Dev& d, uint32_t* row, uint32_t key) {
+  const int hmask = (1 << d.ptxBits) - 1;
+  int hsl = ptx_hash(key, d.ptxBits);
   for (int probe = 0; probe <= hmask; ++probe) {
-    const unsigned int cur = sH[hsl];
-    if (cur == 0) return 0;
-    if ((cur & ~0xFFu) == key) return (int)(cur & 0xFF);
+    const uint32_t cur = __hip_atomic_load(&row[hsl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == 0u) return 0;
+    if ((cur & ~0xFFu) == key) return (int)(cur & 0xFFu);
     hsl = (hsl + 1) & hmask;
   }
   return 0;
@@ -293,16 +288,13 @@ __device__ __forceinline__ void put_served(const Dev& d, const int32_t* pool, co
 // squatters, the dynamic peertx hash, phantom ids and the cuts; the honest
 // instantiation carries none of them.
 template <int WPL, bool ADV>
-__global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict__ dp, int64_t h, int64_t now, int cur,
-                                                int head, int cutModeArg) {
-  const Dev& d = *dp;  // from device memory, as k_phase_a
+__device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t h, int64_t now, int cur, int head,
+                                             int cutModeArg) {
   const int cutMode = ADV ? cutModeArg : 0;
-  if (!gossip_host(d, d.n0 + (int)blockIdx.x)) return;  // FloodSubRouter / RandomSubRouter.HandleRPC: no-ops
+  if (!gossip_host(d, v)) return;  // FloodSubRouter / RandomSubRouter.HandleRPC: no-ops
   __shared__ uint64_t scache[64 * WPL];  // v's mcache windows (handleIWant, step 2)
   uint64_t* const sseen = scache;        // then v's seen row (handleIHave, step 3)
-  // step 2's peertx hash; the step-3 arrays below live in the same LDS once
-  // step 2 has written the table back to its list form
-  __shared__ __attribute__((aligned(16))) unsigned int sH[GS_PTXH];
+  __shared__ __attribute__((aligned(16))) unsigned int sH[768];  // step 3's per-sender arrays
   __shared__ double sterm[64];
   __shared__ int sIt[64];                // per-sender exclusive item prefix
   __shared__ int sReqOff[64], sReqN[64]; // step 2: request list of each sender
@@ -316,8 +308,7 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
   int* const sSlot = (int*)(sH + 448);
   uint32_t* const sHas = (uint32_t*)(sH + 512);  // step 3: items with a want (<= 64 senders x 64 items)
   uint32_t* const sCand = (uint32_t*)(sH + 640); // step 3: items that held their sender's smallest key
-  static_assert(640 + 64 * 64 / 32 <= GS_PTXH, "step-3 arrays must fit in the peertx hash");
-  const int v = d.n0 + blockIdx.x;
+  static_assert(640 + 64 * 64 / 32 <= 768, "step-3 arrays must fit in sH");
   const int lane = lane_id();
   const int prv = cur ^ 1;
   const int W = d.W;
@@ -518,28 +509,11 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
   uint32_t srvB = 0, srvBS = 0;
   if (__ballot(gateIWant || gateSpam)) {
     __shared__ int sSpOff[64], sSpN[64], sItI[64], sCntS[64], sRow[64];
-    // the peertx hash: static, or a larger dynamic table (IWANT-spam runs)
-    extern __shared__ __attribute__((aligned(16))) uint32_t smemH[];
-    const bool big = ADV && d.ptxCap > GS_PTX;
-    unsigned int* const hT = big ? (unsigned int*)(smemH + GS_CUTLDS / 4) : sH;
-    const int ptxCap = ADV ? d.ptxCap : GS_PTX;  // the honest instantiation always has GS_PTX
+    uint32_t* const prow = ptx_row(d, v);  // v's peertx table (HBM hash)
     const int nI = gateIWant ? (int)(iwRec & 0xFFFFFF) : 0;
     const int nS = gateSpam ? (int)(spRec & 0xFFFFFF) : 0;
-    // the large table is sized to this node's load (entries it holds plus the
-    // keys this hop can add, at most half full), so a lightly loaded node
-    // clears and writes back a small table; lookups use the same size
-    int hbits = 10;
-    if (big) {
-      int tot;
-      (void)lane_prefix(nI + nS, &tot);
-      const int need = 2 * (d.ptxN[v] + tot);
-      hbits = 10;
-      while (hbits < d.ptxHBits && (1 << hbits) < need) ++hbits;
-    }
-    const int hN = 1 << hbits;
     __shared__ uint64_t sNeedW[GS_MAX_WPL];  // the mcache words the requests name (bit per word)
     if (lane < GS_MAX_WPL) sNeedW[lane] = 0ull;
-    for (int k = lane; k < hN; k += 64) hT[k] = 0u;
     const int itI = (nI + 15) >> 4, itS = (nS + 15) >> 4;
     int totalItems;
     sIt[lane] = lane_prefix(itI + itS, &totalItems);
@@ -555,14 +529,9 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
     sCntS[lane] = 0;
     sCur[lane] = 0;
     __syncthreads();
-    const int ptxN = d.ptxN[v];
-    for (int q = lane; q < ptxN; q += 64) {
-      const unsigned long long ent = d.ptx[(int64_t)v * ptxCap + q];
-      const unsigned int e32 = ptx_to32(ent);
-      int hsl = ptx_hash(e32 & ~0xFFu, hbits);
-      while (atomicCAS(&hT[hsl], 0u, e32) != 0u) hsl = (hsl + 1) & (hN - 1);
-    }
-    __syncthreads();
+#ifdef GS_STAMPS_PB2
+    GS_STAMPB(5);
+#endif
     // item b: 16 ids of the IHAVE-reply list (k < itI) or of the spam list
     auto item = [&](int b, int& i, int& off, int& cnt, bool& sp) {
       int k;
@@ -577,6 +546,18 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
         cnt = min(16, sReqN[i] - 16 * k);
       }
     };
+    // the request ids of an item, four loads in flight: fn(q, slot)
+    const int32_t* const req = prv ? d.pool[1] : d.pool[0];
+    auto ids = [&](int off, int cnt, auto&& fn) {
+      for (int q0 = 0; q0 < cnt; q0 += 4) {
+        int sl[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sl[q] = q0 + q < cnt ? req[off + q0 + q] : -1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (sl[q] >= 0) fn(q0 + q, sl[q]);
+      }
+    };
     // mcache.GetForPeer finds the id (mcache.go:66-80); a phantom id is never served
     auto cached = [&](int slot) {
       return ((scache[slot >> 6] >> (slot & 63)) & 1) && !(ADV && d.slotKind[slot] == GS_MSG_PHANTOM);
@@ -587,54 +568,119 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
       int i, off, cnt;
       bool sp;
       item(b, i, off, cnt, sp);
-      for (int q = 0; q < cnt; ++q) {
-        const int w = d.pool[prv][off + q] >> 6;
+      ids(off, cnt, [&](int, int slot) {
+        const int w = slot >> 6;
         atomicOr((unsigned long long*)&sNeedW[w >> 6], 1ull << (w & 63));
-      }
+      });
     }
     __syncthreads();
-    for (int w = lane; w < W; w += 64) {
-      if (!((sNeedW[w >> 6] >> (w & 63)) & 1)) continue;
-      uint64_t x = 0;
-      for (int k = 0; k < d.HL; ++k) x |= d.hist[((int64_t)((head + k) % d.R) * d.nOwnH + (v - d.n0)) * W + w];
-      scache[w] = x;
+    int nW = 0;  // needed words
+#pragma unroll
+    for (int j = 0; j < GS_MAX_WPL; ++j) nW += __popcll(sNeedW[j]);
+    for (int w = lane; w < W; w += 64)
+      if ((sNeedW[w >> 6] >> (w & 63)) & 1) scache[w] = 0ull;
+    __syncthreads();
+    // one (needed word, window) load per lane: every load in flight at once
+    for (int p = lane; p < nW * d.HL; p += 64) {
+      const int wi = p / d.HL, k = p - wi * d.HL;
+      int j = 0, r = wi;
+      while (r >= __popcll(sNeedW[j])) r -= __popcll(sNeedW[j++]);
+      const int w = 64 * j + kth_bit(sNeedW[j], r);
+      const uint64_t x = d.hist[((int64_t)((head + k) % d.R) * d.nOwnH + (v - d.n0)) * W + w];
+      if (x) atomicOr((unsigned long long*)&scache[w], x);
     }
     __syncthreads();
+#ifdef GS_STAMPS_PB2
+    GS_STAMPB(6);
+#endif
     // pass a: increments and per-sender served counts.  A spammer's two lists
     // may name the same message (a copy dropped by the validation queue stays
     // unseen, so it is asked for again after the IHAVE): its re-request RPC was
-    // sent first (phase A of the previous hop), so that list is counted first,
-    // and each request's own verdict is kept (pflag) for pass b.
-    const bool flags = ADV && d.pflag[0] != nullptr;
-    auto passA = [&](int which) {  // 0: IHAVE-reply lists, 1: spam lists, 2: both
+    // sent first (phase A of the previous hop), so that list is counted first.
+    // Each request's verdict is kept for pass b, which walks the same items in
+    // the same lanes: 16 bits per item in a register for a lane's first 4
+    // items, in pflag (IWANT-spam runs) past them.
+    uint64_t vbits = 0;
+    int nIns = 0;  // keys inserted into the peertx table
+    const bool flags = ADV && d.pflag[0] != nullptr;  // also read by the RPC trace (step 4)
+    // (without flags an item past a lane's fourth is looked up again in pass
+    // b: an id is asked for at most once per hop, so its count is the verdict)
+    auto verdict = [&](int b, int q, int off, bool srv) {
+      const int j = (b - lane) >> 6;
+      if (flags) d.pflag[prv][off + q] = srv ? 1 : 0;
+      if (j < 4 && srv) vbits |= 1ull << (16 * j + q);
+    };
+    auto passA = [&](int which) {  // 0: IHAVE-reply lists, 1: spam lists
       for (int b = lane; b < totalItems; b += 64) {
         int i, off, cnt;
         bool sp;
         item(b, i, off, cnt, sp);
-        if (which != 2 && sp != (which == 1)) continue;
+        if (sp != (which == 1)) continue;
         int c = 0;
-        for (int q = 0; q < cnt; ++q) {
-          const int slot = d.pool[prv][off + q];
-          bool srv = false;
-          if (cached(slot)) {
-            const uint64_t key = ((uint64_t)(uint32_t)slot << 32) | ((uint64_t)i << 8);
-            const int count = (ADV && sRow[i] >= 0) ? spam_incr(d, sRow[i], slot) : ptx_incr(d, hT, hbits, key);
-            srv = count >= 1 && count <= d.GR;
+        if (ADV && sRow[i] >= 0) {
+          // a spammer's counts in HBM: the adds of four requests issued back to
+          // back (independent words or nibbles), then their few take-backs
+          for (int q0 = 0; q0 < cnt; q0 += 4) {
+            int sl[4], cn[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) sl[q] = q0 + q < cnt ? req[off + q0 + q] : -1;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              cn[q] = 0;
+              if (sl[q] >= 0 && cached(sl[q]))
+                cn[q] = (int)((atomicAdd(spam_word(d, sRow[i], sl[q]), 1u << ((sl[q] & 7) * 4)) >> ((sl[q] & 7) * 4)) & 0xF) + 1;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              if (cn[q] > d.GR + 1) atomicSub(spam_word(d, sRow[i], sl[q]), 1u << ((sl[q] & 7) * 4));
+              const bool srv = cn[q] >= 1 && cn[q] <= d.GR;
+              if (srv) ++c;
+              if (q0 + q < cnt) verdict(b, q0 + q, off, srv);
+            }
           }
-          if (srv) ++c;
-          if (flags) d.pflag[prv][off + q] = srv ? 1 : 0;
+        } else {
+          // v's peertx table: the first CAS(0 -> key | 1) of four requests
+          // issued back to back, then each settled (found: +1; taken: probe on)
+          for (int q0 = 0; q0 < cnt; q0 += 4) {
+            int sl[4];
+            uint32_t key[4], pv[4];
+            int hs[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) sl[q] = q0 + q < cnt ? req[off + q0 + q] : -1;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const bool go = sl[q] >= 0 && cached(sl[q]);
+              key[q] = ptx_key32(((uint64_t)(uint32_t)(go ? sl[q] : 0) << 32) | ((uint64_t)i << 8));
+              hs[q] = ptx_hash(key[q], d.ptxBits);
+              pv[q] = go ? atomicCAS(&prow[hs[q]], 0u, key[q] | 1u) : 0xFFFFFFFFu;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              bool srv = false;
+              if (pv[q] != 0xFFFFFFFFu) {
+                bool ins = false;
+                const int count = ptx_settle(d, prow, key[q], hs[q], pv[q], ins);
+                nIns += ins ? 1 : 0;
+                srv = count >= 1 && count <= d.GR;
+              }
+              if (srv) ++c;
+              if (q0 + q < cnt) verdict(b, q0 + q, off, srv);
+            }
+          }
         }
         if (c) atomicAdd(sp ? &sCntS[i] : &sCnt[i], c);
       }
     };
-    if (flags) {
+    if (ADV && __ballot(nS > 0)) {
       passA(1);
       __syncthreads();
-      passA(0);
-    } else {
-      passA(2);
     }
+    passA(0);
     __syncthreads();
+    {
+      const int ins = wave_sum_int(nIns);
+      if (lane == 0 && ins) d.ptxN[v] += ins;
+    }
     int totalServed;
     const int myServed = sCnt[lane] + sCntS[lane];
     nSrv = (sCnt[lane] > 0 ? 1 : 0) + (sCntS[lane] > 0 ? 1 : 0);
@@ -653,21 +699,23 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
         if (myServed) respRec = ((int64_t)(poolBase + myOff) << 24) | (int64_t)myServed;
         cServed = totalServed;
         __syncthreads();
-        // pass b: write the served ids (without two lists per sender a request's
-        // verdict is its final count: an id is asked for at most once)
+        // pass b: write the served ids by each request's verdict
         for (int b = lane; b < totalItems; b += 64) {
           int i, off, cnt;
           bool sp;
           item(b, i, off, cnt, sp);
-          for (int q = 0; q < cnt; ++q) {
-            const int slot = d.pool[prv][off + q];
+          const int j = (b - lane) >> 6;
+          const uint32_t vb = j < 4 ? (uint32_t)(vbits >> (16 * j)) & 0xFFFFu : 0u;
+          if (j < 4 && vb == 0u) continue;
+          ids(off, cnt, [&](int q, int slot) {
             bool srv;
-            if (flags) {
+            if (j < 4) {
+              srv = ((vb >> q) & 1) != 0;
+            } else if (flags) {
               srv = d.pflag[prv][off + q] != 0;
             } else {
-              if (!cached(slot)) continue;
-              const uint64_t key = ((uint64_t)(uint32_t)slot << 32) | ((uint64_t)i << 8);
-              const int count = (ADV && sRow[i] >= 0) ? spam_count(d, sRow[i], slot) : ptx_count(hT, hbits, key);
+              const uint32_t key = ptx_key32(((uint64_t)(uint32_t)slot << 32) | ((uint64_t)i << 8));
+              const int count = cached(slot) ? ptx_count_g(d, prow, key) : 0;
               srv = count >= 1 && count <= d.GR;
             }
             if (srv) {
@@ -675,26 +723,16 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
               if (d.rpcB != nullptr)
                 atomicAdd(sp ? &sSrvBS[i] : &sSrvB[i], (uint32_t)d.acc[(int)__umulhi((unsigned)slot, d.stMagic)].msgF);
             }
-          }
+          });
         }
       }
     }
     __syncthreads();
+#ifdef GS_STAMPS_PB2
+    GS_STAMPB(7);
+#endif
     srvB = sSrvB[lane];
     srvBS = sSrvBS[lane];
-    {  // peertx table back to its list form
-      __syncthreads();
-      int kept = 0;
-      for (int q0 = 0; q0 < hN; q0 += 64) {
-        const unsigned int e32 = hT[q0 + lane];
-        int tot;
-        const int pos = kept + lane_prefix(e32 != 0u ? 1 : 0, &tot);
-        if (e32 && pos < ptxCap) d.ptx[(int64_t)v * ptxCap + pos] = ptx_to64(e32);
-        kept += tot;
-      }
-      if (kept > ptxCap && lane == 0) set_err(d, E_PEERTX);
-      if (lane == 0) d.ptxN[v] = kept < ptxCap ? kept : ptxCap;
-    }
     __syncthreads();  // sH is reused by step 3
   }
 
@@ -860,7 +898,9 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
       }
     }
     __syncthreads();
+#ifndef GS_STAMPS_PB2
     GS_STAMPB(5);
+#endif
     // pass a2: the smallest mid among the wants holding the smallest key (only
     // the candidate items can hold it)
     for (int b = lane; b < totalItems; b += 64) {
@@ -882,7 +922,9 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
       });
     }
     __syncthreads();
+#ifndef GS_STAMPS_PB2
     GS_STAMPB(6);
+#endif
     // the sender cut: iask = MaxIHaveLength - iasked of the smallest keys
     const int myWantAll = sCnt[lane];
     const bool iaCut = gateIHave && myWantAll > 0 && myWantAll + ia > d.MaxIHaveLength;
@@ -978,7 +1020,9 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
       }
     }
     __syncthreads();
+#ifndef GS_STAMPS_PB2
     GS_STAMPB(7);
+#endif
   }
   cIwantSent = (long long)wave_sum_ll(cIwantSent);
   cGray = (long long)wave_sum_ll(cGray);  // per-lane (sender) counts
@@ -1139,6 +1183,13 @@ __global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict_
     if (cGray) ctr_add(d, C_GRAYLISTED, (unsigned long long)cGray);
   }
   GS_STAMPB(4);
+}
+
+template <int WPL, bool ADV>
+__global__ __launch_bounds__(64) GS_OCC_PB void k_phase_b(const Dev* __restrict__ dp, int64_t h, int64_t now, int cur,
+                                                int head, int cutModeArg) {
+  const Dev& d = *dp;  // from device memory, as k_phase_a
+  phase_b_node<WPL, ADV>(d, d.n0 + (int)blockIdx.x, h, now, cur, head, cutModeArg);
 }
 
 // ---------------------------------------------------------------- heartbeat prelude
@@ -1957,33 +2008,49 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
     if (p) ctr_add(d, C_PRUNES, (unsigned long long)p);
     if (ih) ctr_add(d, C_IHAVE, (unsigned long long)ih);
   }
-  // mcache.Shift (mcache.go:94-104): drop the IWANT retransmission counters of
-  // messages leaving the cache (pre-shift window HL-1), then clear the ring
-  // slot that becomes window 0.  The dropped window stays readable as the
-  // "ghost" slot until the next shift (IHAVE payload of this heartbeat).
-  const int n = d.ptxN[v];
-  if (n > 0) {
-    const int last = (head + d.HL - 1) % d.R;
-    const uint64_t* lastw = d.hist + ((int64_t)last * d.nOwnH + (v - d.n0)) * d.W;
-    int kept = 0;
-    for (int base = 0; base < n; base += 64) {
-      const int q = base + lane;
-      uint64_t ent = 0;
-      bool live = q < n;
-      if (live) {
-        ent = d.ptx[(int64_t)v * d.ptxCap + q];
-        const int slot = (int)(ent >> 32);
-        if ((lastw[slot >> 6] >> (slot & 63)) & 1) live = false;
-      }
-      const unsigned long long lm = __ballot(live);
-      const int pos = kept + __popcll(lm & ((1ull << lane) - 1));
-      if (live) d.ptx[(int64_t)v * d.ptxCap + pos] = ent;  // pos <= q: in-place compaction is safe
-      kept += __popcll(lm);
-    }
-    if (lane == 0) d.ptxN[v] = kept;
-  }
+  // mcache.Shift (mcache.go:94-104): clear the ring slot that becomes window 0
+  // (the peertx counters of the messages leaving the cache are dropped by
+  // k_ptx_rebuild after this launch).  The dropped window stays readable as
+  // the "ghost" slot until the next shift (IHAVE payload of this heartbeat).
   for (int w = lane; w < d.W; w += 64) d.hist[((int64_t)newhead * d.nOwnH + (v - d.n0)) * d.W + w] = 0;
   GS_STAMPH(5, GS_CLK());
+}
+
+// mcache.Shift's peertx part (mcache.go:94-104): the counters of the
+// messages leaving the cache (pre-shift window `last`, still readable after
+// k_heartbeat) are dropped and the node's table is rebuilt without them (an
+// open-addressing table cannot delete in place).  One wave per node, the table
+// staged in LDS (dynamic: 4 << ptxBits bytes); a node without entries is
+// skipped.
+__global__ __launch_bounds__(64) void k_ptx_rebuild(Dev d, int last) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sT[];
+  const int v = d.n0 + blockIdx.x;
+  if (d.ptxN[v] == 0) return;
+  const int lane = lane_id();
+  const int hN = 1 << d.ptxBits;
+  uint32_t* const row = ptx_row(d, v);
+  const uint64_t* lastw = d.hist + ((int64_t)last * d.nOwnH + (v - d.n0)) * d.W;
+  for (int k = lane; k < hN / 4; k += 64) ((uint4*)sT)[k] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  int kept = 0;
+  for (int k0 = 0; k0 < hN; k0 += 64 * 4) {
+    uint4 q = ((const uint4*)row)[(k0 >> 2) + lane];
+    uint32_t ent[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t x = ent[j];
+      if (!x) continue;
+      const int slot = (int)(x >> 14);
+      if ((lastw[slot >> 6] >> (slot & 63)) & 1) continue;  // leaves the cache
+      int hsl = ptx_hash(x & ~0xFFu, d.ptxBits);
+      while (atomicCAS(&sT[hsl], 0u, x) != 0u) hsl = (hsl + 1) & (hN - 1);
+      ++kept;
+    }
+  }
+  __syncthreads();
+  for (int k = lane; k < hN / 4; k += 64) ((uint4*)row)[k] = ((const uint4*)sT)[k];
+  kept = wave_sum_int(kept);
+  if (lane == 0) d.ptxN[v] = kept;
 }
 
 // gs_read_deliveries gather

@@ -340,8 +340,10 @@ int gs_set_behaviour(gs_engine* eng, const uint8_t* behaviour /*[N]*/);
  *   GS_EV_JOIN (a, topic b): node a subscribes (handleAddSubscription
  *     pubsub.go:692-713): announce, then Join (gossipsub.go:1011-1060).
  * An event that finds its state already (a connection down twice, a topic
- * left twice) does nothing.  Not supported together with the peer gater
- * (GS_EUNSUPPORTED); a partitioned engine applies every event on every rank,
+ * left twice) does nothing.  With the peer gater, a disconnect is its
+ * RemovePeer (the IP's stats expire RetainStats after its last peer left,
+ * peer_gater.go:366-383) and a connect its AddPeer (a live stats object is
+ * revived); a partitioned engine applies every event on every rank,
  * each rank launching the side of a connection it owns.
  * Direct peers (gs_set_graph's direct flags) that are not connected are
  * dialled by the connector at hop ceil(DirectConnectInitialDelay / hop_ns)

@@ -62,7 +62,11 @@ def main():
         for i, nm in enumerate(["step1", "step2 iwant", "step3 ihave", "step4"]):
             print(f"  {nm}: mean {db[:, i].mean():.0f} cycles  p50 {np.median(db[:, i]):.0f}  p99 {np.percentile(db[:, i], 99):.0f}")
         sub = bb[(bb[:, 5] > 0) & (bb[:, 7] > 0)]
-        if len(sub):
+        if len(sub) and os.environ.get("GS_STAMPS_PB2"):
+            print("  step2 (nodes serving, %d): setup %.0f, table load + windows %.0f, passes a/b %.0f, write-back %.0f" % (
+                len(sub), (sub[:, 5] - sub[:, 1]).mean(), (sub[:, 6] - sub[:, 5]).mean(), (sub[:, 7] - sub[:, 6]).mean(),
+                (sub[:, 2] - sub[:, 7]).mean()))
+        elif len(sub):
             print("  step3 (nodes with IHAVE work, %d): setup %.0f, pass a %.0f, pass a2 %.0f, pass b + arena %.0f" % (
                 len(sub), (sub[:, 5] - sub[:, 2]).mean() - (sub[:, 5] - sub[:, 5]).mean(), 0, 0, 0)
                   if False else "  step3 (nodes with IHAVE work, %d): to pass a end %.0f, pass a2 %.0f, pass b + arena %.0f, promises + rest %.0f" % (
