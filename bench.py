@@ -147,13 +147,18 @@ def algorithmic_bytes(kernel, eng, wl, per_hop):
         mesh = eng.mesh()[e0:e1]
         fwd_edges = int((mesh != 0).sum())          # edges with a forwarding topic
         items = per_hop["deliveries"] + per_hop["published"]   # frontier-list entries written per hop
-        list_reads = 4.0 * items * fwd_edges / N     # each list is read by the neighbours it forwards to
+        # each copy sent is one 16-bit slot of the sender's pushed segment for
+        # that edge (k_push), read once by its receiver, plus the segment's
+        # 8-byte record; the receiver writes its own frontier list (4 B per entry)
+        copies = per_hop["transmissions"] - per_hop["iwant_served"]  # served ids: 4 B each from the pool
+        list_reads = 2.0 * copies + 8.0 * fwd_edges + 4.0 * per_hop["iwant_served"]
         list_writes = 4.0 * items
         pending = 8.0 * T * E                        # pending-delivery counts, read + write per (edge, topic)
         seen = 16.0 * N * per_hop["active_words"]    # seen words of the active window, read + write
         meta = 49.0 * E                              # rev, col, fwd masks, IWANT ref, S0 memo, direct, mesh
         b = list_reads + list_writes + pending + seen + meta
-        return b, dict(fwd_edges=fwd_edges, list_entries_per_hop=items, active_words=per_hop["active_words"],
+        return b, dict(fwd_edges=fwd_edges, list_entries_per_hop=items, copies_per_hop=copies,
+                       active_words=per_hop["active_words"],
                        bytes_lists=int(list_reads + list_writes), bytes_pending=int(pending),
                        bytes_seen=int(seen), bytes_meta=int(meta))
     if kernel == "refresh":
@@ -382,6 +387,8 @@ def main():
     per_hop = {"events_per_round": {k: v / args.steps for k, v in events.items()},
                "deliveries": (c1["deliveries"] - c0["deliveries"]) / nh,
                "published": (c1["published"] - c0["published"]) / nh,
+               "transmissions": (c1["transmissions"] - c0["transmissions"]) / nh,
+               "iwant_served": (c1["iwant_served"] - c0["iwant_served"]) / nh,
                "active_words": float(np.mean([active_words(eng, wl, hop0 + i) for i in range(nh)])),
                "mesh_pairs": int(np.bitwise_count(eng.mesh()[eng.edge_range[0]:eng.edge_range[1]]).sum(dtype=np.int64))}
     # the roofline is the heaviest kernel with an algorithmic byte model (phase

@@ -53,7 +53,10 @@
 #endif
 #define GS_QCAP 320    // phase A delivery queue (>= 63 pending + 256 appended per sub-round)
 #define GS_BMAP 32     // phase A: list blocks mapped to senders without a search (64 per entry)
-#define GS_PTX_BITS 10 // mcache.peertx hash slots per node: 2^10 (2^13 when IWANT spammers run)
+// push arena: the senders' allocations spread over this many counters (a
+// single counter serialised a million per-wave atomics at one L2 address)
+#define GS_IBX_SUB 512
+#define GS_PTX_BITS 10 // mcache.peertx hash slots per node: 2^10 (2^12 when IWANT spammers run)
 #define GS_CUTS 64     // IHAVE entries above MaxIHaveLength one node can cut per hop
 // phase B dynamic LDS: the MaxIHaveLength-cut tables (cut mode)
 #define GS_CUTLDS (256 * 4 + GS_CUTS * 4 + GS_CUTS * 16 + 64 * 16 + 128 * 4 + 16)
@@ -228,6 +231,17 @@ struct Dev {
   // edge e, so a receiver reads its in-edges' sets as one coalesced row
   // (maintained by k_fwd on change, k_edge_down and the exchange)
   ulonglong2* fwdIn[2];
+  // push: the copies each owned sender sends on each edge to an owned receiver
+  // (its frontier list filtered by the edge's forwarding sets, the ReceivedFrom
+  // and author exclusions and randomsub's targets), k_push after the hop's
+  // publishes; the receiver's phase A reads its in-edges' segments instead of
+  // the senders' whole lists.  A segment is n 16-bit slots at an 8-aligned
+  // arena offset; ibxRec[p][rev[e]] = off << 24 | n, -1 = read the list (the
+  // arena was full)
+  uint16_t* ibx[2];
+  int64_t* ibxRec[2];
+  unsigned long long* ibxCnt;  // [2][GS_IBX_SUB] fill of each sub-arena (one per 128 B)
+  int64_t ibxCap;              // arena entries per parity (GS_IBX_SUB sub-arenas of ibxCap / GS_IBX_SUB)
   uint8_t* jrIn;  // [E] position of the receiver in the sender's row: rev[e] - rowptr[col[e]]
   double* score0;  // hop-start score memo (S0)
   double* score1;  // after the message phase (S1) / heartbeat memo
@@ -265,8 +279,13 @@ struct Dev {
   unsigned long long* pxqN;
   int64_t pxqCap;
   double acceptPX;
-  unsigned long long* poolCnt;  // [2] bump pointers
+  // each rank's arena segment [rank * poolSeg, +poolSeg) is split into poolSub
+  // sub-arenas of poolSubCap ids, each with its own bump counter (128 B apart)
+  unsigned long long* poolCnt;  // [2][poolSub * 16]
   int64_t poolCap;     // ids per arena
+  int64_t poolBase0;   // rank * poolSeg
+  int64_t poolSubCap;
+  int32_t poolSub;
   // message slots
   int32_t* slotSrc;
   int64_t* slotPubHop;
@@ -346,6 +365,18 @@ __device__ __forceinline__ int64_t prune_entry(const Dev& d, int64_t e, int t) {
   return px_peer(d, e) ? d.acc[t].pruneEnt : d.acc[t].pruneEnt10;
 }
 __device__ __forceinline__ void set_err(const Dev& d, int code);
+// n ids of this hop's arena (cur) for one wave or lane; ~0 = full (E_POOL
+// set).  The sub-arena is picked by blockIdx: a single counter serialised
+// about a million per-wave atomics at one L2 address.
+__device__ __forceinline__ unsigned long long pool_take(const Dev& d, int cur, unsigned long long n) {
+  const int s = (int)(blockIdx.x % (unsigned)d.poolSub);
+  const unsigned long long o = atomicAdd(&d.poolCnt[((int64_t)cur * d.poolSub + s) * 16], n);
+  if ((int64_t)(o + n) > d.poolSubCap) {
+    set_err(d, E_POOL);
+    return ~0ull;
+  }
+  return (unsigned long long)(d.poolBase0 + (int64_t)s * d.poolSubCap) + o;
+}
 __device__ __forceinline__ void trace_emit(const Dev& d, int64_t hop, int type, int node, int peer, int topic,
                                            int64_t msg, int phase, int reason = 0) {
   const unsigned long long k = atomicAdd(d.traceN, 1ull);
@@ -741,12 +772,9 @@ __device__ __forceinline__ int64_t arena_write(const Dev& d, int buf, const uint
   }
   if (total == 0) return -1;
   unsigned long long off = 0;
-  if (lane == 0) off = atomicAdd(&d.poolCnt[buf], (unsigned long long)total);
+  if (lane == 0) off = pool_take(d, buf, (unsigned long long)total);
   off = lane_get64(off, 0);
-  if ((int64_t)(off + total) > d.poolCap) {
-    if (lane == 0) set_err(d, E_POOL);
-    return -1;
-  }
+  if (off == ~0ull) return -1;
   int rowBase = (int)off;
 #pragma unroll
   for (int j = 0; j < WPL; ++j) {

@@ -646,6 +646,15 @@ int gs_engine::start() {
     x.fl[k] = dalloc<uint32_t>((size_t)N * x.FC); chk(x.fl[k]);
     x.fln[k] = dalloc<int32_t>(N); chk(x.fln[k]);
   }
+  // push arena: 32 copies per owned edge per hop (config4: about 25); a sender
+  // that finds it full leaves its edges to the list walk
+  x.ibxCap = std::max<int64_t>(1 << 20, 32 * (int64_t)(e1 - e0));
+  x.ibxCap = (x.ibxCap + 8 * GS_IBX_SUB - 1) / (8 * GS_IBX_SUB) * (8 * GS_IBX_SUB);  // 8-aligned sub-arenas
+  for (int k = 0; k < 2; ++k) {
+    x.ibx[k] = dalloc<uint16_t>((size_t)x.ibxCap); chk(x.ibx[k]);
+    x.ibxRec[k] = dalloc<int64_t>(E, 0xFF); chk(x.ibxRec[k]);
+  }
+  x.ibxCnt = dalloc<unsigned long long>(2 * GS_IBX_SUB * 16); chk(x.ibxCnt);
   x.maxDeg = std::max(1, maxdeg);
   x.stMagic = (uint32_t)(((1ull << 32) + (uint64_t)St - 1) / (uint64_t)St);
   x.tDivM = T == 1 ? 0 : ~0ull / (uint64_t)T + 1;  // ceil(2^64 / T)
@@ -688,11 +697,12 @@ int gs_engine::start() {
   const size_t NQ = (size_t)nOwnN * x.promCap;
   x.promMid = dalloc<int64_t>(NQ); x.promExp = dalloc<int64_t>(NQ); x.promSlot = dalloc<int32_t>(NQ);
   x.promEdge = dalloc<uint8_t>(NQ); x.promN = dalloc<int32_t>(nOwnN);
-  // mcache.peertx: a hash of 1024 entries per node in HBM.  With IWANT
-  // spammers present the honest requests grow too (messages dropped by
-  // validation queues come back through gossip), so those runs get 8192; the
-  // spammers' own requests, one per (message, spammer), are counted in spamCnt
-  x.ptxBits = (behaveAll & GS_BEHAVE_IWANT_SPAM) ? 13 : GS_PTX_BITS;
+  // mcache.peertx: a hash of 1024 slots per node in HBM.  With IWANT spammers
+  // present the honest requests grow too (messages dropped by validation
+  // queues come back through gossip; config5 at 1M peers: 43 live entries per
+  // node on average, 881 at most), so those runs get 4096; the spammers' own
+  // requests, one per (message, spammer), are counted in spamCnt
+  x.ptxBits = (behaveAll & GS_BEHAVE_IWANT_SPAM) ? 12 : GS_PTX_BITS;
   x.ptxT = dalloc<uint32_t>((size_t)nOwnN << x.ptxBits); x.ptxN = dalloc<int32_t>(nOwnN);
   chk(x.promMid); chk(x.promExp); chk(x.promSlot); chk(x.promEdge); chk(x.promN);
   chk(x.ptxT); chk(x.ptxN);
@@ -738,8 +748,18 @@ int gs_engine::start() {
   poolSeg = cfg.router == GS_ROUTER_GOSSIPSUB ? std::max<int64_t>((1 << 24) / world, 4 * (e1 - e0)) : 16;
   poolSeg = (poolSeg + 63) & ~63ll;
   x.poolCap = (int64_t)(rank + 1) * poolSeg;
+  // sub-arenas of at least 2^20 ids (one counter each) on an unpartitioned
+  // engine; a partitioned one keeps one counter so its used ids stay one
+  // prefix of its segment (the exchange ships that prefix)
+  {
+    int sub = 1;
+    while (world == 1 && sub < 256 && (poolSeg / (2 * sub)) >= (1 << 20)) sub *= 2;
+    x.poolSub = sub;
+    x.poolSubCap = poolSeg / sub;
+    x.poolBase0 = (int64_t)rank * poolSeg;
+  }
   for (int k = 0; k < 2; ++k) { x.pool[k] = dalloc<int32_t>((size_t)poolSeg * world); chk(x.pool[k]); }
-  x.poolCnt = dalloc<unsigned long long>(2); chk(x.poolCnt);
+  x.poolCnt = dalloc<unsigned long long>((size_t)2 * x.poolSub * 16); chk(x.poolCnt);
   x.doPX = doPX ? 1 : 0;
   x.PrunePeers = gp.PrunePeers;
   x.acceptPX = thr.AcceptPXThreshold;
@@ -1284,7 +1304,8 @@ int gs_engine::stepOne() {
     if (std::find(retireWords.begin(), retireWords.end(), w) == retireWords.end()) retireWords.push_back(w);
   }
   HIPCHECK(hipMemsetAsync(d.pubmask[cur], 0, (size_t)W * 8, stream));
-  k_set_u64<<<1, 1, 0, stream>>>(d.poolCnt + cur, (unsigned long long)rank * (unsigned long long)poolSeg);
+  HIPCHECK(hipMemsetAsync(d.poolCnt + (size_t)cur * d.poolSub * 16, 0, (size_t)d.poolSub * 16 * 8, stream));
+  HIPCHECK(hipMemsetAsync(d.ibxCnt + (size_t)cur * GS_IBX_SUB * 16, 0, GS_IBX_SUB * 16 * 8, stream));
   const int nOwn = n1 - n0;
   const int64_t eOwn = e1 - e0;
   const unsigned eb = nblk(eOwn, 256);
@@ -1381,6 +1402,8 @@ int gs_engine::stepOne() {
     k_publist<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, cur);
     if (d.sel) k_publish_rs<<<n, 64, 0, stream>>>(d, (int)b);
   }
+  // the copies the owned senders send next hop, per edge (phase A reads them)
+  if (nOwn) TIMED(this, GS_K_FWD, (k_push<<<nOwn, 64, 0, stream>>>(d, cur)));
   if (gossip) {
     if (scoring) TIMED(this, GS_K_SCORE, (score_rows<2>(d, eOwn, T, nullptr, stream)));
     // MaxIHaveLength cuts are possible only if the messages (phantom ids
@@ -1515,7 +1538,7 @@ int gs_engine::deviceErrorCode(int32_t err) {
                    "at most 512)");
       return GS_ECAPACITY;
     case E_PEERTX:
-      gs_set_error("per-node IWANT retransmission table overflow (1024 entries; 8192 with IWANT spammers)");
+      gs_set_error("per-node IWANT retransmission table overflow (1024 slots; 4096 with IWANT spammers)");
       return GS_ECAPACITY;
     case E_LATE:
       gs_set_error("a message was first delivered later than the message window allows; raise slots_per_topic");
@@ -1586,7 +1609,8 @@ int gs_engine::exchange(int cur, bool hb) {
   packLists();
   HIPCHECK(hipMemcpyAsync(xHost, xCnt, (size_t)world * 8, hipMemcpyDeviceToHost, stream));
   HIPCHECK(hipMemcpyAsync(xHost + world, bump, 8, hipMemcpyDeviceToHost, stream));
-  HIPCHECK(hipMemcpyAsync(xHost + world + 1, d.poolCnt + cur, 8, hipMemcpyDeviceToHost, stream));
+  HIPCHECK(hipMemcpyAsync(xHost + world + 1, d.poolCnt + (size_t)cur * d.poolSub * 16, 8, hipMemcpyDeviceToHost,
+                          stream));  // (poolSub == 1 when partitioned)
   // this rank's device error word travels with the sizes below, so every rank
   // stops at the same hop (a rank returning alone would leave the others
   // waiting in the next hop's collectives)
@@ -1596,7 +1620,7 @@ int gs_engine::exchange(int cur, bool hb) {
   const int32_t myErr = (int32_t)xHost[world + 2];
   const int64_t nEnt = (int64_t)xHost[world];
   const int64_t poolBase = (int64_t)rank * poolSeg;
-  const int64_t nPool = std::max<int64_t>(0, std::min<int64_t>((int64_t)xHost[world + 1], x_poolEnd()) - poolBase);
+  const int64_t nPool = std::min<int64_t>((int64_t)xHost[world + 1], poolSeg);
   const size_t entBytes = align8((size_t)nEnt * 4), poolBytes = align8((size_t)nPool * 4);
   const size_t gwBytes = hb ? (size_t)nOwn * W * 8 : 0;
   const size_t bcast = hdrBytes + entBytes + poolBytes + gwBytes;

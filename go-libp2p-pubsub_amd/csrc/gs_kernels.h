@@ -657,6 +657,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   __shared__ uint64_t sRelay[64], sPub[64];
   __shared__ int sSnd[64];        // sender node | jr << 24 | graylisted << 31
   __shared__ int sLn[64];
+  __shared__ int64_t sAddr[64];   // a sender's copies: its pushed segment, or its list
   __shared__ uint32_t sQ[GS_QCAP];         // sent copies awaiting delivery: slot | sender << 16
   __shared__ uint16_t sRk[64 * GS_MAX_WPL];  // rank of word w in amR, 0xFFFF = outside
   __shared__ uint16_t sYp[64 * GS_MAX_WPL];  // [rank] young slots in the amR words before it
@@ -674,6 +675,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   const bool scoring = d.scoring != 0 && gossipV;
   // in-edge metadata (lane = in-edge)
   int u = 0, jr = -1, Ln = 0;
+  int64_t pOff = -1;  // the pushed segment of this in-edge (k_push), -1 = the sender's list
   uint64_t relay = 0, pub = 0, relayAll = 0, pubAll = 0;
   bool gray = false;
   int irOff = 0, irN = 0;
@@ -695,8 +697,19 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
       irN = (int)(ir & 0xFFFFFF);
     }
     gray = scoring && !d.direct[e] && d.score0[e] < d.graylistThr;
-    if (relayAll | pubAll) Ln = d.fln[prv][u];
+    if (relayAll | pubAll) {
+      // an owned sender pushed this edge's copies (k_push): read that segment
+      if (u >= d.n0 && u < d.n1) {
+        const int64_t rec = d.ibxRec[prv][e];
+        if (rec >= 0) {
+          pOff = rec >> 24;
+          Ln = (int)(rec & 0xFFFFFF);
+        }
+      }
+      if (pOff < 0) Ln = d.fln[prv][u];
+    }
   }
+  const uint64_t pushM = __ballot(pOff >= 0);  // senders whose copies were pushed
   GS_STAMP(0);
   const bool authV = d.nAuth[v] > 0;  // v authored a live message: author exclusion possible
   for (int k = lane; k < nCntW / 4; k += 64) ((uint4*)scnt)[k] = make_uint4(0, 0, 0, 0);
@@ -769,6 +782,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   // sender node | jr << 24 | randomsub sender << 30 | graylisted << 31
   sSnd[lane] = valid ? (u | (jr << 24) | (rs_host(d, u) ? (1 << 30) : 0) | (gray ? (1 << 31) : 0)) : 0;
   sLn[lane] = Ln;
+  sAddr[lane] = pOff >= 0 ? pOff : (int64_t)u * FC;
   const uint64_t scoredT = __ballot(lane < T && scoring && d.tp[lane].scored);  // scored topics
   __syncthreads();
   GS_STAMP(1);
@@ -868,6 +882,16 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   // are compacted into an LDS queue and handed to fn 64 at a time by all lanes.
   // fn(i, slot) sees every sent, non-graylisted copy; walk() also counts
   // nSent / nGray when `count` (the first walk).
+  // block kb of sender i: four list entries (16 B), or four pushed slots (8 B)
+  const uint32_t* const flPrv = prv ? d.fl[1] : d.fl[0];
+  const uint16_t* const ibxPrv = prv ? d.ibx[1] : d.ibx[0];
+  auto load_block = [&](int i, int kb) -> uint4 {
+    if ((pushM >> i) & 1) {
+      const uint2 p = *(const uint2*)(ibxPrv + sAddr[i] + 4 * kb);
+      return make_uint4(p.x, p.y, 0u, 0u);
+    }
+    return *(const uint4*)(flPrv + sAddr[i] + 4 * kb);
+  };
   auto walk = [&](auto&& fn, bool count) {
     int qh = 0, qt = 0;  // queue head / tail (wave-uniform)
     int rankPrev = -1;   // rank (among non-empty senders) of the sender of the block before the window
@@ -892,7 +916,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
             const uint64_t ce = sComp[rank];
             si[rr] = (int)(ce >> 48);
             kb[rr] = bidx - (int)((ce >> 24) & 0xFFFFFF);
-            q[rr] = *(const uint4*)(d.fl[prv] + (int64_t)(ce & 0xFFFFFF) * FC + 4 * kb[rr]);
+            q[rr] = load_block(si[rr], kb[rr]);
           }
         } else if (bidx < totalBlk) {
           int lo = 0, hi = 63;  // last sender whose first block is <= bidx
@@ -902,8 +926,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
           }
           si[rr] = lo;
           kb[rr] = bidx - sBlk[lo];
-          const int uu = sSnd[lo] & 0xFFFFFF;
-          q[rr] = *(const uint4*)(d.fl[prv] + (int64_t)uu * FC + 4 * kb[rr]);
+          q[rr] = load_block(lo, kb[rr]);
         }
       }
 #pragma unroll
@@ -919,6 +942,22 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
           const bool isGray = snd < 0;
           const uint64_t rl = sRelay[i], pb = sPub[i];
           const int n = si[rr] < 0 ? 0 : min(4, sLn[i] - 4 * kb[rr]);
+          if ((pushM >> i) & 1) {
+            // pushed: every copy was sent; the topics v left are only counted
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const uint32_t wd = c < 2 ? q[rr].x : q[rr].y;
+              const int slot = (int)((c & 1) ? (wd >> 16) : (wd & 0xFFFFu));
+              const int t = (int)__umulhi((unsigned)slot, d.stMagic);
+              const bool sent = c < n && !(authV && d.slotSrc[slot] == v);  // never to the author
+              if (count) {
+                nSent += sent;
+                if (sent && isGray) ++nGray;
+              }
+              sn[c] = sent && !isGray && ((sv >> t) & 1);
+              en[c] = (uint32_t)slot | ((uint32_t)i << 16);
+            }
+          } else {
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const uint32_t ent = c == 0 ? q[rr].x : (c == 1 ? q[rr].y : (c == 2 ? q[rr].z : q[rr].w));
@@ -935,6 +974,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
             }
             sn[c] = sent && !isGray;
             en[c] = (uint32_t)slot | ((uint32_t)i << 16);
+          }
           }
         }
         // c-major positions (delivery order does not matter: every update is
@@ -1004,7 +1044,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
     // copies of topics v is not subscribed to: transmitted, then ignored
     // (churn runs only: a mesh or announced peer that has just left)
     const uint64_t ru = relayAll & ~sv, pu = pubAll & ~sv;
-    if ((ru | pu) && valid) {
+    if ((ru | pu) && valid && pOff < 0) {  // (a pushed segment's were counted by the walk)
       const uint32_t* L = d.fl[prv] + (int64_t)u * FC;
       for (int k = 0; k < Ln; ++k) {
         const uint32_t ent = L[k];
@@ -1369,7 +1409,8 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
       // received from this sender (its accepted copies), in an extra RPC
       auto each = [&](auto&& fn) {
         const uint32_t* L = d.fl[prv] + (int64_t)u * FC;
-        for (int k = 0; k < Ln; ++k) {
+        const int nL = pOff >= 0 ? d.fln[prv][u] : Ln;  // the sender's whole list
+        for (int k = 0; k < nL; ++k) {
           const uint32_t ent = L[k];
           const int slot = (int)(ent & 0xFFFF), tag = (int)(ent >> 16);
           const int t = (int)__umulhi((unsigned)slot, d.stMagic);
@@ -1384,9 +1425,8 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
       int n = 0;
       each([&](int) { ++n; });
       if (n) {
-        const unsigned long long off = atomicAdd(&d.poolCnt[cur], (unsigned long long)n);
-        if ((int64_t)(off + n) > d.poolCap) {
-          set_err(d, E_POOL);
+        const unsigned long long off = pool_take(d, cur, (unsigned long long)n);
+        if (off == ~0ull) {  // arena full (E_POOL)
         } else {
           int p = (int)off;
           each([&](int slot) { d.pool[cur][p++] = slot; });
@@ -1602,6 +1642,122 @@ __global__ void k_publist(Dev d, int b, int n, int cur) {
     ++len;
   }
   d.fln[cur][src] = len;
+}
+
+// Lane t gets column t of the 64 x 64 bit matrix whose row j is lane j's x:
+// bit j of the result = bit t of lane j's x (butterfly block swaps).
+__device__ __forceinline__ uint64_t wave_transpose64(uint64_t x) {
+  const int lane = lane_id();
+  const uint64_t lo[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
+                          0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const int s = 32 >> k;
+    const uint64_t m = lo[k];
+    const uint64_t y = shfl_u64(x, lane ^ s);
+    x = (lane & s) ? (((y & ~m) >> s) | (x & ~m)) : ((x & m) | ((y & m) << s));
+  }
+  return x;
+}
+
+// Push (Dev::ibx): the copies owned sender u sends on each edge to an owned
+// receiver in the next hop's phase A — its frontier list fl[cur][u] (first
+// deliveries of this hop and its publishes) filtered per edge as the
+// receiver's list walk would: the edge's forwarding sets (relay for first
+// deliveries, pub for tag 255; every topic of the sets, the receiver drops
+// the topics it left), never back to the first deliverer (tag == the
+// receiver's position in u's row, gossipsub.go:1003), and randomsub's
+// targets.  The author exclusion stays with the receiver (a cheap test there).
+// One wave per sender: the edges' sets transposed to per-topic edge masks,
+// then lane = list entry: its edge mask, a count pass (LDS counters), one
+// arena allocation for the sender's segments (each 8-aligned, in row order),
+// the slots staged in LDS (order within a segment is free: the receiver's
+// updates commute) and stored coalesced; a sender with more than GS_PUSHL
+// copies stores them directly.  Records go to the receiver's in-edge; an edge
+// to a receiver on another rank is left to the receiver's list walk, as is
+// every edge of a sender that finds the arena full (record -1).
+#define GS_PUSHL 4096
+__global__ __launch_bounds__(64) void k_push(Dev d, int cur) {
+  __shared__ uint64_t sMR[64], sMP[64];
+  __shared__ int sCnt[64], sRun[64], sPre[64];
+  __shared__ __attribute__((aligned(16))) uint16_t sOut[GS_PUSHL];
+  __shared__ unsigned long long sBase;
+  const int u = d.n0 + blockIdx.x;
+  const int lane = lane_id();
+  const int64_t base = d.rowptr[u];
+  const int deg = (int)(d.rowptr[u + 1] - base);
+  const int64_t e = base + lane;
+  bool local = false;
+  uint64_t relay = 0, pub = 0;
+  int64_t re = 0;
+  if (lane < deg) {
+    const int recv = d.col[e];
+    local = recv >= d.n0 && recv < d.n1;
+    if (local) {
+      re = d.rev[e];
+      relay = d.fwdRelay[cur][e];
+      pub = d.fwdPub[cur][e];
+    }
+  }
+  const int Ln = __ballot((relay | pub) != 0) ? d.fln[cur][u] : 0;
+  if (Ln == 0) {
+    if (local) d.ibxRec[cur][re] = 0;  // nothing sent
+    return;
+  }
+  sMR[lane] = wave_transpose64(relay);  // edges whose relay set holds topic `lane`
+  sMP[lane] = wave_transpose64(pub);
+  sCnt[lane] = 0;
+  sRun[lane] = 0;
+  __syncthreads();
+  const bool rs = rs_host(d, u);
+  const uint32_t* L = d.fl[cur] + (int64_t)u * d.FC;
+  // the edges entry k goes out on
+  auto dest = [&](int k, int& slot) -> uint64_t {
+    const uint32_t ent = L[k];
+    slot = (int)(ent & 0xFFFF);
+    const int tag = (int)(ent >> 16);
+    const int t = (int)__umulhi((unsigned)slot, d.stMagic);
+    uint64_t m = tag == 255 ? sMP[t] : (sMR[t] & ~(1ull << (tag & 63)));
+    if (rs) m &= d.sel[(int64_t)u * d.S + slot];
+    return m;
+  };
+  for (int k = lane; k < Ln; k += 64) {
+    int slot;
+    for (uint64_t m = dest(k, slot); m; m &= m - 1) atomicAdd(&sCnt[__ffsll((long long)m) - 1], 1);
+  }
+  __syncthreads();
+  const int cnt = sCnt[lane];
+  const int seg = (cnt + 7) & ~7;
+  const int incl = wave_incl_sum(seg);
+  const int total = wave_last(incl);
+  const int pre = incl - seg;
+  sPre[lane] = pre;
+  // sub-arena blockIdx % GS_IBX_SUB: its own counter, 16 words apart
+  const int64_t subCap = d.ibxCap / GS_IBX_SUB;
+  const int sub = (int)(blockIdx.x & (GS_IBX_SUB - 1));
+  if (lane == 0) sBase = atomicAdd(&d.ibxCnt[((int64_t)cur * GS_IBX_SUB + sub) * 16], (unsigned long long)total);
+  __syncthreads();
+  const unsigned long long A = (unsigned long long)(sub * subCap) + sBase;
+  if (sBase + total > (unsigned long long)subCap) {
+    if (local) d.ibxRec[cur][re] = -1;  // arena full: the receiver walks u's list
+    return;
+  }
+  const bool staged = total <= GS_PUSHL;
+  uint16_t* const out = staged ? sOut : d.ibx[cur] + A;
+  for (int k = lane; k < Ln; k += 64) {
+    int slot;
+    for (uint64_t m = dest(k, slot); m; m &= m - 1) {
+      const int j = __ffsll((long long)m) - 1;
+      out[sPre[j] + atomicAdd(&sRun[j], 1)] = (uint16_t)slot;
+    }
+  }
+  if (staged) {
+    __syncthreads();
+    const uint4* src = (const uint4*)sOut;
+    uint4* dst = (uint4*)(d.ibx[cur] + A);
+    for (int k = lane; k < total / 8; k += 64) dst[k] = src[k];
+  }
+  if (local) d.ibxRec[cur][re] = ((int64_t)(A + pre) << 24) | (int64_t)cnt;
 }
 
 // Randomsub targets of the messages published this hop (one wave per message).

@@ -119,11 +119,8 @@ __device__ __forceinline__ void px_append(const Dev& d, int cur, int64_t re, int
   const int64_t old = d.cPx[cur][re];
   const int on = old >= 0 ? (int)(old & 0xFFFFFF) : 0;
   const int64_t oo = old >= 0 ? (old >> 24) : 0;
-  const unsigned long long off = atomicAdd(&d.poolCnt[cur], (unsigned long long)(on + k));
-  if ((int64_t)(off + on + k) > d.poolCap) {
-    set_err(d, E_POOL);
-    return;
-  }
+  const unsigned long long off = pool_take(d, cur, (unsigned long long)(on + k));
+  if (off == ~0ull) return;
   for (int q = 0; q < on; ++q) d.pool[cur][off + q] = d.pool[cur][oo + q];
   int w = on;
   for (uint64_t m = list; m; m &= m - 1)
@@ -687,12 +684,11 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
     srvR = sCnt[lane];
     srvS = sCntS[lane];
     const int myOff = lane_prefix(myServed, &totalServed);
-    if (lane == 0 && totalServed) sBase = atomicAdd(&d.poolCnt[cur], (unsigned long long)totalServed);
+    if (lane == 0 && totalServed) sBase = pool_take(d, cur, (unsigned long long)totalServed);
     __syncthreads();
     if (totalServed) {
       const unsigned long long poolBase = sBase;
-      if (poolBase + totalServed > (unsigned long long)d.poolCap) {
-        if (lane == 0) set_err(d, E_POOL);
+      if (poolBase == ~0ull) {  // arena full (E_POOL)
         nSrv = 0;
       } else {
         sOut[lane] = (int)poolBase + myOff;
@@ -977,12 +973,11 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
     const uint64_t cutSenders = __ballot(iaCut);
     int totalWant;
     const int myOff = lane_prefix(myWant, &totalWant);
-    if (lane == 0 && totalWant) sBase = atomicAdd(&d.poolCnt[cur], (unsigned long long)totalWant);
+    if (lane == 0 && totalWant) sBase = pool_take(d, cur, (unsigned long long)totalWant);
     __syncthreads();
     if (totalWant) {
       const unsigned long long poolBase = sBase;
-      if (poolBase + totalWant > (unsigned long long)d.poolCap) {
-        if (lane == 0) set_err(d, E_POOL);
+      if (poolBase == ~0ull) {  // arena full (E_POOL)
       } else {
         sOut[lane] = (int)poolBase + myOff;
         __syncthreads();
