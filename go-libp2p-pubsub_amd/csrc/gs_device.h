@@ -53,9 +53,8 @@
 #endif
 #define GS_QCAP 320    // phase A delivery queue (>= 63 pending + 256 appended per sub-round)
 #define GS_BMAP 32     // phase A: list blocks mapped to senders without a search (64 per entry)
-// push arena: the senders' allocations spread over this many counters (a
-// single counter serialised a million per-wave atomics at one L2 address)
-#define GS_IBX_SUB 512
+// push arena: a region of this many 16-bit slots per owned sender
+#define GS_PUSHR 2048
 #define GS_PTX_BITS 10 // mcache.peertx hash slots per node: 2^10 (2^12 when IWANT spammers run)
 #define GS_CUTS 64     // IHAVE entries above MaxIHaveLength one node can cut per hop
 // phase B dynamic LDS: the MaxIHaveLength-cut tables (cut mode)
@@ -233,15 +232,13 @@ struct Dev {
   ulonglong2* fwdIn[2];
   // push: the copies each owned sender sends on each edge to an owned receiver
   // (its frontier list filtered by the edge's forwarding sets, the ReceivedFrom
-  // and author exclusions and randomsub's targets), k_push after the hop's
-  // publishes; the receiver's phase A reads its in-edges' segments instead of
-  // the senders' whole lists.  A segment is n 16-bit slots at an 8-aligned
-  // arena offset; ibxRec[p][rev[e]] = off << 24 | n, -1 = read the list (the
-  // arena was full)
-  uint16_t* ibx[2];
+  // exclusion and randomsub's targets), k_push after the hop's publishes; the
+  // receiver's phase A reads its in-edges' segments instead of the senders'
+  // whole lists.  A segment is n 16-bit slots at an 8-aligned offset of the
+  // sender's GS_PUSHR-slot region; ibxRec[p][rev[e]] = off << 24 | n, -1 =
+  // read the list (the sender's copies overflowed its region)
+  uint16_t* ibx[2];  // [owned senders][GS_PUSHR]
   int64_t* ibxRec[2];
-  unsigned long long* ibxCnt;  // [2][GS_IBX_SUB] fill of each sub-arena (one per 128 B)
-  int64_t ibxCap;              // arena entries per parity (GS_IBX_SUB sub-arenas of ibxCap / GS_IBX_SUB)
   uint8_t* jrIn;  // [E] position of the receiver in the sender's row: rev[e] - rowptr[col[e]]
   double* score0;  // hop-start score memo (S0)
   double* score1;  // after the message phase (S1) / heartbeat memo

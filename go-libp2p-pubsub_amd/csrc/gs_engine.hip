@@ -646,15 +646,11 @@ int gs_engine::start() {
     x.fl[k] = dalloc<uint32_t>((size_t)N * x.FC); chk(x.fl[k]);
     x.fln[k] = dalloc<int32_t>(N); chk(x.fln[k]);
   }
-  // push arena: 32 copies per owned edge per hop (config4: about 25); a sender
-  // that finds it full leaves its edges to the list walk
-  x.ibxCap = std::max<int64_t>(1 << 20, 32 * (int64_t)(e1 - e0));
-  x.ibxCap = (x.ibxCap + 8 * GS_IBX_SUB - 1) / (8 * GS_IBX_SUB) * (8 * GS_IBX_SUB);  // 8-aligned sub-arenas
+  // push arena: a region of GS_PUSHR slots (4 KiB) per owned sender and parity
   for (int k = 0; k < 2; ++k) {
-    x.ibx[k] = dalloc<uint16_t>((size_t)x.ibxCap); chk(x.ibx[k]);
+    x.ibx[k] = dalloc<uint16_t>((size_t)std::max<int64_t>(nOwnN, 1) * GS_PUSHR); chk(x.ibx[k]);
     x.ibxRec[k] = dalloc<int64_t>(E, 0xFF); chk(x.ibxRec[k]);
   }
-  x.ibxCnt = dalloc<unsigned long long>(2 * GS_IBX_SUB * 16); chk(x.ibxCnt);
   x.maxDeg = std::max(1, maxdeg);
   x.stMagic = (uint32_t)(((1ull << 32) + (uint64_t)St - 1) / (uint64_t)St);
   x.tDivM = T == 1 ? 0 : ~0ull / (uint64_t)T + 1;  // ceil(2^64 / T)
@@ -1305,7 +1301,6 @@ int gs_engine::stepOne() {
   }
   HIPCHECK(hipMemsetAsync(d.pubmask[cur], 0, (size_t)W * 8, stream));
   HIPCHECK(hipMemsetAsync(d.poolCnt + (size_t)cur * d.poolSub * 16, 0, (size_t)d.poolSub * 16 * 8, stream));
-  HIPCHECK(hipMemsetAsync(d.ibxCnt + (size_t)cur * GS_IBX_SUB * 16, 0, GS_IBX_SUB * 16 * 8, stream));
   const int nOwn = n1 - n0;
   const int64_t eOwn = e1 - e0;
   const unsigned eb = nblk(eOwn, 256);

@@ -1061,18 +1061,36 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
       }
     }
   }
-  // ---- pass 1b: IWANT responses (in the sender's reply RPCs, rare)
+  // ---- pass 1b: IWANT responses (in the sender's reply RPCs): every served
+  // id of every accepted sender is one work item, spread over the lanes (an
+  // IWANT spammer gets hundreds from one sender)
   nSent += irN;
-  if (!gray) {
-    if (ADV && ctlGated) {
-      nGatedCopies += nSrvRpc;  // the served replies' payload is ignored
-    } else {
-      for (int k = 0; k < irN; ++k) {
-        const int slot = d.pool[prv][irOff + k];
-        if ((sv >> (int)__umulhi((unsigned)slot, d.stMagic)) & 1) deliver(lane, slot, false);
-      }
-    }
+  if (!gray && ADV && ctlGated) nGatedCopies += nSrvRpc;  // the served replies' payload is ignored
+  __shared__ int sIrP[65], sIrO[64];  // exclusive prefix of the accepted senders' served ids, their arena offsets
+  int irTot;
+  {
+    const int myIr = (!gray && !(ADV && ctlGated)) ? irN : 0;
+    const int incl = wave_incl_sum(myIr);
+    irTot = wave_last(incl);
+    sIrP[lane] = incl - myIr;
+    if (lane == 0) sIrP[64] = irTot;
+    sIrO[lane] = irOff;
   }
+  __syncthreads();
+  // fn(sender, slot) for every accepted served id
+  auto eachIr = [&](auto&& fn) {
+    for (int idx = lane; idx < irTot; idx += 64) {
+      int lo = 0, hi = 63;  // last sender whose first item is <= idx
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (sIrP[mid] <= idx) lo = mid; else hi = mid - 1;
+      }
+      fn(lo, d.pool[prv][sIrO[lo] + idx - sIrP[lo]]);
+    }
+  };
+  eachIr([&](int i, int slot) {
+    if ((sv >> (int)__umulhi((unsigned)slot, d.stMagic)) & 1) deliver(i, slot, false);
+  });
   if constexpr (ADV) {
     if (ctlGated) throttled |= 1ull << lane;
     // lane-uniform set of throttled senders
@@ -1115,6 +1133,9 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
     }
   }
   bool anyDrop = false;
+  bool staged = false;          // ADV: the validator topics' fresh messages staged (cs / ck)
+  int cs[4] = {-1, -1, -1, -1};
+  unsigned long long ck[4] = {0, 0, 0, 0};
   if constexpr (ADV) {
     // ---- the validation queue: the first valQueue fresh messages of topics
     // with a validator, in arrival order (first deliverer, then message id),
@@ -1129,7 +1150,49 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
     }
     const int candIncl = wave_incl_sum(nCand);
     const int nAll = wave_last(candIncl);
+    // up to 256 candidates are staged in registers (four per lane, slot and
+    // key ff << 56 | mid, their loads in flight together): the selection and
+    // the verdicts below run lane-parallel instead of one lane per word
+    staged = nAll <= 256;
+    if (staged && nAll > 0) {
+      int pos = candIncl - nCand;
+#pragma unroll
+      for (int j = 0; j < WPL; ++j) {
+        const int w = lane + 64 * j;
+        const int t = (int)__umulhi((unsigned)(w * 64), d.stMagic);
+        if (!((d.topicVal >> t) & 1)) continue;
+        for (uint64_t y = Uw[j] & ~Sw[j]; y; y &= y - 1) sQ[pos++] = (uint32_t)(w * 64 + __ffsll((long long)y) - 1);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 4; ++k) cs[k] = lane + 64 * k < nAll ? (int)sQ[lane + 64 * k] : -1;
+      __syncthreads();  // sQ is the selection's histogram below
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (cs[k] < 0) continue;
+        const int slot = cs[k];
+        ck[k] = ((unsigned long long)sFirst[fidx(sRk[slot >> 6], slot & 63)] << 56) |
+                (unsigned long long)d.slotMid[slot];
+      }
+    }
     if (d.valQueue > 0 && nAll > d.valQueue) {
+      unsigned long long K;
+      long long M;
+      if (staged) {
+        auto each = [&](auto&& fn) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (cs[k] >= 0) fn(ck[k], (long long)d.slotMid[cs[k]]);
+        };
+        select_kth(each, d.valQueue, sQ, K, M);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (cs[k] < 0 || ck[k] <= K) continue;
+          const int slot = cs[k];
+          atomicOr((unsigned long long*)&sDrop[sRk[slot >> 6]], 1ull << (slot & 63));
+          if (prow >= 0) d.pmask[(int64_t)prow * d.S + slot] = 0;  // never seen: no record
+        }
+      } else {
       // the valQueue-th smallest key ff << 56 | mid (radix select over the
       // lanes' own fresh words; the walk queue's LDS is free now)
       auto each = [&](auto&& fn) {
@@ -1147,8 +1210,6 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
           }
         }
       };
-      unsigned long long K;
-      long long M;
       select_kth(each, d.valQueue, sQ, K, M);
 #pragma unroll
       for (int j = 0; j < WPL; ++j) {
@@ -1167,7 +1228,24 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
           }
         }
       }
+      }
       anyDrop = true;
+      __syncthreads();
+    }
+    if (staged && nAll > 0) {
+      // verdicts of the staged candidates that were not dropped: REJECT /
+      // IGNORE are seen but not delivered; sD (pass 1's delivered words, read
+      // above) collects them per word rank
+      for (int k = lane; k < nR; k += 64) sD[k] = 0ull;
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (cs[k] < 0) continue;
+        const int slot = cs[k], rk = sRk[slot >> 6];
+        if (anyDrop && ((sDrop[rk] >> (slot & 63)) & 1)) continue;
+        const int kd = d.slotKind[slot];
+        if (kd == GS_MSG_REJECT || kd == GS_MSG_IGNORE) atomicOr((unsigned long long*)&sD[rk], 1ull << (slot & 63));
+      }
       __syncthreads();
     }
     nValidated = nAll < d.valQueue || d.valQueue == 0 ? nAll : d.valQueue;
@@ -1180,7 +1258,9 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
       if (Uw[j]) {
         if (anyDrop) Uw[j] &= ~sDrop[rkw[j]];
         const int t = (int)__umulhi((unsigned)(w * 64), d.stMagic);
-        if ((d.topicVal >> t) & 1) {
+        if (staged) {
+          if ((d.topicVal >> t) & 1) Xw[j] = sD[rkw[j]] & Uw[j];  // the staged verdicts
+        } else if ((d.topicVal >> t) & 1) {
           // verdicts: REJECT / IGNORE are seen but not delivered
           uint64_t y = Uw[j];
           while (y) {
@@ -1237,8 +1317,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
       // tables), the gater's throttle, and it fulfils promises (gossip_tracer.go:133)
       dropPass = true;
       walk(onCopy, false);
-      if (!gray && !ctlGated)
-        for (int k = 0; k < irN; ++k) drop(lane, d.pool[prv][irOff + k], false);
+      eachIr([&](int i, int slot) { drop(i, slot, false); });
       __syncthreads();
     }
     if (scoring && (anyDrop || throttled)) {
@@ -1404,6 +1483,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
         }
       }
     }
+    GS_STAMP(6);
     if (d.cSpam[cur] != nullptr && valid && !gray && behaves(d, v, GS_BEHAVE_IWANT_SPAM) && mesh_peer(d, base + lane)) {
       // IWANT spam (gossipsub_spam_test.go:113-128): one request per message
       // received from this sender (its accepted copies), in an extra RPC
@@ -1445,9 +1525,18 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
       }
     }
   }
+  GS_STAMP(7);
   // ---- pass 2b: the stores of the first deliveries (after pass 3's loads,
   // which would otherwise wait for them)
   int running = 0;  // rank of the next entry of v's own frontier list
+  // loop invariants read once (the ADV Dev lives in device memory, and every
+  // store below could alias it for the compiler)
+  const bool noFwd = behaves(d, v, GS_BEHAVE_NO_FORWARD);  // a squatter relays nothing
+  const bool needAge = d.needAge, record = d.record;
+  int16_t* const ageRow = needAge ? d.age + (int64_t)v * d.S : nullptr;
+  uint8_t* const ffRow = record ? d.ffrom + (int64_t)v * d.S : nullptr;
+  const int64_t* const pubHop = d.slotPubHop;
+  uint64_t* const pmRow = prow >= 0 ? d.pmask + (int64_t)prow * d.S : nullptr;
 #pragma unroll
   for (int j = 0; j < WPL; ++j) {
     const int w = lane + 64 * j;
@@ -1462,26 +1551,44 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
       d.seen[(int64_t)v * W + w] = Sw[j] | U;
       if (gossipV && Ud) d.hist[((int64_t)head * d.nOwnH + (v - d.n0)) * W + w] = Hw[j] | Ud;
       nDeliv += k;
-      uint64_t y = Ud;
-      while (y) {
-        const int b = __ffsll((long long)y) - 1;
-        y &= y - 1;
+      // one first delivery: trace, drec.peers, v's frontier list, age / deliverer
+      auto put = [&](int b, int64_t ph) {
         const int slot = w * 64 + b;
         const int ff = sFirst[fidx(rkw[j], b)];
         if (trv)  // pubsub.go:1057, ReceivedFrom = the first deliverer
           trace_emit(d, h, GS_TRACE_DELIVER_MESSAGE, v, d.col[base + ff], (int)__umulhi((unsigned)slot, d.stMagic),
                      d.slotMid[slot], 2);
-        if (prow >= 0)  // DeliverMessage does not add the deliverer to drec.peers
-          atomicAnd((unsigned long long*)&d.pmask[(int64_t)prow * d.S + slot], ~(1ull << ff));
-        if (!behaves(d, v, GS_BEHAVE_NO_FORWARD)) {  // a squatter relays nothing
+        if (pmRow != nullptr)  // DeliverMessage does not add the deliverer to drec.peers
+          atomicAnd((unsigned long long*)&pmRow[slot], ~(1ull << ff));
+        if (!noFwd) {
           if (rank < FC) Lv[rank] = (uint32_t)slot | ((uint32_t)ff << 16);
           else set_err(d, E_FCAP);
         }
         ++rank;
-        if (d.needAge || d.record) {
-          const int64_t a = h - d.slotPubHop[slot];
-          if (d.needAge) d.age[(int64_t)v * d.S + slot] = (int16_t)a;
-          if (d.record) d.ffrom[(int64_t)v * d.S + slot] = (uint8_t)ff;
+        if (needAge) ageRow[slot] = (int16_t)(h - ph);
+        if (record) ffRow[slot] = (uint8_t)ff;
+      };
+      uint64_t y = Ud;
+      if (needAge) {
+        while (y) {  // four messages at a time: their publish hops in flight together
+          int bs[4];
+          int64_t ph[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            bs[q] = y ? __ffsll((long long)y) - 1 : -1;
+            y &= y ? y - 1 : 0ull;
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ph[q] = bs[q] >= 0 ? pubHop[w * 64 + bs[q]] : 0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (bs[q] >= 0) put(bs[q], ph[q]);
+        }
+      } else {
+        while (y) {
+          const int b = __ffsll((long long)y) - 1;
+          y &= y - 1;
+          put(b, 0);
         }
       }
     }
@@ -1669,24 +1776,28 @@ __device__ __forceinline__ uint64_t wave_transpose64(uint64_t x) {
 // receiver's position in u's row, gossipsub.go:1003), and randomsub's
 // targets.  The author exclusion stays with the receiver (a cheap test there).
 // One wave per sender: the edges' sets transposed to per-topic edge masks,
-// then lane = list entry: its edge mask, a count pass (LDS counters), one
-// arena allocation for the sender's segments (each 8-aligned, in row order),
-// the slots staged in LDS (order within a segment is free: the receiver's
-// updates commute) and stored coalesced; a sender with more than GS_PUSHL
-// copies stores them directly.  Records go to the receiver's in-edge; an edge
-// to a receiver on another rank is left to the receiver's list walk, as is
-// every edge of a sender that finds the arena full (record -1).
-#define GS_PUSHL 4096
+// then lane = list entry: its edge mask, a count pass (LDS counters), the
+// segments laid out 8-aligned in row order in the sender's own region of the
+// arena (GS_PUSHR slots, no allocation), staged in LDS (order within a
+// segment is free: the receiver's updates commute) and stored coalesced.
+// Records go to the receiver's in-edge; an edge to a receiver on another
+// rank is left to the receiver's list walk, as is every edge of a sender
+// whose copies overflow its region (record -1).
 __global__ __launch_bounds__(64) void k_push(Dev d, int cur) {
   __shared__ uint64_t sMR[64], sMP[64];
   __shared__ int sCnt[64], sRun[64], sPre[64];
-  __shared__ __attribute__((aligned(16))) uint16_t sOut[GS_PUSHL];
-  __shared__ unsigned long long sBase;
+  __shared__ __attribute__((aligned(16))) uint16_t sOut[GS_PUSHR];
   const int u = d.n0 + blockIdx.x;
   const int lane = lane_id();
   const int64_t base = d.rowptr[u];
   const int deg = (int)(d.rowptr[u + 1] - base);
   const int64_t e = base + lane;
+  const uint32_t* L = d.fl[cur] + (int64_t)u * d.FC;
+  // everything the wave needs first, loaded at once: the list length, the
+  // first 64 entries (speculatively: a list slot past fln holds stale data),
+  // the edges' sets
+  const int Ln0 = d.fln[cur][u];
+  const uint32_t ent0 = L[lane];
   bool local = false;
   uint64_t relay = 0, pub = 0;
   int64_t re = 0;
@@ -1699,7 +1810,7 @@ __global__ __launch_bounds__(64) void k_push(Dev d, int cur) {
       pub = d.fwdPub[cur][e];
     }
   }
-  const int Ln = __ballot((relay | pub) != 0) ? d.fln[cur][u] : 0;
+  const int Ln = __ballot((relay | pub) != 0) ? Ln0 : 0;
   if (Ln == 0) {
     if (local) d.ibxRec[cur][re] = 0;  // nothing sent
     return;
@@ -1710,10 +1821,8 @@ __global__ __launch_bounds__(64) void k_push(Dev d, int cur) {
   sRun[lane] = 0;
   __syncthreads();
   const bool rs = rs_host(d, u);
-  const uint32_t* L = d.fl[cur] + (int64_t)u * d.FC;
   // the edges entry k goes out on
-  auto dest = [&](int k, int& slot) -> uint64_t {
-    const uint32_t ent = L[k];
+  auto dest = [&](uint32_t ent, int& slot) -> uint64_t {
     slot = (int)(ent & 0xFFFF);
     const int tag = (int)(ent >> 16);
     const int t = (int)__umulhi((unsigned)slot, d.stMagic);
@@ -1723,7 +1832,7 @@ __global__ __launch_bounds__(64) void k_push(Dev d, int cur) {
   };
   for (int k = lane; k < Ln; k += 64) {
     int slot;
-    for (uint64_t m = dest(k, slot); m; m &= m - 1) atomicAdd(&sCnt[__ffsll((long long)m) - 1], 1);
+    for (uint64_t m = dest(k < 64 ? ent0 : L[k], slot); m; m &= m - 1) atomicAdd(&sCnt[__ffsll((long long)m) - 1], 1);
   }
   __syncthreads();
   const int cnt = sCnt[lane];
@@ -1731,33 +1840,25 @@ __global__ __launch_bounds__(64) void k_push(Dev d, int cur) {
   const int incl = wave_incl_sum(seg);
   const int total = wave_last(incl);
   const int pre = incl - seg;
-  sPre[lane] = pre;
-  // sub-arena blockIdx % GS_IBX_SUB: its own counter, 16 words apart
-  const int64_t subCap = d.ibxCap / GS_IBX_SUB;
-  const int sub = (int)(blockIdx.x & (GS_IBX_SUB - 1));
-  if (lane == 0) sBase = atomicAdd(&d.ibxCnt[((int64_t)cur * GS_IBX_SUB + sub) * 16], (unsigned long long)total);
-  __syncthreads();
-  const unsigned long long A = (unsigned long long)(sub * subCap) + sBase;
-  if (sBase + total > (unsigned long long)subCap) {
-    if (local) d.ibxRec[cur][re] = -1;  // arena full: the receiver walks u's list
+  if (total > GS_PUSHR) {
+    if (local) d.ibxRec[cur][re] = -1;  // region overflow: the receiver walks u's list
     return;
   }
-  const bool staged = total <= GS_PUSHL;
-  uint16_t* const out = staged ? sOut : d.ibx[cur] + A;
+  sPre[lane] = pre;
+  __syncthreads();
   for (int k = lane; k < Ln; k += 64) {
     int slot;
-    for (uint64_t m = dest(k, slot); m; m &= m - 1) {
+    for (uint64_t m = dest(k < 64 ? ent0 : L[k], slot); m; m &= m - 1) {
       const int j = __ffsll((long long)m) - 1;
-      out[sPre[j] + atomicAdd(&sRun[j], 1)] = (uint16_t)slot;
+      sOut[sPre[j] + atomicAdd(&sRun[j], 1)] = (uint16_t)slot;
     }
   }
-  if (staged) {
-    __syncthreads();
-    const uint4* src = (const uint4*)sOut;
-    uint4* dst = (uint4*)(d.ibx[cur] + A);
-    for (int k = lane; k < total / 8; k += 64) dst[k] = src[k];
-  }
-  if (local) d.ibxRec[cur][re] = ((int64_t)(A + pre) << 24) | (int64_t)cnt;
+  __syncthreads();
+  const int64_t A = (int64_t)(u - d.n0) * GS_PUSHR;
+  const uint4* src = (const uint4*)sOut;
+  uint4* dst = (uint4*)(d.ibx[cur] + A);
+  for (int k = lane; k < total / 8; k += 64) dst[k] = src[k];
+  if (local) d.ibxRec[cur][re] = ((A + pre) << 24) | (int64_t)cnt;
 }
 
 // Randomsub targets of the messages published this hop (one wave per message).

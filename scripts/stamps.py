@@ -40,9 +40,12 @@ def main():
     s5 = s5[(s5[:, 0] > 0) & (s5[:, 4] > 0) & (s5[:, 5] > 0)]
     if len(s5):
         print(f"  pass3 rmw only: mean {(s5[:, 5] - s5[:, 3]).mean():.0f}, pass2b stores: mean {(s5[:, 4] - s5[:, 5]).mean():.0f}")
-    c = buf.reshape(-1, 8)[: len(buf) // 16, 5:8].astype(np.int64)
-    print("copies/node mean", c[:, 0].mean(), "pass-1 list-load cycles mean", c[:, 1].mean(), "pass-1 delivery-drain cycles mean",
-          c[:, 2].mean())
+    s8 = buf.reshape(-1, 8)[: len(buf) // 16, :8].astype(np.int64)
+    s8 = s8[(s8[:, 3] > 0) & (s8[:, 5] > 0) & (s8[:, 6] > 0) & (s8[:, 7] > 0) & (s8[:, 4] > 0)]
+    if len(s8):
+        print(f"  pass3 split: rmw {(s8[:, 5] - s8[:, 3]).mean():.0f}, P4 + gater {(s8[:, 6] - s8[:, 5]).mean():.0f}, "
+              f"IWANT spam {(s8[:, 7] - s8[:, 6]).mean():.0f} (p99 {np.percentile(s8[:, 7] - s8[:, 6], 99):.0f}), "
+              f"pass2b {(s8[:, 4] - s8[:, 7]).mean():.0f} (p99 {np.percentile(s8[:, 4] - s8[:, 7], 99):.0f})")
     hb = hbbuf.reshape(-1, 8).astype(np.int64)
     hb = hb[(hb[:, 0] > 0) & (hb[:, 5] > 0)]
     if len(hb):
