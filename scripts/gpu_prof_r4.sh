@@ -10,7 +10,7 @@ WL=${2:-config4}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 CMD="bench.py --gpus 1 --steps 20 --warmup 5 --workload $WL"
-RE='k_phase_a|k_heartbeat|k_phase_b|k_score|k_refresh|k_fwd'
+RE='k_phase_a|k_heartbeat|k_phase_b|k_score|k_refresh|k_fwd|k_push|k_ptx_rebuild|k_hb_pre'
 pass() {
   local name=$1
   shift
