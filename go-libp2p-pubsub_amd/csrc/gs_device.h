@@ -250,7 +250,10 @@ struct Dev {
   int32_t anyImd;                 // 0: no invalid delivery ever recorded, imd is all 0 (P4 = 0)
   uint32_t* dlt;                  // [E][T]: deliveries not yet folded into fmd / mmd,
                                   // (+1s to fmd) | (+1s to mmd) << 16 (see eff_fmd)
-  int64_t *graftTime, *meshTime;  // [T][E]
+  int64_t *graftTime, *meshTime;  // [T][E]; meshTime holds the value of a pair that left the
+                                  // mesh (a mesh pair's is mesh_time_of(): refreshScores
+                                  // no longer writes it)
+  int64_t lastRefresh;            // time of the last refreshScores, INT64_MIN = none yet
   uint8_t* flags;                 // [T][E] bit0 inMesh, bit1 P3 active
   double* bp;                     // [E] behaviourPenalty
   int32_t *peerhave, *iasked;     // [E]
@@ -549,11 +552,19 @@ struct TermIn {
   uint32_t q;
   uint8_t fl;
 };
+// topicStats.meshTime of a mesh pair: refreshScores sets it to now - graftTime
+// (score.go:518-520) and a graft to 0, so between refreshes it is the last
+// refresh's now - graftTime, or 0 for a pair grafted since (graftTime is then
+// past the last refresh).  A pair out of the mesh keeps what it had when it
+// left (stats_prune / RemovePeer store it).
+__device__ __forceinline__ int64_t mesh_time_of(int64_t lastRefresh, int64_t gt) {
+  return gt <= lastRefresh ? lastRefresh - gt : 0;
+}
 __device__ __forceinline__ TermIn term_load(const Dev& d, int64_t i) {
   TermIn x;
   x.fl = d.flags[i];
   x.q = d.dlt[i];
-  x.mt = d.meshTime[i];
+  x.mt = mesh_time_of(d.lastRefresh, d.graftTime[i]);  // read only for mesh pairs (fl & 1)
   x.mm = d.mmd[i];
   x.fmd = d.fmd[i];
   x.mfp = d.mfp[i];
@@ -714,6 +725,7 @@ __device__ __forceinline__ void stats_prune(const Dev& d, int64_t e, int t) {
     const double deficit = thr - mm;
     d.mfp[i] += deficit * deficit;
   }
+  if (fl & 1) d.meshTime[i] = mesh_time_of(d.lastRefresh, d.graftTime[i]);  // kept as it was at the prune
   d.flags[i] = fl & ~1;
 }
 

@@ -826,6 +826,7 @@ int gs_engine::start() {
   x.gConn = nullptr;
   x.gExp = nullptr;
   x.gRetain = gaterP.RetainStats;
+  x.lastRefresh = INT64_MIN;
   if (gaterOn) {
     x.gThreshold = gaterP.Threshold; x.gGlobalDecay = gaterP.GlobalDecay; x.gSourceDecay = gaterP.SourceDecay;
     x.gDecayToZero = gaterP.DecayToZero; x.gDupW = gaterP.DuplicateWeight; x.gIgnW = gaterP.IgnoreWeight;
@@ -1390,7 +1391,8 @@ int gs_engine::stepOne() {
     const int rc = upload(dRetire, retireWords.data(), retireWords.size() * 4);
     if (rc) return rc;
     const int nw = (int)retireWords.size();
-    if (nOwn) k_retire<<<nblk((int64_t)nOwn * nw, 256), 256, 0, stream>>>(d, cur, dRetire, nw);
+    if (nOwn && (d.spamRow != nullptr || d.pmaskRow != nullptr))
+      k_retire<<<nblk((int64_t)nOwn * nw, 256), 256, 0, stream>>>(d, cur, dRetire, nw);
   }
   if (n > 0) {
     TIMED(this, GS_K_PUBLISH, (k_publish<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, h, cur, head)));
@@ -1398,7 +1400,9 @@ int gs_engine::stepOne() {
     if (d.sel) k_publish_rs<<<n, 64, 0, stream>>>(d, (int)b);
   }
   // the copies the owned senders send next hop, per edge (phase A reads them)
-  if (nOwn) TIMED(this, GS_K_FWD, (k_push<<<nOwn, 64, 0, stream>>>(d, cur)));
+  if (nOwn)
+    TIMED(this, GS_K_FWD, (k_push<<<nOwn, 64, 0, stream>>>(d, cur, dRetire, (int)retireWords.size())));
+  if (n > 0) k_author_seen<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n);
   if (gossip) {
     if (scoring) TIMED(this, GS_K_SCORE, (score_rows<2>(d, eOwn, T, nullptr, stream)));
     // MaxIHaveLength cuts are possible only if the messages (phantom ids
@@ -1439,6 +1443,7 @@ int gs_engine::stepOne() {
       TIMED(this, GS_K_REFRESH, (k_refresh_rows<false, false><<<rb, 64, 0, stream>>>(d, now)));
     if (churnOn && p6Live() && nOwn) k_p6<<<nOwn, 64, 0, stream>>>(d, dP6w);  // expired records
     refreshedHop = h;
+    d.lastRefresh = now;  // the kernels launched from here on derive mesh pairs' meshTime from it
     hopsSinceFold = 0;
   } else if (scoring && ++hopsSinceFold >= foldEvery) {
     // pending delivery counts are 16-bit: fold them before they can overflow
@@ -2367,7 +2372,12 @@ int gs_read_topic_stats(gs_engine* g, double* fmd, double* mmd, double* mfp, dou
   if ((rc = copy_back_pairs(g, imd, g->d.imd))) return rc;
   if ((rc = copy_back_pairs(g, mesh_time, (const int64_t*)g->d.meshTime))) return rc;
   if ((rc = copy_back_pairs(g, graft_time, (const int64_t*)g->d.graftTime))) return rc;
-  return copy_back_pairs(g, flags, (const uint8_t*)g->d.flags);
+  if ((rc = copy_back_pairs(g, flags, (const uint8_t*)g->d.flags))) return rc;
+  // a mesh pair's meshTime is derived (mesh_time_of, gs_device.h)
+  const int64_t lr = g->d.lastRefresh;
+  for (int64_t i = 0; i < (int64_t)g->E * g->T; ++i)
+    if (flags[i] & 1) mesh_time[i] = graft_time[i] <= lr ? lr - graft_time[i] : 0;
+  return GS_OK;
 }
 int gs_read_behaviour_penalty(gs_engine* g, double* bp) { return copy_back(g, bp, g->d.bp, g->E * 8); }
 

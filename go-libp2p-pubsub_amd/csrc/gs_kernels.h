@@ -225,15 +225,22 @@ __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t no
         x.im = v;
         x.fl = fl[k];
         x.mt = 0;
+#ifdef GS_EXP_FULLW
+        d.dlt[i] = 0;
+        d.fmd[i] = x.fmd;
+        d.mmd[i] = x.mm;
+        d.mfp[i] = x.mfp;
+        if (d.anyImd) d.imd[i] = x.im;
+#else
         // unchanged counters (mostly zeros staying zero) are not written back
         if (q[k]) d.dlt[i] = 0;
         if (x.fmd != fmd[k]) d.fmd[i] = x.fmd;
         if (x.mm != mmd[k]) d.mmd[i] = x.mm;
         if (x.mfp != mfp[k]) d.mfp[i] = x.mfp;
         if (d.anyImd && x.im != imd[k]) d.imd[i] = x.im;
+#endif
         if (x.fl & 1) {
-          x.mt = now - gt[k];
-          d.meshTime[i] = x.mt;
+          x.mt = now - gt[k];  // meshTime (score.go:518-520): mesh_time_of() from here on
           if (x.mt > tp.MmdActivation) {
             x.fl |= 2;
             d.flags[i] = x.fl;
@@ -315,7 +322,7 @@ __global__ void k_gather_pairs(Dev d, const int64_t* __restrict__ edges, int64_t
   o[nk + k] = eff_mmd(tp, d.mmd[i], q);
   o[2 * nk + k] = d.mfp[i];
   o[3 * nk + k] = d.imd[i];
-  oi[4 * nk + k] = d.meshTime[i];
+  oi[4 * nk + k] = (d.flags[i] & 1) ? mesh_time_of(d.lastRefresh, d.graftTime[i]) : d.meshTime[i];
   oi[5 * nk + k] = d.graftTime[i];
   of[k] = d.flags[i];
 }
@@ -1406,7 +1413,11 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
           const int pl = lane + 64 * (k0 + kk);
           const bool ok = pl < nP;
           const uint32_t nq = upd(ok ? pl : 0, ok ? iv[kk] : 0, ok ? tv[kk] : 0, q[kk]);
+#ifdef GS_EXP_SKIPW
+          if (ok && nq != q[kk]) pv[pl] = nq;
+#else
           *(ok ? pv + pl : scr) = nq;
+#endif
         }
       }
     };
@@ -1645,12 +1656,13 @@ __global__ void k_oldmask(Dev d, int64_t h) {
 // Clears the seen bits of recycled message slots (the slots published in
 // this hop held messages retired from the window).  One thread per
 // (node, word) of the words[] list.
+// (the seen bits themselves are cleared by k_push, after the publishes; this
+// kernel runs only for the adversarial model's per-slot state)
 __global__ void k_retire(Dev d, int cur, const int32_t* __restrict__ words, int nwords) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= (int64_t)(d.n1 - d.n0) * nwords) return;
   const int v = d.n0 + (int)(k / nwords);
   const int w = words[k % nwords];
-  d.seen[(int64_t)v * d.W + w] &= ~d.pubmask[cur][w];
   if (d.spamRow != nullptr && d.pubmask[cur][w]) {
     // a recycled slot starts with no peertx counts from v's spammer peers
     const uint64_t pm = d.pubmask[cur][w];
@@ -1783,12 +1795,18 @@ __device__ __forceinline__ uint64_t wave_transpose64(uint64_t x) {
 // Records go to the receiver's in-edge; an edge to a receiver on another
 // rank is left to the receiver's list walk, as is every edge of a sender
 // whose copies overflow its region (record -1).
-__global__ __launch_bounds__(64) void k_push(Dev d, int cur) {
+__global__ __launch_bounds__(64) void k_push(Dev d, int cur, const int32_t* __restrict__ rwords, int nrw) {
   __shared__ uint64_t sMR[64], sMP[64];
   __shared__ int sCnt[64], sRun[64], sPre[64];
   __shared__ __attribute__((aligned(16))) uint16_t sOut[GS_PUSHR];
   const int u = d.n0 + blockIdx.x;
   const int lane = lane_id();
+  // k_retire's seen part for this node: the slots published this hop start
+  // unseen (k_author_seen marks them again at their authors right after)
+  for (int k = lane; k < nrw; k += 64) {
+    const int w = rwords[k];
+    d.seen[(int64_t)u * d.W + w] &= ~d.pubmask[cur][w];
+  }
   const int64_t base = d.rowptr[u];
   const int deg = (int)(d.rowptr[u + 1] - base);
   const int64_t e = base + lane;
@@ -1859,6 +1877,17 @@ __global__ __launch_bounds__(64) void k_push(Dev d, int cur) {
   uint4* dst = (uint4*)(d.ibx[cur] + A);
   for (int k = lane; k < total / 8; k += 64) dst[k] = src[k];
   if (local) d.ibxRec[cur][re] = ((A + pre) << 24) | (int64_t)cnt;
+}
+
+// The author's seen bit of each message published this hop (k_publish set it
+// before k_push cleared the recycled slots' bits on every node).
+__global__ void k_author_seen(Dev d, int b, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int src = d.mSrc[b + i];
+  if (src < d.n0 || src >= d.n1) return;
+  const int slot = d.mSlot[b + i];
+  atomicOr((unsigned long long*)&d.seen[(int64_t)src * d.W + (slot >> 6)], 1ull << (slot & 63));
 }
 
 // Randomsub targets of the messages published this hop (one wave per message).

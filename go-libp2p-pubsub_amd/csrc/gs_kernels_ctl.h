@@ -2137,6 +2137,7 @@ __global__ __launch_bounds__(64) void k_edge_down(Dev d, const int32_t* __restri
       const double deficit = tp.MmdThreshold - mm;
       d.mfp[i] += deficit * deficit;
     }
+    if (fl & 1) d.meshTime[i] = mesh_time_of(d.lastRefresh, d.graftTime[i]);  // the retained record's
     d.flags[i] = fl & ~1;
   }
   if (lane == 0) {
