@@ -87,6 +87,10 @@ struct gs_engine {
   std::vector<uint64_t> subA;          // announced subscriptions (host copy of d.subA)
   std::vector<uint8_t> aliveH;         // [E] host copy of d.alive
   bool churnOn = false;
+  // push (k_push + phase A reading per-edge segments) pays where an edge
+  // forwards a fraction of its sender's list: several topics.  With one topic
+  // a forwarding edge carries the whole list and phase A reads the lists.
+  bool pushOn = false;
   bool churnWindow = false;            // events scheduled before the first publish: wide window
   uint64_t* dSubA = nullptr;
   uint64_t* dSubOwn = nullptr;
@@ -438,6 +442,7 @@ int gs_engine::start() {
     if (rc) return rc;
   }
   bool anyRandom = cfg.router == GS_ROUTER_RANDOMSUB;  // some host runs randomsub (d.sel)
+  pushOn = T >= 4;
   if (!routerH.empty()) {
     anyRandom = false;
     for (uint8_t r : routerH) anyRandom = anyRandom || r == GS_ROUTER_RANDOMSUB;
@@ -648,6 +653,9 @@ int gs_engine::start() {
   }
   // push arena: a region of GS_PUSHR slots (4 KiB) per owned sender and parity
   for (int k = 0; k < 2; ++k) {
+    x.ibx[k] = nullptr;
+    x.ibxRec[k] = nullptr;
+    if (!pushOn) continue;
     x.ibx[k] = dalloc<uint16_t>((size_t)std::max<int64_t>(nOwnN, 1) * GS_PUSHR); chk(x.ibx[k]);
     x.ibxRec[k] = dalloc<int64_t>(E, 0xFF); chk(x.ibxRec[k]);
   }
@@ -1401,7 +1409,8 @@ int gs_engine::stepOne() {
   }
   // the copies the owned senders send next hop, per edge (phase A reads them)
   if (nOwn)
-    TIMED(this, GS_K_FWD, (k_push<<<nOwn, 64, 0, stream>>>(d, cur, dRetire, (int)retireWords.size())));
+    TIMED(this, GS_K_FWD,
+          (k_push<<<nOwn, 64, 0, stream>>>(d, cur, dRetire, (int)retireWords.size(), pushOn ? 1 : 0)));
   if (n > 0) k_author_seen<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n);
   if (gossip) {
     if (scoring) TIMED(this, GS_K_SCORE, (score_rows<2>(d, eOwn, T, nullptr, stream)));

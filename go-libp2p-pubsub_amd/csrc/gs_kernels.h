@@ -706,7 +706,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
     gray = scoring && !d.direct[e] && d.score0[e] < d.graylistThr;
     if (relayAll | pubAll) {
       // an owned sender pushed this edge's copies (k_push): read that segment
-      if (u >= d.n0 && u < d.n1) {
+      if (u >= d.n0 && u < d.n1 && d.ibxRec[0] != nullptr) {
         const int64_t rec = d.ibxRec[prv][e];
         if (rec >= 0) {
           pOff = rec >> 24;
@@ -1795,7 +1795,7 @@ __device__ __forceinline__ uint64_t wave_transpose64(uint64_t x) {
 // Records go to the receiver's in-edge; an edge to a receiver on another
 // rank is left to the receiver's list walk, as is every edge of a sender
 // whose copies overflow its region (record -1).
-__global__ __launch_bounds__(64) void k_push(Dev d, int cur, const int32_t* __restrict__ rwords, int nrw) {
+__global__ __launch_bounds__(64) void k_push(Dev d, int cur, const int32_t* __restrict__ rwords, int nrw, int push) {
   __shared__ uint64_t sMR[64], sMP[64];
   __shared__ int sCnt[64], sRun[64], sPre[64];
   __shared__ __attribute__((aligned(16))) uint16_t sOut[GS_PUSHR];
@@ -1807,6 +1807,7 @@ __global__ __launch_bounds__(64) void k_push(Dev d, int cur, const int32_t* __re
     const int w = rwords[k];
     d.seen[(int64_t)u * d.W + w] &= ~d.pubmask[cur][w];
   }
+  if (!push) return;  // (records stay -1: phase A reads the senders' lists)
   const int64_t base = d.rowptr[u];
   const int deg = (int)(d.rowptr[u + 1] - base);
   const int64_t e = base + lane;
