@@ -1417,12 +1417,21 @@ int gs_engine::stepOne() {
     // MaxIHaveLength cuts are possible only if the messages (phantom ids
     // included) that can sit in one gossip window outnumber MaxIHaveLength:
     // published within HistoryGossip + 1 heartbeats plus the delivery age bound
+    // Bit 0: one topic's ids may exceed it (emitGossip's cut of a sender's
+    // item); bit 1: a sender's ids over all topics may (handleIHave's iask
+    // cut of its wants).  Both run in either phase-B instantiation.
     int cutMode = 0;
     {
       const int64_t lo = h - (int64_t)(gp.HistoryGossip + 1) * H - maxAge - 2;
       const auto a = std::lower_bound(mHop.begin(), mHop.end(), lo);
       const auto b2 = std::upper_bound(mHop.begin(), mHop.end(), h);
-      cutMode = (int64_t)(b2 - a) > (int64_t)gp.MaxIHaveLength ? 1 : 0;
+      if ((int64_t)(b2 - a) > (int64_t)gp.MaxIHaveLength) {
+        cutMode |= 2;
+        std::vector<int64_t> perT((size_t)T, 0);
+        for (auto it = a; it != b2; ++it) perT[(size_t)mTopic[(size_t)(it - mHop.begin())]]++;
+        for (int t = 0; t < T; ++t)
+          if (perT[(size_t)t] > (int64_t)gp.MaxIHaveLength) cutMode |= 1;
+      }
     }
     const size_t ldsB = cutMode ? GS_CUTLDS : 0;
     if (nOwn) {
@@ -1433,10 +1442,10 @@ int gs_engine::stepOne() {
           launch_wpl(W, [&](auto wpl) {
             constexpr int WV = decltype(wpl)::value;
             if (!nOwn) return;
-            if (topicVal != 0 || gaterOn || behaveAll != 0 || anyPhantom || cutMode)
+            if (topicVal != 0 || gaterOn || behaveAll != 0 || anyPhantom)
               k_phase_b<WV, true><<<nOwn, 64, ldsB, stream>>>(dDev, h, now, cur, head, cutMode);
             else
-              k_phase_b<WV, false><<<nOwn, 64, ldsB, stream>>>(dDev, h, now, cur, head, 0);
+              k_phase_b<WV, false><<<nOwn, 64, ldsB, stream>>>(dDev, h, now, cur, head, cutMode);
           }));
   }
   if (refreshDue(now)) {

@@ -287,7 +287,7 @@ __device__ __forceinline__ void put_served(const Dev& d, const int32_t* pool, co
 template <int WPL, bool ADV>
 __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t h, int64_t now, int cur, int head,
                                              int cutModeArg) {
-  const int cutMode = ADV ? cutModeArg : 0;
+  const int cutMode = cutModeArg;  // bit 0: a topic's item may be cut; bit 1: a sender's wants may be cut
   if (!gossip_host(d, v)) return;  // FloodSubRouter / RandomSubRouter.HandleRPC: no-ops
   __shared__ uint64_t scache[64 * WPL];  // v's mcache windows (handleIWant, step 2)
   uint64_t* const sseen = scache;        // then v's seen row (handleIHave, step 3)
@@ -777,7 +777,7 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
     uint32_t* const cBits = (uint32_t*)(iM + 64);                   // [128] item is cut
     int* const cN = (int*)(cBits + 128);
     int nCut = 0;
-    if (cutMode) {
+    if (cutMode & 1) {
       for (int k = lane; k < 128; k += 64) cBits[k] = 0u;
       if (lane == 0) *cN = 0;
       __syncthreads();
@@ -925,7 +925,7 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
     const int myWantAll = sCnt[lane];
     const bool iaCut = gateIHave && myWantAll > 0 && myWantAll + ia > d.MaxIHaveLength;
     const int myWant = iaCut ? d.MaxIHaveLength - ia : myWantAll;
-    if (cutMode) {
+    if (cutMode & 2) {
       unsigned long long cm = __ballot(iaCut);
       while (cm) {
         const int i = __ffsll((long long)cm) - 1;
