@@ -1797,7 +1797,7 @@ __device__ __forceinline__ uint64_t wave_transpose64(uint64_t x) {
 // whose copies overflow its region (record -1).
 __global__ __launch_bounds__(64) void k_push(Dev d, int cur, const int32_t* __restrict__ rwords, int nrw, int push) {
   __shared__ uint64_t sMR[64], sMP[64];
-  __shared__ int sCnt[64], sRun[64], sPre[64];
+  __shared__ uint16_t sSlot[64];
   __shared__ __attribute__((aligned(16))) uint16_t sOut[GS_PUSHR];
   const int u = d.n0 + blockIdx.x;
   const int lane = lane_id();
@@ -1836,8 +1836,6 @@ __global__ __launch_bounds__(64) void k_push(Dev d, int cur, const int32_t* __re
   }
   sMR[lane] = wave_transpose64(relay);  // edges whose relay set holds topic `lane`
   sMP[lane] = wave_transpose64(pub);
-  sCnt[lane] = 0;
-  sRun[lane] = 0;
   __syncthreads();
   const bool rs = rs_host(d, u);
   // the edges entry k goes out on
@@ -1849,12 +1847,17 @@ __global__ __launch_bounds__(64) void k_push(Dev d, int cur, const int32_t* __re
     if (rs) m &= d.sel[(int64_t)u * d.S + slot];
     return m;
   };
-  for (int k = lane; k < Ln; k += 64) {
+  // lane = entry: its edge mask; transposed, lane = edge: its entries of the
+  // chunk (the first two chunks' kept in registers for the write pass)
+  const int nch = (Ln + 63) >> 6;
+  int s0 = 0, s1 = 0;
+  const uint64_t E0 = wave_transpose64(lane < Ln ? dest(ent0, s0) : 0ull);
+  const uint64_t E1 = nch > 1 ? wave_transpose64(64 + lane < Ln ? dest(L[64 + lane], s1) : 0ull) : 0ull;
+  int cnt = __popcll(E0) + __popcll(E1);
+  for (int c = 2; c < nch; ++c) {
     int slot;
-    for (uint64_t m = dest(k < 64 ? ent0 : L[k], slot); m; m &= m - 1) atomicAdd(&sCnt[__ffsll((long long)m) - 1], 1);
+    cnt += __popcll(wave_transpose64(64 * c + lane < Ln ? dest(L[64 * c + lane], slot) : 0ull));
   }
-  __syncthreads();
-  const int cnt = sCnt[lane];
   const int seg = (cnt + 7) & ~7;
   const int incl = wave_incl_sum(seg);
   const int total = wave_last(incl);
@@ -1863,16 +1866,22 @@ __global__ __launch_bounds__(64) void k_push(Dev d, int cur, const int32_t* __re
     if (local) d.ibxRec[cur][re] = -1;  // region overflow: the receiver walks u's list
     return;
   }
-  sPre[lane] = pre;
-  __syncthreads();
-  for (int k = lane; k < Ln; k += 64) {
-    int slot;
-    for (uint64_t m = dest(k < 64 ? ent0 : L[k], slot); m; m &= m - 1) {
-      const int j = __ffsll((long long)m) - 1;
-      sOut[sPre[j] + atomicAdd(&sRun[j], 1)] = (uint16_t)slot;
-    }
+  // lane j (edge j) writes its entries of each chunk contiguously from its
+  // segment start
+  int run = pre;
+  auto put = [&](uint64_t E, int slot) {
+    sSlot[lane] = (uint16_t)slot;
+    __syncthreads();
+    for (; E; E &= E - 1) sOut[run++] = sSlot[__ffsll((long long)E) - 1];
+    __syncthreads();
+  };
+  put(E0, s0);
+  if (nch > 1) put(E1, s1);
+  for (int c = 2; c < nch; ++c) {
+    int slot = 0;
+    const uint64_t E = wave_transpose64(64 * c + lane < Ln ? dest(L[64 * c + lane], slot) : 0ull);
+    put(E, slot);
   }
-  __syncthreads();
   const int64_t A = (int64_t)(u - d.n0) * GS_PUSHR;
   const uint4* src = (const uint4*)sOut;
   uint4* dst = (uint4*)(d.ibx[cur] + A);
