@@ -148,21 +148,31 @@ def algorithmic_bytes(kernel, eng, wl, per_hop):
     if kernel == "phase_a":
         mesh = eng.mesh()[e0:e1]
         fwd_edges = int((mesh != 0).sum())          # edges with a forwarding topic
-        items = per_hop["deliveries"] + per_hop["published"]   # frontier-list entries written per hop
+        W = per_hop["active_words"]
+        # SURVEY.md §8(d) "Propagation hop": B_hop = (E_fwd + 3N) * W * 8 --
+        # one sender frontier word per forwarding edge, and per node its seen
+        # words read and written and its next frontier written, over the active
+        # message window (the words phase A touches: messages younger than the
+        # delivery horizon).  This is the line's `achieved` model.
+        b = (fwd_edges + 3.0 * N) * W * 8.0
+        # the engine's own representation, for comparison with the PMC traffic:
         # each copy sent is one 16-bit slot of the sender's pushed segment for
         # that edge (k_push), read once by its receiver, plus the segment's
-        # 8-byte record; the receiver writes its own frontier list (4 B per entry)
+        # 8-byte record; the receiver writes its own frontier list (4 B per
+        # entry), read-modify-writes the pending counts per (edge, topic), its
+        # seen words, and per-edge metadata
+        items = per_hop["deliveries"] + per_hop["published"]   # frontier-list entries written per hop
         copies = per_hop["transmissions"] - per_hop["iwant_served"]  # served ids: 4 B each from the pool
         list_reads = 2.0 * copies + 8.0 * fwd_edges + 4.0 * per_hop["iwant_served"]
         list_writes = 4.0 * items
         pending = 8.0 * T * E                        # pending-delivery counts, read + write per (edge, topic)
-        seen = 16.0 * N * per_hop["active_words"]    # seen words of the active window, read + write
+        seen = 16.0 * N * W                          # seen words of the active window, read + write
         meta = 49.0 * E                              # rev, col, fwd masks, IWANT ref, S0 memo, direct, mesh
-        b = list_reads + list_writes + pending + seen + meta
-        return b, dict(fwd_edges=fwd_edges, list_entries_per_hop=items, copies_per_hop=copies,
-                       active_words=per_hop["active_words"],
-                       bytes_lists=int(list_reads + list_writes), bytes_pending=int(pending),
-                       bytes_seen=int(seen), bytes_meta=int(meta))
+        eb = list_reads + list_writes + pending + seen + meta
+        return b, dict(model="SURVEY 8(d): (E_fwd + 3N) * W * 8", fwd_edges=fwd_edges, active_words=W,
+                       engine_model_bytes=int(eb), list_entries_per_hop=items, copies_per_hop=copies,
+                       engine_bytes_lists=int(list_reads + list_writes), engine_bytes_pending=int(pending),
+                       engine_bytes_seen=int(seen), engine_bytes_meta=int(meta))
     if kernel == "refresh":
         # 80 B per (edge, topic) (the four f64 counters read
         # and written 64, meshTime written 8, graft time read, flags r+w,

@@ -250,6 +250,12 @@ struct Dev {
   int32_t anyImd;                 // 0: no invalid delivery ever recorded, imd is all 0 (P4 = 0)
   uint32_t* dlt;                  // [E][T]: deliveries not yet folded into fmd / mmd,
                                   // (+1s to fmd) | (+1s to mmd) << 16 (see eff_fmd)
+  uint16_t* dltN;                 // the narrow layout (exactly one of dlt / dltN is set):
+                                  // (+1s to fmd) | (+1s to mmd) << 8, used when at most
+                                  // 255 messages per topic can be delivered between two
+                                  // folds (slots per topic <= 255, T even; the host folds
+                                  // early otherwise, gs_engine.hip foldDue).  Half the
+                                  // bytes of phase A's per-hop read-modify-write.
   int64_t *graftTime, *meshTime;  // [T][E]; meshTime holds the value of a pair that left the
                                   // mesh (a mesh pair's is mesh_time_of(): refreshScores
                                   // no longer writes it)
@@ -367,15 +373,19 @@ __device__ __forceinline__ int64_t prune_entry(const Dev& d, int64_t e, int t) {
 __device__ __forceinline__ void set_err(const Dev& d, int code);
 // n ids of this hop's arena (cur) for one wave or lane; ~0 = full (E_POOL
 // set).  The sub-arena is picked by blockIdx: a single counter serialised
-// about a million per-wave atomics at one L2 address.
+// about a million per-wave atomics at one L2 address.  A full sub-arena hands
+// the request on to the next ones (its counter stays past the cap, so later
+// requests skip it after one add), so skewed loads (high-degree or
+// IWANT-heavy nodes on one sub-arena) use the whole segment before E_POOL.
 __device__ __forceinline__ unsigned long long pool_take(const Dev& d, int cur, unsigned long long n) {
-  const int s = (int)(blockIdx.x % (unsigned)d.poolSub);
-  const unsigned long long o = atomicAdd(&d.poolCnt[((int64_t)cur * d.poolSub + s) * 16], n);
-  if ((int64_t)(o + n) > d.poolSubCap) {
-    set_err(d, E_POOL);
-    return ~0ull;
+  const int s0 = (int)(blockIdx.x % (unsigned)d.poolSub);
+  for (int k = 0; k < d.poolSub; ++k) {
+    const int s = (s0 + k) & (d.poolSub - 1);  // poolSub is a power of two
+    const unsigned long long o = atomicAdd(&d.poolCnt[((int64_t)cur * d.poolSub + s) * 16], n);
+    if ((int64_t)(o + n) <= d.poolSubCap) return (unsigned long long)(d.poolBase0 + (int64_t)s * d.poolSubCap) + o;
   }
-  return (unsigned long long)(d.poolBase0 + (int64_t)s * d.poolSubCap) + o;
+  set_err(d, E_POOL);
+  return ~0ull;
 }
 __device__ __forceinline__ void trace_emit(const Dev& d, int64_t hop, int type, int node, int peer, int topic,
                                            int64_t msg, int phase, int reason = 0) {
@@ -537,6 +547,20 @@ __device__ __forceinline__ double add_ones_capped(double x, int n, double cap) {
 // counter and for good at refreshScores, before the decay.  Applying n then m
 // steps equals applying n + m steps, so the result is independent of when
 // the fold happens as long as it precedes the decay.
+// The pending counts of pair i as (+1s to fmd) | (+1s to mmd) << 16 in either
+// layout, and their store (a narrow count is <= 255: the host's fold policy
+// and phase A's E_DELTA check guarantee it).
+__device__ __forceinline__ uint32_t dlt_get(const Dev& d, int64_t i) {
+  if (d.dltN != nullptr) {
+    const uint32_t x = d.dltN[i];
+    return (x & 0xFFu) | ((x >> 8) << 16);
+  }
+  return d.dlt[i];
+}
+__device__ __forceinline__ void dlt_put(const Dev& d, int64_t i, uint32_t q) {
+  if (d.dltN != nullptr) d.dltN[i] = (uint16_t)((q & 0xFFu) | ((q >> 16) << 8));
+  else d.dlt[i] = q;
+}
 __device__ __forceinline__ double eff_fmd(const TopicP& tp, double fmd, uint32_t q) {
   return (q & 0xFFFF) ? add_ones_capped(fmd, (int)(q & 0xFFFF), tp.FmdCap) : fmd;
 }
@@ -563,7 +587,7 @@ __device__ __forceinline__ int64_t mesh_time_of(int64_t lastRefresh, int64_t gt)
 __device__ __forceinline__ TermIn term_load(const Dev& d, int64_t i) {
   TermIn x;
   x.fl = d.flags[i];
-  x.q = d.dlt[i];
+  x.q = dlt_get(d, i);
   x.mt = mesh_time_of(d.lastRefresh, d.graftTime[i]);  // read only for mesh pairs (fl & 1)
   x.mm = d.mmd[i];
   x.fmd = d.fmd[i];
@@ -713,12 +737,12 @@ __device__ __forceinline__ void stats_prune(const Dev& d, int64_t e, int t) {
   d.sdirty[e] = 1;
   const uint8_t fl = d.flags[i];
   const TopicP& tp = d.tp[t];
-  const uint32_t q = d.dlt[i];
+  const uint32_t q = dlt_get(d, i);
   double mm = d.mmd[i];
   if (q >> 16) {  // fold the pending mesh deliveries: the deficit reads the counter
     mm = eff_mmd(tp, mm, q);
     d.mmd[i] = mm;
-    d.dlt[i] = q & 0xFFFF;
+    dlt_put(d, i, q & 0xFFFF);
   }
   const double thr = tp.MmdThreshold;
   if ((fl & 2) && mm < thr) {

@@ -58,6 +58,18 @@ struct gs_engine {
   int64_t retireHops = 0;
   std::vector<int32_t> topicLive;  // per-topic live message count (phase-A counter width)
   int64_t hopsSinceFold = 0, foldEvery = 1;  // pending-delivery fold cadence (dlt)
+  // the 16-bit pending counts (Dev::dltN): counts accumulate from foldStart;
+  // a pair's count is bounded by the messages of its topic that can be
+  // delivered since then, so the host folds before that bound could pass 255
+  bool narrowDlt = false;
+  int64_t foldStart = 0;
+  bool narrowFoldDue(int64_t h) {
+    auto it = std::lower_bound(mHop.begin(), mHop.end(), foldStart - retireHops);
+    std::fill(topicLive.begin(), topicLive.end(), 0);
+    for (size_t k = (size_t)(it - mHop.begin()); k < mHop.size() && mHop[k] <= h; ++k)
+      if (++topicLive[mTopic[k]] > 255) return true;
+    return false;
+  }
   std::vector<uint64_t> yWord, yTabH;          // phase A young-slot tables (per hop)
   int64_t refreshedHop = -1;                 // hop of the last refreshScores (S0 exact after it)
   int maxAge = 0;
@@ -738,12 +750,22 @@ int gs_engine::start() {
   x.backoff = dalloc<int64_t>(TE);
   x.boMask = dalloc<uint64_t>(E); chk(x.boMask);
   x.fmd = dalloc<double>(TE); x.mmd = dalloc<double>(TE); x.mfp = dalloc<double>(TE); x.imd = dalloc<double>(TE);
-  x.dlt = dalloc<uint32_t>(TE); chk(x.dlt);
+  // 16-bit pending counts when a topic's slots (at most St + 1 messages live at
+  // one hop) fit a byte and the pairs of an edge pack into whole words
+  narrowDlt = St <= 254 && (T % 2) == 0;
+  x.dlt = nullptr;
+  x.dltN = nullptr;
+  if (narrowDlt) {
+    x.dltN = dalloc<uint16_t>(TE); chk(x.dltN);
+  } else {
+    x.dlt = dalloc<uint32_t>(TE); chk(x.dlt);
+  }
   x.graftTime = dalloc<int64_t>(TE); x.meshTime = dalloc<int64_t>(TE); x.flags = dalloc<uint8_t>(TE);
   chk(x.backoff); chk(x.fmd); chk(x.mmd); chk(x.mfp); chk(x.imd); chk(x.graftTime); chk(x.meshTime); chk(x.flags);
   if (!ok) { gs_set_error("device allocation failed (per-(edge, topic) state)"); return GS_ENOMEM; }
   x.backoff -= shift; x.fmd -= shift; x.mmd -= shift; x.mfp -= shift; x.imd -= shift;
-  x.dlt -= shift; x.graftTime -= shift; x.meshTime -= shift; x.flags -= shift;
+  if (narrowDlt) x.dltN -= shift; else x.dlt -= shift;
+  x.graftTime -= shift; x.meshTime -= shift; x.flags -= shift;
   x.bp = dalloc<double>(E); x.peerhave = dalloc<int32_t>(E); x.iasked = dalloc<int32_t>(E);
   chk(x.score0); chk(x.score1); chk(x.backoff); chk(x.fmd); chk(x.mmd); chk(x.mfp); chk(x.imd);
   chk(x.graftTime); chk(x.meshTime); chk(x.flags); chk(x.bp); chk(x.peerhave); chk(x.iasked);
@@ -1304,8 +1326,10 @@ int gs_engine::stepOne() {
     }
   }
   std::vector<int32_t> retireWords;
+  WMask amP{};  // words of the slots published this hop (phase A clears their old seen bits)
   for (size_t k = b; k < e; ++k) {
     const int w = mSlot[k] >> 6;
+    amP.m[w >> 6] |= 1ull << (w & 63);
     if (std::find(retireWords.begin(), retireWords.end(), w) == retireWords.end()) retireWords.push_back(w);
   }
   HIPCHECK(hipMemsetAsync(d.pubmask[cur], 0, (size_t)W * 8, stream));
@@ -1314,6 +1338,12 @@ int gs_engine::stepOne() {
   const int64_t eOwn = e1 - e0;
   const unsigned eb = nblk(eOwn, 256);
   const unsigned pb = nblk(eOwn * T, 256);
+  if (scoring && narrowDlt && narrowFoldDue(h)) {
+    // this hop's counts could take a 16-bit pending word past 255 per field:
+    // fold what has accumulated since foldStart first
+    if (eOwn) k_fold_all<<<pb, 256, 0, stream>>>(d);
+    foldStart = h;
+  }
   if (scoring) TIMED(this, GS_K_SCORE, (score_rows<1>(d, eOwn, T, nullptr, stream)));
   if (h == 0 && gossip && nOwn) TIMED(this, GS_K_JOIN, (k_join<<<nOwn, 64, 0, stream>>>(d, h, now, cur)));
   if (gossip && !floodPublish && n > 0) {
@@ -1378,13 +1408,13 @@ int gs_engine::stepOne() {
             constexpr int WV = decltype(w)::value;
             if (adv) {
               if (narrow)
-                k_phase_a<WV, true, true><<<nOwn, 64, lds, stream>>>(dDev, h, cur, head, amR, amW, nR, nYp);
+                k_phase_a<WV, true, true><<<nOwn, 64, lds, stream>>>(dDev, h, cur, head, amR, amW, amP, nR, nYp);
               else
-                k_phase_a<WV, false, true><<<nOwn, 64, lds, stream>>>(dDev, h, cur, head, amR, amW, nR, nYp);
+                k_phase_a<WV, false, true><<<nOwn, 64, lds, stream>>>(dDev, h, cur, head, amR, amW, amP, nR, nYp);
             } else if (narrow) {
-              k_phase_a<WV, true, false><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR, nYp);
+              k_phase_a<WV, true, false><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, amP, nR, nYp);
             } else {
-              k_phase_a<WV, false, false><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, nR, nYp);
+              k_phase_a<WV, false, false><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, amP, nR, nYp);
             }
           }));
   }
@@ -1408,10 +1438,7 @@ int gs_engine::stepOne() {
     if (d.sel) k_publish_rs<<<n, 64, 0, stream>>>(d, (int)b);
   }
   // the copies the owned senders send next hop, per edge (phase A reads them)
-  if (nOwn)
-    TIMED(this, GS_K_FWD,
-          (k_push<<<nOwn, 64, 0, stream>>>(d, cur, dRetire, (int)retireWords.size(), pushOn ? 1 : 0)));
-  if (n > 0) k_author_seen<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n);
+  if (nOwn && pushOn) TIMED(this, GS_K_PUSH, (k_push<<<nOwn, 64, 0, stream>>>(d, cur)));
   if (gossip) {
     if (scoring) TIMED(this, GS_K_SCORE, (score_rows<2>(d, eOwn, T, nullptr, stream)));
     // MaxIHaveLength cuts are possible only if the messages (phantom ids
@@ -1463,7 +1490,8 @@ int gs_engine::stepOne() {
     refreshedHop = h;
     d.lastRefresh = now;  // the kernels launched from here on derive mesh pairs' meshTime from it
     hopsSinceFold = 0;
-  } else if (scoring && ++hopsSinceFold >= foldEvery) {
+    foldStart = h + 1;
+  } else if (scoring && !narrowDlt && ++hopsSinceFold >= foldEvery) {
     // pending delivery counts are 16-bit: fold them before they can overflow
     k_fold_all<<<pb, 256, 0, stream>>>(d);
     hopsSinceFold = 0;
@@ -1550,7 +1578,7 @@ int gs_engine::deviceErrorText(int32_t err, int64_t atHop) {
 int gs_engine::deviceErrorCode(int32_t err) {
   switch (err) {
     case E_NONE: return GS_OK;
-    case E_POOL: gs_set_error("IWANT payload arena overflow (4 ids per edge per hop)"); return GS_ECAPACITY;
+    case E_POOL: gs_set_error("IWANT payload arena overflow (max(2^24 / ranks, 4 x owned edges) ids per rank per hop)"); return GS_ECAPACITY;
     case E_PROMISES:
       gs_set_error("per-node promise table overflow (degree x (IWantFollowupTime / HeartbeatInterval + 2) entries, "
                    "at most 512)");
@@ -1569,7 +1597,8 @@ int gs_engine::deviceErrorCode(int32_t err) {
                    "frontier list holds (min(slots + 64, 2^31 / num_nodes) entries)");
       return GS_ECAPACITY;
     case E_DELTA:
-      gs_set_error("pending delivery count of one (edge, topic) overflowed 65535 between two score refreshes");
+      gs_set_error("pending delivery count of one (edge, topic) overflowed 65535 (255 in the 16-bit layout) "
+                   "between two folds");
       return GS_ECAPACITY;
     case E_TRACE:
       gs_set_error("more trace events between two gs_trace_read calls than the capacity given to gs_set_trace");

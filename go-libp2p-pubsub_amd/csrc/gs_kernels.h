@@ -175,7 +175,7 @@ __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t no
     for (int k = 0; k < GS_RB; ++k) {
       const int pl = min(lane + 64 * (k0 + k), np - 1);
       const int64_t i = p0 + pl;
-      q[k] = d.dlt[i];
+      q[k] = dlt_get(d, i);
       fmd[k] = d.fmd[i];
       mmd[k] = d.mmd[i];
       mfp[k] = d.mfp[i];
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t no
         // a retained record is not decayed; past its expiry it is dropped
         // (score.go:500-509); the host then recounts P6 (removeIPs)
         if (st == 2 && now > d.rexpire[e]) {
-          d.fmd[i] = 0; d.mmd[i] = 0; d.mfp[i] = 0; d.imd[i] = 0; d.dlt[i] = 0;
+          d.fmd[i] = 0; d.mmd[i] = 0; d.mfp[i] = 0; d.imd[i] = 0; dlt_put(d, i, 0);
           d.meshTime[i] = 0; d.graftTime[i] = 0; d.flags[i] = 0;
         } else if (act) {
           term = topic_term(d, tp, i);  // the stored record as it is
@@ -226,14 +226,14 @@ __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t no
         x.fl = fl[k];
         x.mt = 0;
 #ifdef GS_EXP_FULLW
-        d.dlt[i] = 0;
+        dlt_put(d, i, 0);
         d.fmd[i] = x.fmd;
         d.mmd[i] = x.mm;
         d.mfp[i] = x.mfp;
         if (d.anyImd) d.imd[i] = x.im;
 #else
         // unchanged counters (mostly zeros staying zero) are not written back
-        if (q[k]) d.dlt[i] = 0;
+        if (q[k]) dlt_put(d, i, 0);
         if (x.fmd != fmd[k]) d.fmd[i] = x.fmd;
         if (x.mm != mmd[k]) d.mmd[i] = x.mm;
         if (x.mfp != mfp[k]) d.mfp[i] = x.mfp;
@@ -287,7 +287,7 @@ __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t no
 __global__ void k_fold_all(Dev d) {
   const int64_t p = d.e0 * d.T + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= d.e1 * d.T) return;
-  const uint32_t q = d.dlt[p];
+  const uint32_t q = dlt_get(d, p);
   if (!q) return;
   int64_t e;
   int t;
@@ -295,7 +295,7 @@ __global__ void k_fold_all(Dev d) {
   const TopicP& tp = d.tp[t];
   d.fmd[p] = eff_fmd(tp, d.fmd[p], q);
   d.mmd[p] = eff_mmd(tp, d.mmd[p], q);
-  d.dlt[p] = 0;
+  dlt_put(d, p, 0);
 }
 
 // gs_read_topic_stats_edges: the counters of n chosen edges, out[i*T + t],
@@ -317,7 +317,7 @@ __global__ void k_gather_pairs(Dev d, const int64_t* __restrict__ edges, int64_t
   }
   const int64_t i = tix(d, t, e);
   const TopicP& tp = d.tp[t];
-  const uint32_t q = d.dlt[i];
+  const uint32_t q = dlt_get(d, i);
   o[k] = eff_fmd(tp, d.fmd[i], q);
   o[nk + k] = eff_mmd(tp, d.mmd[i], q);
   o[2 * nk + k] = d.mfp[i];
@@ -332,12 +332,12 @@ __global__ void k_fold(Dev d, int t) {
   const int64_t e = d.e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= d.e1) return;
   const int64_t i = tix(d, t, e);
-  const uint32_t q = d.dlt[i];
+  const uint32_t q = dlt_get(d, i);
   if (!q) return;
   const TopicP& tp = d.tp[t];
   d.fmd[i] = eff_fmd(tp, d.fmd[i], q);
   d.mmd[i] = eff_mmd(tp, d.mmd[i], q);
-  d.dlt[i] = 0;
+  dlt_put(d, i, 0);
 }
 
 // SetTopicScoreParams recap — score.go:215-229
@@ -634,7 +634,7 @@ __device__ __forceinline__ const Dev& dev_of(const Dev& d) { return d; }
 __device__ __forceinline__ const Dev& dev_of(const Dev* d) { return *d; }
 template <int WPL, bool NARROW, bool ADV>
 __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, int64_t h, int cur, int head,
-                                                WMask amR, WMask amW, int nR, int nY) {
+                                                WMask amR, WMask amW, WMask amP, int nR, int nY) {
   const Dev& d = dev_of(dArg);
   extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
   const int nCnt = (d.T * d.maxDeg + 7) & ~7;
@@ -1116,7 +1116,14 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   // launch still walks the lists again (queue drops) and loads them later
   if (!ADV && scoring) sRelay[lane] = valid ? d.mesh[base + lane] : 0ull;
   long long nDeliv = 0;
-  uint64_t Uw[WPL], Sw[WPL], Hw[WPL], Ow[WPL];
+  // the slots published this hop (words amP, slots pubmask[cur]) recycle their
+  // previous messages (mcache.go:94-104 has let them go, retireHops): their
+  // seen bits are cleared here, in the write of the node's seen word that pass
+  // 2b does anyway for most of them.  No copy of either occupant can arrive in
+  // this hop (the new one is published after phase A, the old one is past
+  // every delivery horizon), so clearing before or after the deliveries is the
+  // same.  k_publish then sets the authors' bits.
+  uint64_t Uw[WPL], Sw[WPL], Hw[WPL], Ow[WPL], Rw[WPL];
   uint64_t Xw[WPL];  // ADV: fresh messages validated as REJECT / IGNORE (seen, not delivered)
   int rkw[WPL];  // rank of the lane's word in amR
   // index of young slot b of the amR word of rank rk in sFirst
@@ -1124,8 +1131,10 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
 #pragma unroll
   for (int j = 0; j < WPL; ++j) {
     const int w = lane + 64 * j;
-    Uw[j] = Sw[j] = Hw[j] = Ow[j] = Xw[j] = 0;
+    Uw[j] = Sw[j] = Hw[j] = Ow[j] = Xw[j] = Rw[j] = 0;
     rkw[j] = 0;
+    const bool ret = w < W && wm_has(amP, w);
+    if (ret) Rw[j] = d.pubmask[cur][w];
     if (w < W && wm_has(amR, w)) {
       rkw[j] = wm_rank(amR, w);
       const uint64_t D = sD[rkw[j]];
@@ -1136,7 +1145,11 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
         Uw[j] = D;  // & ~seen below
         Ow[j] = d.oldm[w];
         if (gossipV) Hw[j] = d.hist[((int64_t)head * d.nOwnH + (v - d.n0)) * W + w];
+      } else if (ret) {
+        Sw[j] = d.seen[(int64_t)v * W + w];
       }
+    } else if (ret) {
+      Sw[j] = d.seen[(int64_t)v * W + w];
     }
   }
   bool anyDrop = false;
@@ -1378,8 +1391,74 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
     // coalesced, branch-free read-modify-write per pair, every load of a batch
     // issued before its first store (no full-queue drains).
     const int nP = deg * T;
-    uint32_t* const pv = d.dlt + base * T;
     uint32_t* const scr = (uint32_t*)(d.pad + ((int64_t)(blockIdx.x & 255) * 64 + lane) * 2);
+    if (d.dltN != nullptr) {
+      // 16-bit pending words (Dev::dltN), two pairs per lane: word wi of v's
+      // rows holds pairs 2 wi (in-edge i, topic t) and 2 wi + 1 (i, t + 1; T is
+      // even), so one 4-byte load covers both and a wave moves 128 pairs
+      const int nWd = nP >> 1;
+      uint32_t* const pw = (uint32_t*)(d.dltN + base * T);
+      const int q128 = 128 / T, r128 = 128 - q128 * T;
+      int ic = (2 * lane) / T, tc = 2 * lane - ((2 * lane) / T) * T;
+      auto upd2 = [&](int wi, int i, int t, uint32_t q) -> uint32_t {
+        uint32_t out = 0;
+        bool over = false;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int pl = 2 * wi + hh, tt = t + hh;
+          const bool sc = (scoredT >> tt) & 1;
+          uint32_t c = 0;
+          if (sc) c = NARROW ? ((scnt[wi] >> (16 * hh)) & 0xFFFF) : scnt[pl];
+          const int copies = NARROW ? (int)(c & 0xFF) : (int)(c & 0xFFFF);
+          const int nf = NARROW ? (int)(c >> 8) : (int)(c >> 16);
+          int credited = copies - nf;
+          if (hasUnc && sc) credited -= (int)sUnc[pl];
+          const uint32_t addM = ((sRelay[i] >> tt) & 1) ? (uint32_t)(nf + credited) : 0u;
+          const uint32_t old = (q >> (16 * hh)) & 0xFFFF;
+          const uint32_t f = (old & 0xFF) + (uint32_t)nf, m = (old >> 8) + addM;
+          over |= f > 0xFF || m > 0xFF;
+          out |= (f | (m << 8)) << (16 * hh);
+        }
+        if (over) set_err(d, E_DELTA);
+        return out;
+      };
+      auto rmw2 = [&](auto bsC) {
+        constexpr int BS = decltype(bsC)::value;
+        uint32_t q[BS];
+        int iv[BS], tv[BS];
+        for (int k0 = 0; 64 * k0 < nWd; k0 += BS) {
+#pragma unroll
+          for (int kk = 0; kk < BS; ++kk) {
+            const int wi = lane + 64 * (k0 + kk);
+            q[kk] = pw[wi < nWd ? wi : nWd - 1];
+            iv[kk] = ic;
+            tv[kk] = tc;
+            ic += q128;
+            tc += r128;
+            if (tc >= T) { tc -= T; ++ic; }
+          }
+#pragma unroll
+          for (int kk = 0; kk < BS; ++kk) {
+            const int wi = lane + 64 * (k0 + kk);
+            const bool ok = wi < nWd;
+            const uint32_t nq = upd2(ok ? wi : 0, ok ? iv[kk] : 0, ok ? tv[kk] : 0, q[kk]);
+            *(ok ? pw + wi : scr) = nq;
+          }
+        }
+      };
+#ifndef GS_EXP_NOPASS3
+      if (nWd > 8 * 64) {
+        rmw2(std::integral_constant<int, 16>{});
+      } else if (nWd > 2 * 64) {
+        rmw2(std::integral_constant<int, 8>{});
+      } else if (nWd > 64) {
+        rmw2(std::integral_constant<int, 2>{});
+      } else {
+        rmw2(std::integral_constant<int, 1>{});
+      }
+#endif
+    } else {
+    uint32_t* const pv = d.dlt + base * T;
     const int q64 = 64 / T, r64 = 64 - q64 * T;
     int ic = lane / T, tc = lane - (lane / T) * T;  // (in-edge, topic) of the lane's next pair
     auto upd = [&](int pl, int i, int t, uint32_t q) -> uint32_t {
@@ -1434,6 +1513,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
       rmw(std::integral_constant<int, 1>{});
     }
 #endif
+    }
     GS_STAMP(5);
     if constexpr (ADV) {
       // P4: every non-dropped copy of a rejected message is an invalid delivery
@@ -1557,9 +1637,9 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
     const int incl = wave_incl_sum(k);
     int rank = running + incl - k;
     running += wave_last(incl);
+    if (U | Rw[j]) d.seen[(int64_t)v * W + w] = (Sw[j] & ~Rw[j]) | U;
     if (U) {
       if ((U & Ow[j]) || !wm_has(amW, w)) set_err(d, E_LATE);
-      d.seen[(int64_t)v * W + w] = Sw[j] | U;
       if (gossipV && Ud) d.hist[((int64_t)head * d.nOwnH + (v - d.n0)) * W + w] = Hw[j] | Ud;
       nDeliv += k;
       // one first delivery: trace, drec.peers, v's frontier list, age / deliverer
@@ -1795,19 +1875,12 @@ __device__ __forceinline__ uint64_t wave_transpose64(uint64_t x) {
 // Records go to the receiver's in-edge; an edge to a receiver on another
 // rank is left to the receiver's list walk, as is every edge of a sender
 // whose copies overflow its region (record -1).
-__global__ __launch_bounds__(64) void k_push(Dev d, int cur, const int32_t* __restrict__ rwords, int nrw, int push) {
+__global__ __launch_bounds__(64) void k_push(Dev d, int cur) {
   __shared__ uint64_t sMR[64], sMP[64];
   __shared__ uint16_t sSlot[64];
   __shared__ __attribute__((aligned(16))) uint16_t sOut[GS_PUSHR];
   const int u = d.n0 + blockIdx.x;
   const int lane = lane_id();
-  // k_retire's seen part for this node: the slots published this hop start
-  // unseen (k_author_seen marks them again at their authors right after)
-  for (int k = lane; k < nrw; k += 64) {
-    const int w = rwords[k];
-    d.seen[(int64_t)u * d.W + w] &= ~d.pubmask[cur][w];
-  }
-  if (!push) return;  // (records stay -1: phase A reads the senders' lists)
   const int64_t base = d.rowptr[u];
   const int deg = (int)(d.rowptr[u + 1] - base);
   const int64_t e = base + lane;
@@ -1887,17 +1960,6 @@ __global__ __launch_bounds__(64) void k_push(Dev d, int cur, const int32_t* __re
   uint4* dst = (uint4*)(d.ibx[cur] + A);
   for (int k = lane; k < total / 8; k += 64) dst[k] = src[k];
   if (local) d.ibxRec[cur][re] = ((A + pre) << 24) | (int64_t)cnt;
-}
-
-// The author's seen bit of each message published this hop (k_publish set it
-// before k_push cleared the recycled slots' bits on every node).
-__global__ void k_author_seen(Dev d, int b, int n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int src = d.mSrc[b + i];
-  if (src < d.n0 || src >= d.n1) return;
-  const int slot = d.mSlot[b + i];
-  atomicOr((unsigned long long*)&d.seen[(int64_t)src * d.W + (slot >> 6)], 1ull << (slot & 63));
 }
 
 // Randomsub targets of the messages published this hop (one wave per message).

@@ -2121,17 +2121,17 @@ __global__ __launch_bounds__(64) void k_edge_down(Dev d, const int32_t* __restri
   for (int t = lane; t < d.T; t += 64) {
     const int64_t i = tix(d, t, e);
     if (drop) {
-      d.fmd[i] = 0; d.mmd[i] = 0; d.mfp[i] = 0; d.imd[i] = 0; d.dlt[i] = 0;
+      d.fmd[i] = 0; d.mmd[i] = 0; d.mfp[i] = 0; d.imd[i] = 0; dlt_put(d, i, 0);
       d.meshTime[i] = 0; d.graftTime[i] = 0; d.flags[i] = 0;
       continue;
     }
     if (!d.tp[t].scored) continue;
     const TopicP& tp = d.tp[t];
-    const uint32_t q = d.dlt[i];
+    const uint32_t q = dlt_get(d, i);
     const double mm = eff_mmd(tp, d.mmd[i], q);  // the pending mesh deliveries count
     d.mmd[i] = mm;
     d.fmd[i] = 0;
-    d.dlt[i] = 0;
+    dlt_put(d, i, 0);
     const uint8_t fl = d.flags[i];
     if ((fl & 1) && (fl & 2) && mm < tp.MmdThreshold) {
       const double deficit = tp.MmdThreshold - mm;

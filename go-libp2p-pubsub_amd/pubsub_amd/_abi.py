@@ -212,7 +212,7 @@ RCCL_FUNCTIONS = [
 ]
 
 KERNEL_NAMES = ["score", "refresh", "join", "fanout", "fwd", "phase_a", "publish", "phase_b",
-                "hb_pre", "heartbeat"]
+                "hb_pre", "heartbeat", "push"]
 
 
 def bind(path):

@@ -563,7 +563,8 @@ int gs_trace_encode(const gs_trace_event* ev, int64_t n, int32_t format, int64_t
 #define GS_K_PHASE_B 7   /* HandleRPC control processing                 */
 #define GS_K_HB_PRE 8    /* heartbeat prelude (backoff, penalties)       */
 #define GS_K_HEARTBEAT 9 /* mesh maintenance + emitGossip + mcache shift */
-#define GS_NUM_KERNELS 10
+#define GS_K_PUSH 10     /* per-edge copies for the next hop (k_push)    */
+#define GS_NUM_KERNELS 11
 /* Starts/stops per-kernel timing and clears the accumulators.  The oracle
  * accepts the call and reports zeros. */
 int gs_set_profiling(gs_engine* eng, int on);

@@ -10,6 +10,7 @@
 // (score_test.go, score_params_test.go, mcache_test.go, gossip_tracer_test.go,
 // peer_gater_test.go) restated in tests/test_oracle_*.py.
 #pragma once
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -18,6 +19,8 @@
 #include <map>
 #include <set>
 #include <string>
+#include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../include/gossip_engine.h"
@@ -169,11 +172,25 @@ struct PeerStats {  // score.go:17-35
   double behaviourPenalty = 0;
 };
 
+// drec.peers (a Go map[peer.ID]struct{}): a sorted vector, iterated ascending
+// like the std::set it replaces (a few peers per record; a tree node per peer
+// made the mid-size goldens' millions of records the oracle's memory bound).
+struct PeerSet {
+  std::vector<int> v;
+  size_t count(int p) const { return std::binary_search(v.begin(), v.end(), p) ? 1 : 0; }
+  void insert(int p) {
+    auto it = std::lower_bound(v.begin(), v.end(), p);
+    if (it == v.end() || *it != p) v.insert(it, p);
+  }
+  void clear() { std::vector<int>().swap(v); }
+  std::vector<int>::const_iterator begin() const { return v.begin(); }
+  std::vector<int>::const_iterator end() const { return v.end(); }
+};
 struct DeliveryRecord {  // score.go:98-103
   int status = deliveryUnknown;
   int64_t firstSeen = 0;
   int64_t validated = kTimeZero;
-  std::set<int> peers;
+  PeerSet peers;
 };
 
 struct Msg {  // the fields of pb.Message the hot path reads
@@ -188,7 +205,7 @@ class PeerScore {
   std::map<int, gs_topic_score_params> topics;  // params.Topics
   std::map<int, PeerStats> peerStats;
   std::map<uint32_t, std::set<int>> peerIPs;
-  std::map<int64_t, DeliveryRecord> records;    // messageDeliveries.records
+  std::unordered_map<int64_t, DeliveryRecord> records;  // messageDeliveries.records (never iterated)
   std::deque<std::pair<int64_t, int64_t>> gcQueue;  // (id, expire) head..tail
   std::function<double(int)> appSpecificScore = [](int) { return 0.0; };
   std::vector<std::pair<uint32_t, uint32_t>> whitelist;  // (net, mask)

@@ -68,7 +68,7 @@ struct Node {
   std::set<int> direct;                  // gs.direct
   std::map<int, std::set<int>> topics;   // p.topics (static subscriptions of peers)
   uint64_t mySubs = 0;                   // p.mySubs
-  std::set<int64_t> seen;                // p.seenMessages (timecache, no expiry in-window)
+  std::unordered_set<int64_t> seen;      // p.seenMessages (timecache, no expiry in-window; never iterated)
   std::set<int> dead;                    // neighbours whose connection is down (not in p.peers)
   // gossipsub router state — gossipsub.go:400-457
   std::map<int, std::set<int>> mesh, fanout;

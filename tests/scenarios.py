@@ -56,11 +56,12 @@ def gossipsub_dense(lib, seed=1, msgs=100, extra=()):
 
 def gossipsub_scored(lib, n=300, k=20, topics=1, seed=3, msgs=300, hb=12, flood=False, sub_frac=1.0,
                      app_neg_frac=0.0, ip_groups=0, params=None, window=1024, extra=(), app_neg=-150.0,
-                     direct_frac=0.0, topic0_frac=0.0):
+                     direct_frac=0.0, topic0_frac=0.0, burst=None):
     """gossipsub v1.1 with Eth2-derived scoring over a random regular graph.
     window = slots_per_topic; direct_frac: fraction of the undirected edges
     made direct peers on both ends (WithDirectPeers); topic0_frac: fraction of
-    the messages forced onto topic 0."""
+    the messages forced onto topic 0; burst = (node, count, hop): `count` more
+    messages by `node` at `hop`, on random topics."""
     rng = np.random.default_rng(seed)
     g = graphs.random_regular(n, k, seed)
     if direct_frac:
@@ -102,7 +103,16 @@ def gossipsub_scored(lib, n=300, k=20, topics=1, seed=3, msgs=300, hb=12, flood=
     if topic0_frac:
         top[rng2.random(msgs) < topic0_frac] = 0
     hops = (5 + (np.arange(msgs) * (hb * 10 - 20)) // msgs).astype(np.int64)
+    if burst is not None:
+        bn, bc, bh = burst
+        src = np.concatenate([src, np.full(bc, bn, np.int32)])
+        top = np.concatenate([top, rng2.integers(0, topics, bc).astype(np.int32)])
+        hops = np.concatenate([hops, np.full(bc, bh, np.int64)])
+        order = np.argsort(hops, kind="stable")
+        src, top, hops = src[order], top[order], hops[order]
+        msgs += bc
     e.publish(src, top, hops)
+    e.sched_top, e.sched_hops = top, hops
     st = window
     if msgs > st:
         # the engine reads back only messages whose slot is not recycled yet:
@@ -150,8 +160,23 @@ HEAVY = {
     # config3: 1 topic x 10048 slots -> W = 157 words (3 per lane)
     "c3shape": lambda lib, x=(): gossipsub_scored(lib, n=2000, k=32, topics=1, window=10048, msgs=2000, hb=8,
                                                   seed=23, extra=x),
+    # config4's steady-state phase B: an honest engine with
+    # T = 4 whose gossip bound holds more than MaxIHaveLength ids over all
+    # topics but fewer in any one, so from hop ~90 on phase B runs the honest
+    # sender-cut instantiation (cutMode == 2: handleIHave's iasked cut,
+    # gossipsub.go:625-667) with push active (T >= 4); 1536 slots per topic are
+    # recycled once (k_push's seen retirement, mcache.go:94-104)
+    "cut_honest_4t": lambda lib, x=(): gossipsub_scored(lib, n=200, k=16, topics=4, window=1536, msgs=9000, hb=18,
+                                                        seed=25, extra=x),
+    # k_push's region overflow (more than GS_PUSHR = 2048 copies from one sender
+    # in one hop: record -1, its receivers walk its frontier list): flood
+    # publish of a 150-message burst by node 0 to its 24 peers, T = 4
+    "push_overflow": lambda lib, x=(): gossipsub_scored(lib, n=200, k=24, topics=4, flood=True, window=512,
+                                                        msgs=400, hb=10, seed=27, burst=(0, 150, 40), extra=x),
 }
 SCENARIOS.update(HEAVY)
+
+
 
 
 def snapshot(e, msg_ids):
@@ -795,5 +820,8 @@ MIXED = {
     "mixed_scored": lambda lib, x=(): mixed_scored(lib, extra=x),
     "mixed_randomsub": lambda lib, x=(): mixed_randomsub(lib, extra=x),
     "acct_mixed": lambda lib, x=(): mixed_scored(lib, px=False, seed=84, extra=(_acct(3),) + tuple(x)),
+    # T >= 4: k_push is on, so its randomsub filter (rs_host && sel) and the
+    # floodsub-peer publish filter run in the pushed segments
+    "mixed_scored_4t": lambda lib, x=(): mixed_scored(lib, topics=4, seed=85, msgs=400, extra=x),
 }
 SCENARIOS.update(MIXED)

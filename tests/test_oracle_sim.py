@@ -52,3 +52,25 @@ def test_negative_app_score_peers_are_graylisted(oracle_path):
     # app score -150 gives score -150 < gossip threshold -100 but > graylist -300
     assert a["counters"]["deliveries"] > 0
     assert (a["scores"] <= -150).any()
+
+
+def test_cut_honest_4t_reaches_the_sender_cut_mode(oracle_path):
+    """cut_honest_4t is built to run the honest engine's phase B in its
+    sender-cut instantiation (gs_engine.hip stepOne: cutMode bit 1 when more
+    than MaxIHaveLength ids were published within the gossip bound of
+    (HistoryGossip + 1) heartbeats + the delivery age + 2 hops, bit 0 only if
+    one topic alone exceeds it).  The schedule must reach bit 1 for many hops
+    and never bit 0, and the run must carry IHAVE/IWANT traffic there."""
+    e, hops = scenarios.SCENARIOS["cut_honest_4t"](oracle_path)
+    top, hop = e.sched_top, e.sched_hops
+    bound = (5 + 1) * 10 + 3 * 10 + 2
+    cut_hops = 0
+    for h in range(hops):
+        live = (hop >= h - bound) & (hop <= h)
+        if live.sum() > 5000:
+            cut_hops += 1
+            assert np.bincount(top[live], minlength=4).max() <= 5000
+    assert cut_hops >= 60, cut_hops
+    e.step(hops)
+    c = e.counters()
+    assert c["ihave_sent"] > 0 and c["iwant_sent"] > 0 and c["deliveries"] == 9000 * 199
