@@ -53,13 +53,20 @@ WORKLOADS = {
     # 32-entry queue per hop.  500 msgs/round: the adversarial delivery
     # window keeps 200 hops of messages alive (10240 slots).
     "config5": dict(n=1_000_000, k=32, topics=1, slots=10240, msgs=500, adversarial=True),
-    # SURVEY.md §8(d) config 4's other variant: every peer in topic 0 plus 2
-    # random subnets of the 64 (the Eth2 attestation-subnet shape); the
-    # 1000 msgs/round go round-robin over the 64 topics as in config4
-    # (a subnet variant — topic 0 plus 2 random subnets per peer — is not a
-    # workload: its sparse subnet meshes deliver through gossip later than the
-    # honest message window's 3 heartbeats, E_LATE)
+    # BASELINE configs[1]: floodsub, and randomsub with size 100 (size = N
+    # degenerates to floodsub), on a 100k-peer random 32-regular
+    # graph, one topic, 10,000 messages published at one hop from uniform random
+    # sources.  One step = that batch published and propagated: 32 hops (the
+    # floodsub message window recycles a slot after maxAge + 2 = 32 hops; the
+    # copies stop after ~6 of them, the rest are cheap empty hops).
+    "config2": dict(n=100_000, k=32, topics=1, slots=10048, msgs=10_000, router="floodsub", hops=32),
+    "config2_rs100": dict(n=100_000, k=32, topics=1, slots=10048, msgs=10_000, router="randomsub", size=100,
+                          hops=32),
 }
+
+
+def hops_per_step(wl):
+    return wl.get("hops", HOPS_PER_ROUND)
 
 
 def build_engine(wl, rounds, seed, device, lib=None, n=None, msgs_per_round=None, extra=()):
@@ -68,6 +75,25 @@ def build_engine(wl, rounds, seed, device, lib=None, n=None, msgs_per_round=None
     msgs_per_round = msgs_per_round or wl.get("msgs", MSGS_PER_ROUND)
     g = graphs.random_regular_fast(n, wl["k"], seed)
     subs = graphs.all_subscribed(n, T)
+    if wl.get("router") in ("floodsub", "randomsub"):
+        # config2: the batch of each step published at its first hop
+        from pubsub_amd import NewFloodSub, NewRandomSub
+        opts = [WithMessageWindow(wl["slots"]), WithSeed(seed)]
+        if lib is None or "libgossip_engine" in os.path.basename(lib):
+            opts.append(WithDevice(device))
+        if wl["router"] == "floodsub":
+            eng = NewFloodSub(n, T, g, subs, *opts, *extra, lib=lib)
+        else:
+            eng = NewRandomSub(n, T, g, subs, wl["size"], *opts, *extra, lib=lib)
+        rng = np.random.default_rng(seed + 7)
+        hps = hops_per_step(wl)
+        hops = np.repeat(1 + hps * np.arange(rounds, dtype=np.int64), msgs_per_round)
+        src = rng.integers(0, n, len(hops)).astype(np.int32)
+        top = np.zeros(len(hops), np.int32)
+        eng.publish(src, top, hops)
+        eng.schedule = (top, hops)
+        eng.kinds, eng.srcs, eng.ipv4 = None, src, None
+        return eng, g
     if wl.get("subnets"):
         # topic 0 + `subnets` distinct random topics of 1..T-1 per peer
         srng = np.random.default_rng(seed + 13)
@@ -146,8 +172,12 @@ def algorithmic_bytes(kernel, eng, wl, per_hop):
     (n0, n1), (e0, e1) = eng.node_range, eng.edge_range
     N, E, T = n1 - n0, e1 - e0, wl["topics"]
     if kernel == "phase_a":
-        mesh = eng.mesh()[e0:e1]
-        fwd_edges = int((mesh != 0).sum())          # edges with a forwarding topic
+        scored = not wl.get("router") in ("floodsub", "randomsub")
+        if scored:
+            mesh = eng.mesh()[e0:e1]
+            fwd_edges = int((mesh != 0).sum())      # edges with a forwarding topic
+        else:
+            fwd_edges = E                           # floodsub / randomsub: every edge may forward
         W = per_hop["active_words"]
         # SURVEY.md §8(d) "Propagation hop": B_hop = (E_fwd + 3N) * W * 8 --
         # one sender frontier word per forwarding edge, and per node its seen
@@ -155,6 +185,10 @@ def algorithmic_bytes(kernel, eng, wl, per_hop):
         # message window (the words phase A touches: messages younger than the
         # delivery horizon).  This is the line's `achieved` model.
         b = (fwd_edges + 3.0 * N) * W * 8.0
+        if per_hop.get("prop_hops_per_step") is not None:
+            # config2: only the hops with copies on the wire propagate; the
+            # per-launch average spreads them over the step's launches
+            b *= per_hop["prop_hops_per_step"] / hops_per_step(wl)
         # the engine's own representation, for comparison with the PMC traffic:
         # each copy sent is one 16-bit slot of the sender's pushed segment for
         # that edge (k_push), read once by its receiver, plus the segment's
@@ -165,7 +199,10 @@ def algorithmic_bytes(kernel, eng, wl, per_hop):
         copies = per_hop["transmissions"] - per_hop["iwant_served"]  # served ids: 4 B each from the pool
         list_reads = 2.0 * copies + 8.0 * fwd_edges + 4.0 * per_hop["iwant_served"]
         list_writes = 4.0 * items
-        pending = 8.0 * T * E                        # pending-delivery counts, read + write per (edge, topic)
+        # pending-delivery counts, read + write per (edge, topic): 16-bit words
+        # when a topic's slots fit a byte count (gs_engine.hip narrowDlt)
+        pend_b = 0.0 if not scored else (4.0 if wl["slots"] <= 254 and T % 2 == 0 else 8.0)
+        pending = pend_b * T * E
         seen = 16.0 * N * W                          # seen words of the active window, read + write
         meta = 49.0 * E                              # rev, col, fwd masks, IWANT ref, S0 memo, direct, mesh
         eb = list_reads + list_writes + pending + seen + meta
@@ -240,6 +277,8 @@ def cpu_baseline(wl, seconds=20.0):
     if not os.path.exists(lib):
         return None
     threads = ctypes.CDLL(lib).gs_oracle_threads()  # OMP_NUM_THREADS: 16 on the GPU box (its CPU share)
+    if wl.get("router") in ("floodsub", "randomsub"):
+        return cpu_baseline_config2(wl, lib, threads, seconds)
     n = 2000
     swl = dict(wl, n=n)
     rounds = 8
@@ -266,6 +305,29 @@ def cpu_baseline(wl, seconds=20.0):
                       f"{wl['topics']} topics, Eth2 scoring, {wl.get('msgs', MSGS_PER_ROUND)} msgs/round"
                       f"{' (config-5 adversarial mix)' if wl.get('adversarial') else ''}, {hops} hops "
                       f"after 1 warm-up round, {dt:.1f} s"}
+
+
+def cpu_baseline_config2(wl, lib, threads, seconds):
+    """config2 on the oracle: the same router, degree and one-hop batches on a
+    20,000-peer graph, 200-message batches (each step fully propagated),
+    stepped until about `seconds` have passed."""
+    n, m = 20_000, 200
+    swl = dict(wl, n=n, msgs=m)
+    hps = hops_per_step(wl)
+    eng, _ = build_engine(swl, 50, 11, 0, lib=lib, n=n)
+    t0 = time.perf_counter()
+    steps = 0
+    while steps < 50 and (steps == 0 or time.perf_counter() - t0 < seconds):
+        eng.step(hps)
+        steps += 1
+    dt = time.perf_counter() - t0
+    dlv = eng.counters()["deliveries"]
+    return {"value": dlv / dt, "unit": "deliveries/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_info(), "nproc": os.cpu_count(),
+            "sample": f"oracle/ (C++ restatement, OpenMP {threads} threads), {wl['router']}"
+                      f"{' size ' + str(wl['size']) if wl.get('size') else ''}, {n} peers k={wl['k']}, "
+                      f"{steps} batches of {m} messages each published at one hop and propagated "
+                      f"({hps} hops), {dt:.1f} s"}
 
 
 def main():
@@ -335,6 +397,8 @@ def main():
         wl["n"] = args.peers
     if args.slots:
         wl["slots"] = args.slots
+    hps = hops_per_step(wl)
+    gossip = wl.get("router", "gossipsub") == "gossipsub"
     rounds = args.warmup + args.steps + 1
     t_setup = time.perf_counter()
     # partitioned ranks simulate ONE graph and schedule (same seed); replicas differ
@@ -350,7 +414,19 @@ def main():
     free0 = dev_free()
     eng, g = build_engine(wl, rounds, 3 if partitioned else 3 + rank, local, extra=extra, lib=args.lib)
     # hop 0 (Join) + warm-up rounds: meshes form, the message window fills
-    eng.step(1 + args.warmup * HOPS_PER_ROUND)
+    eng.step(1)
+    prop_hops = None
+    if not gossip:
+        # config2: the hops of a step in which copies are on the wire (the
+        # roofline model's propagation hops), from the first warm-up step
+        prop_hops = 0
+        for _ in range(hps):
+            t0c = eng.counters()["transmissions"]
+            eng.step(1)
+            prop_hops += eng.counters()["transmissions"] > t0c
+        eng.step(max(0, args.warmup - 1) * hps)
+    else:
+        eng.step(args.warmup * hps)
     eng.sync()
     free1 = dev_free()
     device_gb = round((free0 - free1) / 2**30, 2) if free0 is not None and free1 is not None else None
@@ -367,7 +443,7 @@ def main():
     eng.set_profiling(True)
     barrier()
     t0 = time.perf_counter()
-    eng.step(args.steps * HOPS_PER_ROUND)
+    eng.step(args.steps * hps)
     eng.sync()
     barrier()
     t1 = time.perf_counter()
@@ -395,13 +471,15 @@ def main():
         dist.destroy_process_group()
         return
 
-    nh = args.steps * HOPS_PER_ROUND
+    nh = args.steps * hps
     per_hop = {"events_per_round": {k: v / args.steps for k, v in events.items()},
                "deliveries": (c1["deliveries"] - c0["deliveries"]) / nh,
                "published": (c1["published"] - c0["published"]) / nh,
                "transmissions": (c1["transmissions"] - c0["transmissions"]) / nh,
                "iwant_served": (c1["iwant_served"] - c0["iwant_served"]) / nh,
-               "active_words": float(np.mean([active_words(eng, wl, hop0 + i) for i in range(nh)])),
+               "active_words": float(np.mean([active_words(eng, wl, hop0 + i) for i in range(nh)])) if gossip
+               else wl["topics"] * wl["slots"] / 64.0,
+               "prop_hops_per_step": prop_hops, "steps": args.steps,
                "mesh_pairs": int(np.bitwise_count(eng.mesh()[eng.edge_range[0]:eng.edge_range[1]]).sum(dtype=np.int64))}
     # the roofline is the heaviest kernel with an algorithmic byte model (phase
     # B's control work has none: config3's steady state and config5 can be
@@ -465,19 +543,21 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if partitioned else "weak",
         "vs_baseline": None,
-        "dtype": "f64+u64",
+        "dtype": "f64+u64" if gossip else "u64",
         "data": "synthetic (seeded random 32-regular graph, seeded publish schedule)",
         "config": {"workload": f"{args.workload}: {wl['n'] / 1e6:g}M peers, {wl['topics']} topic"
-                   f"{'s' if wl['topics'] > 1 else ''}, k=32, gossipsub v1.1 + Eth2 scoring, "
-                   f"{msgs_round} msgs/round, 10 hops/round" +
+                   f"{'s' if wl['topics'] > 1 else ''}, k=32, " +
+                   (f"gossipsub v1.1 + Eth2 scoring, {msgs_round} msgs/round, 10 hops/round" if gossip else
+                    f"{wl['router']}{' size ' + str(wl['size']) if wl.get('size') else ''}, {msgs_round} msgs "
+                    f"published at one hop per step, {hps} hops/step ({prop_hops} with copies on the wire)") +
                    (f", each peer in topic 0 + {wl['subnets']} random subnets" if wl.get("subnets") else "") +
                    (", 20% Sybils (IWANT / GRAFT / phantom-IHAVE spam, invalid messages, 20 per IP), "
                     "peer gater, validation queue 32" if wl.get("adversarial") else ""),
                    "peers": wl["n"], "topics": wl["topics"], "degree": wl["k"],
-                   "msgs_per_round": msgs_round, "hops_per_round": HOPS_PER_ROUND,
+                   "msgs_per_round": msgs_round, "hops_per_round": hps,
                    "parallelism": f"partition{world}" if partitioned else f"replicas{world}"},
         "rounds_per_sec": rounds_per_s * (1 if partitioned else world),
-        "hops_per_sec": rounds_per_s * HOPS_PER_ROUND,
+        "hops_per_sec": rounds_per_s * (hps if gossip else prop_hops),
         "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kstats.items() if v[1]},
         "events_per_step": {k: v // args.steps for k, v in events.items()},
         # the control counters depend on the canonical schedule: each

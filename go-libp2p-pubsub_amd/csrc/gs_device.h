@@ -58,7 +58,7 @@
 #define GS_PTX_BITS 10 // mcache.peertx hash slots per node: 2^10 (2^12 when IWANT spammers run)
 #define GS_CUTS 64     // IHAVE entries above MaxIHaveLength one node can cut per hop
 // phase B dynamic LDS: the MaxIHaveLength-cut tables (cut mode)
-#define GS_CUTLDS (256 * 4 + GS_CUTS * 4 + GS_CUTS * 16 + 64 * 16 + 128 * 4 + 16)
+#define GS_CUTLDS (256 * 4 + GS_CUTS * 4 + GS_CUTS * 16 + 64 * 16 + 128 * 4 + 16 + GS_SEL_CAP * 16 + 16 + GS_CUTS * 4)
 
 // device counter slots (same order as gs_counters)
 enum {
@@ -922,4 +922,101 @@ __device__ __forceinline__ void select_kth(F&& each, int k, uint32_t* hist, unsi
     prev = best;
   }
   M = prev;
+}
+
+// select_kth for n candidates with uniformly random keys (Philox outputs:
+// emitGossip's and handleIHave's keyed shuffles), in ONE pass of `each` in
+// the common case instead of about three.  The k-th smallest key's top byte
+// is expected near 256 k / n (its standard deviation is about 256 *
+// sqrt(k (n - k) / n^3), ~1.2 bins at config3's 5000 of 6000), so the pass
+// builds the top-byte histogram and keeps every candidate whose top byte lies
+// within GS_SEL_WIN bins of that estimate in LDS (cand: GS_SEL_CAP (key, id)
+// pairs + a counter).  If the k-th falls into a kept bin and nothing
+// overflowed, the k-th smallest (key, id) of that bin is ranked among the kept
+// entries; otherwise select_kth runs as before.  Either way the result is the
+// exact k-th smallest (key, id).  n = the number of candidates each() yields.
+#define GS_SEL_WIN 3
+#define GS_SEL_CAP 192
+template <class F>
+__device__ __forceinline__ void select_kth_est(F&& each, int k, int n, uint32_t* hist, unsigned long long* cand,
+                                               unsigned long long& K, long long& M) {
+  const int lane = lane_id();
+  if (k >= n) {  // every candidate is taken
+    K = ~0ull;
+    M = INT64_MAX;
+    return;
+  }
+  const int est = (int)(((int64_t)k << 8) / n);
+  const int lo = max(0, est - GS_SEL_WIN), hi = min(255, est + GS_SEL_WIN);
+  uint32_t* const cnt = (uint32_t*)(cand + 2 * GS_SEL_CAP);
+  for (int q = lane; q < 256; q += 64) hist[q] = 0u;
+  if (lane == 0) *cnt = 0u;
+  __syncthreads();
+  each([&](unsigned long long key, long long id) {
+    const int top = (int)(key >> 56);
+    atomicAdd(&hist[top], 1u);
+    if (top >= lo && top <= hi) {
+      const uint32_t pos = atomicAdd(cnt, 1u);
+      if (pos < GS_SEL_CAP) {
+        cand[2 * pos] = key;
+        cand[2 * pos + 1] = (unsigned long long)id;
+      }
+    }
+  });
+  __syncthreads();
+  const uint32_t c0 = hist[4 * lane], c1 = hist[4 * lane + 1], c2 = hist[4 * lane + 2], c3 = hist[4 * lane + 3];
+  const int sum = (int)(c0 + c1 + c2 + c3);
+  const int incl = wave_incl_sum(sum);
+  const int excl = incl - sum;
+  const bool mine = excl < k && k <= incl;
+  int digit = 0, below = 0;
+  if (mine) {
+    const uint32_t cs[4] = {c0, c1, c2, c3};
+    int acc = excl, dd = 0;
+    for (; dd < 3; ++dd) {
+      if (acc + (int)cs[dd] >= k) break;
+      acc += (int)cs[dd];
+    }
+    digit = 4 * lane + dd;
+    below = acc;
+  }
+  const unsigned long long m = __ballot(mine);
+  const int src = __ffsll((long long)m) - 1;  // k < n: some lane holds the k-th
+  digit = lane_get(digit, src);
+  below = lane_get(below, src);
+  const int nc = (int)*cnt;
+  __syncthreads();
+  if (digit < lo || digit > hi || nc > GS_SEL_CAP) {
+    select_kth(each, k, hist, K, M);  // the estimate missed: the multi-pass select
+    return;
+  }
+  // the (k - below)-th smallest (key, id) among the kept entries of bin `digit`
+  const int kk = k - below;
+  unsigned long long fk = 0;
+  long long fm = 0;
+  bool found = false;
+  for (int j0 = 0; j0 < nc; j0 += 64) {
+    const int j = j0 + lane;
+    const unsigned long long key = j < nc ? cand[2 * j] : ~0ull;
+    const long long id = j < nc ? (long long)cand[2 * j + 1] : INT64_MAX;
+    if (j < nc && (int)(key >> 56) == digit) {
+      int rank = 0;
+      for (int q = 0; q < nc; ++q) {
+        const unsigned long long qk = cand[2 * q];
+        if ((int)(qk >> 56) != digit) continue;
+        const long long qm = (long long)cand[2 * q + 1];
+        rank += (qk < key || (qk == key && qm < id)) ? 1 : 0;
+      }
+      if (rank == kk - 1) {
+        fk = key;
+        fm = id;
+        found = true;
+      }
+    }
+  }
+  const unsigned long long f = __ballot(found);
+  const int fl = __ffsll((long long)f) - 1;
+  K = lane_get64(fk, fl);
+  M = (long long)lane_get64((uint64_t)fm, fl);
+  __syncthreads();
 }

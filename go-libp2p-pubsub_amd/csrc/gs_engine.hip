@@ -156,7 +156,17 @@ struct gs_engine {
   size_t xSendCap = 0, xRecvCap = 0, xSendECap = 0, xRecvECap = 0;
   unsigned long long* xCnt = nullptr;  // device: [world] record counts, [world] cursors, bump
   int64_t* xOff = nullptr;             // device: [world] record offsets
-  unsigned long long* xHost = nullptr; // pinned: world counts, bump, poolCnt
+  unsigned long long* xHost = nullptr; // pinned: world counts, bump, poolCnt, error, push counts [2 world]
+  // cross-rank push (gs_exchange.h k_xp_*): send blocks, device counters
+  // ([world] records, [world] slots, then the same as cursors), block offsets
+  // and record counts ([world] each); a parity's receive area is ibx[k] past
+  // the owned senders' regions (ibxOwnSlots), ibxCapB[k] bytes in all
+  uint8_t* xSendP = nullptr;
+  size_t xSendPCap = 0;
+  unsigned long long* xpCnt = nullptr;
+  int64_t* xpOff = nullptr;
+  int64_t ibxOwnSlots = 0;
+  size_t ibxCapB[2] = {0, 0};
   double xMs = 0.0;                    // host wall time spent in exchanges
   int64_t xBytes = 0;                  // bytes received by this rank
   int exchange(int cur, bool hb);
@@ -286,7 +296,7 @@ struct gs_engine {
       if (st.p) (void)hipHostFree(st.p);
     }
     for (hipEvent_t ev : evPool) (void)hipEventDestroy(ev);
-    for (uint8_t* p : {xSend, xRecv, xSendE, xRecvE}) if (p) (void)hipFree(p);
+    for (uint8_t* p : {xSend, xRecv, xSendE, xRecvE, xSendP}) if (p) (void)hipFree(p);
     if (xHost) (void)hipHostFree(xHost);
     if (errRing) (void)hipHostFree(errRing);
     for (void* p : allocs) (void)hipFree(p);
@@ -668,7 +678,9 @@ int gs_engine::start() {
     x.ibx[k] = nullptr;
     x.ibxRec[k] = nullptr;
     if (!pushOn) continue;
-    x.ibx[k] = dalloc<uint16_t>((size_t)std::max<int64_t>(nOwnN, 1) * GS_PUSHR); chk(x.ibx[k]);
+    ibxOwnSlots = (int64_t)std::max<int64_t>(nOwnN, 1) * GS_PUSHR;
+    x.ibx[k] = dalloc<uint16_t>((size_t)ibxOwnSlots); chk(x.ibx[k]);
+    ibxCapB[k] = (size_t)ibxOwnSlots * 2;
     x.ibxRec[k] = dalloc<int64_t>(E, 0xFF); chk(x.ibxRec[k]);
   }
   x.maxDeg = std::max(1, maxdeg);
@@ -932,6 +944,8 @@ int gs_engine::start() {
     uint8_t* nr = dalloc<uint8_t>(N); chk(nr);
     xCnt = dalloc<unsigned long long>(2 * world + 1); chk(xCnt);
     xOff = dalloc<int64_t>(world); chk(xOff);
+    xpCnt = dalloc<unsigned long long>(4 * world); chk(xpCnt);
+    xpOff = dalloc<int64_t>(2 * world); chk(xpOff);
     if (ok) {
       std::vector<uint8_t> h(N);
       for (int r = 0; r < world; ++r)
@@ -940,7 +954,7 @@ int gs_engine::start() {
       HIPCHECK(hipStreamSynchronize(stream));
     }
     x.nodeRank = nr;
-    HIPCHECK(hipHostMalloc((void**)&xHost, (size_t)(world + 3) * 8, hipHostMallocDefault));
+    HIPCHECK(hipHostMalloc((void**)&xHost, (size_t)(3 * world + 3) * 8, hipHostMallocDefault));
   }
   if (!ok) {
     gs_set_error("device allocation failed (state); reduce num_nodes or slots_per_topic");
@@ -1644,6 +1658,12 @@ int gs_engine::exchange(int cur, bool hb) {
   // 1. counts + lists (into a buffer that usually suffices; re-packed if not)
   HIPCHECK(hipMemsetAsync(xCnt, 0, (size_t)(2 * world + 1) * 8, stream));
   if (eOwn) k_x_count<<<nblk(eOwn, 256), 256, 0, stream>>>(d, cur, cnt);
+  const bool xpush = d.ibxRec[0] != nullptr;  // k_push ran: cross-rank edges' segments travel too
+  if (xpush) {
+    HIPCHECK(hipMemsetAsync(xpCnt, 0, (size_t)4 * world * 8, stream));
+    if (eOwn) k_xp_count<<<nblk(eOwn, 256), 256, 0, stream>>>(d, cur, xpCnt);
+    HIPCHECK(hipMemcpyAsync(xHost + world + 3, xpCnt, (size_t)2 * world * 8, hipMemcpyDeviceToHost, stream));
+  }
   if (xSendCap < hdrBytes + (16u << 20)) {
     int rc = growDev(xSend, xSendCap, hdrBytes + (16u << 20));
     if (rc) return rc;
@@ -1699,17 +1719,47 @@ int gs_engine::exchange(int cur, bool hb) {
     HIPCHECK(hipMemcpyAsync(xOff, sendOff.data(), (size_t)world * 8, hipMemcpyHostToDevice, stream));
     k_x_pack<<<nblk(eOwn, 256), 256, 0, stream>>>(d, cur, xOff, cursor, (XRec*)xSendE);
   }
+  // 2b. pushed segments of cross-rank edges, one block per destination rank:
+  //     [PRec x records][slots]
+  std::vector<int64_t> pRec(world, 0), pSlots(world, 0), pBytes(world, 0), pOff(world, 0);
+  if (xpush) {
+    int64_t tot = 0;
+    for (int r = 0; r < world; ++r) {
+      pRec[r] = (int64_t)xHost[world + 3 + r];
+      pSlots[r] = (int64_t)xHost[world + 3 + world + r];
+      pBytes[r] = 16 * pRec[r] + 2 * pSlots[r];
+      pOff[r] = tot;
+      tot += pBytes[r];
+    }
+    int rc = growDev(xSendP, xSendPCap, (size_t)std::max<int64_t>(tot, 16));
+    if (rc) return rc;
+    if (tot) {
+      std::vector<int64_t> offRec(2 * (size_t)world);
+      for (int r = 0; r < world; ++r) {
+        offRec[(size_t)r] = pOff[r];
+        offRec[(size_t)world + r] = pRec[r];
+      }
+      HIPCHECK(hipMemcpyAsync(xpOff, offRec.data(), (size_t)2 * world * 8, hipMemcpyHostToDevice, stream));
+      HIPCHECK(hipMemsetAsync(xpCnt + 2 * world, 0, (size_t)2 * world * 8, stream));
+      k_xp_pack<<<nblk(eOwn, 256), 256, 0, stream>>>(d, cur, xpOff, xpOff + world, xpCnt + 2 * world, xSendP);
+    }
+  }
   HIPCHECK(hipStreamSynchronize(stream));  // sendOff is pageable; the transport reads the buffers
   // 3. sizes of every rank: [bcast bytes, list entries, arena ids, gw rows?,
-  //    records to rank 0..world-1, device error word]
+  //    records to rank 0..world-1, device error word, dials, push records to
+  //    rank 0..world-1, push slots to rank 0..world-1]
   // the connector's dials of this hop (peer exchange): every rank applies all
   // of them at the next hop's start (each launching the sides it owns)
-  const int nS = 6 + world;
+  const int nS = 6 + 3 * world;
   std::vector<int64_t> mine(nS), all((size_t)nS * world);
   mine[5 + world] = (int64_t)pxPend.size();
   mine[0] = (int64_t)bcast; mine[1] = nEnt; mine[2] = nPool; mine[3] = hb ? 1 : 0;
   for (int r = 0; r < world; ++r) mine[4 + r] = sendRec[r];
   mine[4 + world] = myErr;
+  for (int r = 0; r < world; ++r) {
+    mine[6 + world + r] = pRec[r];
+    mine[6 + 2 * world + r] = pSlots[r];
+  }
   const auto t0 = std::chrono::steady_clock::now();
   if (tr.allgather_i64(tr.user, mine.data(), nS, all.data()) != 0) {
     gs_set_error("transport allgather_i64 failed");
@@ -1769,6 +1819,36 @@ int gs_engine::exchange(int cur, bool hb) {
     gs_set_error("transport alltoallv failed");
     return GS_EDEVICE;
   }
+  // the pushed segments land behind the owned senders' regions of ibx[cur]
+  std::vector<int64_t> pInRec(world, 0), pInOff(world, 0);
+  int64_t pIn = 0;
+  if (xpush) {
+    std::vector<int64_t> pInB(world, 0);
+    for (int r = 0; r < world; ++r) {
+      pInRec[r] = all[(size_t)r * nS + 6 + world + rank];
+      pInB[r] = 16 * pInRec[r] + 2 * all[(size_t)r * nS + 6 + 2 * world + rank];
+      pInOff[r] = pIn;
+      pIn += pInB[r];
+    }
+    const size_t own = (size_t)ibxOwnSlots * 2;
+    if (own + (size_t)pIn > ibxCapB[cur]) {
+      // grow this parity's buffer, keeping the owned regions (this hop's
+      // segments for local receivers)
+      uint8_t* p = reinterpret_cast<uint8_t*>(d.ibx[cur]);
+      const uint8_t* old = p;
+      int rc = growDev(p, ibxCapB[cur], own + (size_t)pIn, own);
+      if (rc) return rc;
+      for (void*& a : allocs)
+        if (a == old) a = nullptr;  // freed by growDev
+      allocs.push_back(p);
+      d.ibx[cur] = reinterpret_cast<uint16_t*>(p);
+    }
+    if (tr.alltoallv(tr.user, xSendP, pBytes.data(), reinterpret_cast<uint8_t*>(d.ibx[cur]) + own, pInB.data()) != 0) {
+      gs_set_error("transport alltoallv failed (pushed segments)");
+      return GS_EDEVICE;
+    }
+    xBytes += pIn;
+  }
   xMs += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   // 4. unpack the other ranks' parts into the mirrors
   for (int r = 0; r < world; ++r) {
@@ -1790,6 +1870,12 @@ int gs_engine::exchange(int cur, bool hb) {
   if (totIn) {
     const int64_t n = totIn / (int64_t)sizeof(XRec);
     k_x_unpack<<<nblk(n, 256), 256, 0, stream>>>(d, cur, (const XRec*)xRecvE, n);
+  }
+  for (int r = 0; r < world; ++r) {
+    if (!pInRec[r]) continue;
+    const uint8_t* blk = reinterpret_cast<const uint8_t*>(d.ibx[cur]) + (size_t)ibxOwnSlots * 2 + pInOff[r];
+    const int64_t slotBase = ibxOwnSlots + (pInOff[r] + 16 * pInRec[r]) / 2;
+    k_xp_unpack<<<nblk(pInRec[r], 256), 256, 0, stream>>>(d, cur, (const PRec*)blk, pInRec[r], slotBase);
   }
   HIPCHECK(hipGetLastError());
   return GS_OK;

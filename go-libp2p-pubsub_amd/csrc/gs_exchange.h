@@ -160,4 +160,80 @@ __global__ __launch_bounds__(64) void k_x_unlists(Dev d, int cur, const int64_t*
   if (lane == 0) d.fln[cur][u] = len;
 }
 
+// ---- pushed copies of cross-rank edges (k_push's segments, Dev::ibx) ----
+// A sender's k_push lays out the copies of EVERY out-edge, and writes each
+// edge's record at ibxRec[cur][rev[e]] (the receiver's in-edge).  For an edge
+// whose receiver lives on another rank, the record and its slots travel in a
+// second all-to-all-v, one block per destination rank:
+//   [PRec x nRec][slots, each segment 8-aligned]
+// and the receiver's alltoallv lands the blocks right behind its own senders'
+// regions in ibx[cur], so its phase A reads a remote sender's copies exactly
+// like a local one's (pOff into ibx), instead of walking the sender's whole
+// frontier list.  A record travels for every edge the sender forwards on
+// (fwdRelay | fwdPub != 0 -- exactly the edges whose fwdIn mirror makes the
+// receiver read its record); -1 (the sender's region overflowed) keeps the
+// list walk.
+struct PRec {  // 16 bytes
+  int32_t ri;   // the receiver's in-edge (rev[e])
+  int32_t n;    // copies, -1 = walk the sender's list
+  int64_t off;  // first slot of the segment, in slots from the block's slot region
+};
+static_assert(sizeof(PRec) == 16, "PRec layout");
+
+__device__ __forceinline__ bool xp_needed(const Dev& d, int cur, int64_t e, int& dest) {
+  dest = d.nodeRank[d.col[e]];
+  if (dest == d.rank) return false;
+  return (d.fwdRelay[cur][e] | d.fwdPub[cur][e]) != 0;
+}
+__device__ __forceinline__ int xp_slots(int64_t rec) {  // slots a record's segment occupies (8-aligned)
+  return rec > 0 ? (int)(((rec & 0xFFFFFF) + 7) & ~7) : 0;
+}
+
+// Records and slots per destination rank: cnt[dest], cnt[world + dest].
+__global__ void k_xp_count(Dev d, int cur, unsigned long long* __restrict__ cnt) {
+  const int64_t e = d.e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.e1) return;
+  int dest;
+  if (!xp_needed(d, cur, e, dest)) return;
+  atomicAdd(&cnt[dest], 1ull);
+  const int ns = xp_slots(d.ibxRec[cur][d.rev[e]]);
+  if (ns) atomicAdd(&cnt[d.world + dest], (unsigned long long)ns);
+}
+
+// Packs the records and segments; boff[dest] = block byte offset in `out`,
+// nrec[dest] = the block's record count, cursors [world] records, [world] slots.
+__global__ void k_xp_pack(Dev d, int cur, const int64_t* __restrict__ boff, const int64_t* __restrict__ nrec,
+                          unsigned long long* __restrict__ cursor, uint8_t* __restrict__ out) {
+  const int64_t e = d.e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.e1) return;
+  int dest;
+  if (!xp_needed(d, cur, e, dest)) return;
+  const int64_t ri = d.rev[e];
+  const int64_t rec = d.ibxRec[cur][ri];
+  const int ns = xp_slots(rec);
+  uint8_t* blk = out + boff[dest];
+  const int64_t k = (int64_t)atomicAdd(&cursor[dest], 1ull);
+  int64_t so = 0;
+  if (ns) {
+    so = (int64_t)atomicAdd(&cursor[d.world + dest], (unsigned long long)ns);
+    const uint4* src = (const uint4*)(d.ibx[cur] + (rec >> 24));  // 8-aligned segment: 16-B aligned
+    uint4* dst = (uint4*)(blk + 16 * nrec[dest] + 2 * so);
+    for (int j = 0; j < ns / 8; ++j) dst[j] = src[j];
+  }
+  PRec p;
+  p.ri = (int32_t)ri;
+  p.n = rec < 0 ? -1 : (int32_t)(rec & 0xFFFFFF);
+  p.off = so;
+  ((PRec*)blk)[k] = p;
+}
+
+// One source rank's block, received at slot index `slot0` of ibx[cur] (its
+// slot region starts after the records): the receiver's records point at it.
+__global__ void k_xp_unpack(Dev d, int cur, const PRec* __restrict__ in, int64_t n, int64_t slotBase) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const PRec p = in[k];
+  d.ibxRec[cur][p.ri] = p.n < 0 ? -1 : (((slotBase + p.off) << 24) | (int64_t)p.n);
+}
+
 __global__ void k_set_u64(unsigned long long* p, unsigned long long v) { *p = v; }

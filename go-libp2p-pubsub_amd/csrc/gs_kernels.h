@@ -705,8 +705,9 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
     }
     gray = scoring && !d.direct[e] && d.score0[e] < d.graylistThr;
     if (relayAll | pubAll) {
-      // an owned sender pushed this edge's copies (k_push): read that segment
-      if (u >= d.n0 && u < d.n1 && d.ibxRec[0] != nullptr) {
+      // the sender pushed this edge's copies (k_push; a remote sender's record
+      // and segment arrived with the exchange): read that segment
+      if (d.ibxRec[0] != nullptr) {
         const int64_t rec = d.ibxRec[prv][e];
         if (rec >= 0) {
           pOff = rec >> 24;
@@ -1872,9 +1873,10 @@ __device__ __forceinline__ uint64_t wave_transpose64(uint64_t x) {
 // segments laid out 8-aligned in row order in the sender's own region of the
 // arena (GS_PUSHR slots, no allocation), staged in LDS (order within a
 // segment is free: the receiver's updates commute) and stored coalesced.
-// Records go to the receiver's in-edge; an edge to a receiver on another
-// rank is left to the receiver's list walk, as is every edge of a sender
-// whose copies overflow its region (record -1).
+// Records go to the receiver's in-edge (a receiver on another rank gets the
+// record and the segment through the exchange, gs_exchange.h); every edge of
+// a sender whose copies overflow its region gets -1: the receiver walks the
+// sender's list.
 __global__ __launch_bounds__(64) void k_push(Dev d, int cur) {
   __shared__ uint64_t sMR[64], sMP[64];
   __shared__ uint16_t sSlot[64];
@@ -1890,17 +1892,15 @@ __global__ __launch_bounds__(64) void k_push(Dev d, int cur) {
   // the edges' sets
   const int Ln0 = d.fln[cur][u];
   const uint32_t ent0 = L[lane];
-  bool local = false;
+  // every out-edge gets a record; one to a receiver on another rank travels
+  // with the hop's exchange (gs_exchange.h k_xp_pack)
+  const bool local = lane < deg;
   uint64_t relay = 0, pub = 0;
   int64_t re = 0;
-  if (lane < deg) {
-    const int recv = d.col[e];
-    local = recv >= d.n0 && recv < d.n1;
-    if (local) {
-      re = d.rev[e];
-      relay = d.fwdRelay[cur][e];
-      pub = d.fwdPub[cur][e];
-    }
+  if (local) {
+    re = d.rev[e];
+    relay = d.fwdRelay[cur][e];
+    pub = d.fwdPub[cur][e];
   }
   const int Ln = __ballot((relay | pub) != 0) ? Ln0 : 0;
   if (Ln == 0) {

@@ -776,6 +776,8 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
     long long* const iM = (long long*)(iK + 64);                   // [64] sender cut id
     uint32_t* const cBits = (uint32_t*)(iM + 64);                   // [128] item is cut
     int* const cN = (int*)(cBits + 128);
+    unsigned long long* const cand = (unsigned long long*)(cN + 4);  // select_kth_est's kept pairs + counter
+    int* const cNm = (int*)(cand + 2 * GS_SEL_CAP + 2);             // [GS_CUTS] ids of a cut item
     int nCut = 0;
     if (cutMode & 1) {
       for (int k = lane; k < 128; k += 64) cBits[k] = 0u;
@@ -794,6 +796,7 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
           const int pos = atomicAdd(cN, 1);
           if (pos < GS_CUTS) {
             cItem[pos] = tb;
+            cNm[pos] = nm;
             atomicOr(&cBits[tb >> 5], 1u << (tb & 31));
           } else {
             set_err(d, E_TRUNCATE);
@@ -822,7 +825,7 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
         };
         unsigned long long K;
         long long M;
-        select_kth(each, d.MaxIHaveLength, cHist, K, M);
+        select_kth_est(each, d.MaxIHaveLength, cNm[c], cHist, cand, K, M);
         if (lane == 0) {
           cK[c] = K;
           cM[c] = M;
@@ -960,7 +963,7 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
         };
         unsigned long long K;
         long long M;
-        select_kth(each, kk, cHist, K, M);
+        select_kth_est(each, kk, lane_get(myWantAll, i), cHist, cand, K, M);
         if (lane == 0) {
           iK[i] = K;
           iM[i] = M;

@@ -128,6 +128,12 @@ def run_partitioned(world, name, oracle):
     (3, "px_star"),
     (2, "direct_churn"),
     (2, "px_gater"),
+    # T >= 4: k_push's segments of cross-rank edges travel in the exchange and
+    # the receivers read them as local ones (gs_exchange.h k_xp_*); a sender
+    # whose region overflows sends -1 records (its receivers walk its list)
+    (2, "c4shape"),
+    (3, "cut_honest_4t"),
+    (2, "push_overflow"),
 ])
 def test_partitioned_engine_matches_oracle(world, name, oracle_path):
     res = run_partitioned(world, name, oracle_path)
