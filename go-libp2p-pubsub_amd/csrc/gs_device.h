@@ -247,6 +247,9 @@ struct Dev {
   uint64_t* boMask;  // [E] bit t: backoff of (e, t) is set (the heartbeat's candidate filter
                      // reads one coalesced word per edge instead of a strided expiry per topic)
   double *fmd, *mmd, *mfp, *imd;  // per-(edge, topic) rows (tix)
+  uint64_t* mfpM;                 // [E] bit t: mfp of (e, t) may be non-zero (clear => 0.0); the
+                                  // refresh reads only those mfp entries (P3b is rare: a prune
+                                  // with a delivery deficit, decaying to zero again)
   int32_t anyImd;                 // 0: no invalid delivery ever recorded, imd is all 0 (P4 = 0)
   uint32_t* dlt;                  // [E][T]: deliveries not yet folded into fmd / mmd,
                                   // (+1s to fmd) | (+1s to mmd) << 16 (see eff_fmd)
@@ -748,6 +751,7 @@ __device__ __forceinline__ void stats_prune(const Dev& d, int64_t e, int t) {
   if ((fl & 2) && mm < thr) {
     const double deficit = thr - mm;
     d.mfp[i] += deficit * deficit;
+    atomicOr((unsigned long long*)&d.mfpM[e], 1ull << t);
   }
   if (fl & 1) d.meshTime[i] = mesh_time_of(d.lastRefresh, d.graftTime[i]);  // kept as it was at the prune
   d.flags[i] = fl & ~1;

@@ -469,8 +469,8 @@ int gs_engine::start() {
     anyRandom = false;
     for (uint8_t r : routerH) anyRandom = anyRandom || r == GS_ROUTER_RANDOMSUB;
   }
-  if (doPX && (behaveAll != 0 || acctOn)) {
-    gs_set_error("peer exchange is supported by an honest engine without RPC accounting");
+  if (doPX && acctOn) {
+    gs_set_error("peer exchange is supported without RPC accounting (PX record sizes are not modelled)");
     return GS_EUNSUPPORTED;
   }
   if (doPX && N >= (1 << 26)) {  // a PX arena entry is topic << 26 | peer (gs_kernels_ctl.h px_append)
@@ -762,6 +762,7 @@ int gs_engine::start() {
   x.backoff = dalloc<int64_t>(TE);
   x.boMask = dalloc<uint64_t>(E); chk(x.boMask);
   x.fmd = dalloc<double>(TE); x.mmd = dalloc<double>(TE); x.mfp = dalloc<double>(TE); x.imd = dalloc<double>(TE);
+  x.mfpM = dalloc<uint64_t>(E); chk(x.mfpM);
   // 16-bit pending counts when a topic's slots (at most St + 1 messages live at
   // one hop) fit a byte and the pairs of an edge pack into whole words
   narrowDlt = St <= 254 && (T % 2) == 0;

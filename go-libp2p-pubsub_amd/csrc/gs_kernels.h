@@ -160,12 +160,21 @@ __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t no
   // lane's edge, loaded with the first batch instead of after the topic sums
   // (one edge per lane when the wave covers at most 64 edges)
   double tApp = 0.0, tP6 = 0.0, tBp = 0.0;
+  // the mfp mask of the lane's edge (Dev::mfpM): with one edge per lane and a
+  // lane per topic (LANE_T), a pair reads mfp only where its bit is set, and
+  // the refreshed mask is a ballot; otherwise every mfp is read and the mask
+  // (a "may be non-zero" hint) is left as it is
+  constexpr bool kMask = LANE_T;
+  uint64_t mM = ~0ull;
   if (epw <= 64 && lane < ng) {
     const int64_t e = e0 + lane;
     tApp = d.app[d.col[e]];
     tP6 = d.p6[e];
     tBp = d.bp[e];
+    if (kMask) mM = d.mfpM[e];
   }
+  const bool useMask = kMask && epw <= 64;
+  uint64_t nM = 0;  // the refreshed mask of the lane's edge
   for (int k0 = 0; 64 * k0 < np; k0 += GS_RB) {
     uint32_t q[GS_RB];
     double fmd[GS_RB], mmd[GS_RB], mfp[GS_RB], imd[GS_RB];
@@ -178,11 +187,19 @@ __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t no
       q[k] = dlt_get(d, i);
       fmd[k] = d.fmd[i];
       mmd[k] = d.mmd[i];
-      mfp[k] = d.mfp[i];
+      bool mf = true;
+      if (useMask) {  // the mask of the pair's edge pl / T (of this wave), held by lane pl / T
+        const uint64_t em = T == 64 ? lane_get64(mM, pl >> 6) : (uint64_t)__shfl((unsigned long long)mM, pl / T);
+        mf = (em >> tLane) & 1;
+      }
+      mfp[k] = mf ? d.mfp[i] : 0.0;
       imd[k] = d.anyImd ? d.imd[i] : 0.0;
       gt[k] = d.graftTime[i];
       fl[k] = d.flags[i];
     }
+    bool nz[GS_RB];  // the pair's mfp is non-zero after the refresh
+#pragma unroll
+    for (int k = 0; k < GS_RB; ++k) nz[k] = mfp[k] != 0.0;
 #pragma unroll
     for (int k = 0; k < GS_RB; ++k) {
       const int pl = lane + 64 * (k0 + k);
@@ -205,6 +222,7 @@ __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t no
         if (st == 2 && now > d.rexpire[e]) {
           d.fmd[i] = 0; d.mmd[i] = 0; d.mfp[i] = 0; d.imd[i] = 0; dlt_put(d, i, 0);
           d.meshTime[i] = 0; d.graftTime[i] = 0; d.flags[i] = 0;
+          nz[k] = false;
         } else if (act) {
           term = topic_term(d, tp, i);  // the stored record as it is
         }
@@ -220,6 +238,7 @@ __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t no
         v = mfp[k] * tp.MfpDecay;
         if (v < d.DecayToZero) v = 0;
         x.mfp = v;
+        nz[k] = v != 0.0;
         v = imd[k] * tp.ImdDecay;
         if (v < d.DecayToZero) v = 0;
         x.im = v;
@@ -250,8 +269,19 @@ __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t no
       }
       sT[rp_pad(pl)] = term;
     }
+    if (useMask) {
+      // lane = topic: one ballot holds the masks of 64 / T whole edges
+#pragma unroll
+      for (int k = 0; k < GS_RB; ++k) {
+        const uint64_t bal = __ballot(nz[k] && lane + 64 * (k0 + k) < np);
+        const int eb = (64 * (k0 + k)) / T;  // the ballot's first edge (of the wave)
+        for (int s = 0; s < 64 / T; ++s)
+          if (lane == eb + s) nM = T == 64 ? bal : (bal >> (s * T)) & ((1ull << T) - 1);
+      }
+    }
   }
   __syncthreads();
+  if (useMask && lane < ng && nM != mM) d.mfpM[e0 + lane] = nM;
   for (int j = lane; j < ng; j += 64) {
     const int64_t e = e0 + j;
     bool frozen = false, dropped = false;
@@ -939,6 +969,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
       }
 #pragma unroll
       for (int rr = 0; rr < PB; ++rr) {
+        if (b0 + rr * 64 >= totalBlk) break;  // (wave-uniform) no block of this window is left
         uint32_t en[4];
         bool sn[4];
         {

@@ -2139,6 +2139,7 @@ __global__ __launch_bounds__(64) void k_edge_down(Dev d, const int32_t* __restri
     if ((fl & 1) && (fl & 2) && mm < tp.MmdThreshold) {
       const double deficit = tp.MmdThreshold - mm;
       d.mfp[i] += deficit * deficit;
+      atomicOr((unsigned long long*)&d.mfpM[e], 1ull << t);
     }
     if (fl & 1) d.meshTime[i] = mesh_time_of(d.lastRefresh, d.graftTime[i]);  // the retained record's
     d.flags[i] = fl & ~1;

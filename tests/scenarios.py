@@ -364,12 +364,14 @@ def sinkhole(lib, extra=()):
 
 
 def adversarial_mix(lib, n=400, k=16, seed=51, sybil_frac=0.2, queue=6, msgs=600, hb=10, gater=True,
-                    window=2048, churn=0, retain=None, extra=()):
+                    window=2048, churn=0, retain=None, px=0.0, extra=()):
     """A config-5-like mix: 20% Sybils split over IWANT spam,
     GRAFT spam, phantom-IHAVE spam and invalid-message publishing, 20 Sybils
     per shared IP (P6), the peer gater, topic validator with a bounded queue,
     Eth2 scoring.  churn: connections going down per 3 hops (each back after
-    5-40 hops); retain: the gater's RetainStats."""
+    5-40 hops); retain: the gater's RetainStats; px: peer exchange on, with
+    this fraction of the connections starting down (PX dials bring them up;
+    pxConnect's PrunePeers truncation, gossipsub.go:856-905)."""
     rng = np.random.default_rng(seed)
     g = graphs.random_regular(n, k, seed)
     sybil = rng.random(n) < sybil_frac
@@ -390,6 +392,12 @@ def adversarial_mix(lib, n=400, k=16, seed=51, sybil_frac=0.2, queue=6, msgs=600
         if retain is not None:
             gpar.RetainStats = retain
         opts.append(WithPeerGater(gpar))
+    if px:
+        rowptr, col, _ = g
+        pairs = [(u, int(v)) for u in range(n) for v in col[rowptr[u]:rowptr[u + 1]] if u < v]
+        prng = np.random.default_rng(seed + 91)
+        dormant = [pairs[i] for i in np.flatnonzero(prng.random(len(pairs)) < px)]
+        opts += [WithPeerExchange(True), WithDormant(dormant)]
     e = NewGossipSub(n, 1, g, graphs.all_subscribed(n, 1), *opts, *extra, ipv4=ipv4, lib=lib)
     if churn:
         crng = np.random.default_rng(seed + 77)
@@ -724,6 +732,10 @@ PX = {
     "direct_churn": lambda lib, x=(): direct_churn(lib, extra=x),
     "px_scored": lambda lib, x=(): px_scored(lib, extra=x),
     "px_gater": lambda lib, x=(): px_scored(lib, extra=x, gater=True),
+    # PX beside the attackers: GRAFT spammers' PRUNE replies
+    # and the honest hosts' heartbeat prunes of negative-score peers, dials into
+    # slots that start down, IWANT spam on the new connections
+    "px_adversarial": lambda lib, x=(): adversarial_mix(lib, n=300, seed=67, hb=12, px=0.15, extra=x),
 }
 SCENARIOS.update(PX)
 

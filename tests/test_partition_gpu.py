@@ -43,12 +43,13 @@ def _worker(rank, world, port, name, oracle, q):
         traced = [0, 1] if name.startswith("spam_") else [u for u in TRACED if u < 20]  # spam pairs: 2 nodes
         e, hops = scenarios.SCENARIOS[name](PRODUCT_LIB, (WithPartition(rank, world, tr), WithEventTracer(traced)))
         e.step(hops)
-        got = scenarios.snapshot(e, range(e.n_published))
+        ids = getattr(e, "snapshot_ids", range(e.n_published))  # (slots not recycled yet)
+        got = scenarios.snapshot(e, ids)
         got["node_range"], got["edge_range"] = e.node_range, e.edge_range
         ev = e.trace_events()
         eo, _ = scenarios.SCENARIOS[name](oracle, (WithEventTracer(traced),))
         eo.step(hops)
-        ref = scenarios.snapshot(eo, range(eo.n_published))
+        ref = scenarios.snapshot(eo, ids)
         evo = eo.trace_events()
         T = got["ts_fmd"].shape[0]
         ref_part = dict(ref, node_range=got["node_range"], edge_range=got["edge_range"])

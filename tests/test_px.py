@@ -90,6 +90,25 @@ def test_oracle_px_scored_rules(oracle_path):
         assert (a, b) in offered or (b, a) in offered, (a, b)
 
 
+def test_oracle_px_adversarial_dials(oracle_path):
+    """PX beside the attackers: PRUNEs carry peer lists, the pruned hosts dial
+    connection slots that start down, and every list pxConnect sees holds at
+    most PrunePeers suggestions (gossipsub.go:856-905)."""
+    nodes = list(range(300))
+    e, hops, ev = _run(oracle_path, "px_adversarial", nodes)
+    n_px = 0
+    for hd, items in blocks(ev):
+        if hd["type"] != SEND:
+            continue
+        px = items[items["reason"] == _abi.GS_RPC_ITEM_PX]
+        for t in set(px["topic"].tolist()):
+            assert (px["topic"] == t).sum() <= 16  # PrunePeers
+        n_px += len(px)
+    assert n_px > 0
+    late = ev[(ev["type"] == T("ADD_PEER")) & (ev["hop"] > 0)]
+    assert len(late) > 0
+
+
 def _rows():
     rows = [dict(hop=3, msg=(4 << 40), type=SEND, node=1, peer=2, topic=-1, phase=4, reason=0),
             dict(hop=3, msg=-1, type=ITEM, node=1, peer=2, topic=-1, phase=4, reason=_abi.GS_RPC_ITEM_CTL),
@@ -119,9 +138,9 @@ def test_encode_prune_peers():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["px_star", "px_scored"])
+@pytest.mark.parametrize("name", ["px_star", "px_scored", "px_adversarial"])
 def test_gpu_px_trace_equals_oracle(name, oracle_path):
-    nodes = list(range(20)) if name == "px_star" else list(range(200))
+    nodes = list(range(20)) if name == "px_star" else list(range(300 if name == "px_adversarial" else 200))
     _, _, ew = _run(oracle_path, name, nodes)
     _, _, eg = _run(PRODUCT_LIB, name, nodes)
     assert len(eg) == len(ew) and np.array_equal(eg, ew)
