@@ -32,10 +32,21 @@
 #else
 #define GS_OCC_HB
 #endif
+// refresh: 4 waves/SIMD (<= 128 VGPRs): at 141 VGPRs (3 waves) the config4
+// refresh took 44 ms per launch instead of 33 (round 5)
+#ifndef GS_WPE_RF
+#define GS_WPE_RF 4
+#endif
 #ifdef GS_WPE_RF
 #define GS_OCC_RF GS_WPE_(GS_WPE_RF)
 #else
 #define GS_OCC_RF
+#endif
+// phase A: at least 3 waves/SIMD (<= 168 VGPRs): the adversarial 3-word
+// instantiation at 171 VGPRs ran 2 waves and config5's phase A went 185 -> 228
+// ms per round (round 5); LDS keeps phase A at about 10 waves per CU anyway
+#ifndef GS_WPE_PA
+#define GS_WPE_PA 3
 #endif
 #ifdef GS_WPE_PA
 #define GS_OCC_PA GS_WPE_(GS_WPE_PA)
@@ -58,7 +69,10 @@
 #define GS_PTX_BITS 10 // mcache.peertx hash slots per node: 2^10 (2^12 when IWANT spammers run)
 #define GS_CUTS 64     // IHAVE entries above MaxIHaveLength one node can cut per hop
 // phase B dynamic LDS: the MaxIHaveLength-cut tables (cut mode)
-#define GS_CUTLDS (256 * 4 + GS_CUTS * 4 + GS_CUTS * 16 + 64 * 16 + 128 * 4 + 16 + GS_SEL_CAP * 16 + 16 + GS_CUTS * 4)
+#define GS_CUTLDS (256 * 4 + GS_CUTS * 4 + GS_CUTS * 16 + 64 * 16 + 128 * 4 + 16)
+// phase B's extra LDS when a topic's item may be cut (cutMode bit 0, config3's
+// steady state): select_kth_est's kept pairs and the cut items' id counts
+#define GS_SELLDS (GS_SEL_CAP * 16 + 16 + GS_CUTS * 4)
 
 // device counter slots (same order as gs_counters)
 enum {
@@ -239,6 +253,7 @@ struct Dev {
   // read the list (the sender's copies overflowed its region)
   uint16_t* ibx[2];  // [owned senders][GS_PUSHR]
   int64_t* ibxRec[2];
+  int32_t* pushOvf;  // a sender's copies overflowed its region this hop (partitioned: its rank ships its lists)
   uint8_t* jrIn;  // [E] position of the receiver in the sender's row: rev[e] - rowptr[col[e]]
   double* score0;  // hop-start score memo (S0)
   double* score1;  // after the message phase (S1) / heartbeat memo
@@ -247,9 +262,6 @@ struct Dev {
   uint64_t* boMask;  // [E] bit t: backoff of (e, t) is set (the heartbeat's candidate filter
                      // reads one coalesced word per edge instead of a strided expiry per topic)
   double *fmd, *mmd, *mfp, *imd;  // per-(edge, topic) rows (tix)
-  uint64_t* mfpM;                 // [E] bit t: mfp of (e, t) may be non-zero (clear => 0.0); the
-                                  // refresh reads only those mfp entries (P3b is rare: a prune
-                                  // with a delivery deficit, decaying to zero again)
   int32_t anyImd;                 // 0: no invalid delivery ever recorded, imd is all 0 (P4 = 0)
   uint32_t* dlt;                  // [E][T]: deliveries not yet folded into fmd / mmd,
                                   // (+1s to fmd) | (+1s to mmd) << 16 (see eff_fmd)
@@ -564,6 +576,21 @@ __device__ __forceinline__ void dlt_put(const Dev& d, int64_t i, uint32_t q) {
   if (d.dltN != nullptr) d.dltN[i] = (uint16_t)((q & 0xFFu) | ((q >> 16) << 8));
   else d.dlt[i] = q;
 }
+// the same with the layout known at compile time (the streaming refresh)
+template <bool NDLT>
+__device__ __forceinline__ uint32_t dlt_get_t(const Dev& d, int64_t i) {
+  if constexpr (NDLT) {
+    const uint32_t x = d.dltN[i];
+    return (x & 0xFFu) | ((x >> 8) << 16);
+  } else {
+    return d.dlt[i];
+  }
+}
+template <bool NDLT>
+__device__ __forceinline__ void dlt_put_t(const Dev& d, int64_t i, uint32_t q) {
+  if constexpr (NDLT) d.dltN[i] = (uint16_t)((q & 0xFFu) | ((q >> 16) << 8));
+  else d.dlt[i] = q;
+}
 __device__ __forceinline__ double eff_fmd(const TopicP& tp, double fmd, uint32_t q) {
   return (q & 0xFFFF) ? add_ones_capped(fmd, (int)(q & 0xFFFF), tp.FmdCap) : fmd;
 }
@@ -751,7 +778,6 @@ __device__ __forceinline__ void stats_prune(const Dev& d, int64_t e, int t) {
   if ((fl & 2) && mm < thr) {
     const double deficit = thr - mm;
     d.mfp[i] += deficit * deficit;
-    atomicOr((unsigned long long*)&d.mfpM[e], 1ull << t);
   }
   if (fl & 1) d.meshTime[i] = mesh_time_of(d.lastRefresh, d.graftTime[i]);  // kept as it was at the prune
   d.flags[i] = fl & ~1;

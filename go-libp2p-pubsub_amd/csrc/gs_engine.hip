@@ -683,6 +683,7 @@ int gs_engine::start() {
     ibxCapB[k] = (size_t)ibxOwnSlots * 2;
     x.ibxRec[k] = dalloc<int64_t>(E, 0xFF); chk(x.ibxRec[k]);
   }
+  x.pushOvf = (pushOn && world > 1) ? dalloc<int32_t>(1) : nullptr;
   x.maxDeg = std::max(1, maxdeg);
   x.stMagic = (uint32_t)(((1ull << 32) + (uint64_t)St - 1) / (uint64_t)St);
   x.tDivM = T == 1 ? 0 : ~0ull / (uint64_t)T + 1;  // ceil(2^64 / T)
@@ -762,7 +763,6 @@ int gs_engine::start() {
   x.backoff = dalloc<int64_t>(TE);
   x.boMask = dalloc<uint64_t>(E); chk(x.boMask);
   x.fmd = dalloc<double>(TE); x.mmd = dalloc<double>(TE); x.mfp = dalloc<double>(TE); x.imd = dalloc<double>(TE);
-  x.mfpM = dalloc<uint64_t>(E); chk(x.mfpM);
   // 16-bit pending counts when a topic's slots (at most St + 1 messages live at
   // one hop) fit a byte and the pairs of an edge pack into whole words
   narrowDlt = St <= 254 && (T % 2) == 0;
@@ -955,7 +955,7 @@ int gs_engine::start() {
       HIPCHECK(hipStreamSynchronize(stream));
     }
     x.nodeRank = nr;
-    HIPCHECK(hipHostMalloc((void**)&xHost, (size_t)(3 * world + 3) * 8, hipHostMallocDefault));
+    HIPCHECK(hipHostMalloc((void**)&xHost, (size_t)(3 * world + 4) * 8, hipHostMallocDefault));
   }
   if (!ok) {
     gs_set_error("device allocation failed (state); reduce num_nodes or slots_per_topic");
@@ -1406,6 +1406,10 @@ int gs_engine::stepOne() {
       for (size_t k = (size_t)(it - mHop.begin()); k < mHop.size() && mHop[k] <= h; ++k)
         if (++topicLive[mTopic[k]] > 255) { narrow = false; break; }
     }
+    if (narrowDlt && !narrow) {  // St <= 254 bounds a topic's live slots by 255: cannot happen
+      gs_set_error("internal: 16-bit pending counts without narrow phase-A counters");
+      return GS_EDEVICE;
+    }
     const size_t nCnt = ((size_t)T * d.maxDeg + 7) & ~(size_t)7;
     const int nYp = (nY + 15) & ~15;
     // the adversarial model (validators, gater, attackers) has its own
@@ -1453,6 +1457,7 @@ int gs_engine::stepOne() {
     if (d.sel) k_publish_rs<<<n, 64, 0, stream>>>(d, (int)b);
   }
   // the copies the owned senders send next hop, per edge (phase A reads them)
+  if (d.pushOvf) HIPCHECK(hipMemsetAsync(d.pushOvf, 0, 4, stream));
   if (nOwn && pushOn) TIMED(this, GS_K_PUSH, (k_push<<<nOwn, 64, 0, stream>>>(d, cur)));
   if (gossip) {
     if (scoring) TIMED(this, GS_K_SCORE, (score_rows<2>(d, eOwn, T, nullptr, stream)));
@@ -1475,7 +1480,7 @@ int gs_engine::stepOne() {
           if (perT[(size_t)t] > (int64_t)gp.MaxIHaveLength) cutMode |= 1;
       }
     }
-    const size_t ldsB = cutMode ? GS_CUTLDS : 0;
+    const size_t ldsB = cutMode ? GS_CUTLDS + ((cutMode & 1) ? GS_SELLDS : 0) : 0;
     if (nOwn) {
       const int rc = upload(dDev, &d, sizeof(Dev));
       if (rc) return rc;
@@ -1493,14 +1498,24 @@ int gs_engine::stepOne() {
   if (refreshDue(now)) {
     const unsigned rb = nblk(eOwn, GS_RP / T);
     const bool laneT = (64 % T) == 0;  // a lane keeps one topic
-    if (churnOn && laneT)
-      TIMED(this, GS_K_REFRESH, (k_refresh_rows<true, true><<<rb, 64, 0, stream>>>(d, now)));
-    else if (churnOn)
-      TIMED(this, GS_K_REFRESH, (k_refresh_rows<true, false><<<rb, 64, 0, stream>>>(d, now)));
-    else if (laneT)
-      TIMED(this, GS_K_REFRESH, (k_refresh_rows<false, true><<<rb, 64, 0, stream>>>(d, now)));
-    else
-      TIMED(this, GS_K_REFRESH, (k_refresh_rows<false, false><<<rb, 64, 0, stream>>>(d, now)));
+    auto refresh = [&](auto churnC, auto laneC, auto ndltC) {
+      TIMED(this, GS_K_REFRESH,
+            (k_refresh_rows<decltype(churnC)::value, decltype(laneC)::value, decltype(ndltC)::value>
+             <<<rb, 64, 0, stream>>>(d, now)));
+    };
+    using TT = std::true_type;
+    using FF = std::false_type;
+    if (narrowDlt) {  // (St <= 254 and T even)
+      if (churnOn && laneT) refresh(TT{}, TT{}, TT{});
+      else if (churnOn) refresh(TT{}, FF{}, TT{});
+      else if (laneT) refresh(FF{}, TT{}, TT{});
+      else refresh(FF{}, FF{}, TT{});
+    } else {
+      if (churnOn && laneT) refresh(TT{}, TT{}, FF{});
+      else if (churnOn) refresh(TT{}, FF{}, FF{});
+      else if (laneT) refresh(FF{}, TT{}, FF{});
+      else refresh(FF{}, FF{}, FF{});
+    }
     if (churnOn && p6Live() && nOwn) k_p6<<<nOwn, 64, 0, stream>>>(d, dP6w);  // expired records
     refreshedHop = h;
     d.lastRefresh = now;  // the kernels launched from here on derive mesh pairs' meshTime from it
@@ -1669,9 +1684,23 @@ int gs_engine::exchange(int cur, bool hb) {
     int rc = growDev(xSend, xSendCap, hdrBytes + (16u << 20));
     if (rc) return rc;
   }
+  // A receiver reads this rank's frontier lists only where it walks them:
+  // without push (T < 4), for an IWANT spammer's re-requests, or for a sender
+  // whose copies overflowed its push region (record -1).  Otherwise every
+  // cross-rank edge's copies travel as pushed segments (2b below) and the
+  // lists stay home.
+  bool shipLists = true;
+  if (xpush && d.cSpam[cur] == nullptr) {
+    int32_t ovf = 0;
+    HIPCHECK(hipMemcpyAsync(&xHost[world + 3 + 2 * world], d.pushOvf, 4, hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
+    ovf = (int32_t)(xHost[world + 3 + 2 * world] & 0xFFFFFFFFu);
+    shipLists = ovf != 0;
+  }
+  const size_t hdrB = shipLists ? hdrBytes : 0;
   auto packLists = [&]() {
     const int64_t capEnt = (int64_t)((xSendCap - hdrBytes) / 4);
-    if (nOwn)
+    if (nOwn && shipLists)
       k_x_lists<<<nOwn, 64, 0, stream>>>(d, cur, bump, (int64_t*)xSend, (uint32_t*)(xSend + hdrBytes), capEnt);
   };
   packLists();
@@ -1691,7 +1720,7 @@ int gs_engine::exchange(int cur, bool hb) {
   const int64_t nPool = std::min<int64_t>((int64_t)xHost[world + 1], poolSeg);
   const size_t entBytes = align8((size_t)nEnt * 4), poolBytes = align8((size_t)nPool * 4);
   const size_t gwBytes = hb ? (size_t)nOwn * W * 8 : 0;
-  const size_t bcast = hdrBytes + entBytes + poolBytes + gwBytes;
+  const size_t bcast = hdrB + entBytes + poolBytes + gwBytes;
   if (bcast > xSendCap) {  // grow (keeps nothing) and pack the lists again
     int rc = growDev(xSend, xSendCap, bcast);
     if (rc) return rc;
@@ -1699,10 +1728,10 @@ int gs_engine::exchange(int cur, bool hb) {
     packLists();
   }
   if (nPool)
-    HIPCHECK(hipMemcpyAsync(xSend + hdrBytes + entBytes, d.pool[cur] + poolBase, (size_t)nPool * 4,
+    HIPCHECK(hipMemcpyAsync(xSend + hdrB + entBytes, d.pool[cur] + poolBase, (size_t)nPool * 4,
                             hipMemcpyDeviceToDevice, stream));
   if (gwBytes)
-    HIPCHECK(hipMemcpyAsync(xSend + hdrBytes + entBytes + poolBytes, d.gw + (size_t)n0 * W, gwBytes,
+    HIPCHECK(hipMemcpyAsync(xSend + hdrB + entBytes + poolBytes, d.gw + (size_t)n0 * W, gwBytes,
                             hipMemcpyDeviceToDevice, stream));
   // 2. edge records, one block per destination rank
   std::vector<int64_t> sendRec(world), sendOff(world);
@@ -1754,7 +1783,7 @@ int gs_engine::exchange(int cur, bool hb) {
   const int nS = 6 + 3 * world;
   std::vector<int64_t> mine(nS), all((size_t)nS * world);
   mine[5 + world] = (int64_t)pxPend.size();
-  mine[0] = (int64_t)bcast; mine[1] = nEnt; mine[2] = nPool; mine[3] = hb ? 1 : 0;
+  mine[0] = (int64_t)bcast; mine[1] = nEnt; mine[2] = nPool; mine[3] = (hb ? 1 : 0) | (shipLists ? 2 : 0);
   for (int r = 0; r < world; ++r) mine[4 + r] = sendRec[r];
   mine[4 + world] = myErr;
   for (int r = 0; r < world; ++r) {
@@ -1856,14 +1885,15 @@ int gs_engine::exchange(int cur, bool hb) {
     if (r == rank) continue;
     const int nr = part[r + 1] - part[r];
     const int64_t* a = &all[(size_t)r * nS];
-    const size_t hB = align8((size_t)nr * 8), eB = align8((size_t)a[1] * 4), pB = align8((size_t)a[2] * 4);
+    const bool lists = (a[3] & 2) != 0;  // rank r shipped its frontier lists
+    const size_t hB = lists ? align8((size_t)nr * 8) : 0, eB = align8((size_t)a[1] * 4), pB = align8((size_t)a[2] * 4);
     const uint8_t* c = xRecv + (size_t)r * chunk;
     xBytes += a[0];
-    if (nr) k_x_unlists<<<nr, 64, 0, stream>>>(d, cur, (const int64_t*)c, (const uint32_t*)(c + hB), part[r]);
+    if (nr && lists) k_x_unlists<<<nr, 64, 0, stream>>>(d, cur, (const int64_t*)c, (const uint32_t*)(c + hB), part[r]);
     if (a[2])
       HIPCHECK(hipMemcpyAsync(d.pool[cur] + (size_t)r * poolSeg, c + hB + eB, (size_t)a[2] * 4,
                               hipMemcpyDeviceToDevice, stream));
-    if (a[3] && nr)
+    if ((a[3] & 1) && nr)
       HIPCHECK(hipMemcpyAsync(d.gw + (size_t)part[r] * W, c + hB + eB + pB, (size_t)nr * W * 8,
                               hipMemcpyDeviceToDevice, stream));
   }

@@ -143,7 +143,7 @@ __global__ __launch_bounds__(64) void k_score_rows(Dev d, double* __restrict__ o
 // ascending topic order, as the reference's loop does.
 // CHURN: some connection may be down (gs_schedule_events): retained records
 // are not decayed and expire; the honest instantiation carries none of it.
-template <bool CHURN, bool LANE_T>
+template <bool CHURN, bool LANE_T, bool NDLT>
 __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t now) {
   __shared__ double sT[GS_RP + GS_RP / 64];
   const int lane = lane_id();
@@ -160,21 +160,12 @@ __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t no
   // lane's edge, loaded with the first batch instead of after the topic sums
   // (one edge per lane when the wave covers at most 64 edges)
   double tApp = 0.0, tP6 = 0.0, tBp = 0.0;
-  // the mfp mask of the lane's edge (Dev::mfpM): with one edge per lane and a
-  // lane per topic (LANE_T), a pair reads mfp only where its bit is set, and
-  // the refreshed mask is a ballot; otherwise every mfp is read and the mask
-  // (a "may be non-zero" hint) is left as it is
-  constexpr bool kMask = LANE_T;
-  uint64_t mM = ~0ull;
   if (epw <= 64 && lane < ng) {
     const int64_t e = e0 + lane;
     tApp = d.app[d.col[e]];
     tP6 = d.p6[e];
     tBp = d.bp[e];
-    if (kMask) mM = d.mfpM[e];
   }
-  const bool useMask = kMask && epw <= 64;
-  uint64_t nM = 0;  // the refreshed mask of the lane's edge
   for (int k0 = 0; 64 * k0 < np; k0 += GS_RB) {
     uint32_t q[GS_RB];
     double fmd[GS_RB], mmd[GS_RB], mfp[GS_RB], imd[GS_RB];
@@ -184,22 +175,14 @@ __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t no
     for (int k = 0; k < GS_RB; ++k) {
       const int pl = min(lane + 64 * (k0 + k), np - 1);
       const int64_t i = p0 + pl;
-      q[k] = dlt_get(d, i);
+      q[k] = dlt_get_t<NDLT>(d, i);
       fmd[k] = d.fmd[i];
       mmd[k] = d.mmd[i];
-      bool mf = true;
-      if (useMask) {  // the mask of the pair's edge pl / T (of this wave), held by lane pl / T
-        const uint64_t em = T == 64 ? lane_get64(mM, pl >> 6) : (uint64_t)__shfl((unsigned long long)mM, pl / T);
-        mf = (em >> tLane) & 1;
-      }
-      mfp[k] = mf ? d.mfp[i] : 0.0;
+      mfp[k] = d.mfp[i];
       imd[k] = d.anyImd ? d.imd[i] : 0.0;
       gt[k] = d.graftTime[i];
       fl[k] = d.flags[i];
     }
-    bool nz[GS_RB];  // the pair's mfp is non-zero after the refresh
-#pragma unroll
-    for (int k = 0; k < GS_RB; ++k) nz[k] = mfp[k] != 0.0;
 #pragma unroll
     for (int k = 0; k < GS_RB; ++k) {
       const int pl = lane + 64 * (k0 + k);
@@ -220,9 +203,8 @@ __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t no
         // a retained record is not decayed; past its expiry it is dropped
         // (score.go:500-509); the host then recounts P6 (removeIPs)
         if (st == 2 && now > d.rexpire[e]) {
-          d.fmd[i] = 0; d.mmd[i] = 0; d.mfp[i] = 0; d.imd[i] = 0; dlt_put(d, i, 0);
+          d.fmd[i] = 0; d.mmd[i] = 0; d.mfp[i] = 0; d.imd[i] = 0; dlt_put_t<NDLT>(d, i, 0);
           d.meshTime[i] = 0; d.graftTime[i] = 0; d.flags[i] = 0;
-          nz[k] = false;
         } else if (act) {
           term = topic_term(d, tp, i);  // the stored record as it is
         }
@@ -238,21 +220,20 @@ __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t no
         v = mfp[k] * tp.MfpDecay;
         if (v < d.DecayToZero) v = 0;
         x.mfp = v;
-        nz[k] = v != 0.0;
         v = imd[k] * tp.ImdDecay;
         if (v < d.DecayToZero) v = 0;
         x.im = v;
         x.fl = fl[k];
         x.mt = 0;
 #ifdef GS_EXP_FULLW
-        dlt_put(d, i, 0);
+        dlt_put_t<NDLT>(d, i, 0);
         d.fmd[i] = x.fmd;
         d.mmd[i] = x.mm;
         d.mfp[i] = x.mfp;
         if (d.anyImd) d.imd[i] = x.im;
 #else
         // unchanged counters (mostly zeros staying zero) are not written back
-        if (q[k]) dlt_put(d, i, 0);
+        if (q[k]) dlt_put_t<NDLT>(d, i, 0);
         if (x.fmd != fmd[k]) d.fmd[i] = x.fmd;
         if (x.mm != mmd[k]) d.mmd[i] = x.mm;
         if (x.mfp != mfp[k]) d.mfp[i] = x.mfp;
@@ -269,19 +250,8 @@ __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t no
       }
       sT[rp_pad(pl)] = term;
     }
-    if (useMask) {
-      // lane = topic: one ballot holds the masks of 64 / T whole edges
-#pragma unroll
-      for (int k = 0; k < GS_RB; ++k) {
-        const uint64_t bal = __ballot(nz[k] && lane + 64 * (k0 + k) < np);
-        const int eb = (64 * (k0 + k)) / T;  // the ballot's first edge (of the wave)
-        for (int s = 0; s < 64 / T; ++s)
-          if (lane == eb + s) nM = T == 64 ? bal : (bal >> (s * T)) & ((1ull << T) - 1);
-      }
-    }
   }
   __syncthreads();
-  if (useMask && lane < ng && nM != mM) d.mfpM[e0 + lane] = nM;
   for (int j = lane; j < ng; j += 64) {
     const int64_t e = e0 + j;
     bool frozen = false, dropped = false;
@@ -1155,7 +1125,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   // this hop (the new one is published after phase A, the old one is past
   // every delivery horizon), so clearing before or after the deliveries is the
   // same.  k_publish then sets the authors' bits.
-  uint64_t Uw[WPL], Sw[WPL], Hw[WPL], Ow[WPL], Rw[WPL];
+  uint64_t Uw[WPL], Sw[WPL], Hw[WPL], Ow[WPL];
   uint64_t Xw[WPL];  // ADV: fresh messages validated as REJECT / IGNORE (seen, not delivered)
   int rkw[WPL];  // rank of the lane's word in amR
   // index of young slot b of the amR word of rank rk in sFirst
@@ -1163,10 +1133,12 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
 #pragma unroll
   for (int j = 0; j < WPL; ++j) {
     const int w = lane + 64 * j;
-    Uw[j] = Sw[j] = Hw[j] = Ow[j] = Xw[j] = Rw[j] = 0;
+    Uw[j] = Sw[j] = Hw[j] = Ow[j] = Xw[j] = 0;
     rkw[j] = 0;
+    // a retired word's seen bits of this hop's slots are cleared right away:
+    // no copy of them is delivered in this hop, so fresh = delivered & ~seen
+    // is the same either way, and pass 2b writes the word back
     const bool ret = w < W && wm_has(amP, w);
-    if (ret) Rw[j] = d.pubmask[cur][w];
     if (w < W && wm_has(amR, w)) {
       rkw[j] = wm_rank(amR, w);
       const uint64_t D = sD[rkw[j]];
@@ -1183,6 +1155,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
     } else if (ret) {
       Sw[j] = d.seen[(int64_t)v * W + w];
     }
+    if (ret) Sw[j] &= ~d.pubmask[cur][w];
   }
   bool anyDrop = false;
   bool staged = false;          // ADV: the validator topics' fresh messages staged (cs / ck)
@@ -1424,7 +1397,8 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
     // issued before its first store (no full-queue drains).
     const int nP = deg * T;
     uint32_t* const scr = (uint32_t*)(d.pad + ((int64_t)(blockIdx.x & 255) * 64 + lane) * 2);
-    if (d.dltN != nullptr) {
+    if (NARROW && d.dltN != nullptr) {
+      // (narrow pending words imply narrow phase-A counters: St <= 254)
       // 16-bit pending words (Dev::dltN), two pairs per lane: word wi of v's
       // rows holds pairs 2 wi (in-edge i, topic t) and 2 wi + 1 (i, t + 1; T is
       // even), so one 4-byte load covers both and a wave moves 128 pairs
@@ -1669,7 +1643,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
     const int incl = wave_incl_sum(k);
     int rank = running + incl - k;
     running += wave_last(incl);
-    if (U | Rw[j]) d.seen[(int64_t)v * W + w] = (Sw[j] & ~Rw[j]) | U;
+    if (U || wm_has(amP, w)) d.seen[(int64_t)v * W + w] = Sw[j] | U;
     if (U) {
       if ((U & Ow[j]) || !wm_has(amW, w)) set_err(d, E_LATE);
       if (gossipV && Ud) d.hist[((int64_t)head * d.nOwnH + (v - d.n0)) * W + w] = Hw[j] | Ud;
@@ -1968,6 +1942,7 @@ __global__ __launch_bounds__(64) void k_push(Dev d, int cur) {
   const int pre = incl - seg;
   if (total > GS_PUSHR) {
     if (local) d.ibxRec[cur][re] = -1;  // region overflow: the receiver walks u's list
+    if (lane == 0 && d.pushOvf != nullptr) *d.pushOvf = 1;
     return;
   }
   // lane j (edge j) writes its entries of each chunk contiguously from its

@@ -776,6 +776,7 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
     long long* const iM = (long long*)(iK + 64);                   // [64] sender cut id
     uint32_t* const cBits = (uint32_t*)(iM + 64);                   // [128] item is cut
     int* const cN = (int*)(cBits + 128);
+    // (cutMode bit 0 only: the launch's LDS includes GS_SELLDS)
     unsigned long long* const cand = (unsigned long long*)(cN + 4);  // select_kth_est's kept pairs + counter
     int* const cNm = (int*)(cand + 2 * GS_SEL_CAP + 2);             // [GS_CUTS] ids of a cut item
     int nCut = 0;
@@ -963,7 +964,10 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
         };
         unsigned long long K;
         long long M;
-        select_kth_est(each, kk, lane_get(myWantAll, i), cHist, cand, K, M);
+        if (cutMode & 1)
+          select_kth_est(each, kk, lane_get(myWantAll, i), cHist, cand, K, M);
+        else
+          select_kth(each, kk, cHist, K, M);
         if (lane == 0) {
           iK[i] = K;
           iM[i] = M;
@@ -2139,7 +2143,6 @@ __global__ __launch_bounds__(64) void k_edge_down(Dev d, const int32_t* __restri
     if ((fl & 1) && (fl & 2) && mm < tp.MmdThreshold) {
       const double deficit = tp.MmdThreshold - mm;
       d.mfp[i] += deficit * deficit;
-      atomicOr((unsigned long long*)&d.mfpM[e], 1ull << t);
     }
     if (fl & 1) d.meshTime[i] = mesh_time_of(d.lastRefresh, d.graftTime[i]);  // the retained record's
     d.flags[i] = fl & ~1;
