@@ -70,9 +70,6 @@
 #define GS_CUTS 64     // IHAVE entries above MaxIHaveLength one node can cut per hop
 // phase B dynamic LDS: the MaxIHaveLength-cut tables (cut mode)
 #define GS_CUTLDS (256 * 4 + GS_CUTS * 4 + GS_CUTS * 16 + 64 * 16 + 128 * 4 + 16)
-// phase B's extra LDS when a topic's item may be cut (cutMode bit 0, config3's
-// steady state): select_kth_est's kept pairs and the cut items' id counts
-#define GS_SELLDS (GS_SEL_CAP * 16 + 16 + GS_CUTS * 4)
 
 // device counter slots (same order as gs_counters)
 enum {
@@ -961,12 +958,13 @@ __device__ __forceinline__ void select_kth(F&& each, int k, uint32_t* hist, unsi
 // sqrt(k (n - k) / n^3), ~1.2 bins at config3's 5000 of 6000), so the pass
 // builds the top-byte histogram and keeps every candidate whose top byte lies
 // within GS_SEL_WIN bins of that estimate in LDS (cand: GS_SEL_CAP (key, id)
-// pairs + a counter).  If the k-th falls into a kept bin and nothing
+// pairs + a counter; ~117 expected at config3's 6000 ids, so about one select
+// in twenty falls back).  If the k-th falls into a kept bin and nothing
 // overflowed, the k-th smallest (key, id) of that bin is ranked among the kept
 // entries; otherwise select_kth runs as before.  Either way the result is the
 // exact k-th smallest (key, id).  n = the number of candidates each() yields.
-#define GS_SEL_WIN 3
-#define GS_SEL_CAP 192
+#define GS_SEL_WIN 2
+#define GS_SEL_CAP 143
 template <class F>
 __device__ __forceinline__ void select_kth_est(F&& each, int k, int n, uint32_t* hist, unsigned long long* cand,
                                                unsigned long long& K, long long& M) {
@@ -976,7 +974,7 @@ __device__ __forceinline__ void select_kth_est(F&& each, int k, int n, uint32_t*
     M = INT64_MAX;
     return;
   }
-  const int est = (int)(((int64_t)k << 8) / n);
+  const int est = (int)((((int64_t)k << 9) / n + 1) >> 1);  // 256 k / n, rounded
   const int lo = max(0, est - GS_SEL_WIN), hi = min(255, est + GS_SEL_WIN);
   uint32_t* const cnt = (uint32_t*)(cand + 2 * GS_SEL_CAP);
   for (int q = lane; q < 256; q += 64) hist[q] = 0u;

@@ -1480,7 +1480,7 @@ int gs_engine::stepOne() {
           if (perT[(size_t)t] > (int64_t)gp.MaxIHaveLength) cutMode |= 1;
       }
     }
-    const size_t ldsB = cutMode ? GS_CUTLDS + ((cutMode & 1) ? GS_SELLDS : 0) : 0;
+    const size_t ldsB = cutMode ? GS_CUTLDS : 0;
     if (nOwn) {
       const int rc = upload(dDev, &d, sizeof(Dev));
       if (rc) return rc;

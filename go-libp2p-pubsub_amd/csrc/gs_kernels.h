@@ -792,6 +792,38 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   sLn[lane] = Ln;
   sAddr[lane] = pOff >= 0 ? pOff : (int64_t)u * FC;
   const uint64_t scoredT = __ballot(lane < T && scoring && d.tp[lane].scored);  // scored topics
+  // ---- prefetch (phase A is LDS-bound at ~10 waves per CU, so registers are
+  // free to hold loads in flight across pass 1): pass 3's 16-bit pending
+  // words when the node's fit one batch, and pass 2's seen / mcache / old-slot
+  // words of the active window; none of them is written before this wave's
+  // own passes 2b / 3
+  constexpr int PF3 = 16;
+  const int nWdPf = (NARROW && scoring && d.dltN != nullptr) ? (deg * T) >> 1 : 0;
+  const bool pf3 = nWdPf > 0 && nWdPf <= 64 * PF3;
+  uint32_t q3[PF3];
+  if (pf3) {
+    const uint32_t* const pw = (const uint32_t*)(d.dltN + base * T);
+#pragma unroll
+    for (int k = 0; k < PF3; ++k) {
+      const int wi = lane + 64 * k;
+      q3[k] = pw[wi < nWdPf ? wi : nWdPf - 1];
+    }
+  }
+  // (the honest instantiation only: the adversarial one has no registers to spare)
+  uint64_t Sp[WPL], Hp[WPL], Op[WPL];
+#pragma unroll
+  for (int j = 0; j < WPL; ++j) {
+    const int w = lane + 64 * j;
+    Sp[j] = Hp[j] = Op[j] = 0;
+    if constexpr (!ADV) {
+      const bool act = w < W && wm_has(amR, w);
+      if (act || (w < W && wm_has(amP, w))) Sp[j] = d.seen[(int64_t)v * W + w];
+      if (act) {
+        Op[j] = d.oldm[w];
+        if (gossipV) Hp[j] = d.hist[((int64_t)head * d.nOwnH + (v - d.n0)) * W + w];
+      }
+    }
+  }
   __syncthreads();
   GS_STAMP(1);
 
@@ -1125,7 +1157,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   // this hop (the new one is published after phase A, the old one is past
   // every delivery horizon), so clearing before or after the deliveries is the
   // same.  k_publish then sets the authors' bits.
-  uint64_t Uw[WPL], Sw[WPL], Hw[WPL], Ow[WPL];
+  uint64_t Uw[WPL], Sw[WPL], Hw[WPL], Ow[WPL], Rw[WPL];
   uint64_t Xw[WPL];  // ADV: fresh messages validated as REJECT / IGNORE (seen, not delivered)
   int rkw[WPL];  // rank of the lane's word in amR
   // index of young slot b of the amR word of rank rk in sFirst
@@ -1133,29 +1165,39 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
 #pragma unroll
   for (int j = 0; j < WPL; ++j) {
     const int w = lane + 64 * j;
-    Uw[j] = Sw[j] = Hw[j] = Ow[j] = Xw[j] = 0;
+    Uw[j] = Sw[j] = Hw[j] = Ow[j] = Xw[j] = Rw[j] = 0;
     rkw[j] = 0;
-    // a retired word's seen bits of this hop's slots are cleared right away:
-    // no copy of them is delivered in this hop, so fresh = delivered & ~seen
-    // is the same either way, and pass 2b writes the word back
     const bool ret = w < W && wm_has(amP, w);
-    if (w < W && wm_has(amR, w)) {
-      rkw[j] = wm_rank(amR, w);
-      const uint64_t D = sD[rkw[j]];
-      if (D) {
-        // the pass's loads in one round trip: seen, and (for the first
-        // deliveries it may hold) the old-slot mask and the mcache window
-        Sw[j] = d.seen[(int64_t)v * W + w];
-        Uw[j] = D;  // & ~seen below
-        Ow[j] = d.oldm[w];
-        if (gossipV) Hw[j] = d.hist[((int64_t)head * d.nOwnH + (v - d.n0)) * W + w];
+    if (ret) Rw[j] = d.pubmask[cur][w];
+    if constexpr (!ADV) {
+      Sw[j] = Sp[j];  // (prefetched at wave start)
+      if (w < W && wm_has(amR, w)) {
+        rkw[j] = wm_rank(amR, w);
+        const uint64_t D = sD[rkw[j]];
+        if (D) {
+          Uw[j] = D;  // & ~seen below
+          Ow[j] = Op[j];
+          Hw[j] = Hp[j];
+        }
+      }
+    } else {
+      if (w < W && wm_has(amR, w)) {
+        rkw[j] = wm_rank(amR, w);
+        const uint64_t D = sD[rkw[j]];
+        if (D) {
+          // the pass's loads in one round trip: seen, and (for the first
+          // deliveries it may hold) the old-slot mask and the mcache window
+          Sw[j] = d.seen[(int64_t)v * W + w];
+          Uw[j] = D;  // & ~seen below
+          Ow[j] = d.oldm[w];
+          if (gossipV) Hw[j] = d.hist[((int64_t)head * d.nOwnH + (v - d.n0)) * W + w];
+        } else if (ret) {
+          Sw[j] = d.seen[(int64_t)v * W + w];
+        }
       } else if (ret) {
         Sw[j] = d.seen[(int64_t)v * W + w];
       }
-    } else if (ret) {
-      Sw[j] = d.seen[(int64_t)v * W + w];
     }
-    if (ret) Sw[j] &= ~d.pubmask[cur][w];
   }
   bool anyDrop = false;
   bool staged = false;          // ADV: the validator topics' fresh messages staged (cs / ck)
@@ -1453,7 +1495,20 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
         }
       };
 #ifndef GS_EXP_NOPASS3
-      if (nWd > 8 * 64) {
+      if (pf3) {
+        // the words prefetched at wave start: one batch
+#pragma unroll
+        for (int kk = 0; kk < PF3; ++kk) {
+          const int wi = lane + 64 * kk;
+          const bool ok = wi < nWd;
+          const int iv = ic, tv = tc;
+          ic += q128;
+          tc += r128;
+          if (tc >= T) { tc -= T; ++ic; }
+          const uint32_t nq = upd2(ok ? wi : 0, ok ? iv : 0, ok ? tv : 0, q3[kk]);
+          *(ok ? pw + wi : scr) = nq;
+        }
+      } else if (nWd > 8 * 64) {
         rmw2(std::integral_constant<int, 16>{});
       } else if (nWd > 2 * 64) {
         rmw2(std::integral_constant<int, 8>{});
@@ -1643,7 +1698,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
     const int incl = wave_incl_sum(k);
     int rank = running + incl - k;
     running += wave_last(incl);
-    if (U || wm_has(amP, w)) d.seen[(int64_t)v * W + w] = Sw[j] | U;
+    if (U | Rw[j]) d.seen[(int64_t)v * W + w] = (Sw[j] & ~Rw[j]) | U;
     if (U) {
       if ((U & Ow[j]) || !wm_has(amW, w)) set_err(d, E_LATE);
       if (gossipV && Ud) d.hist[((int64_t)head * d.nOwnH + (v - d.n0)) * W + w] = Hw[j] | Ud;

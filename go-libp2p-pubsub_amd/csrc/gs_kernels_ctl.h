@@ -752,14 +752,8 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
     sNode[lane] = u;
     sCnt[lane] = 0;
     sCur[lane] = 0;
-    sKey[lane] = ~0ull;
-    sMid[lane] = INT64_MAX;
-    sSlot[lane] = -1;
     __syncthreads();
-    // The wanted words of item (sender i, topic t): the advertised window of
-    // the sender minus v's seen row, four words loaded at once.
     const int nHas = (totalItems + 31) >> 5;
-    for (int k = lane; k < nHas; k += 64) sHas[k] = sCand[k] = 0u;
     // ---- MaxIHaveLength cuts (cutMode: the host saw that a topic may hold
     // more gossip ids than that).  Item cut: a sender with more than
     // MaxIHaveLength ids of a topic advertised its own keyed subset to v
@@ -776,9 +770,14 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
     long long* const iM = (long long*)(iK + 64);                   // [64] sender cut id
     uint32_t* const cBits = (uint32_t*)(iM + 64);                   // [128] item is cut
     int* const cN = (int*)(cBits + 128);
-    // (cutMode bit 0 only: the launch's LDS includes GS_SELLDS)
-    unsigned long long* const cand = (unsigned long long*)(cN + 4);  // select_kth_est's kept pairs + counter
-    int* const cNm = (int*)(cand + 2 * GS_SEL_CAP + 2);             // [GS_CUTS] ids of a cut item
+    // the item cuts' scratch lives in static LDS that is free until pass a:
+    // select_kth_est's kept (key, id) pairs + counter in sH past sTm (sKey ..
+    // sCand are initialised after the cuts), the cut items' id counts in step
+    // 2's request offsets
+    unsigned long long* const cand = (unsigned long long*)(sH + 192);
+    static_assert(192 * 4 + GS_SEL_CAP * 16 + 8 <= 768 * 4, "select_kth_est pairs must fit in sH past sTm");
+    int* const cNm = sReqOff;  // [GS_CUTS] ids of a cut item
+    static_assert(GS_CUTS <= 64, "cNm aliases sReqOff[64]");
     int nCut = 0;
     if (cutMode & 1) {
       for (int k = lane; k < 128; k += 64) cBits[k] = 0u;
@@ -834,6 +833,12 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
         __syncthreads();
       }
     }
+    // (sH past sTm was the cuts' scratch until here)
+    sKey[lane] = ~0ull;
+    sMid[lane] = INT64_MAX;
+    sSlot[lane] = -1;
+    for (int k = lane; k < nHas; k += 64) sHas[k] = sCand[k] = 0u;
+    __syncthreads();
     // the advertised wants of item b (topic t, chunk ch): fn(w, want) per word
     // with a want
     auto wants = [&](int b, int uu, int t, int ch, auto&& fn) {
@@ -964,10 +969,7 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
         };
         unsigned long long K;
         long long M;
-        if (cutMode & 1)
-          select_kth_est(each, kk, lane_get(myWantAll, i), cHist, cand, K, M);
-        else
-          select_kth(each, kk, cHist, K, M);
+        select_kth(each, kk, cHist, K, M);  // (sH is live again: the multi-pass select)
         if (lane == 0) {
           iK[i] = K;
           iM[i] = M;
