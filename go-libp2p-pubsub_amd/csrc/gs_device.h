@@ -126,8 +126,12 @@ struct Dev {
   // rows, i.e. edges [e0, e1).  Node kernels run one wave per owned node, edge
   // kernels one lane per owned edge; per-(edge, topic) state is allocated for
   // the owned edges only.  Unpartitioned: n0 = 0, n1 = N, e0 = 0, e1 = E.
+  // Per-edge arrays are owned-only too (a base shifted by e0): the sender's
+  // state at its own edge e, and the receiver-indexed records (outbox, fwdIn,
+  // ibxRec: at the receiver's in-edge ri = rev[e]) with a stage behind the
+  // owned range for the records whose receiver lives on another rank (rxi).
   int32_t n0, n1, rank, world;
-  int64_t e0, e1;
+  int64_t e0, e1, eOwn;
   uint8_t* xmark;   // [E] forwarding set changed since its parity was exchanged (world > 1)
   // RPC byte accounting (gs_set_rpc_accounting); rpcB == nullptr: off
   unsigned long long* rpcB;    // [E] bytes of the RPCs sent over the sender's edge e
@@ -562,6 +566,14 @@ __device__ __forceinline__ double add_ones_capped(double x, int n, double cap) {
 // The pending counts of pair i as (+1s to fmd) | (+1s to mmd) << 16 in either
 // layout, and their store (a narrow count is <= 255: the host's fold policy
 // and phase A's E_DELTA check guarantee it).
+// The slot of a receiver-indexed record (outbox, fwdIn, ibxRec) that the
+// sender of its own edge e writes for the receiver's in-edge ri = rev[e]: the
+// receiver's own slot when this rank owns the receiver, else the stage slot of
+// e behind the owned range (the exchange packs and clears it).  Such arrays
+// hold [e0, e1 + eOwn) on a partitioned rank; unpartitioned, every ri is owned.
+__device__ __forceinline__ int64_t rxi(const Dev& d, int64_t e, int64_t ri) {
+  return (ri >= d.e0 && ri < d.e1) ? ri : d.e1 + (e - d.e0);
+}
 __device__ __forceinline__ uint32_t dlt_get(const Dev& d, int64_t i) {
   if (d.dltN != nullptr) {
     const uint32_t x = d.dltN[i];

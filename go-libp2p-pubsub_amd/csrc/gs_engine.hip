@@ -58,6 +58,7 @@ struct gs_engine {
   int64_t retireHops = 0;
   std::vector<int32_t> topicLive;  // per-topic live message count (phase-A counter width)
   int64_t hopsSinceFold = 0, foldEvery = 1;  // pending-delivery fold cadence (dlt)
+  int64_t eOwn = 0;                          // owned edges e1 - e0 (Dev::eOwn)
   // the 16-bit pending counts (Dev::dltN): counts accumulate from foldStart;
   // a pair's count is bounded by the messages of its topic that can be
   // delivered since then, so the host folds before that bound could pass 255
@@ -311,6 +312,20 @@ struct gs_engine {
     (void)hipMemsetAsync(p, fill, bytes, stream);
     return (X*)p;
   }
+  // Per-edge device arrays (Dev::rxi): a sender-indexed array holds the owned
+  // edges [e0, e1), a receiver-indexed one (outbox, fwdIn, ibxRec) also the
+  // stage [e1, e1 + eOwn) on a partitioned rank; both through a base shifted
+  // by e0.  Unpartitioned: [0, E), as before.
+  template <class X>
+  X* ealloc(int fill = 0) {
+    X* p = dalloc<X>((size_t)std::max<int64_t>(eOwn, 1), fill);
+    return p ? p - e0 : nullptr;
+  }
+  template <class X>
+  X* ralloc(int fill = 0) {
+    X* p = dalloc<X>((size_t)std::max<int64_t>(world > 1 ? 2 * eOwn : eOwn, 1), fill);
+    return p ? p - e0 : nullptr;
+  }
   bool ageWindowNeeded() const {
     for (int t = 0; t < T; ++t)
       if (tscored[t] && tps[t].MeshMessageDeliveriesWindow < retireHops * cfg.hop_ns) return true;
@@ -510,6 +525,7 @@ int gs_engine::start() {
   n1 = part[rank + 1];
   e0 = rowptr[n0];
   e1 = rowptr[n1];
+  eOwn = e1 - e0;
   if (world > 1 && anyRandom) {
     gs_set_error("a partitioned engine supports floodsub and gossipsub (randomsub target masks are not exchanged)");
     return GS_EUNSUPPORTED;
@@ -571,7 +587,7 @@ int gs_engine::start() {
     x.rsTarget = std::max(6, sq);
   }
   x.maxAge = maxAge; x.seed = cfg.seed; x.hop_ns = cfg.hop_ns;
-  x.n0 = n0; x.n1 = n1; x.e0 = e0; x.e1 = e1; x.rank = rank; x.world = world;
+  x.n0 = n0; x.n1 = n1; x.e0 = e0; x.e1 = e1; x.eOwn = eOwn; x.rank = rank; x.world = world;
   x.TopicScoreCap = sp.TopicScoreCap; x.AppW = sp.AppSpecificWeight; x.IPW = sp.IPColocationFactorWeight;
   x.BPW = sp.BehaviourPenaltyWeight; x.BPThr = sp.BehaviourPenaltyThreshold; x.BPDecay = sp.BehaviourPenaltyDecay;
   x.DecayToZero = sp.DecayToZero;
@@ -598,13 +614,13 @@ int gs_engine::start() {
   int32_t* dCol = dalloc<int32_t>(E); chk(dCol);
   int32_t* dEsrc = dalloc<int32_t>(E); chk(dEsrc);
   int32_t* dRev = dalloc<int32_t>(E); chk(dRev);
-  uint8_t* dOut = dalloc<uint8_t>(E); chk(dOut);
-  uint8_t* dDir = dalloc<uint8_t>(E); chk(dDir);
-  uint8_t* dJrIn = dalloc<uint8_t>(E); chk(dJrIn);
+  uint8_t* dOut = ealloc<uint8_t>(); chk(dOut);
+  uint8_t* dDir = ealloc<uint8_t>(); chk(dDir);
+  uint8_t* dJrIn = ealloc<uint8_t>(); chk(dJrIn);
   uint64_t* dSub = dalloc<uint64_t>(N); chk(dSub);
   dSubA = dalloc<uint64_t>(N); chk(dSubA);
   double* dApp = dalloc<double>(N); chk(dApp);
-  double* dP6 = dalloc<double>(E); chk(dP6);
+  double* dP6 = ealloc<double>(); chk(dP6);
   dTp = dalloc<TopicP>(T); chk(dTp);
   if (!ok) { gs_set_error("device allocation failed (graph)"); return GS_ENOMEM; }
   HIPCHECK(hipMemcpyAsync(dRowptr, rowptr.data(), (N + 1) * 8, hipMemcpyHostToDevice, stream));
@@ -616,18 +632,18 @@ int gs_engine::start() {
     for (int64_t e = 0; e < E; ++e) jr[e] = (uint8_t)(rev[e] - rowptr[col[e]]);
     // on the engine's (non-blocking) stream, after dalloc's memset; the host
     // buffer must outlive the copy
-    HIPCHECK(hipMemcpyAsync(dJrIn, jr.data(), E, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipMemcpyAsync(dJrIn + e0, jr.data() + e0, (size_t)eOwn, hipMemcpyHostToDevice, stream));
     HIPCHECK(hipStreamSynchronize(stream));
   }
-  HIPCHECK(hipMemcpyAsync(dOut, outbound.data(), E, hipMemcpyHostToDevice, stream));
-  HIPCHECK(hipMemcpyAsync(dDir, direct.data(), E, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipMemcpyAsync(dOut + e0, outbound.data() + e0, (size_t)eOwn, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipMemcpyAsync(dDir + e0, direct.data() + e0, (size_t)eOwn, hipMemcpyHostToDevice, stream));
   HIPCHECK(hipMemcpyAsync(dSub, sub.data(), N * 8, hipMemcpyHostToDevice, stream));
   HIPCHECK(hipMemcpyAsync(dSubA, sub.data(), N * 8, hipMemcpyHostToDevice, stream));
   subA = sub;
   dSubOwn = dSub;
   dP6w = dP6;
   HIPCHECK(hipMemcpyAsync(dApp, app.data(), N * 8, hipMemcpyHostToDevice, stream));
-  HIPCHECK(hipMemcpyAsync(dP6, p6.data(), E * 8, hipMemcpyHostToDevice, stream));
+  HIPCHECK(hipMemcpyAsync(dP6 + e0, p6.data() + e0, (size_t)eOwn * 8, hipMemcpyHostToDevice, stream));
   std::vector<TopicP> htp(T);
   for (int t = 0; t < T; ++t) htp[t] = to_dev(tps[t], scoring && tscored[t]);
   HIPCHECK(hipMemcpyAsync(dTp, htp.data(), T * sizeof(TopicP), hipMemcpyHostToDevice, stream));
@@ -681,7 +697,7 @@ int gs_engine::start() {
     ibxOwnSlots = (int64_t)std::max<int64_t>(nOwnN, 1) * GS_PUSHR;
     x.ibx[k] = dalloc<uint16_t>((size_t)ibxOwnSlots); chk(x.ibx[k]);
     ibxCapB[k] = (size_t)ibxOwnSlots * 2;
-    x.ibxRec[k] = dalloc<int64_t>(E, 0xFF); chk(x.ibxRec[k]);
+    x.ibxRec[k] = ralloc<int64_t>(0xFF); chk(x.ibxRec[k]);
   }
   x.pushOvf = (pushOn && world > 1) ? dalloc<int32_t>(1) : nullptr;
   x.maxDeg = std::max(1, maxdeg);
@@ -743,25 +759,25 @@ int gs_engine::start() {
     gs_set_error("GossipRetransmission > 253 is not supported");
     return GS_EUNSUPPORTED;
   }
-  x.mesh = dalloc<uint64_t>(E); x.fanout = dalloc<uint64_t>(E);
+  x.mesh = ealloc<uint64_t>(); x.fanout = ealloc<uint64_t>();
   chk(x.mesh); chk(x.fanout);
   for (int k = 0; k < 2; ++k) {
-    x.fwdRelay[k] = dalloc<uint64_t>(E); x.fwdPub[k] = dalloc<uint64_t>(E);
-    x.fwdIn[k] = dalloc<ulonglong2>(E);
+    x.fwdRelay[k] = ealloc<uint64_t>(); x.fwdPub[k] = ealloc<uint64_t>();
+    x.fwdIn[k] = ralloc<ulonglong2>();
     chk(x.fwdRelay[k]); chk(x.fwdPub[k]); chk(x.fwdIn[k]);
-    x.cPre[k] = dalloc<uint8_t>(E); x.cHb[k] = dalloc<uint8_t>(E);
-    x.cGraftJoin[k] = dalloc<uint64_t>(E); x.cGraftHb[k] = dalloc<uint64_t>(E);
-    x.cPruneReply[k] = dalloc<uint64_t>(E); x.cPruneHb[k] = dalloc<uint64_t>(E);
-    x.cIhave[k] = dalloc<uint64_t>(E);
-    x.cIwant[k] = dalloc<int64_t>(E, 0xFF); x.cIresp[k] = dalloc<int64_t>(E, 0xFF);
+    x.cPre[k] = ralloc<uint8_t>(); x.cHb[k] = ralloc<uint8_t>();
+    x.cGraftJoin[k] = ralloc<uint64_t>(); x.cGraftHb[k] = ralloc<uint64_t>();
+    x.cPruneReply[k] = ralloc<uint64_t>(); x.cPruneHb[k] = ralloc<uint64_t>();
+    x.cIhave[k] = ralloc<uint64_t>();
+    x.cIwant[k] = ralloc<int64_t>(0xFF); x.cIresp[k] = ralloc<int64_t>(0xFF);
     chk(x.cPre[k]); chk(x.cHb[k]); chk(x.cGraftJoin[k]); chk(x.cGraftHb[k]); chk(x.cPruneReply[k]);
     chk(x.cPruneHb[k]); chk(x.cIhave[k]); chk(x.cIwant[k]); chk(x.cIresp[k]);
     x.pubmask[k] = dalloc<uint64_t>(W); chk(x.pubmask[k]);
   }
-  x.score0 = dalloc<double>(E); x.score1 = dalloc<double>(E);
-  x.sdirty = dalloc<uint8_t>(E, 1); chk(x.sdirty);
+  x.score0 = ealloc<double>(); x.score1 = ealloc<double>();
+  x.sdirty = ealloc<uint8_t>(1); chk(x.sdirty);
   x.backoff = dalloc<int64_t>(TE);
-  x.boMask = dalloc<uint64_t>(E); chk(x.boMask);
+  x.boMask = ealloc<uint64_t>(); chk(x.boMask);
   x.fmd = dalloc<double>(TE); x.mmd = dalloc<double>(TE); x.mfp = dalloc<double>(TE); x.imd = dalloc<double>(TE);
   // 16-bit pending counts when a topic's slots (at most St + 1 messages live at
   // one hop) fit a byte and the pairs of an edge pack into whole words
@@ -779,7 +795,7 @@ int gs_engine::start() {
   x.backoff -= shift; x.fmd -= shift; x.mmd -= shift; x.mfp -= shift; x.imd -= shift;
   if (narrowDlt) x.dltN -= shift; else x.dlt -= shift;
   x.graftTime -= shift; x.meshTime -= shift; x.flags -= shift;
-  x.bp = dalloc<double>(E); x.peerhave = dalloc<int32_t>(E); x.iasked = dalloc<int32_t>(E);
+  x.bp = ealloc<double>(); x.peerhave = ealloc<int32_t>(); x.iasked = ealloc<int32_t>();
   chk(x.score0); chk(x.score1); chk(x.backoff); chk(x.fmd); chk(x.mmd); chk(x.mfp); chk(x.imd);
   chk(x.graftTime); chk(x.meshTime); chk(x.flags); chk(x.bp); chk(x.peerhave); chk(x.iasked);
   // IWANT payload arena (slot ids): 4 ids per owned edge per hop, >= 16M in
@@ -806,7 +822,7 @@ int gs_engine::start() {
   x.pxq = x.pxqN = nullptr;
   x.pxqCap = 0;
   if (doPX) {
-    for (int k = 0; k < 2; ++k) { x.cPx[k] = dalloc<int64_t>(E, 0xFF); chk(x.cPx[k]); }
+    for (int k = 0; k < 2; ++k) { x.cPx[k] = ralloc<int64_t>(0xFF); chk(x.cPx[k]); }
     x.pxqCap = std::max<int64_t>(1 << 16, 4 * (int64_t)N);
     x.pxq = dalloc<unsigned long long>((size_t)x.pxqCap); x.pxqN = dalloc<unsigned long long>(1);
     chk(x.pxq); chk(x.pxqN);
@@ -833,8 +849,8 @@ int gs_engine::start() {
     x.behave = b;
     if (behaveAll & GS_BEHAVE_IWANT_SPAM) {
       for (int k = 0; k < 2; ++k) {
-        x.cSpam[k] = dalloc<int64_t>(E, 0xFF); chk(x.cSpam[k]);
-        x.cNSrv[k] = dalloc<uint8_t>(E); chk(x.cNSrv[k]);
+        x.cSpam[k] = ralloc<int64_t>(0xFF); chk(x.cSpam[k]);
+        x.cNSrv[k] = ralloc<uint8_t>(); chk(x.cNSrv[k]);
       }
       std::vector<int32_t> row(N, -1);
       int nsp = 0;
@@ -849,14 +865,15 @@ int gs_engine::start() {
       for (int64_t ee = e0; ee < e1; ++ee)
         if (behaveH[col[ee]] & GS_BEHAVE_IWANT_SPAM) spamRowH[ee] = (int32_t)nrow++;
       if (nrow > INT32_MAX) { gs_set_error("too many IWANT-spammer edges"); return GS_ECAPACITY; }
-      x.spamRow = dalloc<int32_t>(E); chk(x.spamRow);
+      x.spamRow = ealloc<int32_t>(); chk(x.spamRow);
       for (int k = 0; k < 2; ++k) { x.pflag[k] = dalloc<uint8_t>((size_t)poolSeg * world); chk(x.pflag[k]); }
       if (gp.GossipRetransmission >= 14) {  // spam_incr's nibble peaks at GossipRetransmission + 2
         gs_set_error("IWANT spammers need GossipRetransmission < 14 in this build");
         return GS_EUNSUPPORTED;
       }
       x.spamCnt = dalloc<uint32_t>((size_t)std::max<int64_t>(nrow, 1) * (S / 8)); chk(x.spamCnt);
-      if (ok) HIPCHECK(hipMemcpyAsync(x.spamRow, spamRowH.data(), (size_t)E * 4, hipMemcpyHostToDevice, stream));
+      if (ok)
+        HIPCHECK(hipMemcpyAsync(x.spamRow + e0, spamRowH.data() + e0, (size_t)eOwn * 4, hipMemcpyHostToDevice, stream));
       // `row` is pageable and dies with this block: the copy must have read it
       HIPCHECK(hipStreamSynchronize(stream));
     }
@@ -875,8 +892,11 @@ int gs_engine::start() {
     x.gDecayToZero = gaterP.DecayToZero; x.gDupW = gaterP.DuplicateWeight; x.gIgnW = gaterP.IgnoreWeight;
     x.gRejW = gaterP.RejectWeight; x.gQuiet = gaterP.Quiet;
     x.gValidate = dalloc<double>(N); x.gThrottle = dalloc<double>(N); x.gLast = dalloc<int64_t>(N);
-    x.gSt = dalloc<double>(4 * (size_t)E); x.gGrp = dalloc<uint8_t>(E);
-    x.gConn = dalloc<int32_t>(E); x.gExp = dalloc<int64_t>(E);
+    // gSt: [4][eOwn] through the e0-shifted base, stat k of edge e at k * eOwn + e
+    x.gSt = dalloc<double>(4 * (size_t)std::max<int64_t>(eOwn, 1));
+    if (x.gSt) x.gSt -= e0;
+    x.gGrp = ealloc<uint8_t>();
+    x.gConn = ealloc<int32_t>(); x.gExp = ealloc<int64_t>();
     chk(x.gValidate); chk(x.gThrottle); chk(x.gLast); chk(x.gSt); chk(x.gGrp); chk(x.gConn); chk(x.gExp);
     if (ok) {
       // peers of one IP share a stats object (peer_gater.go:262-280); getIP = ipv4, 0 = "<unknown>"
@@ -894,8 +914,8 @@ int gs_engine::start() {
       for (int u = 0; u < N; ++u)
         for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e)
           if (!isDown(e)) conn[rowptr[u] + grp[e]]++;
-      HIPCHECK(hipMemcpyAsync(x.gConn, conn.data(), (size_t)E * 4, hipMemcpyHostToDevice, stream));
-      HIPCHECK(hipMemcpyAsync(x.gGrp, grp.data(), E, hipMemcpyHostToDevice, stream));
+      HIPCHECK(hipMemcpyAsync(x.gConn + e0, conn.data() + e0, (size_t)eOwn * 4, hipMemcpyHostToDevice, stream));
+      HIPCHECK(hipMemcpyAsync(x.gGrp + e0, grp.data() + e0, (size_t)eOwn, hipMemcpyHostToDevice, stream));
       HIPCHECK(hipMemcpyAsync(x.gLast, never.data(), (size_t)N * 8, hipMemcpyHostToDevice, stream));
       HIPCHECK(hipStreamSynchronize(stream));
     }
@@ -906,7 +926,7 @@ int gs_engine::start() {
   x.pad = dalloc<double>(256 * 64 * 2); chk(x.pad);
   x.ctr = dalloc<unsigned long long>((size_t)C_NCOUNTERS * GS_CTR_SPREAD); x.err = dalloc<int32_t>(1);
   chk(x.ctr); chk(x.err);
-  dScoreTmp = dalloc<double>(E); chk(dScoreTmp);
+  dScoreTmp = ealloc<double>(); chk(dScoreTmp);
   dHopOut = dalloc<int32_t>(N); dFromOut = dalloc<int32_t>(N); chk(dHopOut); chk(dFromOut);
   x.xmark = nullptr;
   x.nodeRank = nullptr;
@@ -941,7 +961,7 @@ int gs_engine::start() {
     }
   }
   if (world > 1) {
-    x.xmark = dalloc<uint8_t>(E); chk(x.xmark);
+    x.xmark = ealloc<uint8_t>(); chk(x.xmark);
     uint8_t* nr = dalloc<uint8_t>(N); chk(nr);
     xCnt = dalloc<unsigned long long>(2 * world + 1); chk(xCnt);
     xOff = dalloc<int64_t>(world); chk(xOff);
@@ -983,7 +1003,7 @@ int gs_engine::start() {
   if (acctOn) {
     // partitioned: every RPC is counted by its sender's rank, on the sender's
     // (owned) edge; gs_read_rpc_bytes returns the owned edges
-    x.rpcB = dalloc<unsigned long long>(E); x.rpcN = dalloc<unsigned long long>(E);
+    x.rpcB = ealloc<unsigned long long>(); x.rpcN = ealloc<unsigned long long>();
     AcctT* ac = dalloc<AcctT>(T);
     chk(x.rpcB); chk(x.rpcN); chk(ac);
     if (!ok) { gs_set_error("device allocation failed (RPC accounting)"); return GS_ENOMEM; }
@@ -1005,8 +1025,8 @@ int gs_engine::start() {
         hn[e] = isDown(e) ? 0ull : 1ull;
       }
     HIPCHECK(hipMemcpyAsync(ac, ah.data(), (size_t)T * sizeof(AcctT), hipMemcpyHostToDevice, stream));
-    HIPCHECK(hipMemcpyAsync(x.rpcB, hb.data(), (size_t)E * 8, hipMemcpyHostToDevice, stream));
-    HIPCHECK(hipMemcpyAsync(x.rpcN, hn.data(), (size_t)E * 8, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipMemcpyAsync(x.rpcB + e0, hb.data() + e0, (size_t)eOwn * 8, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipMemcpyAsync(x.rpcN + e0, hn.data() + e0, (size_t)eOwn * 8, hipMemcpyHostToDevice, stream));
     HIPCHECK(hipStreamSynchronize(stream));  // pageable sources
     x.acc = ac;
   }
@@ -2340,7 +2360,7 @@ int gs_set_topic_score_params(gs_engine* g, int32_t topic, const gs_topic_score_
   TopicP tp = to_dev(*p, g->scoring);
   if (g->scoring) k_fold<<<nblk(g->E, 256), 256, 0, g->stream>>>(g->d, topic);  // with the old caps
   HIPCHECK(hipMemcpyAsync(g->dTp + topic, &tp, sizeof(TopicP), hipMemcpyHostToDevice, g->stream));
-  HIPCHECK(hipMemsetAsync(g->d.sdirty, 1, (size_t)g->E, g->stream));  // every score may have changed
+  HIPCHECK(hipMemsetAsync(g->d.sdirty + g->e0, 1, (size_t)g->eOwn, g->stream));  // every score may have changed
   if (existed && g->scoring &&
       (p->FirstMessageDeliveriesCap < old.FirstMessageDeliveriesCap ||
        p->MeshMessageDeliveriesCap < old.MeshMessageDeliveriesCap))
@@ -2395,8 +2415,9 @@ int gs_read_rpc_bytes(gs_engine* g, int64_t* bytes, int64_t* rpcs) {
   }
   std::vector<unsigned long long> b(E), n(E);
   HIPCHECK(hipStreamSynchronize(g->stream));
-  HIPCHECK(hipMemcpy(b.data(), g->d.rpcB, (size_t)E * 8, hipMemcpyDeviceToHost));
-  HIPCHECK(hipMemcpy(n.data(), g->d.rpcN, (size_t)E * 8, hipMemcpyDeviceToHost));
+  // (owned edges only on the device, Dev::rxi)
+  HIPCHECK(hipMemcpy(b.data() + g->e0, g->d.rpcB + g->e0, (size_t)g->eOwn * 8, hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(n.data() + g->e0, g->d.rpcN + g->e0, (size_t)g->eOwn * 8, hipMemcpyDeviceToHost));
   for (int64_t e = 0; e < E; ++e) {
     const bool own = e >= g->e0 && e < g->e1;  // a partitioned rank reports its own edges
     if (bytes) bytes[e] = own ? (int64_t)b[e] : 0;
@@ -2503,8 +2524,10 @@ int gs_read_counters(gs_engine* g, gs_counters* out) {
 int gs_read_scores(gs_engine* g, double* score) {
   if (!g->graphSet) { gs_set_error("graph not set"); return GS_ESTATE; }
   NEED_STARTED(g);
-  score_rows<0>(g->d, g->E, g->d.T, g->dScoreTmp, g->stream);
-  HIPCHECK(hipMemcpyAsync(score, g->dScoreTmp, g->E * 8, hipMemcpyDeviceToHost, g->stream));
+  score_rows<0>(g->d, g->eOwn, g->d.T, g->dScoreTmp, g->stream);
+  // the owned edges (a partitioned rank's others read 0)
+  std::memset(score, 0, (size_t)g->E * 8);
+  HIPCHECK(hipMemcpyAsync(score + g->e0, g->dScoreTmp + g->e0, (size_t)g->eOwn * 8, hipMemcpyDeviceToHost, g->stream));
   HIPCHECK(hipStreamSynchronize(g->stream));
   if (g->mixed)  // only gossipsub hosts keep a peerScore (floodsub / randomsub: none, score 0)
     for (int u = 0; u < g->N; ++u)
@@ -2513,18 +2536,21 @@ int gs_read_scores(gs_engine* g, double* score) {
   return GS_OK;
 }
 
-static int copy_back(gs_engine* g, void* dst, const void* src, size_t bytes) {
-  if (!g->started) {
-    std::memset(dst, 0, bytes);
-    return GS_OK;
-  }
+// A per-edge array (owned edges [e0, e1) on the device, Dev::rxi) into a
+// host array of E entries; a partitioned rank's other entries read 0.
+}  // extern "C"
+template <class X>
+static int copy_back_edges(gs_engine* g, X* dst, const X* src) {
+  std::memset(dst, 0, (size_t)g->E * sizeof(X));
+  if (!g->started) return GS_OK;
   HIPCHECK(hipStreamSynchronize(g->stream));
-  HIPCHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(dst + g->e0, src + g->e0, (size_t)g->eOwn * sizeof(X), hipMemcpyDeviceToHost));
   return GS_OK;
 }
+extern "C" {
 
-int gs_read_mesh(gs_engine* g, uint64_t* mesh) { return copy_back(g, mesh, g->d.mesh, g->E * 8); }
-int gs_read_fanout(gs_engine* g, uint64_t* fanout) { return copy_back(g, fanout, g->d.fanout, g->E * 8); }
+int gs_read_mesh(gs_engine* g, uint64_t* mesh) { return copy_back_edges(g, mesh, g->d.mesh); }
+int gs_read_fanout(gs_engine* g, uint64_t* fanout) { return copy_back_edges(g, fanout, g->d.fanout); }
 int gs_read_backoff(gs_engine* g, int64_t* expire) { return copy_back_pairs(g, expire, g->d.backoff); }
 int gs_read_topic_stats(gs_engine* g, double* fmd, double* mmd, double* mfp, double* imd, int64_t* mesh_time,
                         int64_t* graft_time, uint8_t* flags) {
@@ -2543,7 +2569,7 @@ int gs_read_topic_stats(gs_engine* g, double* fmd, double* mmd, double* mfp, dou
     if (flags[i] & 1) mesh_time[i] = graft_time[i] <= lr ? lr - graft_time[i] : 0;
   return GS_OK;
 }
-int gs_read_behaviour_penalty(gs_engine* g, double* bp) { return copy_back(g, bp, g->d.bp, g->E * 8); }
+int gs_read_behaviour_penalty(gs_engine* g, double* bp) { return copy_back_edges(g, bp, g->d.bp); }
 
 // PubSubRouter.EnoughPeers of every owned host (gossip_engine.h), on the host
 // from the mesh readback and the host mirrors of the announced subscriptions
@@ -2553,7 +2579,7 @@ int gs_enough_peers(gs_engine* g, int32_t topic, int32_t suggested, uint8_t* out
   if (topic < 0 || topic >= g->T || suggested < 0 || !out) { gs_set_error("gs_enough_peers: bad arguments"); return GS_EINVAL; }
   if (!g->started) { gs_set_error("gs_enough_peers: no state before the first step"); return GS_ESTATE; }
   std::vector<uint64_t> mesh((size_t)g->E);
-  int rc = copy_back(g, mesh.data(), g->d.mesh, g->E * 8);
+  int rc = copy_back_edges(g, mesh.data(), g->d.mesh);
   if (rc) return rc;
   const uint64_t bit = 1ull << topic;
   std::memset(out, 0, (size_t)g->N);

@@ -42,7 +42,7 @@ static_assert(sizeof(XRec) == 96, "XRec layout");
 __device__ __forceinline__ bool x_needed(const Dev& d, int cur, int64_t e, int& dest) {
   dest = d.nodeRank[d.col[e]];
   if (dest == d.rank) return false;
-  const int64_t ri = d.rev[e];  // outbox records are indexed by the receiver's in-edge
+  const int64_t ri = rxi(d, e, d.rev[e]);  // the receiver's records of edge e: its stage slot here
   return d.xmark[e] || d.cPre[cur][ri] || d.cHb[cur][ri];
 }
 
@@ -62,7 +62,7 @@ __global__ void k_x_pack(Dev d, int cur, const int64_t* __restrict__ off, unsign
   int dest;
   if (!x_needed(d, cur, e, dest)) return;
   const int64_t k = off[dest] + (int64_t)atomicAdd(&cursor[dest], 1ull);
-  const int64_t ri = d.rev[e];
+  const int64_t ri = rxi(d, e, d.rev[e]);  // the stage slot of edge e
   XRec x;
   x.e = (int32_t)e;
   x.pre = d.cPre[cur][ri];
@@ -109,9 +109,7 @@ __global__ void k_x_unpack(Dev d, int cur, const XRec* __restrict__ in, int64_t 
   if (k >= n) return;
   const XRec x = in[k];
   const int64_t e = x.e;
-  const int64_t ri = d.rev[e];
-  d.fwdRelay[cur][e] = x.relay;
-  d.fwdPub[cur][e] = x.pub;
+  const int64_t ri = d.rev[e];  // this rank's in-edge (the sender's sets live with the sender)
   d.fwdIn[cur][ri] = make_ulonglong2(x.relay, x.pub);
   d.cPre[cur][ri] = x.pre;
   d.cHb[cur][ri] = x.hb;
@@ -196,7 +194,7 @@ __global__ void k_xp_count(Dev d, int cur, unsigned long long* __restrict__ cnt)
   int dest;
   if (!xp_needed(d, cur, e, dest)) return;
   atomicAdd(&cnt[dest], 1ull);
-  const int ns = xp_slots(d.ibxRec[cur][d.rev[e]]);
+  const int ns = xp_slots(d.ibxRec[cur][rxi(d, e, d.rev[e])]);
   if (ns) atomicAdd(&cnt[d.world + dest], (unsigned long long)ns);
 }
 
@@ -209,7 +207,7 @@ __global__ void k_xp_pack(Dev d, int cur, const int64_t* __restrict__ boff, cons
   int dest;
   if (!xp_needed(d, cur, e, dest)) return;
   const int64_t ri = d.rev[e];
-  const int64_t rec = d.ibxRec[cur][ri];
+  const int64_t rec = d.ibxRec[cur][rxi(d, e, ri)];
   const int ns = xp_slots(rec);
   uint8_t* blk = out + boff[dest];
   const int64_t k = (int64_t)atomicAdd(&cursor[dest], 1ull);

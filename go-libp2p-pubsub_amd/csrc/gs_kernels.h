@@ -382,8 +382,9 @@ __global__ __launch_bounds__(64) void k_join(Dev d, int64_t hop, int64_t now, in
   if (silent) gj = 0;
   if (valid) {
     d.mesh[e] = meshl;
-    d.cGraftJoin[cur][d.rev[e]] = gj;
-    d.cPre[cur][d.rev[e]] = (uint8_t)__popcll(gj);
+    const int64_t rj = rxi(d, e, d.rev[e]);
+    d.cGraftJoin[cur][rj] = gj;
+    d.cPre[cur][rj] = (uint8_t)__popcll(gj);
     if (d.rpcB != nullptr && gj) {  // one sendGraft RPC per topic (gossipsub.go:1080-1084)
       int64_t b = 0;
       for (uint64_t m = gj; m; m &= m - 1) b += gs_pb_field(d.acc[__ffsll((long long)m) - 1].graftEnt);
@@ -469,7 +470,7 @@ __global__ void k_fwd(Dev d, int cur) {
   if (d.xmark) d.xmark[e] = 1;
   d.fwdRelay[cur][e] = relay;
   d.fwdPub[cur][e] = pub;
-  d.fwdIn[cur][d.rev[e]] = make_ulonglong2(relay, pub);
+  d.fwdIn[cur][rxi(d, e, d.rev[e])] = make_ulonglong2(relay, pub);
 }
 
 __global__ void k_pubmask(Dev d, int b, int n, int cur) {
@@ -756,7 +757,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
                           !(gv != 0 && gt / gv < d.gThreshold);
       if (active) {
         const int64_t ge = base + d.gGrp[base + lane];
-        const double de = d.gSt[ge], du = d.gSt[d.E + ge], ig = d.gSt[2 * d.E + ge], rj = d.gSt[3 * d.E + ge];
+        const double de = d.gSt[ge], du = d.gSt[d.eOwn + ge], ig = d.gSt[2 * d.eOwn + ge], rj = d.gSt[3 * d.eOwn + ge];
         const double total = de + d.gDupW * du + d.gIgnW * ig + d.gRejW * rj;
         if (total != 0) thr = (1 + de) / (1 + total);
       }
@@ -798,7 +799,11 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   // words of the active window; none of them is written before this wave's
   // own passes 2b / 3
   constexpr int PF3 = 16;
-  const int nWdPf = (NARROW && scoring && d.dltN != nullptr) ? (deg * T) >> 1 : 0;
+#ifndef GS_PF
+#define GS_PF 1  // timing A/B: -DGS_PF=0 builds the phase A without the prefetch
+#endif
+  constexpr bool kPf = GS_PF != 0;
+  const int nWdPf = (kPf && NARROW && scoring && d.dltN != nullptr) ? (deg * T) >> 1 : 0;
   const bool pf3 = nWdPf > 0 && nWdPf <= 64 * PF3;
   uint32_t q3[PF3];
   if (pf3) {
@@ -815,7 +820,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   for (int j = 0; j < WPL; ++j) {
     const int w = lane + 64 * j;
     Sp[j] = Hp[j] = Op[j] = 0;
-    if constexpr (!ADV) {
+    if constexpr (!ADV && kPf) {
       const bool act = w < W && wm_has(amR, w);
       if (act || (w < W && wm_has(amP, w))) Sp[j] = d.seen[(int64_t)v * W + w];
       if (act) {
@@ -1169,7 +1174,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
     rkw[j] = 0;
     const bool ret = w < W && wm_has(amP, w);
     if (ret) Rw[j] = d.pubmask[cur][w];
-    if constexpr (!ADV) {
+    if constexpr (!ADV && kPf) {
       Sw[j] = Sp[j];  // (prefetched at wave start)
       if (w < W && wm_has(amR, w)) {
         rkw[j] = wm_rank(amR, w);
@@ -1615,9 +1620,9 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
         for (int k = 0; k < 4; ++k) {
           const uint32_t n = sPer[k * 64 + lane];
           if (!n) continue;
-          double x = d.gSt[k * d.E + base + lane];
+          double x = d.gSt[k * d.eOwn + base + lane];
           x = gs_add_ones(x, n);
-          d.gSt[k * d.E + base + lane] = x;
+          d.gSt[k * d.eOwn + base + lane] = x;
         }
       }
       const long long thc = (long long)wave_sum_ll(nThrottledCopies);
@@ -1662,7 +1667,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
         } else {
           int p = (int)off;
           each([&](int slot) { d.pool[cur][p++] = slot; });
-          const int64_t rl = d.rev[base + lane];  // the receiver's in-edge
+          const int64_t rl = rxi(d, base + lane, d.rev[base + lane]);  // the receiver's in-edge (or its stage slot)
           d.cSpam[cur][rl] = ((int64_t)off << 24) | (int64_t)n;
           d.cPre[cur][rl] = (uint8_t)(d.cPre[cur][rl] + 1);
           // RPC{control: {iwant: [{n ids}]}}
@@ -1958,7 +1963,7 @@ __global__ __launch_bounds__(64) void k_push(Dev d, int cur) {
   uint64_t relay = 0, pub = 0;
   int64_t re = 0;
   if (local) {
-    re = d.rev[e];
+    re = rxi(d, e, d.rev[e]);
     relay = d.fwdRelay[cur][e];
     pub = d.fwdPub[cur][e];
   }
@@ -2144,8 +2149,8 @@ __global__ void k_gater_decay(Dev d, int64_t now) {
   if (e >= d.e1) return;
   if (d.rowptr[d.esrc[e]] + d.gGrp[e] != e) return;  // not a group's stats edge
   if (d.gConn[e] > 0) {
-    for (int k = 0; k < 4; ++k) d.gSt[k * d.E + e] = gdecay(d.gSt[k * d.E + e], d.gSourceDecay, d.gDecayToZero);
+    for (int k = 0; k < 4; ++k) d.gSt[k * d.eOwn + e] = gdecay(d.gSt[k * d.eOwn + e], d.gSourceDecay, d.gDecayToZero);
   } else if (d.gExp[e] < now) {
-    for (int k = 0; k < 4; ++k) d.gSt[k * d.E + e] = 0.0;  // delete(pg.ipStats, ip)
+    for (int k = 0; k < 4; ++k) d.gSt[k * d.eOwn + e] = 0.0;  // delete(pg.ipStats, ip)
   }
 }

@@ -319,7 +319,7 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
   int64_t r = 0;
   int npre = 0, hb = 0;
   if (valid) {
-    r = d.rev[e];
+    r = rxi(d, e, d.rev[e]);  // where v's replies to this sender go (its in-edge, or the stage slot)
     npre = d.cPre[prv][e];
     hb = d.cHb[prv][e];
   }
@@ -404,7 +404,7 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
       };
       uint64_t pOut = 0;
       int nR = 0;
-      const int64_t reI = d.doPX ? d.rev[ei] : 0;  // the sender's in-edge: our PX record for it
+      const int64_t reI = d.doPX ? rxi(d, ei, d.rev[ei]) : 0;  // the sender's in-edge: our PX record for it
       // makePrune with PX for the rejected topics of one RPC (live scores)
       auto pxPrunes = [&](uint64_t topics) {
         if (!topics) return;
@@ -785,14 +785,22 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
       __syncthreads();
       // cuts are per (sender, topic): topic item tb covers items tb*nCh ..
       const int totalT = totalItems / nCh;
-      for (int tb = lane; tb < totalT; tb += 64) {
+      // an item's id count: long topic windows (config3's 157 words) are
+      // summed by the whole wave, item after item; short ones lane per item
+      const bool waveSum = Wt > 16;
+      for (int tb = waveSum ? 0 : lane; tb < totalT; tb += waveSum ? 1 : 64) {
         int k;
         const int i = item_sender(sIt, tb * nCh, k);
         const int t = kth_bit(sTm[i], k / nCh);
         const int uu = sNode[i];
         int nm = 0;
-        for (int w = t * Wt; w < (t + 1) * Wt; ++w) nm += __popcll(d.gw[(int64_t)uu * W + w]);
-        if (nm > d.MaxIHaveLength) {
+        if (waveSum) {
+          for (int w = t * Wt + lane; w < (t + 1) * Wt; w += 64) nm += __popcll(d.gw[(int64_t)uu * W + w]);
+          nm = wave_last(wave_incl_sum(nm));
+        } else {
+          for (int w = t * Wt; w < (t + 1) * Wt; ++w) nm += __popcll(d.gw[(int64_t)uu * W + w]);
+        }
+        if (nm > d.MaxIHaveLength && (!waveSum || lane == 0)) {
           const int pos = atomicAdd(cN, 1);
           if (pos < GS_CUTS) {
             cItem[pos] = tb;
@@ -811,15 +819,25 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
         const int i = item_sender(sIt, tb * nCh, k);
         const int t = kth_bit(sTm[i], k / nCh);
         const int uu = sNode[i];
-        // every gossip id of the sender's topic t, lane-strided over words
+        // every gossip id of the sender's topic t, lane-strided over words;
+        // the ids' message-id loads go out four at a time
         auto each = [&](auto&& fn) {
           for (int w = t * Wt + lane; w < (t + 1) * Wt; w += 64) {
             uint64_t y = d.gw[(int64_t)uu * W + w];
             while (y) {
-              const int bb = __ffsll((long long)y) - 1;
-              y &= y - 1;
-              const int64_t mid = d.slotMid[(int64_t)w * 64 + bb];
-              fn(gs_key64(d.seed, GS_SITE_EMIT_MIDS, uu, v, (uint32_t)mid, (uint32_t)(h - 1)), mid);
+              int bs[4];
+              int64_t mids[4];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                bs[q] = y ? __ffsll((long long)y) - 1 : -1;
+                y &= y ? y - 1 : 0ull;
+              }
+#pragma unroll
+              for (int q = 0; q < 4; ++q) mids[q] = bs[q] >= 0 ? d.slotMid[(int64_t)w * 64 + bs[q]] : 0;
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+                if (bs[q] >= 0)
+                  fn(gs_key64(d.seed, GS_SITE_EMIT_MIDS, uu, v, (uint32_t)mids[q], (uint32_t)(h - 1)), mids[q]);
             }
           }
         };
@@ -1899,7 +1917,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
         const int p = __ffsll((long long)pl) - 1;
         pl &= pl - 1;
         const uint64_t list = px_sel(d, v, base, deg, t, hop, p, ok);
-        if (lane == p) px_append(d, cur, d.rev[e], t, list, base);
+        if (lane == p) px_append(d, cur, rxi(d, e, d.rev[e]), t, list, base);
       }
     }
   }
@@ -1966,7 +1984,7 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
     d.mesh[e] = meshl;
     d.fanout[e] = fanl;
     if (tograft | toprune | ihave) {
-      const int64_t re = d.rev[e];  // outbox records are indexed by the receiver's in-edge
+      const int64_t re = rxi(d, e, d.rev[e]);  // outbox records are indexed by the receiver's in-edge
       d.cGraftHb[cur][re] = tograft;
       d.cPruneHb[cur][re] = toprune;
       d.cIhave[cur][re] = ihave;
@@ -2246,7 +2264,7 @@ __global__ __launch_bounds__(64) void k_leave(Dev d, const int32_t* __restrict__
         const int p = __ffsll((long long)pl) - 1;
         pl &= pl - 1;
         const uint64_t list = px_sel(d, v, base, deg, t, hop, p, (m && lane <= p) ? okPost : okPre);
-        if (lane == p) px_append(d, cur, d.rev[e], t, list, base);
+        if (lane == p) px_append(d, cur, rxi(d, e, d.rev[e]), t, list, base);
       }
     }
     np += __popcll(__ballot(m));
@@ -2254,7 +2272,7 @@ __global__ __launch_bounds__(64) void k_leave(Dev d, const int32_t* __restrict__
   if (valid && pruned) {
     d.mesh[e] = meshl;
     if (!silent) {
-      const int64_t re = d.rev[e];
+      const int64_t re = rxi(d, e, d.rev[e]);
       d.cPruneReply[cur][re] |= pruned;
       d.cPre[cur][re] = (uint8_t)(d.cPre[cur][re] + __popcll(pruned));  // one sendPrune RPC per topic
       if (d.rpcB != nullptr) {
@@ -2265,7 +2283,7 @@ __global__ __launch_bounds__(64) void k_leave(Dev d, const int32_t* __restrict__
       if (rpc_traced(d, v, d.col[e]))
         for (uint64_t m = pruned; m; m &= m - 1) {
           const int t = __ffsll((long long)m) - 1;
-          const int64_t pxr = d.doPX ? d.cPx[cur][d.rev[e]] : -1;
+          const int64_t pxr = d.doPX ? d.cPx[cur][rxi(d, e, d.rev[e])] : -1;
           rpc_trace(d, hop, v, d.col[e], 0, 3, GS_RPC_ORD(0, GS_RPC_O_LEAVE + t), 2 + px_count(d, cur, pxr, 1ull << t),
                     [&](auto put) {
             put(GS_RPC_ITEM_CTL, -1, -1);
@@ -2345,7 +2363,7 @@ __global__ __launch_bounds__(64) void k_join_pairs(Dev d, const int32_t* __restr
     d.mesh[e] = meshl;
     d.fanout[e] = fanl;
     if (grafted && !silent) {
-      const int64_t re = d.rev[e];
+      const int64_t re = rxi(d, e, d.rev[e]);
       d.cGraftJoin[cur][re] |= grafted;
       d.cPre[cur][re] = (uint8_t)(d.cPre[cur][re] + __popcll(grafted));  // one sendGraft RPC per topic
       if (d.rpcB != nullptr) {

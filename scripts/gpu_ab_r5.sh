@@ -15,6 +15,8 @@ for v in "$@"; do
       > "$OUT/${v}_c4.json" 2> "$OUT/${v}_c4.err" || exit 1
 done &&
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/main_c4_again.json" 2> "$OUT/main_c4_again.err" &&
+timeout -k 10 300 python -u bench.py --workload config3 --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/main_c3.json" 2> "$OUT/main_c3.err" &&
+timeout -k 10 300 python -u bench.py --workload config5 --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/main_c5.json" 2> "$OUT/main_c5.err" &&
 for v in "$@"; do
   timeout -k 10 300 python -u bench.py --workload config5 --steps 5 --warmup 5 --no-cpu-baseline \
       --lib "$B/libgossip_engine_var_$v.so" > "$OUT/${v}_c5.json" 2> "$OUT/${v}_c5.err" || exit 1
