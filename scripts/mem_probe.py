@@ -16,6 +16,7 @@ import ctypes as C
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -89,6 +90,13 @@ def main():
     if args.peers:
         wl["n"] = args.peers
     tr = SoloTransport(args.rank, args.world)
+    t_start = time.perf_counter()
+
+    def tick():  # a progress line while the host builds the graph
+        while True:
+            time.sleep(30)
+            print(f"mem_probe: {time.perf_counter() - t_start:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=tick, daemon=True).start()
     free0 = torch.cuda.mem_get_info(0)[0]
     t0 = time.perf_counter()
     eng, g = bench.build_engine(wl, args.rounds + 2, 3, 0, extra=(WithPartition(args.rank, args.world, tr),))
