@@ -968,12 +968,12 @@ __device__ __forceinline__ void select_kth(F&& each, int k, uint32_t* hist, unsi
 // the common case instead of about three.  The k-th smallest key's top byte
 // is expected near 256 k / n (its standard deviation is about 256 *
 // sqrt(k (n - k) / n^3), ~1.2 bins at config3's 5000 of 6000), so the pass
-// builds the top-byte histogram and keeps every candidate whose top byte lies
-// within GS_SEL_WIN bins of that estimate in LDS (cand: GS_SEL_CAP (key, id)
-// pairs + a counter; ~117 expected at config3's 6000 ids, so about one select
-// in twenty falls back).  If the k-th falls into a kept bin and nothing
-// overflowed, the k-th smallest (key, id) of that bin is ranked among the kept
-// entries; otherwise select_kth runs as before.  Either way the result is the
+// counts the keys whose top byte lies below GS_SEL_WIN bins under that
+// estimate and keeps every candidate within GS_SEL_WIN bins of it in LDS
+// (cand: GS_SEL_CAP (key, id) pairs + a counter; ~117 expected at config3's
+// 6000 ids, so about one select in twenty falls back).  If the k-th falls
+// among the kept entries and nothing overflowed, it is ranked among them;
+// otherwise select_kth runs as before.  Either way the result is the
 // exact k-th smallest (key, id).  n = the number of candidates each() yields.
 #define GS_SEL_WIN 2
 #define GS_SEL_CAP 143
@@ -989,12 +989,14 @@ __device__ __forceinline__ void select_kth_est(F&& each, int k, int n, uint32_t*
   const int est = (int)((((int64_t)k << 9) / n + 1) >> 1);  // 256 k / n, rounded
   const int lo = max(0, est - GS_SEL_WIN), hi = min(255, est + GS_SEL_WIN);
   uint32_t* const cnt = (uint32_t*)(cand + 2 * GS_SEL_CAP);
-  for (int q = lane; q < 256; q += 64) hist[q] = 0u;
   if (lane == 0) *cnt = 0u;
   __syncthreads();
+  // no histogram: the keys below bin lo are only counted (a register per
+  // lane), the window's are kept
+  int nLo = 0;
   each([&](unsigned long long key, long long id) {
     const int top = (int)(key >> 56);
-    atomicAdd(&hist[top], 1u);
+    nLo += top < lo ? 1 : 0;
     if (top >= lo && top <= hi) {
       const uint32_t pos = atomicAdd(cnt, 1u);
       if (pos < GS_SEL_CAP) {
@@ -1003,34 +1005,15 @@ __device__ __forceinline__ void select_kth_est(F&& each, int k, int n, uint32_t*
       }
     }
   });
+  const int below = wave_sum_int(nLo);
   __syncthreads();
-  const uint32_t c0 = hist[4 * lane], c1 = hist[4 * lane + 1], c2 = hist[4 * lane + 2], c3 = hist[4 * lane + 3];
-  const int sum = (int)(c0 + c1 + c2 + c3);
-  const int incl = wave_incl_sum(sum);
-  const int excl = incl - sum;
-  const bool mine = excl < k && k <= incl;
-  int digit = 0, below = 0;
-  if (mine) {
-    const uint32_t cs[4] = {c0, c1, c2, c3};
-    int acc = excl, dd = 0;
-    for (; dd < 3; ++dd) {
-      if (acc + (int)cs[dd] >= k) break;
-      acc += (int)cs[dd];
-    }
-    digit = 4 * lane + dd;
-    below = acc;
-  }
-  const unsigned long long m = __ballot(mine);
-  const int src = __ffsll((long long)m) - 1;  // k < n: some lane holds the k-th
-  digit = lane_get(digit, src);
-  below = lane_get(below, src);
   const int nc = (int)*cnt;
   __syncthreads();
-  if (digit < lo || digit > hi || nc > GS_SEL_CAP) {
+  if (!(below < k && k <= below + nc) || nc > GS_SEL_CAP) {
     select_kth(each, k, hist, K, M);  // the estimate missed: the multi-pass select
     return;
   }
-  // the (k - below)-th smallest (key, id) among the kept entries of bin `digit`
+  // the (k - below)-th smallest (key, id) among the kept entries
   const int kk = k - below;
   unsigned long long fk = 0;
   long long fm = 0;
@@ -1039,11 +1022,10 @@ __device__ __forceinline__ void select_kth_est(F&& each, int k, int n, uint32_t*
     const int j = j0 + lane;
     const unsigned long long key = j < nc ? cand[2 * j] : ~0ull;
     const long long id = j < nc ? (long long)cand[2 * j + 1] : INT64_MAX;
-    if (j < nc && (int)(key >> 56) == digit) {
+    if (j < nc) {
       int rank = 0;
       for (int q = 0; q < nc; ++q) {
         const unsigned long long qk = cand[2 * q];
-        if ((int)(qk >> 56) != digit) continue;
         const long long qm = (long long)cand[2 * q + 1];
         rank += (qk < key || (qk == key && qm < id)) ? 1 : 0;
       }

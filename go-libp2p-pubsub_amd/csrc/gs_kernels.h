@@ -771,7 +771,12 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
     else if (irN) nSrvRpc = 1;
   }
   // per-sender view for the block-parallel walk
-  const int nb = (Ln + 3) >> 2;  // 16-byte blocks of the sender's list
+#ifndef GS_PB8
+#define GS_PB8 1  // timing A/B: -DGS_PB8=0 reads pushed segments 4 slots (8 B) per block
+#endif
+  constexpr int EPBP = GS_PB8 ? 8 : 4;  // slots per block of a pushed segment (16 B: 8 slots)
+  // 16-byte blocks of the sender's list (4 entries) or pushed segment (8 slots)
+  const int nb = pOff >= 0 ? (Ln + EPBP - 1) / EPBP : (Ln + 3) >> 2;
   const int bincl = wave_incl_sum(nb);
   const int totalBlk = wave_last(bincl);
   sBlk[lane] = bincl - nb;
@@ -932,6 +937,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   const uint16_t* const ibxPrv = prv ? d.ibx[1] : d.ibx[0];
   auto load_block = [&](int i, int kb) -> uint4 {
     if ((pushM >> i) & 1) {
+      if constexpr (EPBP == 8) return *(const uint4*)(ibxPrv + sAddr[i] + 8 * kb);  // 8-aligned segments
       const uint2 p = *(const uint2*)(ibxPrv + sAddr[i] + 4 * kb);
       return make_uint4(p.x, p.y, 0u, 0u);
     }
@@ -977,8 +983,9 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
 #pragma unroll
       for (int rr = 0; rr < PB; ++rr) {
         if (b0 + rr * 64 >= totalBlk) break;  // (wave-uniform) no block of this window is left
-        uint32_t en[4];
-        bool sn[4];
+        uint32_t en[EPBP];
+        bool sn[EPBP];
+        bool wide = false;  // a pushed block with more than 4 slots
         {
           const int i = si[rr] < 0 ? 0 : si[rr];
           const int snd = sSnd[i];
@@ -987,12 +994,20 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
           const bool rsS = (snd >> 30) & 1;
           const bool isGray = snd < 0;
           const uint64_t rl = sRelay[i], pb = sPub[i];
-          const int n = si[rr] < 0 ? 0 : min(4, sLn[i] - 4 * kb[rr]);
-          if ((pushM >> i) & 1) {
+          const bool pushed = (pushM >> i) & 1;
+          const int epb = pushed ? EPBP : 4;
+          const int n = si[rr] < 0 ? 0 : min(epb, sLn[i] - epb * kb[rr]);
+          wide = n > 4;
+#pragma unroll
+          for (int c = 4; c < EPBP; ++c) {
+            sn[c] = false;
+            en[c] = 0;
+          }
+          if (pushed) {
             // pushed: every copy was sent; the topics v left are only counted
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-              const uint32_t wd = c < 2 ? q[rr].x : q[rr].y;
+            for (int c = 0; c < EPBP; ++c) {
+              const uint32_t wd = c < 2 ? q[rr].x : c < 4 ? q[rr].y : c < 6 ? q[rr].z : q[rr].w;
               const int slot = (int)((c & 1) ? (wd >> 16) : (wd & 0xFFFFu));
               const int t = (int)__umulhi((unsigned)slot, d.stMagic);
               const bool sent = c < n && !(authV && d.slotSrc[slot] == v);  // never to the author
@@ -1024,27 +1039,33 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
           }
         }
         // c-major positions (delivery order does not matter: every update is
-        // a commutative LDS atomic)
+        // a commutative LDS atomic), four entries per lane between drains
+        // (the queue holds 63 pending + 256 appended)
+        const bool wideAny = EPBP > 4 && __ballot(wide) != 0;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const uint64_t m = __ballot(sn[c]);
-          if (sn[c]) sQ[qt + lane_rank(m)] = en[c];
-          qt += __popcll(m);
-        }
-        __syncthreads();
-        if (qt >= 64) {
-          while (qt - qh >= 64) {
-            const uint32_t ent = sQ[qh + lane];
-            fn((int)(ent >> 16), (int)(ent & 0xFFFF));
-            qh += 64;
+        for (int g = 0; g < EPBP / 4; ++g) {
+          if (g > 0 && !wideAny) break;
+#pragma unroll
+          for (int c = 4 * g; c < 4 * g + 4; ++c) {
+            const uint64_t m = __ballot(sn[c]);
+            if (sn[c]) sQ[qt + lane_rank(m)] = en[c];
+            qt += __popcll(m);
           }
-          // move the (< 64) pending copies to the front
-          const uint32_t rest = lane < qt - qh ? sQ[qh + lane] : 0u;
           __syncthreads();
-          if (lane < qt - qh) sQ[lane] = rest;
-          qt -= qh;
-          qh = 0;
-          __syncthreads();
+          if (qt >= 64) {
+            while (qt - qh >= 64) {
+              const uint32_t ent = sQ[qh + lane];
+              fn((int)(ent >> 16), (int)(ent & 0xFFFF));
+              qh += 64;
+            }
+            // move the (< 64) pending copies to the front
+            const uint32_t rest = lane < qt - qh ? sQ[qh + lane] : 0u;
+            __syncthreads();
+            if (lane < qt - qh) sQ[lane] = rest;
+            qt -= qh;
+            qh = 0;
+            __syncthreads();
+          }
         }
       }
     }

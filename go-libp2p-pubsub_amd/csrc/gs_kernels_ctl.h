@@ -819,6 +819,80 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
         const int i = item_sender(sIt, tb * nCh, k);
         const int t = kth_bit(sTm[i], k / nCh);
         const int uu = sNode[i];
+#ifndef GS_CUTBAL
+#define GS_CUTBAL 1  // timing A/B: -DGS_CUTBAL=0 strides the lanes over words instead
+#endif
+        const uint64_t* const g = d.gw + (int64_t)uu * W + t * Wt;  // the sender's words of topic t
+        unsigned long long K;
+        long long M;
+        if constexpr (GS_CUTBAL != 0) {
+          // every gossip id of the sender's topic t in word order, lane l taking
+          // the ids of rank [l n / 64, (l + 1) n / 64): the same count per lane
+          // (a word-strided split leaves a third of the lanes with one word
+          // more), four message-id loads in flight per step
+          int pre[GS_MAX_WPL];  // ids before word 64 j + lane
+          int n = 0;
+#pragma unroll
+          for (int j = 0; j < GS_MAX_WPL; ++j) {
+            const int w = 64 * j + lane;
+            const int pc = w < Wt ? __popcll(g[w]) : 0;
+            const int incl = wave_incl_sum(pc);
+            pre[j] = n + incl - pc;
+            n += wave_last(incl);
+          }
+          auto preAt = [&](int w) {  // (all lanes: the shuffles read every lane)
+            int x = 0;
+#pragma unroll
+            for (int j = 0; j < GS_MAX_WPL; ++j) {
+              const int y = __shfl(pre[j], w & 63);
+              if ((w >> 6) == j) x = y;
+            }
+            return x;
+          };
+          const int r0 = (int)((int64_t)lane * n / 64), r1 = (int)((int64_t)(lane + 1) * n / 64);
+          // the first word holding rank r0: the last w with pre(w) <= r0
+          int lo = 0, hi = Wt - 1;
+          while (__ballot(lo < hi)) {
+            const int mid = (lo + hi + 1) >> 1;
+            const int pm = preAt(lo < hi ? mid : lo);
+            if (lo < hi) {
+              if (pm <= r0) lo = mid; else hi = mid - 1;
+            }
+          }
+          const int wS = lo;
+          uint64_t yS = r0 < r1 ? g[wS] : 0ull;
+          for (int sk = r0 - preAt(wS); sk > 0; --sk) yS &= yS - 1;  // the ids of lower lanes
+          auto each = [&](auto&& fn) {
+            int w = wS;
+            uint64_t y = yS, ny = (r0 < r1 && wS + 1 < Wt) ? g[wS + 1] : 0ull;
+            for (int r = r0; r < r1; r += 4) {
+              int bs[4], ws[4];
+              int64_t mids[4];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                bs[q] = -1;
+                ws[q] = w;
+                if (r + q < r1) {
+                  while (y == 0) {  // (rank r + q exists: some later word holds it)
+                    ++w;
+                    y = ny;
+                    ny = w + 1 < Wt ? g[w + 1] : 0ull;
+                  }
+                  bs[q] = __ffsll((long long)y) - 1;
+                  ws[q] = w;
+                  y &= y - 1;
+                }
+              }
+#pragma unroll
+              for (int q = 0; q < 4; ++q) mids[q] = bs[q] >= 0 ? d.slotMid[(int64_t)(t * Wt + ws[q]) * 64 + bs[q]] : 0;
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+                if (bs[q] >= 0)
+                  fn(gs_key64(d.seed, GS_SITE_EMIT_MIDS, uu, v, (uint32_t)mids[q], (uint32_t)(h - 1)), mids[q]);
+            }
+          };
+          select_kth_est(each, d.MaxIHaveLength, n, cHist, cand, K, M);
+        } else {
         // every gossip id of the sender's topic t, lane-strided over words;
         // the ids' message-id loads go out four at a time
         auto each = [&](auto&& fn) {
@@ -841,9 +915,8 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
             }
           }
         };
-        unsigned long long K;
-        long long M;
         select_kth_est(each, d.MaxIHaveLength, cNm[c], cHist, cand, K, M);
+        }
         if (lane == 0) {
           cK[c] = K;
           cM[c] = M;
