@@ -490,6 +490,19 @@ __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
 // Value of lane i for a wave-uniform i (v_readlane into a scalar register,
 // no LDS permute).
 __device__ __forceinline__ int lane_get(int x, int i) { return __builtin_amdgcn_readlane(x, i); }
+// The value of lane (lane ^ 32), for the half-wave pairs: v_permlane32_swap
+// swaps the halves in a VALU op (a __shfl_xor(x, 32) is a ds_bpermute round
+// trip through the LDS unit).  Every lane must be active.
+__device__ __forceinline__ uint32_t xor32_u32(uint32_t x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return lane_id() < 32 ? r[1] : r[0];
+}
+__device__ __forceinline__ uint64_t xor32_u64(uint64_t x) {
+  return ((uint64_t)xor32_u32((uint32_t)(x >> 32)) << 32) | (uint64_t)xor32_u32((uint32_t)x);
+}
+__device__ __forceinline__ double xor32_f64(double x) {
+  return __longlong_as_double((long long)xor32_u64((uint64_t)__double_as_longlong(x)));
+}
 __device__ __forceinline__ uint64_t lane_get64(uint64_t x, int i) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, i);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), i);

@@ -684,6 +684,10 @@ int gs_engine::start() {
     const int64_t budget = 8ll << 30;
     int64_t fc = std::min<int64_t>(S + 64, budget / (4 * (int64_t)N));
     x.FC = (int32_t)std::max<int64_t>(64, fc & ~3ll);
+    if ((int64_t)N * x.FC >= (1ll << 32)) {  // phase A addresses a list by a 32-bit entry offset
+      gs_set_error("too many peers for the frontier lists");
+      return GS_EUNSUPPORTED;
+    }
   }
   for (int k = 0; k < 2; ++k) {
     x.fl[k] = dalloc<uint32_t>((size_t)N * x.FC); chk(x.fl[k]);
@@ -1436,7 +1440,8 @@ int gs_engine::stepOne() {
     // instantiation: the honest path keeps its LDS budget and code
     const bool adv = topicVal != 0 || gaterOn || behaveAll != 0;
     const bool hasUnc = d.needAge || (adv && d.pmaskRow != nullptr);
-    size_t lds = (narrow ? 2 : 4) * nCnt + 16 * (size_t)nR + (size_t)nYp + (hasUnc ? 4 * nCnt : 0);
+    size_t lds = (narrow ? 2 : 4) * nCnt + 16 * (size_t)nR + ((2 * ((size_t)W + nR) + 15) & ~(size_t)15) +
+                 (size_t)nYp + (hasUnc ? 4 * nCnt : 0);
     if (adv) lds += 4 * nCnt + 4 * 64 * 4 + 8 * 64 + 8 * (size_t)nR;
     if (nOwn) {
       const int rc = upload(dDev, &d, sizeof(Dev));

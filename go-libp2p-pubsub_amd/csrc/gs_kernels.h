@@ -643,7 +643,9 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   uint32_t* scnt = smem32;  // [MD][T] copies | fresh << 16 (NARROW: u16 copies | fresh << 8)
   uint64_t* sD = (uint64_t*)(scnt + nCntW);               // [nR] delivered young slots (non-graylisted)
   uint64_t* sYm = sD + nR;                                // [nR] young-slot mask of each amR word
-  uint8_t* sFirst = (uint8_t*)(sYm + nR);                 // [nY] lowest deliverer per young slot
+  uint16_t* sRk = (uint16_t*)(sYm + nR);                  // [W] rank of word w in amR, 0xFFFF = outside
+  uint16_t* sYp = sRk + d.W;                              // [nR] young slots in the amR words before it
+  uint8_t* sFirst = (uint8_t*)(sYm + nR) + ((2 * (d.W + nR) + 15) & ~15);  // [nY] lowest deliverer per young slot
   uint32_t* sUnc = (uint32_t*)(sFirst + nY);              // [MD][T] uncredited duplicates (needAge / pmask)
   // drec.peers of this node (score.go:786-818): the senders whose duplicate
   // of a message was already counted — tracked only for nodes that re-request
@@ -656,19 +658,16 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
                                                           // rejected / ignored first deliveries
   double* sGThr = (double*)(sPer + 4 * 64);               // [64] gater threshold per sender, < 0 = accept
   uint64_t* sDrop = (uint64_t*)(sGThr + 64);              // [nR] fresh messages dropped by a full queue
-  __shared__ int sBlk[64];        // first list block of each sender
   // block -> sender without a search: a bit per list block where a non-empty
   // sender's list starts (the first GS_BMAP * 64 blocks), and the non-empty
-  // senders in ascending order as node | first block << 24 | sender << 48
+  // senders in ascending order as first block | sender << 24 | copies << 32
+  // (past the map: a binary search over the first blocks)
   __shared__ uint64_t sStart[GS_BMAP];
   __shared__ uint64_t sComp[64];
   __shared__ uint64_t sRelay[64], sPub[64];
   __shared__ int sSnd[64];        // sender node | jr << 24 | graylisted << 31
-  __shared__ int sLn[64];
-  __shared__ int64_t sAddr[64];   // a sender's copies: its pushed segment, or its list
+  __shared__ uint32_t sAddr[64];  // a sender's copies: its pushed segment (in 8-slot units), or its list
   __shared__ uint32_t sQ[GS_QCAP];         // sent copies awaiting delivery: slot | sender << 16
-  __shared__ uint16_t sRk[64 * GS_MAX_WPL];  // rank of word w in amR, 0xFFFF = outside
-  __shared__ uint16_t sYp[64 * GS_MAX_WPL];  // [rank] young slots in the amR words before it
   const int v = d.n0 + blockIdx.x;
   const int lane = lane_id();
   const int prv = cur ^ 1;
@@ -779,7 +778,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   const int nb = pOff >= 0 ? (Ln + EPBP - 1) / EPBP : (Ln + 3) >> 2;
   const int bincl = wave_incl_sum(nb);
   const int totalBlk = wave_last(bincl);
-  sBlk[lane] = bincl - nb;
+  const int nNE = __popcll(__ballot(nb > 0));  // non-empty senders
   {
     const uint64_t ne = __ballot(nb > 0);
     for (int k = lane; k < GS_BMAP; k += 64) sStart[k] = 0ull;
@@ -787,7 +786,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
     const int fb = bincl - nb;
     if (nb > 0) {
       sComp[__popcll(ne & ((1ull << lane) - 1))] =
-          (uint64_t)(unsigned)u | ((uint64_t)(unsigned)fb << 24) | ((uint64_t)lane << 48);
+          (uint64_t)(unsigned)fb | ((uint64_t)lane << 24) | ((uint64_t)(unsigned)Ln << 32);
       if (fb < 64 * GS_BMAP) atomicOr((unsigned long long*)&sStart[fb >> 6], 1ull << (fb & 63));
     }
   }
@@ -795,8 +794,8 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   sPub[lane] = pub;
   // sender node | jr << 24 | randomsub sender << 30 | graylisted << 31
   sSnd[lane] = valid ? (u | (jr << 24) | (rs_host(d, u) ? (1 << 30) : 0) | (gray ? (1 << 31) : 0)) : 0;
-  sLn[lane] = Ln;
-  sAddr[lane] = pOff >= 0 ? pOff : (int64_t)u * FC;
+  // (pushed segments are 8-aligned; N * FC < 2^31, gs_engine.hip)
+  sAddr[lane] = pOff >= 0 ? (uint32_t)(pOff >> 3) : (uint32_t)u * (uint32_t)FC;
   const uint64_t scoredT = __ballot(lane < T && scoring && d.tp[lane].scored);  // scored topics
   // ---- prefetch (phase A is LDS-bound at ~10 waves per CU, so registers are
   // free to hold loads in flight across pass 1): pass 3's 16-bit pending
@@ -937,18 +936,18 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   const uint16_t* const ibxPrv = prv ? d.ibx[1] : d.ibx[0];
   auto load_block = [&](int i, int kb) -> uint4 {
     if ((pushM >> i) & 1) {
-      if constexpr (EPBP == 8) return *(const uint4*)(ibxPrv + sAddr[i] + 8 * kb);  // 8-aligned segments
-      const uint2 p = *(const uint2*)(ibxPrv + sAddr[i] + 4 * kb);
+      if constexpr (EPBP == 8) return *(const uint4*)(ibxPrv + 8 * (size_t)sAddr[i] + 8 * kb);
+      const uint2 p = *(const uint2*)(ibxPrv + 8 * (size_t)sAddr[i] + 4 * kb);
       return make_uint4(p.x, p.y, 0u, 0u);
     }
-    return *(const uint4*)(flPrv + sAddr[i] + 4 * kb);
+    return *(const uint4*)(flPrv + (size_t)sAddr[i] + 4 * kb);
   };
   auto walk = [&](auto&& fn, bool count) {
     int qh = 0, qt = 0;  // queue head / tail (wave-uniform)
     int rankPrev = -1;   // rank (among non-empty senders) of the sender of the block before the window
     constexpr int PB = 8;
     for (int b0 = 0; b0 < totalBlk; b0 += 64 * PB) {
-      int si[PB], kb[PB];
+      int si[PB], kb[PB];  // kb: block index | the sender's copies << 16
       uint4 q[PB];
 #pragma unroll
       for (int rr = 0; rr < PB; ++rr) {
@@ -965,19 +964,22 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
           rankPrev += __popcll(mb);
           if (bidx < totalBlk) {
             const uint64_t ce = sComp[rank];
-            si[rr] = (int)(ce >> 48);
-            kb[rr] = bidx - (int)((ce >> 24) & 0xFFFFFF);
-            q[rr] = load_block(si[rr], kb[rr]);
+            si[rr] = (int)((ce >> 24) & 63);
+            const int k = bidx - (int)(ce & 0xFFFFFF);
+            kb[rr] = k | (int)((ce >> 32) << 16);
+            q[rr] = load_block(si[rr], k);
           }
         } else if (bidx < totalBlk) {
-          int lo = 0, hi = 63;  // last sender whose first block is <= bidx
+          int lo = 0, hi = nNE - 1;  // last non-empty sender whose first block is <= bidx
           while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
-            if (sBlk[mid] <= bidx) lo = mid; else hi = mid - 1;
+            if ((int)(sComp[mid] & 0xFFFFFF) <= bidx) lo = mid; else hi = mid - 1;
           }
-          si[rr] = lo;
-          kb[rr] = bidx - sBlk[lo];
-          q[rr] = load_block(lo, kb[rr]);
+          const uint64_t ce = sComp[lo];
+          si[rr] = (int)((ce >> 24) & 63);
+          const int k = bidx - (int)(ce & 0xFFFFFF);
+          kb[rr] = k | (int)((ce >> 32) << 16);
+          q[rr] = load_block(si[rr], k);
         }
       }
 #pragma unroll
@@ -996,7 +998,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
           const uint64_t rl = sRelay[i], pb = sPub[i];
           const bool pushed = (pushM >> i) & 1;
           const int epb = pushed ? EPBP : 4;
-          const int n = si[rr] < 0 ? 0 : min(epb, sLn[i] - epb * kb[rr]);
+          const int n = si[rr] < 0 ? 0 : min(epb, (kb[rr] >> 16) - epb * (kb[rr] & 0xFFFF));
           wide = n > 4;
 #pragma unroll
           for (int c = 4; c < EPBP; ++c) {
@@ -1133,19 +1135,20 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   // IWANT spammer gets hundreds from one sender)
   nSent += irN;
   if (!gray && ADV && ctlGated) nGatedCopies += nSrvRpc;  // the served replies' payload is ignored
-  __shared__ int sIrP[65], sIrO[64];  // exclusive prefix of the accepted senders' served ids, their arena offsets
-  int irTot;
-  {
-    const int myIr = (!gray && !(ADV && ctlGated)) ? irN : 0;
-    const int incl = wave_incl_sum(myIr);
-    irTot = wave_last(incl);
-    sIrP[lane] = incl - myIr;
-    if (lane == 0) sIrP[64] = irTot;
-    sIrO[lane] = irOff;
-  }
-  __syncthreads();
+  const int myIr = (!gray && !(ADV && ctlGated)) ? irN : 0;
+  const int irTot = wave_last(wave_incl_sum(myIr));
+  // exclusive prefix of the accepted senders' served ids and their arena
+  // offsets, in the walk queue's LDS (free outside a walk): written by each
+  // call, since the ADV path walks again in between
+  int* const sIrP = (int*)sQ;       // [64]
+  int* const sIrO = (int*)sQ + 64;  // [64]
   // fn(sender, slot) for every accepted served id
   auto eachIr = [&](auto&& fn) {
+    if (irTot == 0) return;
+    const int incl = wave_incl_sum(myIr);
+    sIrP[lane] = incl - myIr;
+    sIrO[lane] = irOff;
+    __syncthreads();
     for (int idx = lane; idx < irTot; idx += 64) {
       int lo = 0, hi = 63;  // last sender whose first item is <= idx
       while (lo < hi) {
@@ -1154,6 +1157,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
       }
       fn(lo, d.pool[prv][sIrO[lo] + idx - sIrP[lo]]);
     }
+    __syncthreads();  // the queue's LDS again
   };
   eachIr([&](int i, int slot) {
     if ((sv >> (int)__umulhi((unsigned)slot, d.stMagic)) & 1) deliver(i, slot, false);

@@ -1496,6 +1496,7 @@ __device__ __forceinline__ void hb_pair(const Dev& d, int v, int64_t base, int d
   const bool ihaveSpam = behaves(d, v, GS_BEHAVE_IHAVE_SPAM);
   const bool oppTick = ticks % d.OGT == 0;
   uint64_t jm = joined;
+  uint64_t myT = 0;  // the topics this half handled
   while (jm) {
     const unsigned long long c0 = GS_CLK();
     const int ta = __ffsll((long long)jm) - 1;
@@ -1643,7 +1644,8 @@ __device__ __forceinline__ void hb_pair(const Dev& d, int v, int64_t base, int d
     }
     const unsigned long long c1 = GS_CLK();
     // ---- 2. stats writes and emitGossip's live scores, in topic order
-    const int nm = act ? __shfl(nmT, tt) : 0;  // message ids of t in the gossip windows
+    const int nmA = lane_get(nmT, ta), nmB = tb >= 0 ? lane_get(nmT, tb) : 0;
+    const int nm = act ? (h ? nmB : nmA) : 0;  // message ids of t in the gossip windows
     const bool emits = nm > 0 && !noFwd && !ihaveSpam;
     const bool baseE = emits && vm && inTopic && !m && !dir;
     bool cand = false;
@@ -1670,12 +1672,12 @@ __device__ __forceinline__ void hb_pair(const Dev& d, int v, int64_t base, int d
       }
       if (h == hh) cand = baseE && Slive >= d.gossipThr;
       // the other half continues from this half's live-score state
-      const double sx = __shfl_xor(Slive, 32);
-      const bool dx = __shfl_xor((int)dirty, 32) != 0, ux = __shfl_xor((int)dirtyUp, 32) != 0;
+      const double sx = xor32_f64(Slive);
+      const uint32_t fx = xor32_u32((dirty ? 1u : 0u) | (dirtyUp ? 2u : 0u));
       if (h != hh) {
         Slive = sx;
-        dirty = dx;
-        dirtyUp = ux;
+        dirty = (fx & 1) != 0;
+        dirtyUp = (fx & 2) != 0;
       }
     }
     // ---- 3. IHAVE peer selection of both topics
@@ -1695,21 +1697,29 @@ __device__ __forceinline__ void hb_pair(const Dev& d, int v, int64_t base, int d
       }
       ih = sel ? bit : 0;
     }
-    // ---- merge the two halves' topic bits into both halves
-    const uint64_t clr = bit | (uint64_t)__shfl_xor((unsigned long long)bit, 32);
-    const uint64_t mb = m ? bit : 0, pb = pr ? bit : 0, gb = gr ? bit : 0;
-    const uint64_t mAll = mb | (uint64_t)__shfl_xor((unsigned long long)mb, 32);
-    const uint64_t pAll = pb | (uint64_t)__shfl_xor((unsigned long long)pb, 32);
-    meshl = (meshl & ~clr) | mAll;
-    boM |= pAll;
-    toprune |= pAll;
-    tograft |= gb | (uint64_t)__shfl_xor((unsigned long long)gb, 32);
-    ihave |= ih | (uint64_t)__shfl_xor((unsigned long long)ih, 32);
-    spamGraft |= (uint64_t)__shfl_xor((unsigned long long)spamGraft, 32);
+    // ---- this half's topic bits (a half reads and writes only its own
+    // topics' bits; the halves are merged once, after the loop)
+    myT |= bit;
+    meshl = (meshl & ~bit) | (m ? bit : 0ull);
+    if (pr) {
+      boM |= bit;
+      toprune |= bit;
+    }
+    if (gr) tograft |= bit;
+    ihave |= ih;
     cyMesh += c1 - c0;
     cyEmit += c2 - c1;
     cySel += GS_CLK() - c2;
   }
+  // merge: each half's topics from that half (the rest of meshl is unchanged
+  // in both)
+  const uint64_t otherT = xor32_u64(myT);
+  meshl = (meshl & ~otherT) | (xor32_u64(meshl) & otherT);
+  boM |= xor32_u64(boM) & otherT;
+  toprune |= xor32_u64(toprune);
+  tograft |= xor32_u64(tograft);
+  ihave |= xor32_u64(ihave);
+  spamGraft |= xor32_u64(spamGraft);
 }
 
 // ---------------------------------------------------------------- heartbeat
