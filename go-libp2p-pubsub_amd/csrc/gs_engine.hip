@@ -409,7 +409,7 @@ static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / 
 // T divides 64)
 template <int MODE>
 static void score_rows(const Dev& d, int64_t nEdges, int T, double* out, hipStream_t s) {
-  const unsigned g = nblk(nEdges, score_wave_edges(T));
+  const unsigned g = nblk(nEdges, GS_SCW);
   if (g == 0) return;
   if (64 % T == 0)
     k_score_rows<MODE, true><<<g, 64, 0, s>>>(d, out);

@@ -57,42 +57,51 @@ __device__ __forceinline__ int rp_pad(int pl) { return pl + (pl >> 6); }
 // Edges per wave of k_score_rows: lane = edge for the need test, and the
 // needy edges' T-topic rows fill the lanes in passes of 64 / T edges.
 __host__ __device__ __forceinline__ int score_wave_edges(int T) { return T * 64 <= GS_RP ? 64 : GS_RP / T; }
+// A wave tests GS_SCW consecutive edges (four per lane) and recomputes the
+// needy ones in chunks of score_wave_edges(T) (the LDS term table's edges):
+// at T = 64 a wave per 16 edges made 2M waves per launch for a test that
+// rarely finds work.
+#define GS_SCW 256
 template <int MODE, bool LANE_T>
 __global__ __launch_bounds__(64) void k_score_rows(Dev d, double* __restrict__ out) {
   __shared__ double sT[GS_RP + GS_RP / 64];  // [edge][topic], padded: conflict-free column reads
-  __shared__ int sList[64];
+  __shared__ uint16_t sList[GS_SCW];         // the needy edges (offsets from eb)
   const int lane = lane_id();
   const int T = d.T;
   const int sgw = score_wave_edges(T);
-  const int64_t e0 = d.e0 + (int64_t)blockIdx.x * sgw;
-  const int64_t e = e0 + lane;
-  const bool in = lane < sgw && e < d.e1;
-  double s0 = 0.0;
-  bool need = false;
-  if (in) {
-    if (MODE == 0) {
-      need = true;
-    } else {
-      s0 = d.score0[e];
-      need = MODE == 1 ? (d.sdirty[e] != 0 || !(s0 >= d.publishThr))
-             : MODE == 2 ? !(s0 >= 0.0)
-             : MODE == 4 ? (d.sdirty[e] != 0 || !(s0 >= 0.0))
-                         : d.sdirty[e] != 0;
-    }
-  }
-  if (!d.scoring) {
+  const int64_t eb = d.e0 + (int64_t)blockIdx.x * GS_SCW;
+  int nNeed = 0;
+#pragma unroll
+  for (int k = 0; k < GS_SCW / 64; ++k) {
+    const int64_t e = eb + 64 * k + lane;
+    const bool in = e < d.e1;
+    double s0 = 0.0;
+    bool need = false;
     if (in) {
-      if (MODE == 0) out[e] = 0.0;
-      if (MODE == 1) { d.score0[e] = 0.0; d.sdirty[e] = 0; }
-      if (MODE >= 2) d.score1[e] = 0.0;
+      if (MODE == 0) {
+        need = true;
+      } else {
+        s0 = d.score0[e];
+        need = MODE == 1 ? (d.sdirty[e] != 0 || !(s0 >= d.publishThr))
+               : MODE == 2 ? !(s0 >= 0.0)
+               : MODE == 4 ? (d.sdirty[e] != 0 || !(s0 >= 0.0))
+                           : d.sdirty[e] != 0;
+      }
     }
-    return;
+    if (!d.scoring) {
+      if (in) {
+        if (MODE == 0) out[e] = 0.0;
+        if (MODE == 1) { d.score0[e] = 0.0; d.sdirty[e] = 0; }
+        if (MODE >= 2) d.score1[e] = 0.0;
+      }
+      continue;
+    }
+    if (MODE >= 2 && in && !need) d.score1[e] = s0;
+    const unsigned long long m = __ballot(need);
+    if (need) sList[nNeed + __popcll(m & ((1ull << lane) - 1))] = (uint16_t)(64 * k + lane);
+    nNeed += __popcll(m);
   }
-  if (MODE >= 2 && in && !need) d.score1[e] = s0;
-  const unsigned long long m = __ballot(need);
-  if (!m) return;
-  const int nNeed = __popcll(m);
-  if (need) sList[__popcll(m & ((1ull << lane) - 1))] = lane;
+  if (!d.scoring || nNeed == 0) return;
   __syncthreads();
   // LANE_T (T divides 64): lane = (edge of the pass, topic); else one edge
   // per pass, lane = topic
@@ -102,31 +111,37 @@ __global__ __launch_bounds__(64) void k_score_rows(Dev d, double* __restrict__ o
   const bool lt = LANE_T || lane < T;
   const bool scoredL = lt && d.tp[tl].scored;
   const uint64_t scoredT = __ballot(lane < T && d.tp[lane < T ? lane : 0].scored);
-  const int P = (nNeed + G - 1) / G;
-  for (int p0 = 0; p0 < P; p0 += GS_SB) {
-    // GS_SB passes per batch: every load of the batch in flight at once
-    int js[GS_SB];
+  for (int c0 = 0; c0 < nNeed; c0 += sgw) {
+    const int nc = min(sgw, nNeed - c0);  // the chunk's edges: positions 0 .. nc - 1
+    const int P = (nc + G - 1) / G;
+    for (int p0 = 0; p0 < P; p0 += GS_SB) {
+      // GS_SB passes per batch: every load of the batch in flight at once
+      int js[GS_SB];
 #pragma unroll
-    for (int k = 0; k < GS_SB; ++k) {
-      const int q = (p0 + k) * G + gi;
-      js[k] = (lt && q < nNeed) ? sList[q] : -1;
+      for (int k = 0; k < GS_SB; ++k) {
+        const int q = (p0 + k) * G + gi;
+        js[k] = (lt && q < nc) ? q : -1;
+      }
+      TermIn x[GS_SB];
+#pragma unroll
+      for (int k = 0; k < GS_SB; ++k)
+        x[k] = term_load(d, (eb + sList[c0 + (js[k] < 0 ? 0 : js[k])]) * T + tl);
+#pragma unroll
+      for (int k = 0; k < GS_SB; ++k)
+        if (js[k] >= 0) sT[rp_pad(js[k] * T + tl)] = scoredL ? term_eval(d.tp[tl], x[k]) : 0.0;
     }
-    TermIn x[GS_SB];
-#pragma unroll
-    for (int k = 0; k < GS_SB; ++k) x[k] = term_load(d, (e0 + (js[k] < 0 ? sList[0] : js[k])) * T + tl);
-#pragma unroll
-    for (int k = 0; k < GS_SB; ++k)
-      if (js[k] >= 0) sT[rp_pad(js[k] * T + tl)] = scoredL ? term_eval(d.tp[tl], x[k]) : 0.0;
-  }
-  __syncthreads();
-  if (need) {
-    double score = 0.0;
-    for (int t = 0; t < T; ++t)
-      if ((scoredT >> t) & 1) score += sT[rp_pad(lane * T + t)];
-    score = has_record(d, e) ? score_tail(d, e, score) : 0.0;
-    if (MODE == 0) out[e] = score;
-    if (MODE == 1 || MODE == 3) { d.score0[e] = score; d.sdirty[e] = 0; }
-    if (MODE >= 2) d.score1[e] = score;
+    __syncthreads();
+    for (int j = lane; j < nc; j += 64) {
+      const int64_t e = eb + sList[c0 + j];
+      double score = 0.0;
+      for (int t = 0; t < T; ++t)
+        if ((scoredT >> t) & 1) score += sT[rp_pad(j * T + t)];
+      score = has_record(d, e) ? score_tail(d, e, score) : 0.0;
+      if (MODE == 0) out[e] = score;
+      if (MODE == 1 || MODE == 3) { d.score0[e] = score; d.sdirty[e] = 0; }
+      if (MODE >= 2) d.score1[e] = score;
+    }
+    __syncthreads();  // the term table is the next chunk's
   }
 }
 
