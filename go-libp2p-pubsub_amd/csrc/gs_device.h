@@ -308,6 +308,7 @@ struct Dev {
   int64_t poolBase0;   // rank * poolSeg
   int64_t poolSubCap;
   int32_t poolSub;
+  int32_t poolS0Mask;  // first sub-arena tried = block % poolSub & mask (0: sub-arena 0 first, tests)
   // message slots
   int32_t* slotSrc;
   int64_t* slotPubHop;
@@ -394,7 +395,7 @@ __device__ __forceinline__ void set_err(const Dev& d, int code);
 // requests skip it after one add), so skewed loads (high-degree or
 // IWANT-heavy nodes on one sub-arena) use the whole segment before E_POOL.
 __device__ __forceinline__ unsigned long long pool_take(const Dev& d, int cur, unsigned long long n) {
-  const int s0 = (int)(blockIdx.x % (unsigned)d.poolSub);
+  const int s0 = (int)(blockIdx.x % (unsigned)d.poolSub) & d.poolS0Mask;
   for (int k = 0; k < d.poolSub; ++k) {
     const int s = (s0 + k) & (d.poolSub - 1);  // poolSub is a power of two
     const unsigned long long o = atomicAdd(&d.poolCnt[((int64_t)cur * d.poolSub + s) * 16], n);

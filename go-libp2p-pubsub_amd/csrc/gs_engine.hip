@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <array>
 #include "../../include/gs_rpcsize.h"
 #include <map>
@@ -816,6 +817,14 @@ int gs_engine::start() {
     x.poolSub = sub;
     x.poolSubCap = poolSeg / sub;
     x.poolBase0 = (int64_t)rank * poolSeg;
+    x.poolS0Mask = -1;
+    // tests only: small sub-arenas, every node trying sub-arena 0 first, so
+    // allocations fill it and spill into the next ones (tests/test_parity_gpu.py)
+    if (const char* dbg = std::getenv("GS_DEBUG_POOL_SUB_CAP"))
+      if (world == 1) {
+        x.poolSubCap = std::min<int64_t>(x.poolSubCap, std::max<long long>(1, std::atoll(dbg)));
+        x.poolS0Mask = 0;
+      }
   }
   for (int k = 0; k < 2; ++k) { x.pool[k] = dalloc<int32_t>((size_t)poolSeg * world); chk(x.pool[k]); }
   x.poolCnt = dalloc<unsigned long long>((size_t)2 * x.poolSub * 16); chk(x.poolCnt);

@@ -648,8 +648,17 @@ template <bool ADV>
 using PhaseADev = std::conditional_t<ADV, const Dev*, Dev>;
 __device__ __forceinline__ const Dev& dev_of(const Dev& d) { return d; }
 __device__ __forceinline__ const Dev& dev_of(const Dev* d) { return *d; }
+// occupancy floor: 3 waves/SIMD (<= 168 VGPRs, GS_WPE_PA); the honest wide-
+// counter instantiation (config3: T = 1, St > 254) 4 (<= 128 VGPRs): it is not
+// LDS-bound (a few KB per wave) and ran 98.9 -> 82.7 ms per round at 4 waves
+#ifndef GS_WPE_PA_WIDE
+#define GS_WPE_PA_WIDE 4
+#endif
+template <bool NARROW, bool ADV>
+constexpr int pa_waves = (!NARROW && !ADV) ? GS_WPE_PA_WIDE : GS_WPE_PA;
 template <int WPL, bool NARROW, bool ADV>
-__global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, int64_t h, int cur, int head,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NARROW, ADV>))) void k_phase_a(
+    PhaseADev<ADV> dArg, int64_t h, int cur, int head,
                                                 WMask amR, WMask amW, WMask amP, int nR, int nY) {
   const Dev& d = dev_of(dArg);
   extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
@@ -657,6 +666,12 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
   const int nCntW = NARROW ? nCnt / 2 : nCnt;             // LDS words of the counter table
   uint32_t* scnt = smem32;  // [MD][T] copies | fresh << 16 (NARROW: u16 copies | fresh << 8)
   uint64_t* sD = (uint64_t*)(scnt + nCntW);               // [nR] delivered young slots (non-graylisted)
+  // scnt word of pair (sender i, topic t).  (Rotating each sender's row so
+  // that one topic's copies from different senders fall into different LDS
+  // banks measured slower at config4, 96.1 -> 100.3 ms per round: the address
+  // arithmetic in passes 2 and 3 cost more than the conflicts it removed.)
+  const int cT = d.T;
+  auto cword = [&](int i, int t) -> int { return NARROW ? (i * cT + t) >> 1 : i * cT + t; };
   uint64_t* sYm = sD + nR;                                // [nR] young-slot mask of each amR word
   uint16_t* sRk = (uint16_t*)(sYm + nR);                  // [W] rank of word w in amR, 0xFFFF = outside
   uint16_t* sYp = sRk + d.W;                              // [nR] young slots in the amR words before it
@@ -890,9 +905,9 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
       if (NARROW) {
         // no-return add: the host proved the 8-bit count cannot overflow
         const int pl = i * T + t;
-        atomicAdd(&scnt[pl >> 1], 1u << (16 * (pl & 1)));
+        atomicAdd(&scnt[cword(i, t)], 1u << (16 * (pl & 1)));
       } else {
-        atomicAdd(&scnt[i * T + t], 1u);
+        atomicAdd(&scnt[cword(i, t)], 1u);
       }
     }
     ++nCopies;
@@ -924,6 +939,8 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
       }
     }
     const int ix = sYp[rk] + __popcll(ym & ((1ull << (slot & 63)) - 1));
+    // (an atomic per copy: reading the word first to skip repeats measured
+    // slower, 96.0 -> 97.3 ms per round at config4)
     atomicOr((unsigned long long*)&sD[rk], 1ull << (slot & 63));
     // byte-wise min of the lowest deliverer (senders ascending)
     uint32_t* wp = (uint32_t*)(sFirst + (ix & ~3));
@@ -1107,9 +1124,9 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
     if (kind == GS_MSG_VALID) {
       if (NARROW) {
         const int pl = i * T + t;
-        atomicSub(&scnt[pl >> 1], 1u << (16 * (pl & 1)));
+        atomicSub(&scnt[cword(i, t)], 1u << (16 * (pl & 1)));
       } else {
-        atomicSub(&scnt[i * T + t], 1u);
+        atomicSub(&scnt[cword(i, t)], 1u);
       }
     }
     ++nThrottledCopies;
@@ -1394,9 +1411,10 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
       while (y) {
         const int b = __ffsll((long long)y) - 1;
         y &= y - 1;
-        const int pl = sFirst[fidx(rkw[j], b)] * T + t;
-        if (NARROW) atomicAdd(&scnt[pl >> 1], 1u << (16 * (pl & 1) + 8));
-        else atomicAdd(&scnt[pl], 1u << 16);
+        const int ff = sFirst[fidx(rkw[j], b)];
+        const int pl = ff * T + t;
+        if (NARROW) atomicAdd(&scnt[cword(ff, t)], 1u << (16 * (pl & 1) + 8));
+        else atomicAdd(&scnt[cword(ff, t)], 1u << 16);
       }
     }
   }
@@ -1501,7 +1519,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
           const int pl = 2 * wi + hh, tt = t + hh;
           const bool sc = (scoredT >> tt) & 1;
           uint32_t c = 0;
-          if (sc) c = NARROW ? ((scnt[wi] >> (16 * hh)) & 0xFFFF) : scnt[pl];
+          if (sc) c = NARROW ? ((scnt[cword(i, t)] >> (16 * hh)) & 0xFFFF) : scnt[cword(i, tt)];
           const int copies = NARROW ? (int)(c & 0xFF) : (int)(c & 0xFFFF);
           const int nf = NARROW ? (int)(c >> 8) : (int)(c >> 16);
           int credited = copies - nf;
@@ -1568,7 +1586,7 @@ __global__ __launch_bounds__(64) GS_OCC_PA void k_phase_a(PhaseADev<ADV> dArg, i
     const int q64 = 64 / T, r64 = 64 - q64 * T;
     int ic = lane / T, tc = lane - (lane / T) * T;  // (in-edge, topic) of the lane's next pair
     auto upd = [&](int pl, int i, int t, uint32_t q) -> uint32_t {
-      uint32_t c = ((scoredT >> t) & 1) ? scnt[NARROW ? pl >> 1 : pl] : 0u;
+      uint32_t c = ((scoredT >> t) & 1) ? scnt[cword(i, t)] : 0u;
       if (NARROW) c = (c >> (16 * (pl & 1))) & 0xFFFF;
       const int copies = NARROW ? (int)(c & 0xFF) : (int)(c & 0xFFFF);
       const int nf = NARROW ? (int)(c >> 8) : (int)(c >> 16);

@@ -54,3 +54,32 @@ def _retuned(lib):
 def test_gpu_set_topic_score_params_matches_oracle(oracle_path):
     bad = scenarios.compare(_retuned(oracle_path), _retuned(PRODUCT_LIB))
     assert bad == [], "\n".join(bad)
+
+
+def _scored_with_pool_cap(lib, cap, monkeypatch):
+    monkeypatch.setenv("GS_DEBUG_POOL_SUB_CAP", str(cap))
+    try:
+        e, hops = scenarios.SCENARIOS["gossipsub_scored"](lib)
+        e.step(hops)
+        return scenarios.snapshot(e, range(e.n_published))
+    finally:
+        monkeypatch.delenv("GS_DEBUG_POOL_SUB_CAP")
+
+
+def test_gpu_pool_sub_arena_spill(oracle_path, monkeypatch):
+    """pool_take (gs_device.h): when a node's sub-arena of the IWANT arena is
+    full the allocation spills into the next sub-arena before E_POOL (ADVICE
+    r4).  GS_DEBUG_POOL_SUB_CAP caps the 16 sub-arenas of an unpartitioned
+    engine and makes every node try sub-arena 0 first: at 256 ids each (4096
+    per hop; gossipsub_scored peaks at about 700 request and served ids per
+    hop) every busy hop fills sub-arena 0 and spills, and the run still equals
+    the oracle; at 4 ids each the hop's ids do not fit at all and the engine
+    reports the arena overflow."""
+    from pubsub_amd import GossipEngineError, _abi
+    ref = scenarios.run(oracle_path, "gossipsub_scored")
+    got = _scored_with_pool_cap(PRODUCT_LIB, 256, monkeypatch)
+    bad = scenarios.compare(ref, got)
+    assert bad == [], "\n".join(bad)
+    with pytest.raises(GossipEngineError) as ei:
+        _scored_with_pool_cap(PRODUCT_LIB, 4, monkeypatch)
+    assert ei.value.code == _abi.GS_ECAPACITY and "arena" in str(ei.value)
