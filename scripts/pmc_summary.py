@@ -36,7 +36,8 @@ def main():
         wv = [w[k][i] for i in sorted(w.get(k, {}))][-last:]
         fk = sum(x[0] for x in fv) / len(fv)
         wk = sum(x[0] for x in wv) / len(wv) if wv else 0.0
-        res[k] = {"dispatches": len(fv), "fetch_kib_raw": round(fk), "write_kib": round(wk),
+        res[k] = {"dispatches": len(fv), "dispatches_total": len(f[k]), "last_dispatch": max(f[k]),
+                  "fetch_kib_raw": round(fk), "write_kib": round(wk),
                   "read_bytes_est": int(2 * fk * 1024), "write_bytes": int(wk * 1024),
                   "traffic_bytes_est": int(2 * fk * 1024 + wk * 1024),
                   "ms_under_pmc": round(sum(x[1] for x in fv) / len(fv), 3)}
