@@ -1511,7 +1511,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
       uint32_t* const pw = (uint32_t*)(d.dltN + base * T);
       const int q128 = 128 / T, r128 = 128 - q128 * T;
       int ic = (2 * lane) / T, tc = 2 * lane - ((2 * lane) / T) * T;
+#ifndef GS_UPD2P
+#define GS_UPD2P 1  // timing A/B: -DGS_UPD2P=0 updates the two pairs of a word one after the other
+#endif
       auto upd2 = [&](int wi, int i, int t, uint32_t q) -> uint32_t {
+        if (GS_UPD2P && !hasUnc) {
+          // both pairs of the word at once, a byte per field: counts
+          // [copies | fresh << 8] and pending [fmd | mmd << 8] per 16-bit half;
+          // fmd += fresh, mmd += fresh + credited duplicates = copies while in
+          // the mesh (no uncredited copies without needAge / pmask)
+          const uint32_t sm = (((scoredT >> t) & 1) ? 0x0000FFFFu : 0u) | (((scoredT >> (t + 1)) & 1) ? 0xFFFF0000u : 0u);
+          const uint32_t c = scnt[cword(i, t)] & sm;
+          const uint64_t rl = sRelay[i] >> t;
+          const uint32_t mm = ((rl & 1) ? 0x0000FFFFu : 0u) | ((rl & 2) ? 0xFFFF0000u : 0u);
+          const uint32_t f = (q & 0x00FF00FFu) + ((c >> 8) & 0x00FF00FFu);
+          const uint32_t m = ((q >> 8) & 0x00FF00FFu) + (c & mm & 0x00FF00FFu);
+          if ((f | m) & 0xFF00FF00u) set_err(d, E_DELTA);
+          return f | (m << 8);
+        }
         uint32_t out = 0;
         bool over = false;
 #pragma unroll
