@@ -403,6 +403,11 @@ typedef struct gs_transport {
  * the transport is copied (it may be NULL then).  The oracle supports
  * world == 1 only. */
 int gs_set_partition(gs_engine* eng, int32_t rank, int32_t world, const gs_transport* tr);
+/* A partitioned rank holds the state of its owned nodes and of their edges
+ * [rowptr[node_begin], rowptr[node_end)) only: the per-edge readbacks
+ * (gs_read_mesh, gs_read_fanout, gs_read_scores, gs_read_behaviour_penalty,
+ * gs_read_backoff, gs_read_topic_stats, gs_read_rpc_bytes) fill the owned
+ * edges and zero the rest, so the ranks' arrays together are the whole graph's. */
 /* Nodes [node_begin, node_end) owned by this rank (after gs_set_graph). */
 int gs_partition_range(const gs_engine* eng, int32_t* node_begin, int32_t* node_end);
 /* Host time spent in the transport and bytes received from other ranks. */
