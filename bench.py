@@ -70,11 +70,13 @@ def hops_per_step(wl):
     return wl.get("hops", HOPS_PER_ROUND)
 
 
-def build_engine(wl, rounds, seed, device, lib=None, n=None, msgs_per_round=None, extra=()):
+def build_engine(wl, rounds, seed, device, lib=None, n=None, msgs_per_round=None, extra=(), graph=None):
+    """The workload's engine (graph, subscriptions, params, publish schedule);
+    `graph` reuses a graph this function built before with the same seed."""
     n = n or wl["n"]
     T = wl["topics"]
     msgs_per_round = msgs_per_round or wl.get("msgs", MSGS_PER_ROUND)
-    g = graphs.random_regular_fast(n, wl["k"], seed)
+    g = graph if graph is not None else graphs.random_regular_fast(n, wl["k"], seed)
     subs = graphs.all_subscribed(n, T)
     if wl.get("router") in ("floodsub", "randomsub"):
         # config2: the batch of each step published at its first hop
@@ -95,13 +97,6 @@ def build_engine(wl, rounds, seed, device, lib=None, n=None, msgs_per_round=None
         eng.schedule = (top, hops)
         eng.kinds, eng.srcs, eng.ipv4 = None, src, None
         return eng, g
-    if wl.get("subnets"):
-        # topic 0 + `subnets` distinct random topics of 1..T-1 per peer
-        srng = np.random.default_rng(seed + 13)
-        pick = np.argsort(srng.random((n, T - 1)), axis=1)[:, :wl["subnets"]] + 1
-        subs = np.ones(n, dtype=np.uint64)
-        for j in range(wl["subnets"]):
-            subs |= np.left_shift(np.uint64(1), pick[:, j].astype(np.uint64))
     opts = [WithPeerScore(eth2_peer_score_params(T), eth2_thresholds()), WithHop(100 * Millisecond),
             WithMessageWindow(wl["slots"]), WithSeed(seed)]
     if lib is None or "libgossip_engine" in os.path.basename(lib):
@@ -556,7 +551,6 @@ def main():
                    (f"gossipsub v1.1 + Eth2 scoring, {msgs_round} msgs/round, 10 hops/round" if gossip else
                     f"{wl['router']}{' size ' + str(wl['size']) if wl.get('size') else ''}, {msgs_round} msgs "
                     f"published at one hop per step, {hps} hops/step ({prop_hops} with copies on the wire)") +
-                   (f", each peer in topic 0 + {wl['subnets']} random subnets" if wl.get("subnets") else "") +
                    (", 20% Sybils (IWANT / GRAFT / phantom-IHAVE spam, invalid messages, 20 per IP), "
                     "peer gater, validation queue 32" if wl.get("adversarial") else ""),
                    "peers": wl["n"], "topics": wl["topics"], "degree": wl["k"],

@@ -2674,6 +2674,38 @@ int gs_read_topic_stats_edges(gs_engine* g, int64_t n, const int64_t* edges, dou
   return GS_OK;
 }
 
+int gs_read_backoff_edges(gs_engine* g, int64_t n, const int64_t* edges, int64_t* expire) {
+  if (n < 0 || (n > 0 && (!edges || !expire))) { gs_set_error("gs_read_backoff_edges: bad arguments"); return GS_EINVAL; }
+  for (int64_t i = 0; i < n; ++i)
+    if (edges[i] < 0 || edges[i] >= g->E) { gs_set_error("gs_read_backoff_edges: edge out of range"); return GS_EINVAL; }
+  const int64_t nk = n * g->T;
+  if (!g->started || nk == 0) {
+    std::fill(expire, expire + nk, 0);
+    return GS_OK;
+  }
+  int64_t* dE = nullptr;
+  int64_t* dOut = nullptr;
+  HIPCHECK(hipMalloc(&dE, (size_t)n * 8));
+  if (hipMalloc(&dOut, (size_t)nk * 8) != hipSuccess) {
+    (void)hipFree(dE);
+    gs_set_error("device allocation failed (gs_read_backoff_edges)");
+    return GS_ENOMEM;
+  }
+  hipError_t rc = hipMemcpyAsync(dE, edges, (size_t)n * 8, hipMemcpyHostToDevice, g->stream);
+  if (rc == hipSuccess) {
+    k_gather_backoff<<<nblk(nk, 256), 256, 0, g->stream>>>(g->d, dE, n, dOut);
+    rc = hipMemcpyAsync(expire, dOut, (size_t)nk * 8, hipMemcpyDeviceToHost, g->stream);
+  }
+  if (rc == hipSuccess) rc = hipStreamSynchronize(g->stream);
+  (void)hipFree(dE);
+  (void)hipFree(dOut);
+  if (rc != hipSuccess) {
+    gs_set_error(std::string("HIP error: ") + hipGetErrorString(rc) + " (gs_read_backoff_edges)");
+    return GS_EDEVICE;
+  }
+  return GS_OK;
+}
+
 int gs_read_deliveries(gs_engine* g, int64_t id, int32_t* hop, int32_t* from) {
   if (!g->record) { gs_set_error("GS_FLAG_RECORD_DELIVERIES not set"); return GS_ESTATE; }
   if (id < 0 || id >= (int64_t)g->mId.size()) { gs_set_error("unknown message id"); return GS_EINVAL; }

@@ -342,6 +342,16 @@ __global__ void k_gather_pairs(Dev d, const int64_t* __restrict__ edges, int64_t
   of[k] = d.flags[i];
 }
 
+// gs_read_backoff_edges: the backoff expiries of n chosen edges, out[i*T + t]
+// (0 = no entry; an edge outside this rank's range reads 0).
+__global__ void k_gather_backoff(Dev d, const int64_t* __restrict__ edges, int64_t n, int64_t* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n * d.T) return;
+  const int64_t e = edges[k / d.T];
+  const int t = (int)(k % d.T);
+  out[k] = (e < d.e0 || e >= d.e1) ? 0 : d.backoff[tix(d, t, e)];
+}
+
 // Folds the pending deliveries of topic t into fmd / mmd.
 __global__ void k_fold(Dev d, int t) {
   const int64_t e = d.e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -186,6 +186,7 @@ ABI_FUNCTIONS = [
      [P, C.POINTER(f64), C.POINTER(f64), C.POINTER(f64), C.POINTER(f64), C.POINTER(i64),
       C.POINTER(i64), C.POINTER(u8)]),
     ("gs_read_behaviour_penalty", C.c_int, [P, C.POINTER(f64)]),
+    ("gs_read_backoff_edges", C.c_int, [P, i64, C.POINTER(i64), C.POINTER(i64)]),
     ("gs_read_topic_stats_edges", C.c_int,
      [P, i64, C.POINTER(i64), C.POINTER(f64), C.POINTER(f64), C.POINTER(f64), C.POINTER(f64), C.POINTER(i64),
       C.POINTER(i64), C.POINTER(u8)]),

@@ -383,6 +383,14 @@ class Engine:
         return dict(fmd=fmd.reshape(sh), mmd=mmd.reshape(sh), mfp=mfp.reshape(sh), imd=imd.reshape(sh),
                     mesh_time=mt.reshape(sh), graft_time=gt.reshape(sh), flags=fl.reshape(sh))
 
+    def backoff_at(self, edges):
+        """backoff() of the given edges only, shape (len(edges), T) (gs_read_backoff_edges)."""
+        edges = np.ascontiguousarray(edges, dtype=np.int64)
+        out = np.empty(len(edges) * self.T, dtype=np.int64)
+        _check(self.lib, self.lib.gs_read_backoff_edges(self.h, len(edges), _ptr(edges, C.c_int64),
+                                                        _ptr(out, C.c_int64)))
+        return out.reshape(len(edges), self.T)
+
     def enough_peers(self, topic, suggested=0):
         """PubSubRouter.EnoughPeers(topic, suggested) of every host (bool [N])."""
         out = np.zeros(self.N, dtype=np.uint8)

@@ -458,6 +458,9 @@ int gs_read_behaviour_penalty(gs_engine* eng, double* bp /*[E]*/);
 int gs_read_topic_stats_edges(gs_engine* eng, int64_t n, const int64_t* edges, double* fmd,
                               double* mmd, double* mfp, double* imd, int64_t* mesh_time,
                               int64_t* graft_time, uint8_t* flags);
+/* Backoff expiries (ns, 0 = no entry) of n chosen edges, out[i*T + t]; the
+ * edge-list form of gs_read_backoff for full-size spot checks. */
+int gs_read_backoff_edges(gs_engine* eng, int64_t n, const int64_t* edges, int64_t* expire);
 /* Per node: hop of first delivery of message `id` (-1: never) and the node it
  * was first received from (-1: origin or never).  Valid while the message's
  * slot has not been recycled. */

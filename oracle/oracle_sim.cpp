@@ -177,7 +177,12 @@ struct Sim {
   std::vector<uint32_t> ipv4;
   std::vector<std::pair<uint32_t, uint32_t>> whitelist;
   std::vector<Node> nodes;
+  // gs_oracle_replay: one host simulated alone, its inbox taken from a trace
+  // (nodes stays empty; its events go to its own buffer)
+  Node* solo = nullptr;
+  std::vector<gs_trace_event>& evbuf(int node) { return !nodes.empty() ? nodes[node].ev : solo ? solo->ev : events; }
   bool graphSet = false, started = false;
+  bool mixedChecked = false;  // validateMixed() ran (it negotiates protoE once)
   int64_t hop = 0;
   // messages
   std::vector<Msg> msgs;           // by id
@@ -235,7 +240,13 @@ struct Sim {
     return topicVal[m.topic] ? k : GS_MSG_VALID;
   }
   void start();
+  void initNode(Node& nd, int u);  // start()'s per-host part: router state, AddPeer of every connection
   void step();
+  // the per-host bodies of step()'s phases (also run alone by gs_oracle_replay)
+  void nodeMemo(Node& nd, int64_t t);
+  void nodePhaseA(Node& nd, const std::map<int, std::vector<RPC>>& in);
+  void nodePhaseB(Node& nd, const std::map<int, std::vector<RPC>>& in);
+  void nodeRefOrder(Node& nd, const std::map<int, std::vector<RPC>>& in);
   void applyEvents(std::vector<std::map<int, std::vector<RPC>>>& inbox);
   // RecvRPC (pubsub.go:903) of every RPC in node u's inbox: before AcceptFrom,
   // so graylisted and gated RPCs are traced too
@@ -253,13 +264,13 @@ void Sim::emit(int type, int node, int peer, int topic, int64_t msg, int phase, 
   gs_trace_event e;
   e.hop = hop; e.msg = msg; e.type = type; e.node = node; e.peer = peer;
   e.topic = (int16_t)topic; e.phase = (uint8_t)phase; e.reason = (uint8_t)reason;
-  if (nodes.empty()) events.push_back(e); else nodes[node].ev.push_back(e);
+  evbuf(node).push_back(e);
 }
 
 void Sim::emitRpc(int type, int node, int peer, int phase, int64_t ord, const RPC* r,
                   const std::vector<std::pair<int, int>>& subs) {
   if (!traceRpc || traced.empty() || !traced[node]) return;
-  std::vector<gs_trace_event>& buf = nodes.empty() ? events : nodes[node].ev;
+  std::vector<gs_trace_event>& buf = evbuf(node);
   buf.push_back(gs_trace_event{hop, ord, type, node, peer, -1, (uint8_t)phase, 0});
   auto item = [&](int kind, int topic, int64_t msg) {
     buf.push_back(gs_trace_event{hop, msg, GS_TRACE_RPC_ITEM, node, peer, (int16_t)topic, (uint8_t)phase, (uint8_t)kind});
@@ -283,11 +294,11 @@ void Sim::emitRpc(int type, int node, int peer, int phase, int64_t ord, const RP
 
 void Sim::traceHello(int node, int from) {
   if (!traceRpc || traced.empty() || !traced[node]) return;
-  std::vector<std::pair<int, int>> subs;
-  const uint64_t m = nodes.empty() ? 0 : nodes[from].mySubs;
+  std::vector<std::pair<int, int>> items;
+  const uint64_t m = !nodes.empty() ? nodes[from].mySubs : this->subs.empty() ? 0 : this->subs[from];
   for (int t = 0; t < T; ++t)
-    if ((m >> t) & 1) subs.push_back({t, 1});
-  emitRpc(GS_TRACE_RECV_RPC, node, from, 0, GS_RPC_ORD(0, GS_RPC_O_HELLO), nullptr, subs);
+    if ((m >> t) & 1) items.push_back({t, 1});
+  emitRpc(GS_TRACE_RECV_RPC, node, from, 0, GS_RPC_ORD(0, GS_RPC_O_HELLO), nullptr, items);
 }
 
 gs_counters Sim::total() const {
@@ -1247,49 +1258,50 @@ int Sim::validateMixed() {
   return GS_OK;
 }
 
+void Sim::initNode(Node& nd, int u) {
+  nd.sim = this;
+  nd.id = u;
+  nd.mySubs = subs.empty() ? 0 : subs[u];
+  nd.mcache.init(gp.HistoryGossip, gp.HistoryLength);
+  nd.score.params = sp;
+  for (int t = 0; t < T; ++t)
+    if (tscored[t]) nd.score.topics[t] = tparams[t];
+  nd.score.appSpecificScore = [this](int p) { return appScore.empty() ? 0.0 : appScore[p]; };
+  nd.score.whitelist = whitelist;
+  nd.gtracer.followUpTime = gp.IWantFollowupTime;
+  nd.behave = behave.empty() ? 0 : behave[u];
+  nd.router = nodeRouter.empty() ? cfg.router
+              : nodeRouter[u] == GS_ROUTER_GOSSIPSUB_V10 ? GS_ROUTER_GOSSIPSUB : nodeRouter[u];
+  if (gaterOn) {
+    nd.gater.params = gaterParams;
+    nd.gater.getIP = [this](int p) { return ipv4.empty() ? 0u : ipv4[p]; };  // 0 = "<unknown>"
+  }
+  for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) {
+    int v = col[e];
+    nd.nbrs.push_back(v);
+    nd.proto[v] = protoE[e];
+    if (dormant.count({std::min(u, v), std::max(u, v)})) {  // gs_set_dormant: not connected yet
+      nd.dead.insert(v);
+      nd.outbound[v] = outboundE.empty() ? false : outboundE[e] != 0;
+      if (!directE.empty() && directE[e]) nd.direct.insert(v);
+      continue;
+    }
+    emit(GS_TRACE_ADD_PEER, u, v, -1, -1, 0, mixed ? protoE[e] : 0);  // AddPeer gossipsub.go:507, floodsub.go:45
+    nd.outbound[v] = outboundE.empty() ? false : outboundE[e] != 0;  // AddPeer gossipsub.go:505-532
+    if (!directE.empty() && directE[e]) nd.direct.insert(v);
+    std::vector<uint32_t> ips;
+    if (!ipv4.empty() && ipv4[v] != 0) ips.push_back(ipv4[v]);
+    if (nd.scored()) nd.score.AddPeer(v, ips);
+    if (nd.gatered()) nd.gater.AddPeer(v);  // tracer.AddPeer -> peerGater.AddPeer (peer_gater.go:366-372)
+    for (int t = 0; t < T; ++t)
+      if (!subs.empty() && ((subs[v] >> t) & 1)) nd.topics[t].insert(v);
+  }
+}
+
 void Sim::start() {
   nodes.assign(N, Node());
   if (record) deliv.assign(N, {});
-  for (int u = 0; u < N; ++u) {
-    Node& nd = nodes[u];
-    nd.sim = this;
-    nd.id = u;
-    nd.mySubs = subs.empty() ? 0 : subs[u];
-    nd.mcache.init(gp.HistoryGossip, gp.HistoryLength);
-    nd.score.params = sp;
-    for (int t = 0; t < T; ++t)
-      if (tscored[t]) nd.score.topics[t] = tparams[t];
-    nd.score.appSpecificScore = [this](int p) { return appScore.empty() ? 0.0 : appScore[p]; };
-    nd.score.whitelist = whitelist;
-    nd.gtracer.followUpTime = gp.IWantFollowupTime;
-    nd.behave = behave.empty() ? 0 : behave[u];
-    nd.router = nodeRouter.empty() ? cfg.router
-                : nodeRouter[u] == GS_ROUTER_GOSSIPSUB_V10 ? GS_ROUTER_GOSSIPSUB : nodeRouter[u];
-    if (gaterOn) {
-      nd.gater.params = gaterParams;
-      nd.gater.getIP = [this](int p) { return ipv4.empty() ? 0u : ipv4[p]; };  // 0 = "<unknown>"
-    }
-    for (int64_t e = rowptr[u]; e < rowptr[u + 1]; ++e) {
-      int v = col[e];
-      nd.nbrs.push_back(v);
-      nd.proto[v] = protoE[e];
-      if (dormant.count({std::min(u, v), std::max(u, v)})) {  // gs_set_dormant: not connected yet
-        nd.dead.insert(v);
-        nd.outbound[v] = outboundE.empty() ? false : outboundE[e] != 0;
-        if (!directE.empty() && directE[e]) nd.direct.insert(v);
-        continue;
-      }
-      emit(GS_TRACE_ADD_PEER, u, v, -1, -1, 0, mixed ? protoE[e] : 0);  // AddPeer gossipsub.go:507, floodsub.go:45
-      nd.outbound[v] = outboundE.empty() ? false : outboundE[e] != 0;  // AddPeer gossipsub.go:505-532
-      if (!directE.empty() && directE[e]) nd.direct.insert(v);
-      std::vector<uint32_t> ips;
-      if (!ipv4.empty() && ipv4[v] != 0) ips.push_back(ipv4[v]);
-      if (nd.scored()) nd.score.AddPeer(v, ips);
-      if (nd.gatered()) nd.gater.AddPeer(v);  // tracer.AddPeer -> peerGater.AddPeer (peer_gater.go:366-372)
-      for (int t = 0; t < T; ++t)
-        if (!subs.empty() && ((subs[v] >> t) & 1)) nd.topics[t].insert(v);
-    }
-  }
+  for (int u = 0; u < N; ++u) initNode(nodes[u], u);
   hasDirect = false;
   for (const Node& nd : nodes) hasDirect = hasDirect || (nd.isGossip() && !nd.direct.empty());
   hasDirect = hasDirect && cfg.router == GS_ROUTER_GOSSIPSUB;
@@ -1309,6 +1321,110 @@ void Sim::start() {
       }
   }
   started = true;
+}
+
+// S0 memo and the gater snapshot of one host at the start of hop t
+void Sim::nodeMemo(Node& nd, int64_t t) {
+  nd.memo.clear();
+  if (nd.scored())
+    for (int v : nd.nbrs) nd.memo[v] = nd.score.score(v);
+  if (nd.gatered()) {
+    PeerGater& g = nd.gater;
+    nd.gsnap.thr.clear();
+    nd.gsnap.active = !(g.lastThrottle == kTimeZero || t - g.lastThrottle > g.params.Quiet) &&
+                      g.throttle != 0 && !(g.validate != 0 && g.throttle / g.validate < g.params.Threshold);
+    if (nd.gsnap.active)
+      for (int v : nd.nbrs) {
+        const double th = g.acceptThreshold(v);
+        if (th >= 0) nd.gsnap.thr[v] = th;
+      }
+  }
+}
+
+// handleIncomingRPC per RPC, senders ascending, RPCs in send order
+void Sim::nodeRefOrder(Node& nd, const std::map<int, std::vector<RPC>>& in) {
+  nd.valUsed = 0;
+  traceRecv(nd.id, in);
+  for (auto& kv : in) {
+    const int s = kv.first;
+    std::vector<int64_t> got;  // accepted payload (the IWANT spammer re-requests it)
+    for (const RPC& r : kv.second) {
+      nd.ctr.transmissions += (int64_t)r.publish.size();
+      const int st = nd.acceptFrom(s, r.hasCtl ? 0xFFFFFFFFu : (uint32_t)r.publish[0]);
+      if (st == PeerGater::AcceptNone) { nd.ctr.graylisted++; continue; }  // pubsub.go:947-949
+      if (st == PeerGater::AcceptControl) {                                // pubsub.go:951-955
+        if (!r.publish.empty()) nd.ctr.gated++;
+        if (nd.scored()) nd.gtracer.ThrottlePeer(s);
+      } else {
+        for (int64_t mid : r.publish) nd.handleMessage(s, msgs[mid]);
+        got.insert(got.end(), r.publish.begin(), r.publish.end());
+      }
+      if (r.hasCtl && nd.isGossip()) nd.handleRPC(s, r);  // pubsub.go:969
+    }
+    if ((nd.behave & GS_BEHAVE_IWANT_SPAM) && !got.empty() && nd.isGossip() && nd.meshCap(s)) {
+      std::sort(got.begin(), got.end());
+      RPC r;
+      r.hasCtl = true;
+      r.ctl.iwant = got;
+      r.sp = 2; r.ord = GS_RPC_O_SPAM;
+      nd.sendRPC(s, std::move(r));
+    }
+  }
+}
+
+// phase A: payload messages, senders ascending; a sender's messages in
+// ascending id (their order only matters for the validation queue)
+void Sim::nodePhaseA(Node& nd, const std::map<int, std::vector<RPC>>& in) {
+  nd.acceptStatus.clear();
+  nd.valUsed = 0;
+  traceRecv(nd.id, in);
+  for (auto& kv : in) {
+    int s = kv.first;
+    bool anyCtl = false;
+    for (const RPC& r : kv.second) anyCtl |= r.hasCtl;
+    // one AcceptFrom per RPC; a sender's control RPCs of one hop share one draw
+    const int ctlSt = anyCtl ? nd.acceptFrom(s, 0xFFFFFFFFu) : PeerGater::AcceptAll;
+    nd.acceptStatus[s] = ctlSt;
+    for (const RPC& r : kv.second) nd.ctr.transmissions += (int64_t)r.publish.size();  // copies on the wire
+    bool throttledPeer = anyCtl && ctlSt == PeerGater::AcceptControl;
+    std::vector<int64_t> mids;
+    int64_t gray = 0;
+    for (const RPC& r : kv.second) {
+      const int st = r.hasCtl ? ctlSt : nd.acceptFrom(s, (uint32_t)r.publish[0]);
+      if (st == PeerGater::AcceptNone) { gray++; continue; }          // pubsub.go:947-949
+      if (st == PeerGater::AcceptControl) {                            // pubsub.go:951-955
+        throttledPeer = true;
+        if (!r.publish.empty()) nd.ctr.gated++;
+        continue;
+      }
+      mids.insert(mids.end(), r.publish.begin(), r.publish.end());
+    }
+    nd.ctr.graylisted += gray;
+    if (gray) continue;  // AcceptNone is per sender and hop (the S0 memo)
+    // tracer.ThrottlePeer -> gossipTracer.ThrottlePeer (gossip_tracer.go:163-181)
+    if (throttledPeer && nd.scored()) nd.gtracer.ThrottlePeer(s);
+    std::sort(mids.begin(), mids.end());
+    for (int64_t mid : mids) nd.handleMessage(s, msgs[mid]);
+    if ((nd.behave & GS_BEHAVE_IWANT_SPAM) && !mids.empty() && nd.isGossip() && nd.meshCap(s)) {
+      // re-request every message received from s (gossipsub_spam_test.go:113-128)
+      RPC r;
+      r.hasCtl = true;
+      r.ctl.iwant = mids;
+      r.sp = 2; r.ord = GS_RPC_O_SPAM;
+      nd.sendRPC(s, std::move(r));
+    }
+  }
+}
+
+// phase B: control, per RPC, senders ascending
+void Sim::nodePhaseB(Node& nd, const std::map<int, std::vector<RPC>>& in) {
+  if (!nd.isGossip()) return;  // FloodSubRouter / RandomSubRouter.HandleRPC: no-ops
+  for (auto& kv : in) {
+    int s = kv.first;
+    if (nd.acceptStatus[s] == PeerGater::AcceptNone) continue;
+    for (const RPC& r : kv.second)
+      if (r.hasCtl) nd.handleRPC(s, r);
+  }
 }
 
 void Sim::step() {
@@ -1337,23 +1453,7 @@ void Sim::step() {
   // S0 memo and the gater snapshot
   if (scoring || gaterOn) {
 #pragma omp parallel for schedule(dynamic, 64)
-    for (int u = 0; u < N; ++u) {
-      Node& nd = nodes[u];
-      nd.memo.clear();
-      if (nd.scored())
-        for (int v : nd.nbrs) nd.memo[v] = nd.score.score(v);
-      if (nd.gatered()) {
-        PeerGater& g = nd.gater;
-        nd.gsnap.thr.clear();
-        nd.gsnap.active = !(g.lastThrottle == kTimeZero || t - g.lastThrottle > g.params.Quiet) &&
-                          g.throttle != 0 && !(g.validate != 0 && g.throttle / g.validate < g.params.Threshold);
-        if (nd.gsnap.active)
-          for (int v : nd.nbrs) {
-            const double th = g.acceptThreshold(v);
-            if (th >= 0) nd.gsnap.thr[v] = th;
-          }
-      }
-    }
+    for (int u = 0; u < N; ++u) nodeMemo(nodes[u], t);
   }
   // local publishes of this hop
   while (nextPub < msgs.size() && msgHop[nextPub] == hop) {
@@ -1361,97 +1461,16 @@ void Sim::step() {
     nodes[m.from].localPublish(m);
     nextPub++;
   }
-  if (refOrder) {  // handleIncomingRPC per RPC, senders ascending, RPCs in send order
+  if (refOrder) {
 #pragma omp parallel for schedule(dynamic, 64)
-    for (int u = 0; u < N; ++u) {
-      Node& nd = nodes[u];
-      nd.valUsed = 0;
-      traceRecv(u, inbox[u]);
-      for (auto& kv : inbox[nd.id]) {
-        const int s = kv.first;
-        std::vector<int64_t> got;  // accepted payload (the IWANT spammer re-requests it)
-        for (const RPC& r : kv.second) {
-          nd.ctr.transmissions += (int64_t)r.publish.size();
-          const int st = nd.acceptFrom(s, r.hasCtl ? 0xFFFFFFFFu : (uint32_t)r.publish[0]);
-          if (st == PeerGater::AcceptNone) { nd.ctr.graylisted++; continue; }  // pubsub.go:947-949
-          if (st == PeerGater::AcceptControl) {                                // pubsub.go:951-955
-            if (!r.publish.empty()) nd.ctr.gated++;
-            if (nd.scored()) nd.gtracer.ThrottlePeer(s);
-          } else {
-            for (int64_t mid : r.publish) nd.handleMessage(s, msgs[mid]);
-            got.insert(got.end(), r.publish.begin(), r.publish.end());
-          }
-          if (r.hasCtl && nd.isGossip()) nd.handleRPC(s, r);  // pubsub.go:969
-        }
-        if ((nd.behave & GS_BEHAVE_IWANT_SPAM) && !got.empty() && nd.isGossip() && nd.meshCap(s)) {
-          std::sort(got.begin(), got.end());
-          RPC r;
-          r.hasCtl = true;
-          r.ctl.iwant = got;
-          r.sp = 2; r.ord = GS_RPC_O_SPAM;
-          nd.sendRPC(s, std::move(r));
-        }
-      }
-    }
-  }
-  // phase A: payload messages, senders ascending; a sender's messages in
-  // ascending id (their order only matters for the validation queue)
+    for (int u = 0; u < N; ++u) nodeRefOrder(nodes[u], inbox[u]);
+  } else {
 #pragma omp parallel for schedule(dynamic, 64)
-  for (int u = 0; u < (refOrder ? 0 : N); ++u) {
-    Node& nd = nodes[u];
-    nd.acceptStatus.clear();
-    nd.valUsed = 0;
-    traceRecv(u, inbox[u]);
-    for (auto& kv : inbox[nd.id]) {
-      int s = kv.first;
-      bool anyCtl = false;
-      for (const RPC& r : kv.second) anyCtl |= r.hasCtl;
-      // one AcceptFrom per RPC; a sender's control RPCs of one hop share one draw
-      const int ctlSt = anyCtl ? nd.acceptFrom(s, 0xFFFFFFFFu) : PeerGater::AcceptAll;
-      nd.acceptStatus[s] = ctlSt;
-      for (const RPC& r : kv.second) nd.ctr.transmissions += (int64_t)r.publish.size();  // copies on the wire
-      bool throttledPeer = anyCtl && ctlSt == PeerGater::AcceptControl;
-      std::vector<int64_t> mids;
-      int64_t gray = 0;
-      for (const RPC& r : kv.second) {
-        const int st = r.hasCtl ? ctlSt : nd.acceptFrom(s, (uint32_t)r.publish[0]);
-        if (st == PeerGater::AcceptNone) { gray++; continue; }          // pubsub.go:947-949
-        if (st == PeerGater::AcceptControl) {                            // pubsub.go:951-955
-          throttledPeer = true;
-          if (!r.publish.empty()) nd.ctr.gated++;
-          continue;
-        }
-        mids.insert(mids.end(), r.publish.begin(), r.publish.end());
-      }
-      nd.ctr.graylisted += gray;
-      if (gray) continue;  // AcceptNone is per sender and hop (the S0 memo)
-      // tracer.ThrottlePeer -> gossipTracer.ThrottlePeer (gossip_tracer.go:163-181)
-      if (throttledPeer && nd.scored()) nd.gtracer.ThrottlePeer(s);
-      std::sort(mids.begin(), mids.end());
-      for (int64_t mid : mids) nd.handleMessage(s, msgs[mid]);
-      if ((nd.behave & GS_BEHAVE_IWANT_SPAM) && !mids.empty() && nd.isGossip() && nd.meshCap(s)) {
-        // re-request every message received from s (gossipsub_spam_test.go:113-128)
-        RPC r;
-        r.hasCtl = true;
-        r.ctl.iwant = mids;
-        r.sp = 2; r.ord = GS_RPC_O_SPAM;
-        nd.sendRPC(s, std::move(r));
-      }
-    }
+    for (int u = 0; u < N; ++u) nodePhaseA(nodes[u], inbox[u]);
   }
-  // phase B: control, per RPC, senders ascending
   if (cfg.router == GS_ROUTER_GOSSIPSUB && !refOrder) {
 #pragma omp parallel for schedule(dynamic, 64)
-    for (int u = 0; u < N; ++u) {
-      Node& nd = nodes[u];
-      if (!nd.isGossip()) continue;  // FloodSubRouter / RandomSubRouter.HandleRPC: no-ops
-      for (auto& kv : inbox[nd.id]) {
-        int s = kv.first;
-        if (nd.acceptStatus[s] == PeerGater::AcceptNone) continue;
-        for (const RPC& r : kv.second)
-          if (r.hasCtl) nd.handleRPC(s, r);
-      }
-    }
+    for (int u = 0; u < N; ++u) nodePhaseB(nodes[u], inbox[u]);
   }
   if (refreshDue(t)) {
 #pragma omp parallel for schedule(dynamic, 64)
@@ -1474,6 +1493,124 @@ void Sim::step() {
   ctr.hops++;
   hop++;
 }
+
+
+// ---------------------------------------------------------------- replay
+// gs_oracle_replay_* (test infrastructure): one host of a simulation run on
+// its own, its inbox taken from the RecvRPC blocks of an event trace (the
+// reference's EventTracer view of everything a host receives, trace.go:241-
+// 383).  A host's state is a function of its inbox, its own publishes and the
+// static shared inputs (graph, subscriptions, peer attributes, the publish
+// schedule), so the replay runs exactly the per-host phase bodies Sim::step
+// runs for every host (nodeMemo, nodePhaseA, nodePhaseB, refreshScores,
+// heartbeat), hop by hop, and its events and final router / score state must
+// equal the full run's for that host.  The full-size GPU tests replay sampled
+// hosts of the 1M-peer runs from the engine's own trace this way.
+struct Replay {
+  Sim* sim = nullptr;
+  Node nd;
+  int64_t hop = 0;
+  std::vector<int64_t> myPubs;  // ids of the messages this host publishes, ascending
+  size_t nextPub = 0;
+  // hop -> sender -> (ordinal, RPC), sorted by ordinal before the hop runs
+  std::map<int64_t, std::map<int, std::vector<std::pair<int64_t, RPC>>>> inbox;
+  std::vector<gs_trace_event> pend;
+  size_t pendOut = 0;
+};
+
+static int replay_parse(Replay& r, const gs_trace_event* ev, int64_t n) {
+  Sim& s = *r.sim;
+  const int u = r.nd.id;
+  for (int64_t i = 0; i < n;) {
+    int64_t j = i + 1;
+    if (gs_trace_is_rpc(ev[i]))
+      while (j < n && ev[j].type == GS_TRACE_RPC_ITEM) ++j;
+    const gs_trace_event& hd = ev[i];
+    if (hd.type == GS_TRACE_RECV_RPC && hd.node == u) {
+      const int64_t sp = hd.msg >> 40, ord = hd.msg & (((int64_t)1 << 40) - 1);
+      if (hd.hop < r.hop) { set_error("gs_oracle_replay_run: an RPC for a hop already replayed"); return GS_EINVAL; }
+      if (!(sp == 0 && ord >= GS_RPC_O_ANNOUNCE)) {  // hellos / announcements: the static topic maps
+        RPC rpc;
+        rpc.sp = (int)sp;
+        rpc.ord = ord;
+        const int from = hd.peer;
+        for (int64_t k = i + 1; k < j; ++k) {
+          const gs_trace_event& x = ev[k];
+          switch (x.reason) {
+            case GS_RPC_ITEM_MSG: rpc.publish.push_back(x.msg); break;
+            case GS_RPC_ITEM_CTL: rpc.hasCtl = true; break;
+            case GS_RPC_ITEM_IHAVE:
+              if (rpc.ctl.ihave.empty() || rpc.ctl.ihave.back().topic != x.topic)
+                rpc.ctl.ihave.push_back(IHaveEntry{x.topic, {}});
+              rpc.ctl.ihave.back().mids.push_back(x.msg);
+              break;
+            case GS_RPC_ITEM_IWANT: rpc.ctl.iwant.push_back(x.msg); break;
+            case GS_RPC_ITEM_GRAFT: rpc.ctl.graft.push_back(x.topic); break;
+            case GS_RPC_ITEM_PRUNE: {  // makePrune (gossipsub.go:1803-1839): the sender's PruneBackoff
+              PruneEntry pe;
+              pe.topic = x.topic;
+              pe.hasBackoff = r.nd.pxCap(from);
+              pe.backoff = pe.hasBackoff ? (uint64_t)(s.gp.PruneBackoff / kSecond) : 0;
+              rpc.ctl.prune.push_back(pe);
+              break;
+            }
+            case GS_RPC_ITEM_PX:
+              for (auto it = rpc.ctl.prune.rbegin(); it != rpc.ctl.prune.rend(); ++it)
+                if (it->topic == x.topic) { it->px.push_back((int)x.msg); break; }
+              break;
+            default: break;
+          }
+        }
+        r.inbox[hd.hop][from].push_back({hd.msg, std::move(rpc)});
+      }
+    }
+    i = j;
+  }
+  return GS_OK;
+}
+
+static void replay_hop(Replay& r) {
+  Sim& s = *r.sim;
+  Node& nd = r.nd;
+  s.solo = &nd;
+  s.hop = r.hop;
+  const int64_t t = s.now();
+  nd.out.clear();  // sent last hop (their SendRPC events are recorded)
+  std::map<int, std::vector<RPC>> in;
+  auto ih = r.inbox.find(r.hop);
+  if (ih != r.inbox.end()) {
+    for (auto& kv : ih->second) {
+      auto& v = kv.second;
+      std::stable_sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+      auto& dst = in[kv.first];
+      for (auto& pr : v) dst.push_back(std::move(pr.second));
+    }
+    r.inbox.erase(ih);
+  }
+  if (r.hop == 0)
+    for (int tp = 0; tp < s.T; ++tp)
+      if ((nd.mySubs >> tp) & 1) {
+        s.emit(GS_TRACE_JOIN, nd.id, -1, tp, -1, 0);
+        nd.join(tp);
+      }
+  if (s.scoring || s.gaterOn) s.nodeMemo(nd, t);
+  while (r.nextPub < r.myPubs.size() && s.msgHop[(size_t)r.myPubs[r.nextPub]] <= r.hop) {
+    const int64_t id = r.myPubs[r.nextPub++];
+    if (s.msgHop[(size_t)id] == r.hop) nd.localPublish(s.msgs[(size_t)id]);
+  }
+  if (s.refOrder) {
+    s.nodeRefOrder(nd, in);
+  } else {
+    s.nodePhaseA(nd, in);
+    if (s.cfg.router == GS_ROUTER_GOSSIPSUB) s.nodePhaseB(nd, in);
+  }
+  if (s.refreshDue(t)) nd.score.refreshScores(t);
+  if (s.gaterDecayDue(t)) nd.gater.decayStats(t);
+  if (s.scoring && t > 0 && t % (60 * kSecond) == 0) nd.score.gc(t);
+  if (s.heartbeatDue(t) && nd.isGossip()) nd.heartbeat();
+  r.hop++;
+}
+
 
 }  // namespace oracle
 
@@ -1743,8 +1880,11 @@ int gs_step(gs_engine* eng, int64_t hops) {
   Sim& s = eng->sim;
   if (!s.graphSet) { set_error("graph not set"); return GS_ESTATE; }
   if (!s.started) {
-    const int rc = s.validateMixed();
-    if (rc) return rc;
+    if (!s.mixedChecked) {
+      const int rc = s.validateMixed();
+      if (rc) return rc;
+      s.mixedChecked = true;
+    }
     s.start();
   }
   for (int64_t i = 0; i < hops; ++i) s.step();
@@ -1866,6 +2006,24 @@ int gs_read_topic_stats_edges(gs_engine* eng, int64_t n, const int64_t* edges, d
   return GS_OK;
 }
 
+int gs_read_backoff_edges(gs_engine* eng, int64_t n, const int64_t* edges, int64_t* expire) {
+  Sim& s = eng->sim;
+  if (n < 0 || (n > 0 && (!edges || !expire))) { set_error("gs_read_backoff_edges: bad arguments"); return GS_EINVAL; }
+  for (int64_t i = 0; i < n; ++i)
+    if (edges[i] < 0 || edges[i] >= s.E) { set_error("gs_read_backoff_edges: edge out of range"); return GS_EINVAL; }
+  std::fill(expire, expire + n * s.T, 0);
+  if (!s.started) return GS_OK;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t e = edges[i];
+    const int u = (int)(std::upper_bound(s.rowptr.begin(), s.rowptr.end(), e) - s.rowptr.begin()) - 1;
+    for (auto& kv : s.nodes[u].backoff) {
+      auto be = kv.second.find(s.col[e]);
+      if (be != kv.second.end()) expire[i * s.T + kv.first] = be->second;
+    }
+  }
+  return GS_OK;
+}
+
 int gs_read_behaviour_penalty(gs_engine* eng, double* bp) {
   Sim& s = eng->sim;
   std::fill(bp, bp + s.E, 0.0);
@@ -1977,6 +2135,121 @@ int gs_trace_encode(const gs_trace_event*, int64_t, int32_t, int64_t, const char
   set_error("gs_trace_encode is in the product library");
   return GS_EUNSUPPORTED;
 }
+// ---- gs_oracle_replay: one host replayed from its RecvRPC trace (see Replay)
+int gs_oracle_replay_new(gs_engine* eng, int32_t node, void** out) {
+  Sim& s = eng->sim;
+  if (!out) { set_error("null argument"); return GS_EINVAL; }
+  if (!s.graphSet || s.started) { set_error("gs_oracle_replay_new: set the graph, and do not step the engine"); return GS_ESTATE; }
+  if (node < 0 || node >= s.N) { set_error("gs_oracle_replay_new: bad node"); return GS_EINVAL; }
+  if (!s.sched.empty() || s.doPX || !s.dormant.empty() || s.acct) {
+    set_error("gs_oracle_replay_new: churn, peer exchange, dormant slots and RPC accounting are not replayed");
+    return GS_EUNSUPPORTED;
+  }
+  for (uint8_t d : s.directE)
+    if (d) { set_error("gs_oracle_replay_new: direct peers are not replayed"); return GS_EUNSUPPORTED; }
+  if (!s.mixedChecked) {
+    const int rc = s.validateMixed();
+    if (rc) return rc;
+    s.mixedChecked = true;
+  }
+  if (s.traced.size() != (size_t)s.N) s.traced.assign((size_t)s.N, 0);
+  s.traced[(size_t)node] = 1;
+  s.traceRpc = true;
+  s.record = false;  // the replayed host's deliveries are its DeliverMessage events
+  std::unique_ptr<Replay> r(new Replay());
+  r->sim = &eng->sim;
+  s.solo = &r->nd;
+  s.hop = 0;
+  s.initNode(r->nd, node);
+  for (int64_t e = s.rowptr[node]; e < s.rowptr[node + 1]; ++e) s.traceHello(node, s.col[e]);
+  for (size_t k = 0; k < s.msgs.size(); ++k)
+    if (s.msgs[k].from == node) r->myPubs.push_back((int64_t)k);
+  *out = r.release();
+  return GS_OK;
+}
+
+int gs_oracle_replay_run(void* h, int64_t hops, const gs_trace_event* ev, int64_t n) {
+  Replay& r = *(Replay*)h;
+  if (hops < 0 || n < 0 || (n > 0 && !ev)) { set_error("gs_oracle_replay_run: bad arguments"); return GS_EINVAL; }
+  const int rc = replay_parse(r, ev, n);
+  if (rc) return rc;
+  for (int64_t i = 0; i < hops; ++i) replay_hop(r);
+  return GS_OK;
+}
+
+// The replayed host's events since the last call, in canonical order.
+int gs_oracle_replay_events(void* h, gs_trace_event* out, int64_t cap, int64_t* n) {
+  Replay& r = *(Replay*)h;
+  Sim& s = *r.sim;
+  if (r.pendOut == 0) {
+    r.pend.insert(r.pend.end(), r.nd.ev.begin(), r.nd.ev.end());
+    r.nd.ev.clear();
+    gs_trace_canonical(r.pend, s.cfg.seed, s.gp.MaxIHaveLength);
+  }
+  const int64_t k = std::min<int64_t>(cap, (int64_t)(r.pend.size() - r.pendOut));
+  for (int64_t i = 0; i < k; ++i) out[i] = r.pend[r.pendOut + (size_t)i];
+  r.pendOut += (size_t)k;
+  if (r.pendOut == r.pend.size()) { r.pend.clear(); r.pendOut = 0; }
+  *n = k;
+  return GS_OK;
+}
+
+// The replayed host's router and score state per out-edge (CSR order of its
+// row), per-topic arrays [edge * T + topic]; null pointers are skipped.
+// Backoff reads 0 where the reference's map has no entry.
+int gs_oracle_replay_state(void* h, uint64_t* mesh, uint64_t* fanout, int64_t* backoff, double* score, double* bp,
+                           double* fmd, double* mmd, double* mfp, double* imd, int64_t* mesh_time,
+                           int64_t* graft_time, uint8_t* flags) {
+  Replay& r = *(Replay*)h;
+  Sim& s = *r.sim;
+  Node& nd = r.nd;
+  const int T = s.T;
+  const int deg = (int)nd.nbrs.size();
+  for (int k = 0; k < deg; ++k) {
+    const int p = nd.nbrs[(size_t)k];
+    uint64_t m = 0, f = 0;
+    for (auto& kv : nd.mesh) if (kv.second.count(p)) m |= 1ull << kv.first;
+    for (auto& kv : nd.fanout) if (kv.second.count(p)) f |= 1ull << kv.first;
+    if (mesh) mesh[k] = m;
+    if (fanout) fanout[k] = f;
+    if (score) score[k] = nd.Score(p);
+    auto ps = nd.score.peerStats.find(p);
+    if (bp) bp[k] = ps == nd.score.peerStats.end() ? 0.0 : ps->second.behaviourPenalty;
+    for (int t = 0; t < T; ++t) {
+      const size_t i = (size_t)k * T + t;
+      if (backoff) {
+        auto bt = nd.backoff.find(t);
+        int64_t x = 0;
+        if (bt != nd.backoff.end()) {
+          auto be = bt->second.find(p);
+          if (be != bt->second.end()) x = be->second;
+        }
+        backoff[i] = x;
+      }
+      TopicStats ts;
+      if (ps != nd.score.peerStats.end()) {
+        auto it = ps->second.topics.find(t);
+        if (it != ps->second.topics.end()) ts = it->second;
+      }
+      if (fmd) fmd[i] = ts.firstMessageDeliveries;
+      if (mmd) mmd[i] = ts.meshMessageDeliveries;
+      if (mfp) mfp[i] = ts.meshFailurePenalty;
+      if (imd) imd[i] = ts.invalidMessageDeliveries;
+      if (mesh_time) mesh_time[i] = ts.meshTime;
+      if (graft_time) graft_time[i] = ts.graftTime;
+      if (flags) flags[i] = (uint8_t)((ts.inMesh ? 1 : 0) | (ts.meshMessageDeliveriesActive ? 2 : 0));
+    }
+  }
+  return GS_OK;
+}
+
+void gs_oracle_replay_free(void* h) {
+  Replay* r = (Replay*)h;
+  if (!r) return;
+  if (r->sim->solo == &r->nd) r->sim->solo = nullptr;
+  delete r;
+}
+
 // Oracle-only: OpenMP threads the per-node phases use (bench.py's cpu_baseline).
 int gs_oracle_threads(void) {
   int n = 1;

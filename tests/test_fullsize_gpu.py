@@ -26,6 +26,7 @@ if REPO not in sys.path:
     sys.path.insert(0, REPO)
 
 import bench  # noqa: E402
+from replay import HostReplay, compare_events, compare_state, engine_state  # noqa: E402
 from score_check import oracle_scores, sample_edges  # noqa: E402
 
 pytestmark = pytest.mark.gpu
@@ -77,6 +78,81 @@ def test_config4_full_size(olib):
     from pubsub_amd.params import GossipSubParams
     gp = GossipSubParams()
     assert gp.Dlo <= np.median(sizes) <= gp.Dhi, np.median(sizes)  # meshes maintained per (node, topic)
+
+
+def _replay_check(oracle_path, name, rounds, nhosts, seed=3):
+    """Sampled hosts of the full-size run replayed on the oracle (tests/replay.py):
+    the engine traces `nhosts` random hosts (plus hosts 0 and N-1) with RPC
+    events; after every round each host's RecvRPC blocks drive its oracle
+    replay (the per-host phase bodies of the oracle simulation), and the
+    replay's events -- every DeliverMessage with its first deliverer, every
+    DuplicateMessage, Graft / Prune / Join, every SendRPC with its forwarded
+    messages, IHAVE ids, IWANT lists, GRAFTs and PRUNEs -- must equal the
+    engine's, byte for byte.  At the end the hosts' mesh / fanout masks,
+    backoff expiries, fmd / mmd / mfp / imd, meshTime / graftTime / flags,
+    behaviour penalties and scores must equal the engine's bit for bit.  So
+    every state transition of the sampled hosts is checked, at the
+    benchmarked size, against the reference's restated router and score
+    code (gossipsub.go:591-1552, score.go:256-964, pubsub.go:902-1022)."""
+    from pubsub_amd import WithEventTracer
+    wl = bench.WORKLOADS[name]
+    rng = np.random.default_rng(17)
+    hosts = np.unique(np.concatenate([[0, wl["n"] - 1], rng.choice(wl["n"], nhosts, replace=False)]))
+    e, g = bench.build_engine(wl, rounds, seed, 0, extra=(WithEventTracer(hosts, capacity=1 << 25, rpc=True),))
+    # one never-stepped oracle engine with the run's exact inputs hosts every replay
+    oe, _ = bench.build_engine(wl, rounds, seed, 0, lib=oracle_path, graph=g)
+    reps = {int(u): HostReplay(oe, int(u)) for u in hosts}
+    chunks = [1 + H] + [H] * (rounds - 1) + [3 * H]
+    bad, checked = [], 0
+    for k in chunks:
+        e.step(k)
+        ev = e.trace_events()
+        order = np.argsort(ev["node"], kind="stable")
+        nodes_sorted = ev["node"][order]
+        for u in hosts:
+            lo, hi = np.searchsorted(nodes_sorted, [u, u + 1])
+            mine = ev[np.sort(order[lo:hi])]
+            r = reps[int(u)]
+            r.run(k, mine)
+            bad += compare_events(r.events(), mine, int(u))
+            checked += len(mine)
+        print(f"{name} replay: hop {e.hop}, {len(ev)} events, {checked} host events checked", flush=True)
+        assert not bad, "\n".join(bad[:12])
+    want = engine_state(e, hosts)
+    for u in hosts:
+        bad += compare_state(reps[int(u)].state(), want[int(u)], int(u))
+    assert not bad, "\n".join(bad[:12])
+    for r in reps.values():
+        r.close()
+    oe.close()
+    return e, checked
+
+
+def test_config4_replay_sampled_hosts(oracle_path):
+    """N1 at the headline size: config4 (1M peers x 64 topics, Eth2 scoring,
+    1000 msgs/round) for 16 rounds of publishes plus the drain -- joins, the
+    steady state with recycled slots and every heartbeat -- with 96 sampled
+    hosts replayed bit-exactly on the oracle from their own RPC streams."""
+    e, checked = _replay_check(oracle_path, "config4", 16, 96)
+    assert checked > 1e7, checked
+    c = e.counters()
+    assert c["deliveries"] == 16 * bench.MSGS_PER_ROUND * (e.N - 1), c
+
+
+def test_config3_replay_sampled_hosts(oracle_path):
+    """The same at config3 (1M peers, 1 topic) into the MaxIHaveLength cut
+    steady state: the sampled hosts' IHAVE subsets, IWANT cuts and promises."""
+    e, checked = _replay_check(oracle_path, "config3", 9, 48)
+    assert e.counters()["ihave_sent"] > 0 and checked > 1e6
+
+
+def test_config5_replay_sampled_hosts(oracle_path):
+    """The same at config5's adversarial mix (1M peers, 20% Sybils, gater,
+    validation queue): the sampled hosts' AcceptFrom / gater draws,
+    validation verdicts, P4 / P7 penalties and broken promises."""
+    e, checked = _replay_check(oracle_path, "config5", 7, 48)
+    c = e.counters()
+    assert c["promises_broken"] > 0 and c["gated"] > 0 and checked > 1e6, c
 
 
 def test_config3_full_size_with_ihave_cuts(olib):
