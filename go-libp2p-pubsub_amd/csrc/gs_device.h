@@ -80,7 +80,7 @@ enum {
 // device error codes (first one wins)
 enum {
   E_NONE = 0, E_POOL = 1, E_PROMISES = 2, E_PEERTX = 3, E_LATE = 4, E_TRUNCATE = 5, E_DOUBLE = 6,
-  E_FCAP = 7, E_DELTA = 8, E_TRACE = 9
+  E_FCAP = 7, E_DELTA = 8, E_TRACE = 9, E_STAMP = 10  // (E_STAMP: GS_STAMPS debug builds only)
 };
 
 struct TopicP {  // TopicScoreParams (score_params.go:98-148) + scored flag

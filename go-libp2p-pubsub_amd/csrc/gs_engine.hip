@@ -685,8 +685,11 @@ int gs_engine::start() {
     const int64_t budget = 8ll << 30;
     int64_t fc = std::min<int64_t>(S + 64, budget / (4 * (int64_t)N));
     x.FC = (int32_t)std::max<int64_t>(64, fc & ~3ll);
-    if ((int64_t)N * x.FC >= (1ll << 32)) {  // phase A addresses a list by a 32-bit entry offset
-      gs_set_error("too many peers for the frontier lists");
+    // the budget gives N * FC <= 2^31 entries, the bound phase A's 32-bit list
+    // offsets (sAddr, in entries) rely on; only the 64-entry floor can break
+    // it (N > 2^25)
+    if ((int64_t)N * x.FC > (1ll << 31)) {
+      gs_set_error("too many peers for the frontier lists (N * list capacity must stay <= 2^31)");
       return GS_EUNSUPPORTED;
     }
   }
@@ -824,6 +827,9 @@ int gs_engine::start() {
       if (world == 1) {
         x.poolSubCap = std::min<int64_t>(x.poolSubCap, std::max<long long>(1, std::atoll(dbg)));
         x.poolS0Mask = 0;
+        // never silent: it changes the arena's capacity and allocation order
+        std::fprintf(stderr, "gossip engine: GS_DEBUG_POOL_SUB_CAP=%s active (IWANT sub-arenas of %lld ids, "
+                     "sub-arena 0 first; a test-only setting)\n", dbg, (long long)x.poolSubCap);
       }
   }
   for (int k = 0; k < 2; ++k) { x.pool[k] = dalloc<int32_t>((size_t)poolSeg * world); chk(x.pool[k]); }
@@ -1670,6 +1676,9 @@ int gs_engine::deviceErrorCode(int32_t err) {
     case E_DOUBLE:
       gs_set_error("a peer sent the same message twice in one hop (outside the canonical model)");
       return GS_EUNSUPPORTED;
+    case E_STAMP:
+      gs_set_error("debug cycle stamp index outside its buffer (GS_STAMPS build)");
+      return GS_EDEVICE;
     default: gs_set_error("unknown device error"); return GS_EDEVICE;
   }
 }
@@ -1723,21 +1732,21 @@ int gs_engine::exchange(int cur, bool hb) {
   // whose copies overflowed its push region (record -1).  Otherwise every
   // cross-rank edge's copies travel as pushed segments (2b below) and the
   // lists stay home.
+  // With push and no IWANT spammers the lists travel only if some sender's
+  // push overflowed: that flag rides in the count readback below (one host
+  // round trip per hop), and the lists are packed after it when needed.
   bool shipLists = true;
-  if (xpush && d.cSpam[cur] == nullptr) {
-    int32_t ovf = 0;
+  const bool deferLists = xpush && d.cSpam[cur] == nullptr;
+  if (deferLists) {
+    xHost[world + 3 + 2 * world] = 0;
     HIPCHECK(hipMemcpyAsync(&xHost[world + 3 + 2 * world], d.pushOvf, 4, hipMemcpyDeviceToHost, stream));
-    HIPCHECK(hipStreamSynchronize(stream));
-    ovf = (int32_t)(xHost[world + 3 + 2 * world] & 0xFFFFFFFFu);
-    shipLists = ovf != 0;
   }
-  const size_t hdrB = shipLists ? hdrBytes : 0;
   auto packLists = [&]() {
     const int64_t capEnt = (int64_t)((xSendCap - hdrBytes) / 4);
     if (nOwn && shipLists)
       k_x_lists<<<nOwn, 64, 0, stream>>>(d, cur, bump, (int64_t*)xSend, (uint32_t*)(xSend + hdrBytes), capEnt);
   };
-  packLists();
+  if (!deferLists) packLists();
   HIPCHECK(hipMemcpyAsync(xHost, xCnt, (size_t)world * 8, hipMemcpyDeviceToHost, stream));
   HIPCHECK(hipMemcpyAsync(xHost + world, bump, 8, hipMemcpyDeviceToHost, stream));
   HIPCHECK(hipMemcpyAsync(xHost + world + 1, d.poolCnt + (size_t)cur * d.poolSub * 16, 8, hipMemcpyDeviceToHost,
@@ -1748,6 +1757,15 @@ int gs_engine::exchange(int cur, bool hb) {
   xHost[world + 2] = 0;
   HIPCHECK(hipMemcpyAsync(xHost + world + 2, d.err, 4, hipMemcpyDeviceToHost, stream));
   HIPCHECK(hipStreamSynchronize(stream));
+  if (deferLists) {
+    shipLists = (int32_t)(xHost[world + 3 + 2 * world] & 0xFFFFFFFFu) != 0;
+    if (shipLists) {  // (rare: a sender's copies overflowed its push region)
+      packLists();
+      HIPCHECK(hipMemcpyAsync(xHost + world, bump, 8, hipMemcpyDeviceToHost, stream));
+      HIPCHECK(hipStreamSynchronize(stream));
+    }
+  }
+  const size_t hdrB = shipLists ? hdrBytes : 0;
   const int32_t myErr = (int32_t)xHost[world + 2];
   const int64_t nEnt = (int64_t)xHost[world];
   const int64_t poolBase = (int64_t)rank * poolSeg;

@@ -240,20 +240,12 @@ __global__ __launch_bounds__(64) GS_OCC_RF void k_refresh_rows(Dev d, int64_t no
         x.im = v;
         x.fl = fl[k];
         x.mt = 0;
-#ifdef GS_EXP_FULLW
-        dlt_put_t<NDLT>(d, i, 0);
-        d.fmd[i] = x.fmd;
-        d.mmd[i] = x.mm;
-        d.mfp[i] = x.mfp;
-        if (d.anyImd) d.imd[i] = x.im;
-#else
         // unchanged counters (mostly zeros staying zero) are not written back
         if (q[k]) dlt_put_t<NDLT>(d, i, 0);
         if (x.fmd != fmd[k]) d.fmd[i] = x.fmd;
         if (x.mm != mmd[k]) d.mmd[i] = x.mm;
         if (x.mfp != mfp[k]) d.mfp[i] = x.mfp;
         if (d.anyImd && x.im != imd[k]) d.imd[i] = x.im;
-#endif
         if (x.fl & 1) {
           x.mt = now - gt[k];  // meshTime (score.go:518-520): mesh_time_of() from here on
           if (x.mt > tp.MmdActivation) {
@@ -577,20 +569,26 @@ __device__ __forceinline__ int wave_min_int(int x) {
 // Debug build only (-DGS_STAMPS): cycle stamps at pass boundaries of every
 // 1024th node, read with gs_debug_stamps.
 #ifdef GS_STAMPS
-#define GS_STAMP(k)                                                                            \
-  do {                                                                                         \
-    if ((blockIdx.x & 1023) == 0 && lane == 0) d.stamps[(blockIdx.x >> 10) * 8 + (k)] = clock64(); \
+// every stamp index is checked against the allocation ((N / 1024 + 1) * 24
+// words: phase A | phase B | heartbeat, 8 stamps per sampled node); an index
+// past it (never expected: k <= 7, blockIdx.x < N) flags E_STAMP, no write
+#define GS_STAMP_AT(region, k, val)                                                                \
+  do {                                                                                             \
+    if ((blockIdx.x & 1023) == 0 && lane == 0) {                                                   \
+      const int64_t _i = ((int64_t)d.N / 1024 + 1) * 8 * (region) + (blockIdx.x >> 10) * 8 + (k);  \
+      if ((k) >= 0 && (k) < 8 && _i < ((int64_t)d.N / 1024 + 1) * 24) d.stamps[_i] = (val);        \
+      else set_err(d, E_STAMP);                                                                    \
+    }                                                                                              \
   } while (0)
-#define GS_STAMPB(k)                                                                           \
-  do {                                                                                         \
-    if ((blockIdx.x & 1023) == 0 && lane == 0)                                                 \
-      d.stamps[((int64_t)d.N / 1024 + 1) * 8 + (blockIdx.x >> 10) * 8 + (k)] = clock64();      \
-  } while (0)
+#define GS_STAMP(k) GS_STAMP_AT(0, k, clock64())
+#define GS_STAMPB(k) GS_STAMP_AT(1, k, clock64())
 // heartbeat: stamp k = value v (a clock or an accumulated cycle count)
-#define GS_STAMPH(k, v)                                                                        \
-  do {                                                                                         \
-    if ((blockIdx.x & 1023) == 0 && lane == 0)                                                 \
-      d.stamps[((int64_t)d.N / 1024 + 1) * 16 + (blockIdx.x >> 10) * 8 + (k)] = (v);           \
+#define GS_STAMPH(k, v) GS_STAMP_AT(2, k, v)
+// a node wave that returns early leaves no stale stamps of an earlier hop
+// behind (round 5's negative phase-B intervals were such stale stamps)
+#define GS_STAMPB_CLEAR()                                  \
+  do {                                                     \
+    for (int _k = 0; _k < 8; ++_k) GS_STAMP_AT(1, _k, 0ull); \
   } while (0)
 #define GS_CLK() clock64()
 #else
@@ -603,6 +601,9 @@ __device__ __forceinline__ int wave_min_int(int x) {
   } while (0)
 #define GS_STAMPB(k) \
   do {               \
+  } while (0)
+#define GS_STAMPB_CLEAR() \
+  do {                    \
   } while (0)
 #endif
 
@@ -834,7 +835,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
   sPub[lane] = pub;
   // sender node | jr << 24 | randomsub sender << 30 | graylisted << 31
   sSnd[lane] = valid ? (u | (jr << 24) | (rs_host(d, u) ? (1 << 30) : 0) | (gray ? (1 << 31) : 0)) : 0;
-  // (pushed segments are 8-aligned; N * FC < 2^31, gs_engine.hip)
+  // (pushed segments are 8-aligned; N * FC <= 2^31 entries, checked in gs_engine.hip start)
   sAddr[lane] = pOff >= 0 ? (uint32_t)(pOff >> 3) : (uint32_t)u * (uint32_t)FC;
   const uint64_t scoredT = __ballot(lane < T && scoring && d.tp[lane].scored);  // scored topics
   // ---- prefetch (phase A is LDS-bound at ~10 waves per CU, so registers are
@@ -910,7 +911,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
       atomicAdd(&sPer[i], 1u);
       if (kind == GS_MSG_REJECT) atomicAdd(&sInv[i * T + t], 1u);
     }
-#ifndef GS_EXP_NOADD
     if (kind == GS_MSG_VALID) {
       if (NARROW) {
         // no-return add: the host proved the 8-bit count cannot overflow
@@ -921,7 +921,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
       }
     }
     ++nCopies;
-#endif
     const int rk = sRk[w];
     const uint64_t ym = rk == 0xFFFF ? 0ull : sYm[rk];
     const bool young = (ym >> (slot & 63)) & 1;
@@ -956,10 +955,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
     uint32_t* wp = (uint32_t*)(sFirst + (ix & ~3));
     const int sh = 8 * (ix & 3);
     uint32_t old = *wp;
-#ifdef GS_EXP_NOCAS
-    if ((int)((old >> sh) & 0xFF) > i) *wp = (old & ~(0xFFu << sh)) | ((uint32_t)i << sh);
-    if (0)
-#endif
     while ((int)((old >> sh) & 0xFF) > i) {
       const uint32_t nw = (old & ~(0xFFu << sh)) | ((uint32_t)i << sh);
       const uint32_t prev = atomicCAS(wp, old, nw);
@@ -1584,7 +1579,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
           }
         }
       };
-#ifndef GS_EXP_NOPASS3
       if (pf3) {
         // the words prefetched at wave start: one batch
 #pragma unroll
@@ -1607,7 +1601,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
       } else {
         rmw2(std::integral_constant<int, 1>{});
       }
-#endif
     } else {
     uint32_t* const pv = d.dlt + base * T;
     const int q64 = 64 / T, r64 = 64 - q64 * T;
@@ -1643,15 +1636,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
           const int pl = lane + 64 * (k0 + kk);
           const bool ok = pl < nP;
           const uint32_t nq = upd(ok ? pl : 0, ok ? iv[kk] : 0, ok ? tv[kk] : 0, q[kk]);
-#ifdef GS_EXP_SKIPW
-          if (ok && nq != q[kk]) pv[pl] = nq;
-#else
           *(ok ? pv + pl : scr) = nq;
-#endif
         }
       }
     };
-#ifndef GS_EXP_NOPASS3
     // a batch no larger than the node's pairs need: a batch slot past nP is a
     // scratch store (config3: 32 pairs, one slot)
     if (nP > 16 * 64) {
@@ -1663,7 +1651,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
     } else {
       rmw(std::integral_constant<int, 1>{});
     }
-#endif
     }
     GS_STAMP(5);
     if constexpr (ADV) {
@@ -1884,11 +1871,12 @@ __global__ void k_oldmask(Dev d, int64_t h) {
   if (s < d.S && (s & 63) == 0) d.oldm[s >> 6] = m;
 }
 
-// Clears the seen bits of recycled message slots (the slots published in
-// this hop held messages retired from the window).  One thread per
-// (node, word) of the words[] list.
-// (the seen bits themselves are cleared by k_push, after the publishes; this
-// kernel runs only for the adversarial model's per-slot state)
+// Clears the adversarial model's per-slot state of recycled message slots
+// (the slots published in this hop held messages retired from the window):
+// the IWANT spammers' drec.peers bits and peertx nibbles.  One thread per
+// (node, word) of the words[] list.  (The seen bits themselves are cleared by
+// phase A's pass 2b, the amP / Rw masks, and k_publish then sets the authors'
+// bits; this kernel runs only when spammers exist.)
 __global__ void k_retire(Dev d, int cur, const int32_t* __restrict__ words, int nwords) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= (int64_t)(d.n1 - d.n0) * nwords) return;

@@ -307,6 +307,7 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
   uint32_t* const sCand = (uint32_t*)(sH + 640); // step 3: items that held their sender's smallest key
   static_assert(640 + 64 * 64 / 32 <= 768, "step-3 arrays must fit in sH");
   const int lane = lane_id();
+  GS_STAMPB_CLEAR();
   const int prv = cur ^ 1;
   const int W = d.W;
   const int Wt = d.Wt;

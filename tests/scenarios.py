@@ -165,7 +165,7 @@ HEAVY = {
     # topics but fewer in any one, so from hop ~90 on phase B runs the honest
     # sender-cut instantiation (cutMode == 2: handleIHave's iasked cut,
     # gossipsub.go:625-667) with push active (T >= 4); 1536 slots per topic are
-    # recycled once (k_push's seen retirement, mcache.go:94-104)
+    # recycled once (phase A pass 2b's seen retirement, mcache.go:94-104)
     "cut_honest_4t": lambda lib, x=(): gossipsub_scored(lib, n=200, k=16, topics=4, window=1536, msgs=9000, hb=18,
                                                         seed=25, extra=x),
     # k_push's region overflow (more than GS_PUSHR = 2048 copies from one sender
