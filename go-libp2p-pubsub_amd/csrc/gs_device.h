@@ -186,6 +186,13 @@ struct Dev {
                    // (| in-edge index << 16) and own publishes (| 255 << 16), ascending
   int32_t* fln[2]; // [N] list lengths
   int32_t FC;      // list capacity per node (multiple of 4)
+  // floodsub on dense frontiers (k_flood_a; nullptr: the lists above): the
+  // messages a node first received or published in hop h as a W-word row, and
+  // per edge the copies the sender will not send the receiver next hop
+  uint64_t* fb[2]; // [N][W]
+  int32_t* fex[2]; // [E]
+  int32_t* fbN[2]; // [N] bits in the fb row (0: the row is all zero and is not read)
+  uint64_t* own;   // [N][W] the live messages the node authored
   uint32_t stMagic; // ceil(2^32 / St): topic of slot s = umulhi(s, stMagic) (s < 2^16)
   uint64_t tDivM;   // ceil(2^64 / T) (0 when T == 1): edge of pair p = umul64hi(p, tDivM)
   int32_t maxDeg;  // largest node degree (<= 64)

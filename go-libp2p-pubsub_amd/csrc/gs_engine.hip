@@ -105,6 +105,10 @@ struct gs_engine {
   // forwards a fraction of its sender's list: several topics.  With one topic
   // a forwarding edge carries the whole list and phase A reads the lists.
   bool pushOn = false;
+  // floodsub on dense frontiers (k_flood_a): a single-router floodsub engine
+  // with nothing that needs a per-copy record (trace, RPC accounting, churn,
+  // dormant slots, validators, attackers) on one rank
+  bool denseFlood = false;
   bool churnWindow = false;            // events scheduled before the first publish: wide window
   uint64_t* dSubA = nullptr;
   uint64_t* dSubOwn = nullptr;
@@ -481,6 +485,8 @@ int gs_engine::start() {
   }
   bool anyRandom = cfg.router == GS_ROUTER_RANDOMSUB;  // some host runs randomsub (d.sel)
   pushOn = T >= 4;
+  denseFlood = cfg.router == GS_ROUTER_FLOODSUB && !mixed && routerH.empty() && world == 1 && traceMask.empty() &&
+               !acctOn && events.empty() && dormant.empty() && topicVal == 0 && behaveAll == 0;
   if (!routerH.empty()) {
     anyRandom = false;
     for (uint8_t r : routerH) anyRandom = anyRandom || r == GS_ROUTER_RANDOMSUB;
@@ -696,7 +702,14 @@ int gs_engine::start() {
   for (int k = 0; k < 2; ++k) {
     x.fl[k] = dalloc<uint32_t>((size_t)N * x.FC); chk(x.fl[k]);
     x.fln[k] = dalloc<int32_t>(N); chk(x.fln[k]);
+    x.fb[k] = denseFlood ? dalloc<uint64_t>(NW) : nullptr;
+    x.fex[k] = denseFlood ? dalloc<int32_t>(E) : nullptr;
+    x.fbN[k] = denseFlood ? dalloc<int32_t>(N) : nullptr;
+    if (denseFlood) { chk(x.fb[k]); chk(x.fex[k]); chk(x.fbN[k]); }
   }
+  x.own = denseFlood ? dalloc<uint64_t>(NW) : nullptr;
+  if (denseFlood) chk(x.own);
+  if (!ok) { gs_set_error("device allocation failed (frontiers)"); return GS_ENOMEM; }
   // push arena: a region of GS_PUSHR slots (4 KiB) per owned sender and parity
   for (int k = 0; k < 2; ++k) {
     x.ibx[k] = nullptr;
@@ -1128,6 +1141,10 @@ static void launch_wpl(int W, F f) {
 // states and the P6 inputs, allocated on the first scheduled event.
 int gs_engine::enableChurn() {
   if (churnOn) return GS_OK;
+  if (denseFlood) {  // (its frontiers carry no per-copy lists to replay a lost connection from)
+    gs_set_error("floodsub connection churn must be scheduled before the first step");
+    return GS_EUNSUPPORTED;
+  }
   auto* al = dalloc<uint8_t>(E);
   auto* rs = scoring ? dalloc<uint8_t>(E) : nullptr;
   auto* rx = scoring ? dalloc<int64_t>(E) : nullptr;
@@ -1429,7 +1446,7 @@ int gs_engine::stepOne() {
       TIMED(this, GS_K_FANOUT, (k_fanout_pub<<<np, 64, 0, stream>>>(d, dPairs, np, h, now)));
     }
   }
-  if (eOwn) TIMED(this, GS_K_FWD, (k_fwd<<<eb, 256, 0, stream>>>(d, cur)));
+  if (eOwn && !denseFlood) TIMED(this, GS_K_FWD, (k_fwd<<<eb, 256, 0, stream>>>(d, cur)));
   if (n > 0) k_pubmask<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, cur);
   k_oldmask<<<nblk(S, 256), 256, 0, stream>>>(d, h);
   {
@@ -1465,7 +1482,9 @@ int gs_engine::stepOne() {
     TIMED(this, GS_K_PHASE_A, launch_wpl(W, [&](auto w) {
             if (!nOwn) return;
             constexpr int WV = decltype(w)::value;
-            if (adv) {
+            if (denseFlood) {
+              k_flood_a<WV><<<nOwn, 64, 0, stream>>>(d, h, cur, amR, amW, amP);
+            } else if (adv) {
               if (narrow)
                 k_phase_a<WV, true, true><<<nOwn, 64, lds, stream>>>(dDev, h, cur, head, amR, amW, amP, nR, nYp);
               else
@@ -1493,7 +1512,7 @@ int gs_engine::stepOne() {
   }
   if (n > 0) {
     TIMED(this, GS_K_PUBLISH, (k_publish<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, h, cur, head)));
-    k_publist<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, cur);
+    if (!denseFlood) k_publist<<<nblk(n, 256), 256, 0, stream>>>(d, (int)b, n, cur);
     if (d.sel) k_publish_rs<<<n, 64, 0, stream>>>(d, (int)b);
   }
   // the copies the owned senders send next hop, per edge (phase A reads them)

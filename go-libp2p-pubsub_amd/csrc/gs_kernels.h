@@ -1862,6 +1862,159 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
   }
 }
 
+// Floodsub on dense frontiers (FloodSubRouter.Publish floodsub.go:76-100 for
+// every host that forwarded in the previous hop; pushMsg pubsub.go:978-1022).
+// a frontier is a W-word bitmap fb[u] of the messages
+// u first received (or published) in the previous hop, which u sent to every
+// topic peer except ReceivedFrom and the author; receiver v ORs its senders'
+// bitmaps in ascending sender order, so the first sender holding a bit is its
+// first deliverer.  One wave per receiver, lane = word of v's topics in the
+// active window: every sender's row is one coalesced read, the algorithm's
+// (E_fwd + 3N) * W * 8 bytes per hop.  What a bitmap does not carry -- the
+// copies u did not send v -- is counted exactly all the same: v drops the
+// bits of its own messages (own[v], the author exclusion) itself, and u
+// counted in its previous hop, per in-edge, the fresh messages that sender
+// delivered first and did not author (fex[u's edge to v], ReceivedFrom), so
+// transmissions / duplicates are the reference's per-copy counts.  Used by a
+// floodsub engine without tracing, RPC accounting, churn, mixed routers or
+// partitioning (gs_engine.hip denseFlood); k_phase_a's list walk covers the
+// rest.
+template <int WPL>
+__global__ __launch_bounds__(64) void k_flood_a(Dev d, int64_t h, int cur, WMask amR, WMask amW, WMask amP) {
+  __shared__ int sNb[64];         // v's neighbours, ascending
+  __shared__ uint64_t sSubN[64];  // their subscriptions (what v's topic maps hold)
+  __shared__ int sAuth[64];       // they author a live message (nAuth > 0)
+  __shared__ int sEx[64];         // this hop's ReceivedFrom exclusions toward each neighbour
+  __shared__ int sLive[64];       // the senders whose frontier is not empty, ascending
+  const int v = d.n0 + blockIdx.x;
+  const int lane = lane_id();
+  const int prv = cur ^ 1;
+  const int W = d.W, Wt = d.Wt;
+  const int64_t base = d.rowptr[v];
+  const int deg = (int)(d.rowptr[v + 1] - base);
+  const uint64_t sv = d.sub[v];
+  const bool valid = lane < deg;
+  int ex = 0;  // copies sender `lane` did not send v (v had delivered them to it)
+  bool live = false;
+  if (valid) {
+    const int64_t e = base + lane;
+    const int u = d.col[e];
+    sNb[lane] = u;
+    sSubN[lane] = d.subA[u];
+    sAuth[lane] = d.nAuth[u] > 0;
+    ex = d.fex[prv][d.rev[e]];
+    live = d.fbN[prv][u] != 0;  // (an empty frontier's row is all zero and is not read)
+  }
+  sEx[lane] = 0;
+  const uint64_t lm = __ballot(live);
+  const int nLive = __popcll(lm);
+  if (live) sLive[__popcll(lm & ((1ull << lane) - 1))] = lane;
+  const int oldN = d.fbN[cur][v];  // this parity's row is all zero iff its count is
+  bool anyRet = false;
+#pragma unroll
+  for (int j = 0; j < GS_MAX_WPL; ++j) anyRet |= amP.m[j] != 0;
+  if (nLive == 0 && !anyRet) {
+    // nothing arrives and no slot is recycled: seen and counters stay; the
+    // frontier of the next hop is empty (k_publish may add own publishes)
+    if (oldN != 0) {
+      for (int w = lane; w < W; w += 64) d.fb[cur][(int64_t)v * W + w] = 0ull;
+      if (lane == 0) d.fbN[cur][v] = 0;
+    }
+    if (valid) d.fex[cur][base + lane] = 0;
+    return;
+  }
+  uint64_t acc[WPL], S[WPL], R[WPL], O[WPL];
+  bool act[WPL];
+#pragma unroll
+  for (int j = 0; j < WPL; ++j) {
+    const int w = lane + 64 * j;
+    // v handles the messages of its own topics only (pubsub.go:959)
+    act[j] = w < W && wm_has(amR, w) && ((sv >> (w / Wt)) & 1);
+    const bool ret = w < W && wm_has(amP, w);
+    S[j] = (act[j] || ret) ? d.seen[(int64_t)v * W + w] : 0ull;
+    O[j] = act[j] ? d.own[(int64_t)v * W + w] : 0ull;  // v's own messages: nobody sends them back
+    R[j] = ret ? d.pubmask[cur][w] : 0ull;
+    acc[j] = 0;
+  }
+  __syncthreads();
+  const uint64_t* const fbPrv = d.fb[prv];
+  int16_t* const ageRow = d.needAge ? d.age + (int64_t)v * d.S : nullptr;
+  uint8_t* const ffRow = d.record ? d.ffrom + (int64_t)v * d.S : nullptr;
+  long long sent = 0;
+  for (int k0 = 0; k0 < nLive; k0 += 4) {  // four live senders' rows in flight
+    uint64_t F[4][WPL], A[4][WPL];  // the senders' frontiers, and the messages they authored
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int uq = k0 + q < nLive ? sNb[sLive[k0 + q]] : -1;
+      const bool au = uq >= 0 && sAuth[sLive[k0 + q]] != 0;
+#pragma unroll
+      for (int j = 0; j < WPL; ++j) {
+        F[q][j] = (uq >= 0 && act[j]) ? fbPrv[(int64_t)uq * W + lane + 64 * j] : 0ull;
+        A[q][j] = (au && act[j]) ? d.own[(int64_t)uq * W + lane + 64 * j] : 0ull;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (k0 + q >= nLive) break;
+      const int i = sLive[k0 + q];  // senders ascending: the first holding a bit delivers it
+      const uint64_t subI = sSubN[i];
+      int cnt = 0;
+#pragma unroll
+      for (int j = 0; j < WPL; ++j) {
+        const uint64_t f = F[q][j];
+        sent += __popcll(f & ~O[j]);
+        const uint64_t nb = f & ~acc[j] & ~S[j];  // first deliveries by sender i
+        acc[j] |= f;
+        if (!nb) continue;
+        const int w = lane + 64 * j;
+        if ((subI >> (w / Wt)) & 1) {
+          // v will not send them back to i (ReceivedFrom); those i authored
+          // are i's own messages, which i drops itself (O above)
+          cnt += __popcll(nb & ~A[q][j]);
+        }
+        if (ageRow || ffRow)
+          for (uint64_t y = nb; y; y &= y - 1) {
+            const int slot = w * 64 + __ffsll((long long)y) - 1;
+            if (ageRow) ageRow[slot] = (int16_t)(h - d.slotPubHop[slot]);
+            if (ffRow) ffRow[slot] = (uint8_t)i;
+          }
+      }
+      if (cnt) atomicAdd(&sEx[i], cnt);
+    }
+  }
+  // fresh messages: seen (recycled slots' old bits cleared, k_publish sets the
+  // author's), the frontier of the next hop (k_publish adds own publishes)
+  long long nDeliv = 0;
+#pragma unroll
+  for (int j = 0; j < WPL; ++j) {
+    const int w = lane + 64 * j;
+    if (w >= W) continue;
+    const uint64_t fr = acc[j] & ~S[j];
+    if (fr) {
+      nDeliv += __popcll(fr);
+      if ((fr & d.oldm[w]) || !wm_has(amW, w)) set_err(d, E_LATE);
+    }
+    if (fr | R[j]) d.seen[(int64_t)v * W + w] = (S[j] & ~R[j]) | fr;
+  }
+  const long long deliv = (long long)wave_sum_ll(nDeliv);
+  if (deliv != 0 || oldN != 0) {  // (a row whose count is 0 stays all zero)
+#pragma unroll
+    for (int j = 0; j < WPL; ++j) {
+      const int w = lane + 64 * j;
+      if (w < W) d.fb[cur][(int64_t)v * W + w] = acc[j] & ~S[j];
+    }
+  }
+  __syncthreads();
+  if (lane == 0) d.fbN[cur][v] = (int)deliv;
+  if (valid) d.fex[cur][base + lane] = sEx[lane];
+  const long long copies = (long long)wave_sum_ll(sent) - (long long)wave_sum_ll(ex);
+  if (lane == 0) {
+    if (deliv) ctr_add(d, C_DELIVERIES, (unsigned long long)deliv);
+    if (copies) ctr_add(d, C_TRANSMISSIONS, (unsigned long long)copies);
+    if (copies - deliv) ctr_add(d, C_DUPLICATES, (unsigned long long)(copies - deliv));
+  }
+}
+
 // Slots whose message was published more than maxAge hops ago: a first
 // delivery of one of them in hop h is outside the engine's window (E_LATE).
 __global__ void k_oldmask(Dev d, int64_t h) {
@@ -1919,7 +2072,11 @@ __global__ void k_publish(Dev d, int b, int n, int64_t h, int cur, int head) {
   const int src = d.mSrc[b + i];
   const int prevAuthor = d.slotSrc[slot];  // the retired message of this slot
   // slot metadata is replicated on every rank; the rest belongs to src's rank
-  if (prevAuthor >= d.n0 && prevAuthor < d.n1) atomicSub(&d.nAuth[prevAuthor], 1);
+  if (prevAuthor >= d.n0 && prevAuthor < d.n1) {
+    atomicSub(&d.nAuth[prevAuthor], 1);
+    if (d.own != nullptr)  // k_flood_a's author exclusion: the retired message is no longer prevAuthor's
+      atomicAnd((unsigned long long*)&d.own[(int64_t)prevAuthor * d.W + (slot >> 6)], ~(1ull << (slot & 63)));
+  }
   d.slotSrc[slot] = src;
   d.slotPubHop[slot] = h;
   d.slotMid[slot] = d.mId[b + i];
@@ -1946,6 +2103,11 @@ __global__ void k_publish(Dev d, int b, int n, int64_t h, int cur, int head) {
   const unsigned long long bit = 1ull << (slot & 63);
   atomicOr((unsigned long long*)&d.seen[(int64_t)src * d.W + w], bit);
   if (gossip_host(d, src)) atomicOr((unsigned long long*)&d.hist[((int64_t)head * d.nOwnH + (src - d.n0)) * d.W + w], bit);
+  if (d.fb[0] != nullptr) {  // k_flood_a: the frontier of the next hop, and the author's own messages
+    atomicOr((unsigned long long*)&d.fb[cur][(int64_t)src * d.W + w], bit);
+    atomicAdd(&d.fbN[cur][src], 1);
+    atomicOr((unsigned long long*)&d.own[(int64_t)src * d.W + w], bit);
+  }
   if (d.needAge) d.age[(int64_t)src * d.S + slot] = 0;
   if (d.record) d.ffrom[(int64_t)src * d.S + slot] = 255;
   ctr_add(d, C_PUBLISHED, 1ull);

@@ -33,6 +33,23 @@ def floodsub_dense(lib, seed=1, extra=()):
     return e, int(hops[-1]) + 20
 
 
+def floodsub_multitopic(lib, n=300, k=12, topics=3, seed=4, msgs=240, extra=()):
+    """floodsub.go:76-100 with several topics and partial subscriptions: hosts
+    forward only their own topics' messages, to the peers subscribed to them,
+    and publish to topics they may not be subscribed to (floodsub's Publish
+    needs no subscription).  A dense-frontier engine (k_flood_a) on one GPU."""
+    g = graphs.random_regular(n, k, seed)
+    rng = np.random.default_rng(seed)
+    subs = np.zeros(n, dtype=np.uint64)
+    for t in range(topics):
+        subs |= (rng.random(n) < 0.6).astype(np.uint64) << np.uint64(t)
+    e = NewFloodSub(n, topics, g, subs, WithRecordDeliveries(), WithSeed(seed), WithMessageWindow(128), *extra,
+                    lib=lib)
+    src, top, hops = _publish_schedule(n, topics, msgs, 1, 1, seed + 1)
+    e.publish(src, top, hops)
+    return e, int(hops[-1]) + 20
+
+
 def randomsub(lib, size, n=200, k=16, seed=2, msgs=60, extra=()):
     g = graphs.random_regular(n, k, seed)
     e = NewRandomSub(n, 1, g, graphs.all_subscribed(n, 1), size, WithRecordDeliveries(), WithSeed(seed),
@@ -126,6 +143,7 @@ def gossipsub_scored(lib, n=300, k=20, topics=1, seed=3, msgs=300, hb=12, flood=
 
 SCENARIOS = {
     "floodsub_dense": lambda lib, x=(): floodsub_dense(lib, extra=x),
+    "floodsub_multitopic": lambda lib, x=(): floodsub_multitopic(lib, extra=x),
     "randomsub_100": lambda lib, x=(): randomsub(lib, 100, extra=x),
     "randomsub_N": lambda lib, x=(): randomsub(lib, 200, extra=x),
     "gossipsub_dense": lambda lib, x=(): gossipsub_dense(lib, extra=x),
