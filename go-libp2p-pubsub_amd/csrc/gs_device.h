@@ -243,6 +243,13 @@ struct Dev {
   uint32_t* ptxT;    // [N][2^ptxBits] (owned rows only: shifted by n0 rows)
   int32_t ptxBits;
   int32_t* ptxN;     // [N] entries in the table
+  // the rank's overflow table: a node whose table is full takes further keys
+  // here (mcache.peertx is an unbounded map, mcache.go:66-80), 2^ptxOBits
+  // 64-bit entries (node + 1) << 32 | peertx entry, linear probing
+  unsigned long long* ptxO;
+  int32_t ptxOBits;
+  unsigned int* ptxOCnt;           // [0] live entries, [1] kept by the heartbeat's rebuild, [2] staged
+  unsigned long long* ptxOStage;   // [2^ptxOBits] the rebuild's survivors
   // per-edge state
   uint64_t* mesh;
   uint64_t* fanout;

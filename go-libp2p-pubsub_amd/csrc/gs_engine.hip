@@ -197,6 +197,7 @@ struct gs_engine {
   // RPC events (gs_set_trace_rpc): RECV blocks of hops not run yet, and the
   // connections closed at the start of a hop (their in-flight RPCs are lost)
   bool traceRpc = false;
+  int ptxHomeBits = -1, ptxOvfBits = -1;  // gs_set_peertx_capacity (-1: defaults)
   // peer exchange (GS_FLAG_PEER_EXCHANGE) and connections down at the start
   bool doPX = false;
   std::set<std::pair<int, int>> dormant;       // gs_set_dormant (a < b)
@@ -533,10 +534,6 @@ int gs_engine::start() {
   e0 = rowptr[n0];
   e1 = rowptr[n1];
   eOwn = e1 - e0;
-  if (world > 1 && anyRandom) {
-    gs_set_error("a partitioned engine supports floodsub and gossipsub (randomsub target masks are not exchanged)");
-    return GS_EUNSUPPORTED;
-  }
   // connections down at the start (gs_set_dormant): no score record, no IP
   std::vector<uint8_t> downH;
   if (!dormant.empty()) {
@@ -768,10 +765,16 @@ int gs_engine::start() {
   // queues come back through gossip; config5 at 1M peers: 43 live entries per
   // node on average, 881 at most), so those runs get 4096; the spammers' own
   // requests, one per (message, spammer), are counted in spamCnt
-  x.ptxBits = (behaveAll & GS_BEHAVE_IWANT_SPAM) ? 12 : GS_PTX_BITS;
+  // A node whose table fills takes further keys in the rank's overflow table.
+  const bool spamRun = (behaveAll & GS_BEHAVE_IWANT_SPAM) != 0;
+  x.ptxBits = ptxHomeBits >= 0 ? ptxHomeBits : (spamRun ? 12 : GS_PTX_BITS);
+  x.ptxOBits = ptxOvfBits >= 0 ? ptxOvfBits : (spamRun ? 20 : 16);
   x.ptxT = dalloc<uint32_t>((size_t)nOwnN << x.ptxBits); x.ptxN = dalloc<int32_t>(nOwnN);
+  x.ptxO = dalloc<unsigned long long>((size_t)1 << x.ptxOBits);
+  x.ptxOStage = dalloc<unsigned long long>((size_t)1 << x.ptxOBits);
+  x.ptxOCnt = dalloc<unsigned int>(4);
   chk(x.promMid); chk(x.promExp); chk(x.promSlot); chk(x.promEdge); chk(x.promN);
-  chk(x.ptxT); chk(x.ptxN);
+  chk(x.ptxT); chk(x.ptxN); chk(x.ptxO); chk(x.ptxOStage); chk(x.ptxOCnt);
   if (!ok) { gs_set_error("device allocation failed (promises / peertx)"); return GS_ENOMEM; }
   x.promMid -= (size_t)n0 * x.promCap; x.promExp -= (size_t)n0 * x.promCap;
   x.promSlot -= (size_t)n0 * x.promCap; x.promEdge -= (size_t)n0 * x.promCap; x.promN -= n0;
@@ -1616,7 +1619,13 @@ int gs_engine::stepOne() {
       TIMED(this, GS_K_HEARTBEAT,
             (k_heartbeat<false><<<nOwn, 64, 0, stream>>>(d, h, now, ticks, cur, head, newhead, allExact)));
     // the peertx counters of the window that left the cache (pre-shift HL - 1)
-    if (nOwn && gossip) k_ptx_rebuild<<<nOwn, 64, (size_t)4 << d.ptxBits, stream>>>(d, (head + d.HL - 1) % R);
+    if (nOwn && gossip) {
+      k_ptx_rebuild<<<nOwn, 64, (size_t)4 << d.ptxBits, stream>>>(d, (head + d.HL - 1) % R);
+      const int64_t nO = (int64_t)1 << d.ptxOBits;  // (a table without entries returns at once)
+      k_ptxo_collect<<<nblk(nO, 256), 256, 0, stream>>>(d, (head + d.HL - 1) % R);
+      k_ptxo_reinsert<<<nblk(nO, 256), 256, 0, stream>>>(d);
+      k_ptxo_fin<<<1, 1, 0, stream>>>(d);
+    }
     head = newhead;
     heartbeats++;
   }
@@ -1673,7 +1682,8 @@ int gs_engine::deviceErrorCode(int32_t err) {
                    "at most 512)");
       return GS_ECAPACITY;
     case E_PEERTX:
-      gs_set_error("per-node IWANT retransmission table overflow (1024 slots; 4096 with IWANT spammers)");
+      gs_set_error("IWANT retransmission overflow table full (gs_set_peertx_capacity: 2^16 entries per rank "
+                   "by default, 2^20 with IWANT spammers)");
       return GS_ECAPACITY;
     case E_LATE:
       gs_set_error("a message was first delivered later than the message window allows; raise slots_per_topic");
@@ -1791,18 +1801,24 @@ int gs_engine::exchange(int cur, bool hb) {
   const int64_t nPool = std::min<int64_t>((int64_t)xHost[world + 1], poolSeg);
   const size_t entBytes = align8((size_t)nEnt * 4), poolBytes = align8((size_t)nPool * 4);
   const size_t gwBytes = hb ? (size_t)nOwn * W * 8 : 0;
-  const size_t bcast = hdrB + entBytes + poolBytes + gwBytes;
+  // randomsub hosts' target masks ride with their list entries (a receiver
+  // walking a remote randomsub sender's list filters by them)
+  const size_t selBytes = (shipLists && d.sel != nullptr) ? (size_t)nEnt * 8 : 0;
+  const size_t bcast = hdrB + entBytes + selBytes + poolBytes + gwBytes;
   if (bcast > xSendCap) {  // grow (keeps nothing) and pack the lists again
     int rc = growDev(xSend, xSendCap, bcast);
     if (rc) return rc;
     HIPCHECK(hipMemsetAsync(bump, 0, 8, stream));
     packLists();
   }
+  if (selBytes && nOwn)
+    k_x_sel<<<nOwn, 64, 0, stream>>>(d, (const int64_t*)xSend, (const uint32_t*)(xSend + hdrBytes),
+                                     (uint64_t*)(xSend + hdrB + entBytes));
   if (nPool)
-    HIPCHECK(hipMemcpyAsync(xSend + hdrB + entBytes, d.pool[cur] + poolBase, (size_t)nPool * 4,
+    HIPCHECK(hipMemcpyAsync(xSend + hdrB + entBytes + selBytes, d.pool[cur] + poolBase, (size_t)nPool * 4,
                             hipMemcpyDeviceToDevice, stream));
   if (gwBytes)
-    HIPCHECK(hipMemcpyAsync(xSend + hdrB + entBytes + poolBytes, d.gw + (size_t)n0 * W, gwBytes,
+    HIPCHECK(hipMemcpyAsync(xSend + hdrB + entBytes + selBytes + poolBytes, d.gw + (size_t)n0 * W, gwBytes,
                             hipMemcpyDeviceToDevice, stream));
   // 2. edge records, one block per destination rank
   std::vector<int64_t> sendRec(world), sendOff(world);
@@ -1958,14 +1974,17 @@ int gs_engine::exchange(int cur, bool hb) {
     const int64_t* a = &all[(size_t)r * nS];
     const bool lists = (a[3] & 2) != 0;  // rank r shipped its frontier lists
     const size_t hB = lists ? align8((size_t)nr * 8) : 0, eB = align8((size_t)a[1] * 4), pB = align8((size_t)a[2] * 4);
+    const size_t sB = (lists && d.sel != nullptr) ? (size_t)a[1] * 8 : 0;  // the entries' randomsub masks
     const uint8_t* c = xRecv + (size_t)r * chunk;
     xBytes += a[0];
-    if (nr && lists) k_x_unlists<<<nr, 64, 0, stream>>>(d, cur, (const int64_t*)c, (const uint32_t*)(c + hB), part[r]);
+    if (nr && lists)
+      k_x_unlists<<<nr, 64, 0, stream>>>(d, cur, (const int64_t*)c, (const uint32_t*)(c + hB),
+                                         sB ? (const uint64_t*)(c + hB + eB) : nullptr, part[r]);
     if (a[2])
-      HIPCHECK(hipMemcpyAsync(d.pool[cur] + (size_t)r * poolSeg, c + hB + eB, (size_t)a[2] * 4,
+      HIPCHECK(hipMemcpyAsync(d.pool[cur] + (size_t)r * poolSeg, c + hB + eB + sB, (size_t)a[2] * 4,
                               hipMemcpyDeviceToDevice, stream));
     if ((a[3] & 1) && nr)
-      HIPCHECK(hipMemcpyAsync(d.gw + (size_t)part[r] * W, c + hB + eB + pB, (size_t)nr * W * 8,
+      HIPCHECK(hipMemcpyAsync(d.gw + (size_t)part[r] * W, c + hB + eB + sB + pB, (size_t)nr * W * 8,
                               hipMemcpyDeviceToDevice, stream));
   }
   xBytes += totIn;
@@ -2500,6 +2519,17 @@ int gs_set_dormant(gs_engine* g, int32_t n, const int32_t* a, const int32_t* b) 
     if (!ok) { gs_set_error("gs_set_dormant: not an edge of the graph"); return GS_EINVAL; }
     g->dormant.insert({std::min(a[i], b[i]), std::max(a[i], b[i])});
   }
+  return GS_OK;
+}
+
+int gs_set_peertx_capacity(gs_engine* g, int32_t home_bits, int32_t overflow_bits) {
+  if (g->started) { gs_set_error("the peertx capacity must be set before the first step"); return GS_ESTATE; }
+  if (home_bits < 2 || home_bits > 16 || overflow_bits < 8 || overflow_bits > 30) {
+    gs_set_error("gs_set_peertx_capacity: home_bits in [2, 16], overflow_bits in [8, 30]");
+    return GS_EINVAL;
+  }
+  g->ptxHomeBits = home_bits;
+  g->ptxOvfBits = overflow_bits;
   return GS_OK;
 }
 

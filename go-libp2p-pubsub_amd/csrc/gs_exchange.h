@@ -18,6 +18,7 @@
 // At the end of hop h the parity written in h is exchanged:
 //   broadcast part (all-gather, equal chunks):
 //     [node header: (off << 16 | len) per owned node][list entries]
+//     [randomsub target masks of the entries, engines with randomsub hosts]
 //     [the rank's arena segment][gw rows of owned nodes, heartbeat hops only]
 //   edge records (all-to-all-v, block per destination rank): one XRec per
 //     owned edge whose receiver lives on another rank and whose forwarding set
@@ -145,16 +146,37 @@ __global__ __launch_bounds__(64) void k_x_lists(Dev d, int cur, unsigned long lo
   for (int i = lane; i < len; i += 64) ent[off + i] = L[i];
 }
 
-// Another rank's lists into the mirror: nodes [n0r, n0r + nr).
+// Randomsub target masks of the packed entries (d.sel: a receiver's list walk
+// keeps a randomsub sender's copy only on the edges of its mask, randomsub.go:
+// 115-149), one u64 per entry in the entries' order; 0 for other routers'.
+__global__ __launch_bounds__(64) void k_x_sel(Dev d, const int64_t* __restrict__ hdr, const uint32_t* __restrict__ ent,
+                                              uint64_t* __restrict__ sel) {
+  const int v = d.n0 + blockIdx.x;
+  const int lane = lane_id();
+  const int64_t h = hdr[blockIdx.x];
+  const int len = (int)(h & 0xFFFF);
+  const int64_t off = h >> 16;
+  const bool rs = rs_host(d, v);
+  for (int i = lane; i < len; i += 64) sel[off + i] = rs ? d.sel[(int64_t)v * d.S + (ent[off + i] & 0xFFFF)] : 0ull;
+}
+
+// Another rank's lists into the mirror: nodes [n0r, n0r + nr); with `sel`, the
+// randomsub senders' target masks of those entries too.
 __global__ __launch_bounds__(64) void k_x_unlists(Dev d, int cur, const int64_t* __restrict__ hdr,
-                                                  const uint32_t* __restrict__ ent, int n0r) {
+                                                  const uint32_t* __restrict__ ent, const uint64_t* __restrict__ sel,
+                                                  int n0r) {
   const int u = n0r + blockIdx.x;
   const int lane = lane_id();
   const int64_t h = hdr[blockIdx.x];
   const int len = (int)(h & 0xFFFF);
   const int64_t off = h >> 16;
   uint32_t* L = d.fl[cur] + (int64_t)u * d.FC;
-  for (int i = lane; i < len; i += 64) L[i] = ent[off + i];
+  const bool rs = sel != nullptr && rs_host(d, u);
+  for (int i = lane; i < len; i += 64) {
+    const uint32_t x = ent[off + i];
+    L[i] = x;
+    if (rs) d.sel[(int64_t)u * d.S + (x & 0xFFFF)] = sel[off + i];
+  }
   if (lane == 0) d.fln[cur][u] = len;
 }
 

@@ -2268,7 +2268,8 @@ __global__ __launch_bounds__(64) void k_publish_rs(Dev d, int b) {
   const int i = blockIdx.x;
   const int slot = d.mSlot[b + i];
   const int u = d.mSrc[b + i];
-  if (!rs_host(d, u)) return;  // another router's publish (mixed networks)
+  if (u < d.n0 || u >= d.n1 || !rs_host(d, u)) return;  // another rank's host (its mask travels with
+                                                       // its list), or another router's publish
   const int lane = lane_id();
   const int64_t base = d.rowptr[u];
   const int deg = (int)(d.rowptr[u + 1] - base);

@@ -187,16 +187,61 @@ __device__ __forceinline__ int kth_bit(uint64_t m, int k) {
   return __ffsll((long long)m) - 1;
 }
 
-// ++peertx[slot][edge] (mcache.GetForPeer, mcache.go:66-80) in the node's
+// The overflow table (Dev::ptxO) for node v: ++count of key, inserting it
+// (ins) if absent; 0 with E_PEERTX when this table is full too.
+__device__ __forceinline__ uint64_t ptxo_hash(uint64_t x, int bits) {
+  x ^= x >> 29;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 32;
+  return x >> (64 - bits);
+}
+__device__ __forceinline__ int ptxo_settle(const Dev& d, int v, uint32_t key, bool& ins) {
+  const unsigned long long tag = ((unsigned long long)(uint32_t)(v + 1) << 32) | key;
+  const uint64_t mask = (1ull << d.ptxOBits) - 1;
+  uint64_t hs = ptxo_hash(tag, d.ptxOBits);
+  for (uint64_t probe = 0; probe <= mask; ++probe) {
+    const unsigned long long prev = atomicCAS(&d.ptxO[hs], 0ull, tag | 1ull);
+    if (prev == 0ull) {
+      atomicAdd(&d.ptxOCnt[0], 1u);
+      ins = true;
+      return 1;
+    }
+    if ((prev & ~0xFFull) == tag) {
+      const int c = (int)(atomicAdd(&d.ptxO[hs], 1ull) & 0xFFull) + 1;
+      if (c > d.GR + 1) atomicAdd(&d.ptxO[hs], ~0ull);  // (-1)
+      return c;
+    }
+    hs = (hs + 1) & mask;
+  }
+  set_err(d, E_PEERTX);
+  return 0;
+}
+__device__ __forceinline__ int ptxo_count(const Dev& d, int v, uint32_t key) {
+  const unsigned long long tag = ((unsigned long long)(uint32_t)(v + 1) << 32) | key;
+  const uint64_t mask = (1ull << d.ptxOBits) - 1;
+  uint64_t hs = ptxo_hash(tag, d.ptxOBits);
+  for (uint64_t probe = 0; probe <= mask; ++probe) {
+    const unsigned long long cur = __hip_atomic_load(&d.ptxO[hs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == 0ull) return 0;
+    if ((cur & ~0xFFull) == tag) return (int)(cur & 0xFFull);
+    hs = (hs + 1) & mask;
+  }
+  return 0;
+}
+
+// ++peertx[slot][edge] (mcache.GetForPeer, mcache.go:66-80) in node v's
 // HBM hash, given the outcome `prev` of a first CAS(0 -> key | 1) at the key's
-// home slot hs; returns the new count (0 with E_PEERTX when the table is full),
-// and sets ins when the key was inserted.  handleIWant only compares the count
+// home slot hs; returns the new count and sets ins when the key was inserted.
+// A key that finds the node's table full goes to the overflow table: entries
+// only leave at the heartbeat, so a full table stays full for the rest of the
+// hop and a key's lookup reaches the overflow table exactly when its insert did.  handleIWant only compares the count
 // with GossipRetransmission (GR), so a count is held at GR + 1: an increment
 // past it is taken back (the byte peaks at GR + 2; one request list names an
 // id once and a requester's two lists are counted one after the other, so no
 // two increments of one key race).  Entries are never moved during a hop
 // (k_ptx_rebuild compacts the table at the heartbeat), so a key found stays.
-__device__ __forceinline__ int ptx_settle(const Dev& d, uint32_t* row, uint32_t key, int hs, uint32_t prev, bool& ins) {
+__device__ __forceinline__ int ptx_settle(const Dev& d, int v, uint32_t* row, uint32_t key, int hs, uint32_t prev,
+                                          bool& ins) {
   const int hmask = (1 << d.ptxBits) - 1;
   int hsl = hs;
   for (int probe = 0; probe <= hmask; ++probe) {
@@ -212,12 +257,11 @@ __device__ __forceinline__ int ptx_settle(const Dev& d, uint32_t* row, uint32_t 
     }
     hsl = (hsl + 1) & hmask;
   }
-  set_err(d, E_PEERTX);
-  return 0;
+  return ptxo_settle(d, v, key, ins);
 }
 
-// the count of key in the node's HBM hash (0 = absent)
-__device__ __forceinline__ int ptx_count_g(const Dev& d, uint32_t* row, uint32_t key) {
+// the count of key in node v's HBM hash (0 = absent)
+__device__ __forceinline__ int ptx_count_g(const Dev& d, int v, uint32_t* row, uint32_t key) {
   const int hmask = (1 << d.ptxBits) - 1;
   int hsl = ptx_hash(key, d.ptxBits);
   for (int probe = 0; probe <= hmask; ++probe) {
@@ -226,7 +270,7 @@ __device__ __forceinline__ int ptx_count_g(const Dev& d, uint32_t* row, uint32_t
     if ((cur & ~0xFFu) == key) return (int)(cur & 0xFFu);
     hsl = (hsl + 1) & hmask;
   }
-  return 0;
+  return ptxo_count(d, v, key);  // (the table is full)
 }
 
 // Item b of a per-sender item space (sIt = exclusive prefix of item counts
@@ -657,7 +701,7 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
               bool srv = false;
               if (pv[q] != 0xFFFFFFFFu) {
                 bool ins = false;
-                const int count = ptx_settle(d, prow, key[q], hs[q], pv[q], ins);
+                const int count = ptx_settle(d, v, prow, key[q], hs[q], pv[q], ins);
                 nIns += ins ? 1 : 0;
                 srv = count >= 1 && count <= d.GR;
               }
@@ -712,7 +756,7 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
               srv = d.pflag[prv][off + q] != 0;
             } else {
               const uint32_t key = ptx_key32(((uint64_t)(uint32_t)slot << 32) | ((uint64_t)i << 8));
-              const int count = cached(slot) ? ptx_count_g(d, prow, key) : 0;
+              const int count = cached(slot) ? ptx_count_g(d, v, prow, key) : 0;
               srv = count >= 1 && count <= d.GR;
             }
             if (srv) {
@@ -820,108 +864,106 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
         const int i = item_sender(sIt, tb * nCh, k);
         const int t = kth_bit(sTm[i], k / nCh);
         const int uu = sNode[i];
-#ifndef GS_CUTBAL
-#define GS_CUTBAL 1  // timing A/B: -DGS_CUTBAL=0 strides the lanes over words instead
-#endif
         const uint64_t* const g = d.gw + (int64_t)uu * W + t * Wt;  // the sender's words of topic t
         unsigned long long K;
         long long M;
-        if constexpr (GS_CUTBAL != 0) {
-          // every gossip id of the sender's topic t in word order, lane l taking
-          // the ids of rank [l n / 64, (l + 1) n / 64): the same count per lane
-          // (a word-strided split leaves a third of the lanes with one word
-          // more), four message-id loads in flight per step
-          int pre[GS_MAX_WPL];  // ids before word 64 j + lane
-          int n = 0;
+        // every gossip id of the sender's topic t in word order, by units: a
+        // unit is a slot pair (2j, 2j + 1) with at least one of the two in the
+        // window.  Lane l takes the units of rank [l n / 64, (l + 1) n / 64), the
+        // same count per lane (a word-strided split leaves a third of the lanes
+        // with one word more).  A slot pair holds a message-id pair (2m, 2m + 1)
+        // whenever a topic's ids fill its slots in order (one topic: slot = id
+        // mod St, St even), and then one Philox block keys both ids
+        // (gs_key64_mid); an unpaired neighbour takes a block of its own.
+        auto units = [](uint64_t x) { return (x | (x >> 1)) & 0x5555555555555555ull; };
+        int pre[GS_MAX_WPL];  // units before word 64 j + lane
+        int n = 0;
+#pragma unroll
+        for (int j = 0; j < GS_MAX_WPL; ++j) {
+          const int w = 64 * j + lane;
+          const int pc = w < Wt ? __popcll(units(g[w])) : 0;
+          const int incl = wave_incl_sum(pc);
+          pre[j] = n + incl - pc;
+          n += wave_last(incl);
+        }
+        auto preAt = [&](int w) {  // (all lanes: the shuffles read every lane)
+          int x = 0;
 #pragma unroll
           for (int j = 0; j < GS_MAX_WPL; ++j) {
-            const int w = 64 * j + lane;
-            const int pc = w < Wt ? __popcll(g[w]) : 0;
-            const int incl = wave_incl_sum(pc);
-            pre[j] = n + incl - pc;
-            n += wave_last(incl);
+            const int y = __shfl(pre[j], w & 63);
+            if ((w >> 6) == j) x = y;
           }
-          auto preAt = [&](int w) {  // (all lanes: the shuffles read every lane)
-            int x = 0;
-#pragma unroll
-            for (int j = 0; j < GS_MAX_WPL; ++j) {
-              const int y = __shfl(pre[j], w & 63);
-              if ((w >> 6) == j) x = y;
-            }
-            return x;
-          };
-          const int r0 = (int)((int64_t)lane * n / 64), r1 = (int)((int64_t)(lane + 1) * n / 64);
-          // the first word holding rank r0: the last w with pre(w) <= r0
-          int lo = 0, hi = Wt - 1;
-          while (__ballot(lo < hi)) {
-            const int mid = (lo + hi + 1) >> 1;
-            const int pm = preAt(lo < hi ? mid : lo);
-            if (lo < hi) {
-              if (pm <= r0) lo = mid; else hi = mid - 1;
-            }
+          return x;
+        };
+        const int r0 = (int)((int64_t)lane * n / 64), r1 = (int)((int64_t)(lane + 1) * n / 64);
+        // the first word holding rank r0: the last w with pre(w) <= r0
+        int lo = 0, hi = Wt - 1;
+        while (__ballot(lo < hi)) {
+          const int mid = (lo + hi + 1) >> 1;
+          const int pm = preAt(lo < hi ? mid : lo);
+          if (lo < hi) {
+            if (pm <= r0) lo = mid; else hi = mid - 1;
           }
-          const int wS = lo;
-          uint64_t yS = r0 < r1 ? g[wS] : 0ull;
-          for (int sk = r0 - preAt(wS); sk > 0; --sk) yS &= yS - 1;  // the ids of lower lanes
+        }
+        const int wS = lo;
+        const uint64_t gS = r0 < r1 ? g[wS] : 0ull;
+        uint64_t yS = units(gS);
+        for (int sk = r0 - preAt(wS); sk > 0; --sk) yS &= yS - 1;  // the units of lower lanes
 #ifndef GS_CUTQ
-#define GS_CUTQ 8  // ids (message-id loads and keys) in flight per lane (4: 98.0 ms, 8: 95.8 ms phase B per round at config3)
+#define GS_CUTQ 8  // units (one 16-byte message-id load, one key block each) in flight per lane
 #endif
-          auto each = [&](auto&& fn) {
-            int w = wS;
-            uint64_t y = yS, ny = (r0 < r1 && wS + 1 < Wt) ? g[wS + 1] : 0ull;
-            for (int r = r0; r < r1; r += GS_CUTQ) {
-              int bs[GS_CUTQ], ws[GS_CUTQ];
-              int64_t mids[GS_CUTQ];
-#pragma unroll
-              for (int q = 0; q < GS_CUTQ; ++q) {
-                bs[q] = -1;
-                ws[q] = w;
-                if (r + q < r1) {
-                  while (y == 0) {  // (rank r + q exists: some later word holds it)
-                    ++w;
-                    y = ny;
-                    ny = w + 1 < Wt ? g[w + 1] : 0ull;
-                  }
-                  bs[q] = __ffsll((long long)y) - 1;
-                  ws[q] = w;
-                  y &= y - 1;
-                }
-              }
-#pragma unroll
-              for (int q = 0; q < GS_CUTQ; ++q)
-                mids[q] = bs[q] >= 0 ? d.slotMid[(int64_t)(t * Wt + ws[q]) * 64 + bs[q]] : 0;
-#pragma unroll
-              for (int q = 0; q < GS_CUTQ; ++q)
-                if (bs[q] >= 0)
-                  fn(gs_key64(d.seed, GS_SITE_EMIT_MIDS, uu, v, (uint32_t)mids[q], (uint32_t)(h - 1)), mids[q]);
-            }
-          };
-          select_kth_est(each, d.MaxIHaveLength, n, cHist, cand, K, M);
-        } else {
-        // every gossip id of the sender's topic t, lane-strided over words;
-        // the ids' message-id loads go out four at a time
+        const uint32_t hk = (uint32_t)(h - 1);
         auto each = [&](auto&& fn) {
-          for (int w = t * Wt + lane; w < (t + 1) * Wt; w += 64) {
-            uint64_t y = d.gw[(int64_t)uu * W + w];
-            while (y) {
-              int bs[4];
-              int64_t mids[4];
+          int w = wS;
+          uint64_t gc = gS, y = yS, ng = (r0 < r1 && wS + 1 < Wt) ? g[wS + 1] : 0ull;
+          for (int r = r0; r < r1; r += GS_CUTQ) {
+            int bs[GS_CUTQ], ws[GS_CUTQ];
+            uint32_t pr[GS_CUTQ];  // the unit's slots in the window: bit 0 slot 2j, bit 1 slot 2j + 1
 #pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                bs[q] = y ? __ffsll((long long)y) - 1 : -1;
-                y &= y ? y - 1 : 0ull;
+            for (int q = 0; q < GS_CUTQ; ++q) {
+              bs[q] = -1;
+              ws[q] = w;
+              pr[q] = 0;
+              if (r + q < r1) {
+                while (y == 0) {  // (rank r + q exists: some later word holds it)
+                  ++w;
+                  gc = ng;
+                  y = units(gc);
+                  ng = w + 1 < Wt ? g[w + 1] : 0ull;
+                }
+                bs[q] = __ffsll((long long)y) - 1;
+                ws[q] = w;
+                pr[q] = (uint32_t)(gc >> bs[q]) & 3u;
+                y &= y - 1;
               }
+            }
+            int64_t m0[GS_CUTQ], m1[GS_CUTQ];
 #pragma unroll
-              for (int q = 0; q < 4; ++q) mids[q] = bs[q] >= 0 ? d.slotMid[(int64_t)w * 64 + bs[q]] : 0;
+            for (int q = 0; q < GS_CUTQ; ++q) {
+              m0[q] = m1[q] = 0;
+              if (bs[q] >= 0) {  // both ids of the pair (bs even: a 16-byte aligned load)
+                const int4 p = *reinterpret_cast<const int4*>(d.slotMid + (int64_t)(t * Wt + ws[q]) * 64 + bs[q]);
+                m0[q] = (int64_t)(((uint64_t)(uint32_t)p.y << 32) | (uint32_t)p.x);
+                m1[q] = (int64_t)(((uint64_t)(uint32_t)p.w << 32) | (uint32_t)p.z);
+              }
+            }
 #pragma unroll
-              for (int q = 0; q < 4; ++q)
-                if (bs[q] >= 0)
-                  fn(gs_key64(d.seed, GS_SITE_EMIT_MIDS, uu, v, (uint32_t)mids[q], (uint32_t)(h - 1)), mids[q]);
+            for (int q = 0; q < GS_CUTQ; ++q) {
+              if (bs[q] < 0) continue;
+              const int64_t ma = (pr[q] & 1u) ? m0[q] : m1[q];
+              uint64_t kb[2];
+              gs_key64x2(d.seed, GS_SITE_EMIT_MIDS, uu, v, (uint32_t)ma >> 1, hk, kb);
+              fn((ma & 1) ? kb[1] : kb[0], ma);
+              if (pr[q] == 3u) {
+                const int64_t mb = m1[q];
+                fn(((uint32_t)mb >> 1) == ((uint32_t)ma >> 1) ? ((mb & 1) ? kb[1] : kb[0])
+                                                             : gs_key64_mid(d.seed, GS_SITE_EMIT_MIDS, uu, v, (uint32_t)mb, hk),
+                   mb);
+              }
             }
           }
         };
         select_kth_est(each, d.MaxIHaveLength, cNm[c], cHist, cand, K, M);
-        }
         if (lane == 0) {
           cK[c] = K;
           cM[c] = M;
@@ -961,7 +1003,7 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
               const int bb = __ffsll((long long)y) - 1;
               y &= y - 1;
               const int64_t mid = d.slotMid[(int64_t)(w0 + q) * 64 + bb];
-              const unsigned long long key = gs_key64(d.seed, GS_SITE_EMIT_MIDS, uu, v, (uint32_t)mid, (uint32_t)(h - 1));
+              const unsigned long long key = gs_key64_mid(d.seed, GS_SITE_EMIT_MIDS, uu, v, (uint32_t)mid, (uint32_t)(h - 1));
               if (key > K || (key == K && mid > M)) want &= ~(1ull << bb);
             }
           }
@@ -986,7 +1028,7 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
           const int bb = __ffsll((long long)y) - 1;
           y &= y - 1;
           const int64_t mid = d.slotMid[(int64_t)w * 64 + bb];
-          const uint64_t key = gs_key64(d.seed, GS_SITE_IWANT, v, uu, (uint32_t)mid, (uint32_t)h);
+          const uint64_t key = gs_key64_mid(d.seed, GS_SITE_IWANT, v, uu, (uint32_t)mid, (uint32_t)h);
           bestKey = key < bestKey ? key : bestKey;
         }
       });
@@ -1017,7 +1059,7 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
           const int bb = __ffsll((long long)y) - 1;
           y &= y - 1;
           const int64_t mid = d.slotMid[(int64_t)w * 64 + bb];
-          if (gs_key64(d.seed, GS_SITE_IWANT, v, uu, (uint32_t)mid, (uint32_t)h) == best)
+          if (gs_key64_mid(d.seed, GS_SITE_IWANT, v, uu, (uint32_t)mid, (uint32_t)h) == best)
             atomicMin(&sMid[i], (long long)mid);
         }
       });
@@ -1055,10 +1097,10 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
                 y &= y - 1;
                 const int64_t mid = d.slotMid[(int64_t)w * 64 + bb];
                 if (ci >= 0) {
-                  const unsigned long long ke = gs_key64(d.seed, GS_SITE_EMIT_MIDS, uu, v, (uint32_t)mid, (uint32_t)(h - 1));
+                  const unsigned long long ke = gs_key64_mid(d.seed, GS_SITE_EMIT_MIDS, uu, v, (uint32_t)mid, (uint32_t)(h - 1));
                   if (ke > cK[ci] || (ke == cK[ci] && mid > cM[ci])) continue;
                 }
-                fn(gs_key64(d.seed, GS_SITE_IWANT, v, uu, (uint32_t)mid, (uint32_t)h), mid);
+                fn(gs_key64_mid(d.seed, GS_SITE_IWANT, v, uu, (uint32_t)mid, (uint32_t)h), mid);
               }
             }
           }
@@ -1103,7 +1145,7 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
               const int slot = w * 64 + bb;
               const int64_t mid = d.slotMid[slot];
               if (cutI) {
-                const unsigned long long key = gs_key64(d.seed, GS_SITE_IWANT, v, uu, (uint32_t)mid, (uint32_t)h);
+                const unsigned long long key = gs_key64_mid(d.seed, GS_SITE_IWANT, v, uu, (uint32_t)mid, (uint32_t)h);
                 if (key > iK[i] || (key == iK[i] && mid > iM[i])) continue;
               }
               d.pool[cur][sOut[i] + atomicAdd(&sCur[i], 1)] = slot;
@@ -2164,6 +2206,52 @@ __global__ __launch_bounds__(64) void k_ptx_rebuild(Dev d, int last) {
   for (int k = lane; k < hN / 4; k += 64) ((uint4*)row)[k] = ((const uint4*)sT)[k];
   kept = wave_sum_int(kept);
   if (lane == 0) d.ptxN[v] = kept;
+}
+
+// The overflow table's part of the rebuild, after k_ptx_rebuild: the entries
+// whose message stays in the cache are collected and the table cleared, then
+// each goes back to its node's (rebuilt) table if a slot is free there, else
+// to the overflow table.  Launched every heartbeat over the whole table; a
+// table without entries returns at once.
+__global__ void k_ptxo_collect(Dev d, int last) {
+  if (d.ptxOCnt[0] == 0u) return;
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >> d.ptxOBits) return;
+  const unsigned long long x = d.ptxO[k];
+  if (x == 0ull) return;
+  d.ptxO[k] = 0ull;
+  const int v = (int)(x >> 32) - 1;
+  const int slot = (int)(((uint32_t)x) >> 14);
+  const uint64_t* lastw = d.hist + ((int64_t)last * d.nOwnH + (v - d.n0)) * d.W;
+  if ((lastw[slot >> 6] >> (slot & 63)) & 1) return;  // leaves the cache
+  d.ptxOStage[atomicAdd(&d.ptxOCnt[2], 1u)] = x;
+}
+__global__ void k_ptxo_reinsert(Dev d) {
+  if (d.ptxOCnt[0] == 0u) return;
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= (int64_t)d.ptxOCnt[2]) return;
+  const unsigned long long x = d.ptxOStage[k];
+  const int v = (int)(x >> 32) - 1;
+  const uint32_t ent = (uint32_t)x;
+  uint32_t* const row = ptx_row(d, v);
+  const int hmask = (1 << d.ptxBits) - 1;
+  int hsl = ptx_hash(ent & ~0xFFu, d.ptxBits);
+  for (int probe = 0; probe <= hmask; ++probe) {
+    if (atomicCAS(&row[hsl], 0u, ent) == 0u) {
+      atomicAdd(&d.ptxN[v], 1);
+      return;
+    }
+    hsl = (hsl + 1) & hmask;
+  }
+  const uint64_t mask = (1ull << d.ptxOBits) - 1;
+  uint64_t hs = ptxo_hash(x & ~0xFFull, d.ptxOBits);
+  while (atomicCAS(&d.ptxO[hs], 0ull, x) != 0ull) hs = (hs + 1) & mask;  // (it held them all before)
+  atomicAdd(&d.ptxOCnt[1], 1u);
+}
+__global__ void k_ptxo_fin(Dev d) {
+  d.ptxOCnt[0] = d.ptxOCnt[1];
+  d.ptxOCnt[1] = 0u;
+  d.ptxOCnt[2] = 0u;
 }
 
 // gs_read_deliveries gather

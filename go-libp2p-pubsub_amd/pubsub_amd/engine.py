@@ -152,6 +152,13 @@ def WithProtocols(proto):
     return ("protocols", np.ascontiguousarray(proto, dtype=np.uint8))
 
 
+def WithPeertxCapacity(home_bits, overflow_bits):
+    """mcache.peertx capacity (gs_set_peertx_capacity): 2^home_bits slots per
+    node, and a per-rank overflow table of 2^overflow_bits entries for nodes
+    whose own table is full."""
+    return ("peertx", (int(home_bits), int(overflow_bits)))
+
+
 def WithPartition(rank, world, transport):
     """Simulate only this rank's node range; exchange RPCs with the other
     ranks through `transport` (a pubsub_amd.transport.TorchTransport) once per
@@ -237,6 +244,9 @@ class Engine:
             _check(self.lib, self.lib.gs_set_trace(h, _ptr(mask, C.c_uint8), cap))
             if rpc:
                 _check(self.lib, self.lib.gs_set_trace_rpc(h, 1))
+        ptx = opts.get("peertx")
+        if ptx is not None:
+            _check(self.lib, self.lib.gs_set_peertx_capacity(h, *ptx))
         acct = opts.get("rpc_acct")
         if acct is not None:
             ms, idl, tl = acct

@@ -368,6 +368,14 @@ int gs_schedule_events(gs_engine* eng, int32_t n, const int32_t* kind, const int
                        const int64_t* hop);
 
 /* Advances the simulation by `hops` lock-step hops. */
+/* Before the first step: the mcache.peertx tables (mcache.go:66-80, the
+ * GossipRetransmission counts of handleIWant): 2^home_bits slots per node
+ * (default 10; 12 with IWANT spammers, 2..16) and a per-rank overflow table of
+ * 2^overflow_bits entries (default 16; 20 with IWANT spammers, 8..30) that takes
+ * the keys of nodes whose own table is full.  Only a full overflow table is a
+ * GS_ECAPACITY error of gs_step.  Replaces no reference call: the reference's
+ * peertx is an unbounded Go map. */
+int gs_set_peertx_capacity(gs_engine* eng, int32_t home_bits, int32_t overflow_bits);
 int gs_step(gs_engine* eng, int64_t hops);
 /* Waits for all queued device work (no-op on the oracle). */
 int gs_sync(gs_engine* eng);

@@ -40,8 +40,8 @@ enum {
   GS_SITE_DHI_SHUFFLE = 8,     /* {node, hop, peer, topic}  gossipsub.go:1380 */
   GS_SITE_DHI_TAIL = 9,        /* {node, hop, peer, topic}  gossipsub.go:1387 */
   GS_SITE_EMIT_PEERS = 10,     /* {node, hop, peer, topic}  gossipsub.go:1695 */
-  GS_SITE_EMIT_MIDS = 11,      /* {node, peer, msg_id, hop} gossipsub.go:1707 */
-  GS_SITE_IWANT = 12,          /* {node, peer, msg_id, hop} gossipsub.go:663, gossip_tracer.go:53 */
+  GS_SITE_EMIT_MIDS = 11,      /* {node, peer, msg_id, hop} gossipsub.go:1707 (gs_key64_mid) */
+  GS_SITE_IWANT = 12,          /* {node, peer, msg_id, hop} gossipsub.go:663, gossip_tracer.go:53 (gs_key64_mid) */
   GS_SITE_GATER = 13,          /* {node, peer, hop, 0}      peer_gater.go:357 */
   GS_SITE_PX = 14,             /* {node, hop, peer, pruned << 6 | topic}  gossipsub.go:1813 makePrune's
                                   getPeers (a fresh shuffle per PRUNE: keyed by the pruned peer too) */
@@ -80,6 +80,30 @@ GS_HD uint64_t gs_key64(uint32_t seed, uint32_t site, uint32_t a, uint32_t b, ui
   uint32_t out[4];
   gs_philox4x32_10(ctr, key, out);
   return ((uint64_t)out[0] << 32) | (uint64_t)out[1];
+}
+
+/* Both 64-bit halves of one block: k[0] = hi32:x0 | lo32:x1 (= gs_key64),
+ * k[1] = hi32:x2 | lo32:x3. */
+GS_HD void gs_key64x2(uint32_t seed, uint32_t site, uint32_t a, uint32_t b, uint32_t c, uint32_t d,
+                      uint64_t k[2]) {
+  uint32_t ctr[4] = {a, b, c, d};
+  uint32_t key[2] = {seed, site};
+  uint32_t out[4];
+  gs_philox4x32_10(ctr, key, out);
+  k[0] = ((uint64_t)out[0] << 32) | (uint64_t)out[1];
+  k[1] = ((uint64_t)out[2] << 32) | (uint64_t)out[3];
+}
+
+/* The message-id sites (GS_SITE_EMIT_MIDS, GS_SITE_IWANT: counter word c is a
+ * message id) use the whole block: the key of id m is half (m & 1) of the
+ * block for counter word m >> 1, so ids 2j and 2j + 1 share one Philox
+ * evaluation (the receiver's IHAVE cut hashes a sender's whole gossip window:
+ * gs_kernels_ctl.h, phase B). */
+GS_HD uint64_t gs_key64_mid(uint32_t seed, uint32_t site, uint32_t a, uint32_t b, uint32_t mid,
+                            uint32_t d) {
+  uint64_t k[2];
+  gs_key64x2(seed, site, a, b, mid >> 1, d, k);
+  return (mid & 1u) ? k[1] : k[0];
 }
 
 /* Uniform double in [0,1) from a key (53 high bits), for rand.Float64 sites. */

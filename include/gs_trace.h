@@ -95,9 +95,9 @@ inline void gs_trace_canon_items(gs_trace_event* it, size_t n, uint32_t seed, in
     }
     uint64_t k = 0;
     if (x.reason == GS_RPC_ITEM_IHAVE)
-      k = gs_key64(seed, GS_SITE_EMIT_MIDS, sender, receiver, (uint32_t)x.msg, hopSent);
+      k = gs_key64_mid(seed, GS_SITE_EMIT_MIDS, sender, receiver, (uint32_t)x.msg, hopSent);
     else if (x.reason == GS_RPC_ITEM_IWANT && !spamList)
-      k = gs_key64(seed, GS_SITE_IWANT, sender, receiver, (uint32_t)x.msg, hopSent);
+      k = gs_key64_mid(seed, GS_SITE_IWANT, sender, receiver, (uint32_t)x.msg, hopSent);
     v.push_back({std::make_tuple((int)x.reason, (int)x.topic, k, x.msg), x});
   }
   // IHAVE: ascending ids, or the MaxIHaveLength smallest keys in key order

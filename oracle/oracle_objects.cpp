@@ -158,6 +158,9 @@ void opg_set_ip_expire(PeerGater* g, uint32_t ip, int64_t t) { g->ipStats[ip].ex
 uint64_t orng_key64(uint32_t seed, uint32_t site, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   return gs_key64(seed, site, a, b, c, d);
 }
+uint64_t orng_key64_mid(uint32_t seed, uint32_t site, uint32_t a, uint32_t b, uint32_t mid, uint32_t d) {
+  return gs_key64_mid(seed, site, a, b, mid, d);
+}
 void orng_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out) { gs_philox4x32_10(ctr, key, out); }
 
 }  // extern "C"

@@ -652,7 +652,7 @@ std::vector<int64_t> Node::handleIHave(int p, const Control& ctl) {
   if (iask + iasked[p] > sim->gp.MaxIHaveLength) iask = sim->gp.MaxIHaveLength - iasked[p];
   std::vector<std::pair<uint64_t, int64_t>> keyed;
   for (int64_t mid : iwant)
-    keyed.push_back({gs_key64(sim->cfg.seed, GS_SITE_IWANT, id, p, (uint32_t)mid, (uint32_t)sim->hop), mid});
+    keyed.push_back({gs_key64_mid(sim->cfg.seed, GS_SITE_IWANT, id, p, (uint32_t)mid, (uint32_t)sim->hop), mid});
   std::sort(keyed.begin(), keyed.end());
   std::vector<int64_t> lst;
   for (int i = 0; i < iask; ++i) lst.push_back(keyed[i].second);
@@ -844,7 +844,7 @@ void Node::emitGossip(int topic, const std::set<int>& exclude) {
     if ((int)mids.size() > sim->gp.MaxIHaveLength) {
       std::vector<std::pair<uint64_t, int64_t>> keyed;
       for (int64_t mid : mids)
-        keyed.push_back({gs_key64(sim->cfg.seed, GS_SITE_EMIT_MIDS, id, p, (uint32_t)mid, (uint32_t)sim->hop), mid});
+        keyed.push_back({gs_key64_mid(sim->cfg.seed, GS_SITE_EMIT_MIDS, id, p, (uint32_t)mid, (uint32_t)sim->hop), mid});
       std::sort(keyed.begin(), keyed.end());
       for (int i = 0; i < sim->gp.MaxIHaveLength; ++i) e.mids.push_back(keyed[i].second);
     } else {
@@ -2106,6 +2106,15 @@ int gs_set_trace(gs_engine* g, const uint8_t* node_mask, int64_t capacity) {
   if (g->sim.started) { set_error("tracing must be set before the first step"); return GS_ESTATE; }
   if (node_mask) g->sim.traced.assign(node_mask, node_mask + g->sim.N);
   else g->sim.traced.clear();
+  return GS_OK;
+}
+int gs_set_peertx_capacity(gs_engine* g, int32_t home_bits, int32_t overflow_bits) {
+  // mcache.peertx is a map here (mcache.go:66-80): no capacity to set
+  if (g->sim.started) { set_error("the peertx capacity must be set before the first step"); return GS_ESTATE; }
+  if (home_bits < 2 || home_bits > 16 || overflow_bits < 8 || overflow_bits > 30) {
+    set_error("gs_set_peertx_capacity: home_bits in [2, 16], overflow_bits in [8, 30]");
+    return GS_EINVAL;
+  }
   return GS_OK;
 }
 int gs_set_trace_rpc(gs_engine* g, int32_t on) {

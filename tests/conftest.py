@@ -70,6 +70,7 @@ def olib(oracle_path):
         "opg_has_peer_stats": (C.c_int, [P, i32]), "opg_has_ip_stats": (C.c_int, [P, u32]),
         "opg_set_ip_expire": (None, [P, u32, i64]),
         "orng_key64": (u64, [u32, u32, u32, u32, u32, u32]),
+        "orng_key64_mid": (u64, [u32, u32, u32, u32, u32, u32]),
         "orng_philox": (None, [C.POINTER(u32), C.POINTER(u32), C.POINTER(u32)]),
     }
     for name, (res, args) in sigs.items():

@@ -40,3 +40,28 @@ def test_gpu_golden_repeatable(name):
     from pubsub_amd import PRODUCT_LIB
     for _ in range(3):
         assert digest(scenarios.run(PRODUCT_LIB, name)) == GOLDEN[name]
+
+
+# mcache.peertx spills (mcache.go:66-80 keeps an unbounded map): with 4 slots
+# per node, every node that serves more than 4 (message, requester) IWANT
+# entries within its cache window takes the rest in the rank's overflow table
+# (gs_set_peertx_capacity); the heartbeat's rebuild moves survivors back when
+# a node's own table has room.  The goldens must not move.
+PEERTX_SPILL = ["c3shape", "adversarial_mix", "gossipsub_slot_reuse", "churn_scored", "c4shape", "px_adversarial"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", [n for n in PEERTX_SPILL if n in GOLDEN])
+def test_gpu_peertx_overflow_reproduces_golden(name):
+    from pubsub_amd import PRODUCT_LIB, WithPeertxCapacity
+    assert digest(scenarios.run(PRODUCT_LIB, name, extra=(WithPeertxCapacity(2, 16),))) == GOLDEN[name]
+
+
+@pytest.mark.gpu
+def test_gpu_peertx_overflow_full_is_capacity_error():
+    """An overflow table too small for the live entries is GS_ECAPACITY, not a
+    silent miscount."""
+    from pubsub_amd import PRODUCT_LIB, GossipEngineError, WithPeertxCapacity, _abi
+    with pytest.raises(GossipEngineError) as ei:
+        scenarios.run(PRODUCT_LIB, "c3shape", extra=(WithPeertxCapacity(2, 8),))
+    assert ei.value.code == _abi.GS_ECAPACITY and "overflow table" in str(ei.value)

@@ -135,6 +135,13 @@ def run_partitioned(world, name, oracle):
     (2, "c4shape"),
     (3, "cut_honest_4t"),
     (2, "push_overflow"),
+    # randomsub: a sender's per-message target masks (d.sel) travel with its
+    # frontier list entries (gs_exchange.h k_x_sel); at T >= 4 k_push applies
+    # them on the sender's rank
+    (3, "randomsub_100"),
+    (2, "randomsub_N"),
+    (2, "mixed_randomsub"),
+    (3, "mixed_scored_4t"),
 ])
 def test_partitioned_engine_matches_oracle(world, name, oracle_path):
     res = run_partitioned(world, name, oracle_path)
@@ -197,27 +204,6 @@ def test_partitioned_device_error_stops_every_rank():
     assert all(r[1][0] == _abi.GS_ECAPACITY for r in res), res
     assert res[0][2] == res[1][2], res            # both stopped at the same hop
     assert "rank 0" in res[1][1][1], res          # rank 1 names the failing rank
-
-
-class _NoTransport:
-    """gs_transport whose callbacks fail (never reached in this test)."""
-
-    def __init__(self):
-        from pubsub_amd import _abi
-        self._cb = (_abi.ALLGATHER_I64(lambda *a: -1), _abi.ALLGATHER(lambda *a: -1),
-                    _abi.ALLTOALLV(lambda *a: -1))
-        self.c = _abi.TransportC(None, *self._cb)
-
-
-@pytest.mark.gpu
-def test_partitioned_randomsub_is_refused():
-    """Randomsub's per-message target masks are not exchanged: refused loudly."""
-    from pubsub_amd import GossipEngineError, NewRandomSub, WithPartition, _abi, graphs
-    g = graphs.random_regular(40, 8, 1)
-    e = NewRandomSub(40, 1, g, graphs.all_subscribed(40, 1), 10, WithPartition(0, 2, _NoTransport()))
-    with pytest.raises(GossipEngineError) as ei:
-        e.step(1)
-    assert ei.value.code == _abi.GS_EUNSUPPORTED
 
 
 def _rpc_worker(rank, world, port, name, q):

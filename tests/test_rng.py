@@ -28,3 +28,12 @@ def test_philox_kat_pi(olib):
 def test_key64_layout(olib):
     o = _philox(olib, [1, 2, 3, 4], [7, 12])
     assert olib.orng_key64(7, 12, 1, 2, 3, 4) == (o[0] << 32) | o[1]
+
+
+def test_key64_mid_pairs(olib):
+    """The message-id sites take both halves of a block: ids 2j and 2j + 1 share
+    the block of counter word j (gs_rng.h gs_key64_mid)."""
+    for j in (0, 1, 2500, 0x7FFFFFFF):
+        o = _philox(olib, [5, 9, j, 33], [7, 11])
+        assert olib.orng_key64_mid(7, 11, 5, 9, 2 * j, 33) == (o[0] << 32) | o[1]
+        assert olib.orng_key64_mid(7, 11, 5, 9, 2 * j + 1, 33) == (o[2] << 32) | o[3]
