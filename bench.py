@@ -344,6 +344,9 @@ def main():
                          "has run at world 1 only")
     ap.add_argument("--rpc-accounting", action="store_true",
                     help="also sum RPC bytes per edge (gs_set_rpc_accounting; 1 KB messages, 40-byte ids)")
+    ap.add_argument("--frontier", default="auto", choices=["auto", "lists", "bitmaps"],
+                    help="phase A's reading of the senders' frontiers (gs_set_frontier_mode; same results): "
+                         "the engine's choice (auto), per-copy lists, or bitmaps wherever supported")
     ap.add_argument("--lib", default=None, help="timing experiments only: another build of the product library "
                     "(results are labelled with it)")
     args = ap.parse_args()
@@ -401,6 +404,9 @@ def main():
     if args.rpc_accounting:
         from pubsub_amd import WithRPCAccounting
         extra = tuple(extra) + (WithRPCAccounting(1000, id_len=40),)
+    if args.frontier != "auto":
+        from pubsub_amd import WithFrontierBitmaps, WithFrontierLists
+        extra = tuple(extra) + ((WithFrontierLists if args.frontier == "lists" else WithFrontierBitmaps)(),)
     def dev_free():
         try:
             import torch
@@ -571,6 +577,7 @@ def main():
         # hop handles every payload RPC before any control RPC; the per-RPC order of
         # the oracle's reference mode roughly doubles iwant_sent on gossipsub_scored
         "schedule": "phase split: payload before control per hop (DESIGN.md 3a; per-RPC order ~2x iwant_sent)",
+        "phase_a_reads": "frontier bitmaps" if eng.frontier_dense else "frontier lists",
         "roofline": roofline,
         "rooflines_other": rooflines,
         "device_gib": device_gb,  # device memory the engine holds (free memory before / after its start)

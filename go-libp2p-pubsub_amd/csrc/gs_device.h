@@ -197,7 +197,7 @@ struct Dev {
   uint64_t tDivM;   // ceil(2^64 / T) (0 when T == 1): edge of pair p = umul64hi(p, tDivM)
   int32_t maxDeg;  // largest node degree (<= 64)
   uint64_t* oldm;  // [W] slots whose message is too old to be first-delivered this hop
-  uint64_t* yTab;  // [2][W] phase A: young-slot mask of the amR word of rank k, then its slot prefix
+  uint64_t* yTab;  // [2][W] phase A: young-slot mask of the amR word of rank k, then its slot prefix | word << 32
   int32_t* nAuth;  // [N] live message slots authored by the node
   int32_t needAge, record;
   uint64_t* sel;   // [N][S] randomsub target mask (randomsub only)

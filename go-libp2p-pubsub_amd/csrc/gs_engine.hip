@@ -109,6 +109,11 @@ struct gs_engine {
   // with nothing that needs a per-copy record (trace, RPC accounting, churn,
   // dormant slots, validators, attackers) on one rank
   bool denseFlood = false;
+  // gossipsub on one topic (config3's shape): phase A pass 1 ORs the senders'
+  // frontier bitmaps (k_phase_a DENSE); the lists stay for every other reader
+  bool denseGossip = false;
+  int frontierMode = 0;                // gs_set_frontier_mode: 0 auto, 1 lists only
+  WMask amWPar[2]{};                   // denseGossip: amW of the last hop of each parity
   bool churnWindow = false;            // events scheduled before the first publish: wide window
   uint64_t* dSubA = nullptr;
   uint64_t* dSubOwn = nullptr;
@@ -487,7 +492,13 @@ int gs_engine::start() {
   bool anyRandom = cfg.router == GS_ROUTER_RANDOMSUB;  // some host runs randomsub (d.sel)
   pushOn = T >= 4;
   denseFlood = cfg.router == GS_ROUTER_FLOODSUB && !mixed && routerH.empty() && world == 1 && traceMask.empty() &&
-               !acctOn && events.empty() && dormant.empty() && topicVal == 0 && behaveAll == 0;
+               !acctOn && events.empty() && dormant.empty() && topicVal == 0 && behaveAll == 0 &&
+               frontierMode != GS_FRONTIER_LISTS;
+  // (no P3 window shorter than a message's lifetime: the dense pass counts
+  // duplicates per sender, not per copy's age; one rank: the senders' rows)
+  denseGossip = cfg.router == GS_ROUTER_GOSSIPSUB && T == 1 && !mixed && routerH.empty() && world == 1 &&
+                events.empty() && dormant.empty() && !doPX && topicVal == 0 && behaveAll == 0 && !gaterOn &&
+                !(scoring && ageWindowNeeded()) && frontierMode == GS_FRONTIER_BITMAPS;
   if (!routerH.empty()) {
     anyRandom = false;
     for (uint8_t r : routerH) anyRandom = anyRandom || r == GS_ROUTER_RANDOMSUB;
@@ -696,16 +707,17 @@ int gs_engine::start() {
       return GS_EUNSUPPORTED;
     }
   }
+  const bool denseAny = denseFlood || denseGossip;
   for (int k = 0; k < 2; ++k) {
     x.fl[k] = dalloc<uint32_t>((size_t)N * x.FC); chk(x.fl[k]);
     x.fln[k] = dalloc<int32_t>(N); chk(x.fln[k]);
-    x.fb[k] = denseFlood ? dalloc<uint64_t>(NW) : nullptr;
-    x.fex[k] = denseFlood ? dalloc<int32_t>(E) : nullptr;
-    x.fbN[k] = denseFlood ? dalloc<int32_t>(N) : nullptr;
-    if (denseFlood) { chk(x.fb[k]); chk(x.fex[k]); chk(x.fbN[k]); }
+    x.fb[k] = denseAny ? dalloc<uint64_t>(NW) : nullptr;
+    x.fex[k] = denseAny ? dalloc<int32_t>(E) : nullptr;
+    x.fbN[k] = denseAny ? dalloc<int32_t>(N) : nullptr;
+    if (denseAny) { chk(x.fb[k]); chk(x.fex[k]); chk(x.fbN[k]); }
   }
-  x.own = denseFlood ? dalloc<uint64_t>(NW) : nullptr;
-  if (denseFlood) chk(x.own);
+  x.own = denseAny ? dalloc<uint64_t>(NW) : nullptr;
+  if (denseAny) chk(x.own);
   if (!ok) { gs_set_error("device allocation failed (frontiers)"); return GS_ENOMEM; }
   // push arena: a region of GS_PUSHR slots (4 KiB) per owned sender and parity
   for (int k = 0; k < 2; ++k) {
@@ -1390,7 +1402,7 @@ int gs_engine::stepOne() {
     for (int w = 0; w < W; ++w) {
       if (!((amR.m[w >> 6] >> (w & 63)) & 1)) continue;
       yTabH[rk] = yWord[w];
-      yTabH[(size_t)W + rk] = (uint64_t)nY;
+      yTabH[(size_t)W + rk] = (uint64_t)nY | ((uint64_t)w << 32);  // (the word, for k_phase_a DENSE)
       nY += __builtin_popcountll(yWord[w]);
       ++rk;
     }
@@ -1482,6 +1494,11 @@ int gs_engine::stepOne() {
       const int rc = upload(dDev, &d, sizeof(Dev));
       if (rc) return rc;
     }
+    // denseGossip: the words v's fb row of this parity is written over (this
+    // hop's window, and what the row held two hops ago)
+    WMask amF{};
+    for (int k = 0; k < GS_MAX_WPL; ++k) amF.m[k] = amR.m[k] | amW.m[k] | amWPar[cur].m[k];
+    amWPar[cur] = amW;
     TIMED(this, GS_K_PHASE_A, launch_wpl(W, [&](auto w) {
             if (!nOwn) return;
             constexpr int WV = decltype(w)::value;
@@ -1489,13 +1506,18 @@ int gs_engine::stepOne() {
               k_flood_a<WV><<<nOwn, 64, 0, stream>>>(d, h, cur, amR, amW, amP);
             } else if (adv) {
               if (narrow)
-                k_phase_a<WV, true, true><<<nOwn, 64, lds, stream>>>(dDev, h, cur, head, amR, amW, amP, nR, nYp);
+                k_phase_a<WV, true, true><<<nOwn, 64, lds, stream>>>(dDev, h, cur, head, amR, amW, amP, amF, nR, nYp);
               else
-                k_phase_a<WV, false, true><<<nOwn, 64, lds, stream>>>(dDev, h, cur, head, amR, amW, amP, nR, nYp);
+                k_phase_a<WV, false, true><<<nOwn, 64, lds, stream>>>(dDev, h, cur, head, amR, amW, amP, amF, nR, nYp);
+            } else if (denseGossip) {
+              if (narrow)
+                k_phase_a<WV, true, false, true><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, amP, amF, nR, nYp);
+              else
+                k_phase_a<WV, false, false, true><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, amP, amF, nR, nYp);
             } else if (narrow) {
-              k_phase_a<WV, true, false><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, amP, nR, nYp);
+              k_phase_a<WV, true, false><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, amP, amF, nR, nYp);
             } else {
-              k_phase_a<WV, false, false><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, amP, nR, nYp);
+              k_phase_a<WV, false, false><<<nOwn, 64, lds, stream>>>(d, h, cur, head, amR, amW, amP, amF, nR, nYp);
             }
           }));
   }
@@ -2532,6 +2554,18 @@ int gs_set_peertx_capacity(gs_engine* g, int32_t home_bits, int32_t overflow_bit
   g->ptxOvfBits = overflow_bits;
   return GS_OK;
 }
+
+int gs_set_frontier_mode(gs_engine* g, int32_t mode) {
+  if (g->started) { gs_set_error("the frontier mode must be set before the first step"); return GS_ESTATE; }
+  if (mode != GS_FRONTIER_AUTO && mode != GS_FRONTIER_LISTS && mode != GS_FRONTIER_BITMAPS) {
+    gs_set_error("gs_set_frontier_mode: GS_FRONTIER_AUTO, GS_FRONTIER_LISTS or GS_FRONTIER_BITMAPS");
+    return GS_EINVAL;
+  }
+  g->frontierMode = mode;
+  return GS_OK;
+}
+
+int gs_frontier_dense(const gs_engine* g) { return g->started && (g->denseFlood || g->denseGossip) ? 1 : 0; }
 
 int gs_set_trace_rpc(gs_engine* g, int32_t on) {
   if (g->started) { gs_set_error("tracing must be set before the first step"); return GS_ESTATE; }

@@ -667,10 +667,15 @@ __device__ __forceinline__ const Dev& dev_of(const Dev* d) { return *d; }
 #endif
 template <bool NARROW, bool ADV>
 constexpr int pa_waves = (!NARROW && !ADV) ? GS_WPE_PA_WIDE : GS_WPE_PA;
-template <int WPL, bool NARROW, bool ADV>
+// DENSE (one topic, honest, one rank; gs_engine.hip denseGossip): pass 1 reads
+// the senders' frontier bitmaps fb instead of their lists (see "pass 1, dense"
+// below); passes 1b, 2 and 3 are the same code.  amF: the words the node's fb
+// row of this parity may hold bits in (written over in pass 2b).
+template <int WPL, bool NARROW, bool ADV, bool DENSE = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NARROW, ADV>))) void k_phase_a(
     PhaseADev<ADV> dArg, int64_t h, int cur, int head,
-                                                WMask amR, WMask amW, WMask amP, int nR, int nY) {
+                                                WMask amR, WMask amW, WMask amP, WMask amF, int nR, int nY) {
+  static_assert(!(DENSE && ADV), "the dense pass 1 is honest-only");
   const Dev& d = dev_of(dArg);
   extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
   const int nCnt = (d.T * d.maxDeg + 7) & ~7;
@@ -757,6 +762,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
       }
       if (pOff < 0) Ln = d.fln[prv][u];
     }
+  }
+  // DENSE: the sender's frontier row is read when it relays to v or (as an
+  // author) publishes to v; exD = the copies it did not send v because v had
+  // delivered them to it first (ReceivedFrom, counted by the sender: fex)
+  bool liveD = false;
+  int exD = 0;
+  if constexpr (DENSE) {
+    if (valid && (relayAll | pubAll)) {
+      liveD = d.fbN[prv][u] != 0 && (relayAll != 0 || d.nAuth[u] > 0);
+      exD = d.fex[prv][d.rev[base + lane]];
+    }
+    Ln = 0;
   }
   const uint64_t pushM = __ballot(pOff >= 0);  // senders whose copies were pushed
   GS_STAMP(0);
@@ -1145,6 +1162,103 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
     if (ADV && dropPass) drop(i, slot, true);
     else deliver(i, slot, true);
   };
+  if constexpr (DENSE) {
+    // ---- pass 1, dense (lane = rank of a word in the active window amR): the
+    // senders that sent v anything, ascending; sender i's copies are its
+    // frontier row fb[u] (its first deliveries of the previous hop plus its own
+    // publishes), all of it where it relays to v, its own messages only where it
+    // just publishes to v, less v's own messages (the author exclusion).  A bit
+    // the senders before i did not deliver and v has not seen is a first
+    // delivery by i.  The copies u did not send because v delivered them to u
+    // first (tag == jr in the list) are not in the bitmap's reach and leave the
+    // counts through exD.  Per-copy state the list walk keeps (sD, sFirst, the
+    // (sender, topic) counts, nSent / nGray / nCopies) comes out equal.  The
+    // rows hold bits in amR words only (what a sender first received in the
+    // previous hop was published within its window), so rank space reads just
+    // those: one word per lane at config3, eight senders' rows in flight.
+    int* const sLv = (int*)sComp;  // (the list walk's LDS, unused here)
+    int* const sCs = (int*)sPub;   // per sender: the copies its row holds for v
+    const uint64_t lmD = __ballot(liveD);
+    const int nLv = __popcll(lmD);
+    if (liveD) sLv[__popcll(lmD & ((1ull << lane) - 1))] = lane;
+    sCs[lane] = 0;
+    // (one topic, T == 1: a sender relays / publishes to v or not, and v
+    // either holds the topic or left it, dropping every copy)
+    const bool svT = sv & 1;
+    __syncthreads();
+    const uint64_t* const fbPrv = d.fb[prv];
+    uint64_t lateM = 0;
+    for (int r0 = 0; r0 < nR; r0 += 64) {
+      const int k = r0 + lane;
+      const bool act = k < nR;
+      const int w = act ? (int)(d.yTab[W + k] >> 32) : 0;  // the word of rank k (host table)
+      const uint64_t Y = act ? sYm[k] : 0ull;
+      const uint64_t Sv = act ? d.seen[(int64_t)v * W + w] : 0ull;
+      const uint64_t O = (act && authV) ? d.own[(int64_t)v * W + w] : 0ull;
+      const int yp = act ? (int)sYp[k] : 0;
+      uint64_t D = 0;
+      for (int k0 = 0; k0 < nLv; k0 += 8) {
+        uint64_t F[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int i = k0 + q < nLv ? sLv[k0 + q] : -1;
+          F[q] = (i >= 0 && act) ? fbPrv[(int64_t)(sSnd[i] & 0xFFFFFF) * W + w] : 0ull;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          if (k0 + q >= nLv) break;
+          const int i = sLv[k0 + q];
+          const bool r = lane_get64(relayAll, i) & 1, p = lane_get64(pubAll, i) & 1;
+          // its own messages matter where the relay and pub masks differ (a
+          // peer it publishes to but does not relay to, or the reverse): rare
+          uint64_t A = 0;
+          if (r != p) {
+            const int uq = sSnd[i] & 0xFFFFFF;
+            if (d.nAuth[uq] > 0 && act) A = d.own[(int64_t)uq * W + w];
+          }
+          const uint64_t f = F[q];
+          const uint64_t sb = (r ? (p ? f : f & ~A) : (p ? f & A : 0ull)) & ~O;
+          const int cs = wave_last(wave_incl_sum(__popcll(sb)));
+          if (lane == 0) sCs[i] += cs;
+          if (!svT || sSnd[i] < 0) continue;  // v left the topic / i is graylisted: dropped
+          lateM |= sb & ~Y & ~Sv;
+          const uint64_t y = sb & Y;
+          for (uint64_t nb = y & ~D & ~Sv; nb; nb &= nb - 1)
+            sFirst[yp + __popcll(Y & ((1ull << (__ffsll((long long)nb) - 1)) - 1))] = (uint8_t)i;
+          D |= y;
+        }
+      }
+      if (act) sD[k] = D;
+    }
+    if (lateM) set_err(d, E_LATE);  // a first delivery older than the window
+    __syncthreads();
+    if (liveD) {  // lane = sender: its copies, less the ReceivedFrom ones
+      const int c = sCs[lane] - ((relayAll & 1) ? exD : 0);
+      nSent += c;
+      if (gray) {
+        nGray += c;
+      } else if (svT) {
+        nCopies += c;
+        if (c) atomicAdd(&scnt[cword(lane, 0)], NARROW ? (uint32_t)c << (16 * (lane & 1)) : (uint32_t)c);
+      }
+    }
+    if (trv && valid && !gray && (relay | pub)) {
+      // a traced receiver's copy events, exactly per sent copy (its senders'
+      // lists carry the ReceivedFrom tags the bitmaps do not)
+      const uint32_t* L = d.fl[prv] + (int64_t)u * FC;
+      const int nL = d.fln[prv][u];
+      for (int k = 0; k < nL; ++k) {
+        const uint32_t ent = L[k];
+        const int slot = (int)(ent & 0xFFFF), tag = (int)(ent >> 16);
+        const int t = (int)__umulhi((unsigned)slot, d.stMagic);
+        bool sent = tag == 255 ? ((pub >> t) & 1) : ((relay >> t) & 1);
+        sent = sent && tag != jr;
+        if (sent && authV && d.slotSrc[slot] == v) sent = false;
+        if (sent) trace_emit(d, h, GS_TRACE_COPY, v, u, t, d.slotMid[slot], 2);
+      }
+    }
+    __syncthreads();
+  } else {
   walk(onCopy, true);
   if (__ballot(((relayAll | pubAll) & ~sv) != 0)) {
     // copies of topics v is not subscribed to: transmitted, then ignored
@@ -1166,6 +1280,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
         }
       }
     }
+  }
   }
   // ---- pass 1b: IWANT responses (in the sender's reply RPCs): every served
   // id of every accepted sender is one work item, spread over the lanes (an
@@ -1776,6 +1891,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
     int rank = running + incl - k;
     running += wave_last(incl);
     if (U | Rw[j]) d.seen[(int64_t)v * W + w] = (Sw[j] & ~Rw[j]) | U;
+    // DENSE: v's frontier row of the next hop (k_publish adds own publishes);
+    // amF also covers the words this parity's row held two hops ago
+    if (DENSE && w < W && wm_has(amF, w)) d.fb[cur][(int64_t)v * W + w] = Ud;
     if (U) {
       if ((U & Ow[j]) || !wm_has(amW, w)) set_err(d, E_LATE);
       if (gossipV && Ud) d.hist[((int64_t)head * d.nOwnH + (v - d.n0)) * W + w] = Hw[j] | Ud;
@@ -1789,6 +1907,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
                      d.slotMid[slot], 2);
         if (pmRow != nullptr)  // DeliverMessage does not add the deliverer to drec.peers
           atomicAnd((unsigned long long*)&pmRow[slot], ~(1ull << ff));
+        if (DENSE && d.slotSrc[slot] != (sSnd[ff] & 0xFFFFFF))
+          atomicAdd((int*)sStart + ff, 1);  // v will not send it back to ff (fex below)
         if (!noFwd) {
           if (rank < FC) Lv[rank] = (uint32_t)slot | ((uint32_t)ff << 16);
           else set_err(d, E_FCAP);
@@ -1840,6 +1960,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
   }
   GS_STAMP(4);
   if (lane == 0) d.fln[cur][v] = behaves(d, v, GS_BEHAVE_NO_FORWARD) ? 0 : (running < FC ? running : FC);
+  if constexpr (DENSE) {
+    // per out-edge: the fresh messages of this hop each neighbour delivered
+    // first (and did not author), which v's copies of the next hop leave out
+    __syncthreads();
+    if (valid) d.fex[cur][base + lane] = ((const int*)sStart)[lane];
+    if (lane == 0) d.fbN[cur][v] = running;
+  }
   const long long deliv = (long long)wave_sum_ll(nDeliv);
   const unsigned long long copies = wave_sum_ll(nCopies), s2 = wave_sum_ll(nSent), s3 = wave_sum_ll(nGray);
   if (lane == 0) {

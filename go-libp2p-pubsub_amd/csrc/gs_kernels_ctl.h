@@ -2189,7 +2189,10 @@ __global__ __launch_bounds__(64) void k_ptx_rebuild(Dev d, int last) {
   __syncthreads();
   int kept = 0;
   for (int k0 = 0; k0 < hN; k0 += 64 * 4) {
-    uint4 q = ((const uint4*)row)[(k0 >> 2) + lane];
+    // (a table smaller than the wave's 256 entries: the lanes past it read
+    // nothing, not the next nodes' rows)
+    const int qi = (k0 >> 2) + lane;
+    const uint4 q = qi < (hN >> 2) ? ((const uint4*)row)[qi] : make_uint4(0u, 0u, 0u, 0u);
     uint32_t ent[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {

@@ -15,7 +15,7 @@ from .params import (DefaultGossipSubParams, DefaultPeerGaterParams, GossipSubPa
                      eth2_thresholds, eth2_topic_score_params)
 from .engine import (PRODUCT_LIB, Engine, GossipEngineError, NewFloodSub, NewGossipSub,  # noqa: F401
                      NewRandomSub, PROTOCOLS, WithDevice, WithEventTracer, encode_trace, WithDirectPeers, WithFloodPublish, WithGossipSubParams,
-                     WithHop, WithMessageWindow, WithPartition, WithPeerScore, WithPeertxCapacity, WithRecordDeliveries, WithSeed,
+                     WithHop, WithMessageWindow, WithPartition, WithPeerScore, WithPeertxCapacity, WithFrontierLists, WithFrontierBitmaps, WithRecordDeliveries, WithSeed,
                      WithBehaviour, WithPeerGater, WithRPCAccounting, WithValidation, WithPeerExchange, WithDormant,
                      WithRouters, WithProtocols,
                      load)

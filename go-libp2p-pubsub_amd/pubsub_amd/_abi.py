@@ -196,6 +196,8 @@ ABI_FUNCTIONS = [
     ("gs_set_trace", C.c_int, [P, C.POINTER(u8), i64]),
     ("gs_set_trace_rpc", C.c_int, [P, i32]),
     ("gs_set_peertx_capacity", C.c_int, [P, i32, i32]),
+    ("gs_set_frontier_mode", C.c_int, [P, i32]),
+    ("gs_frontier_dense", C.c_int, [P]),
     ("gs_set_dormant", C.c_int, [P, i32, C.POINTER(i32), C.POINTER(i32)]),
     ("gs_trace_read", C.c_int, [P, P, i64, C.POINTER(i64)]),
     ("gs_trace_encode", C.c_int, [P, i64, i32, i64, C.POINTER(C.c_char_p), C.c_char_p, P, i64, C.POINTER(i64)]),

@@ -159,6 +159,19 @@ def WithPeertxCapacity(home_bits, overflow_bits):
     return ("peertx", (int(home_bits), int(overflow_bits)))
 
 
+def WithFrontierLists():
+    """Phase A reads the senders' per-copy frontier lists even where the engine
+    would OR their frontier bitmaps (gs_set_frontier_mode GS_FRONTIER_LISTS):
+    same results, the other kernel path (A/B runs and parity tests)."""
+    return ("frontier_mode", 1)
+
+
+def WithFrontierBitmaps():
+    """Phase A ORs the senders' frontier bitmaps wherever the engine supports
+    them (GS_FRONTIER_BITMAPS), also where the lists measured faster."""
+    return ("frontier_mode", 2)
+
+
 def WithPartition(rank, world, transport):
     """Simulate only this rank's node range; exchange RPCs with the other
     ranks through `transport` (a pubsub_amd.transport.TorchTransport) once per
@@ -247,6 +260,8 @@ class Engine:
         ptx = opts.get("peertx")
         if ptx is not None:
             _check(self.lib, self.lib.gs_set_peertx_capacity(h, *ptx))
+        if opts.get("frontier_mode"):
+            _check(self.lib, self.lib.gs_set_frontier_mode(h, opts["frontier_mode"]))
         acct = opts.get("rpc_acct")
         if acct is not None:
             ms, idl, tl = acct
@@ -324,6 +339,11 @@ class Engine:
         ms, nb = C.c_double(), C.c_int64()
         _check(self.lib, self.lib.gs_read_exchange_stats(self.h, C.byref(ms), C.byref(nb)))
         return ms.value, nb.value
+
+    @property
+    def frontier_dense(self):
+        """True once started if phase A ORs frontier bitmaps (gs_frontier_dense)."""
+        return bool(self.lib.gs_frontier_dense(self.h))
 
     def step(self, hops=1):
         _check(self.lib, self.lib.gs_step(self.h, int(hops)))

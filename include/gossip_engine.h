@@ -376,6 +376,20 @@ int gs_schedule_events(gs_engine* eng, int32_t n, const int32_t* kind, const int
  * GS_ECAPACITY error of gs_step.  Replaces no reference call: the reference's
  * peertx is an unbounded Go map. */
 int gs_set_peertx_capacity(gs_engine* eng, int32_t home_bits, int32_t overflow_bits);
+/* Before the first step: how phase A reads what the senders forwarded.
+ * GS_FRONTIER_AUTO (default): frontier bitmaps where they measured faster
+ * (floodsub without per-copy records), per-copy lists elsewhere.
+ * GS_FRONTIER_LISTS: lists everywhere.  GS_FRONTIER_BITMAPS: bitmaps wherever
+ * the engine supports them (also gossipsub on one topic without the
+ * adversarial model, churn, PX or a P3 window shorter than a message's
+ * lifetime; one rank).  Results are identical; only speed differs.  Replaces
+ * no reference call (an engine strategy knob).  gs_frontier_dense: 1 once
+ * started if phase A reads bitmaps. */
+#define GS_FRONTIER_AUTO 0
+#define GS_FRONTIER_LISTS 1
+#define GS_FRONTIER_BITMAPS 2
+int gs_set_frontier_mode(gs_engine* eng, int32_t mode);
+int gs_frontier_dense(const gs_engine* eng);
 int gs_step(gs_engine* eng, int64_t hops);
 /* Waits for all queued device work (no-op on the oracle). */
 int gs_sync(gs_engine* eng);

@@ -2117,6 +2117,16 @@ int gs_set_peertx_capacity(gs_engine* g, int32_t home_bits, int32_t overflow_bit
   }
   return GS_OK;
 }
+int gs_set_frontier_mode(gs_engine* g, int32_t mode) {
+  // the oracle walks every copy: no strategy to choose
+  if (g->sim.started) { set_error("the frontier mode must be set before the first step"); return GS_ESTATE; }
+  if (mode != GS_FRONTIER_AUTO && mode != GS_FRONTIER_LISTS && mode != GS_FRONTIER_BITMAPS) {
+    set_error("gs_set_frontier_mode: GS_FRONTIER_AUTO, GS_FRONTIER_LISTS or GS_FRONTIER_BITMAPS");
+    return GS_EINVAL;
+  }
+  return GS_OK;
+}
+int gs_frontier_dense(const gs_engine*) { return 0; }
 int gs_set_trace_rpc(gs_engine* g, int32_t on) {
   if (g->sim.started) { set_error("tracing must be set before the first step"); return GS_ESTATE; }
   g->sim.traceRpc = on != 0;

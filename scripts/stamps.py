@@ -16,7 +16,12 @@ def main():
     wl = bench.WORKLOADS[sys.argv[1] if len(sys.argv) > 1 else "config4"]
     # publish schedule of `rounds` rounds (bench.py: warm-up + steps + 1)
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 4
-    eng, _ = bench.build_engine(wl, rounds, 3, 0, lib=LIB)
+    extra = ()
+    fm = os.environ.get("GS_STAMPS_FRONTIER")  # phase A's frontier mode: lists / bitmaps (default: auto)
+    if fm in ("lists", "bitmaps"):
+        from pubsub_amd import WithFrontierBitmaps, WithFrontierLists
+        extra = ((WithFrontierLists if fm == "lists" else WithFrontierBitmaps)(),)
+    eng, _ = bench.build_engine(wl, rounds, 3, 0, lib=LIB, extra=extra)
     hops = int(sys.argv[2]) if len(sys.argv) > 2 else 1 + 2 * bench.HOPS_PER_ROUND + 3
     eng.step(hops)
     raw = C.CDLL(LIB)
