@@ -766,15 +766,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
   // DENSE: the sender's frontier row is read when it relays to v or (as an
   // author) publishes to v; exD = the copies it did not send v because v had
   // delivered them to it first (ReceivedFrom, counted by the sender: fex)
-  bool liveD = false;
+  bool liveD = false, authU = false;
   int exD = 0;
   if constexpr (DENSE) {
+    authU = valid && d.nAuth[u] > 0;
     if (valid && (relayAll | pubAll)) {
-      liveD = d.fbN[prv][u] != 0 && (relayAll != 0 || d.nAuth[u] > 0);
+      liveD = d.fbN[prv][u] != 0 && (relayAll != 0 || authU);
       exD = d.fex[prv][d.rev[base + lane]];
     }
     Ln = 0;
   }
+  const uint64_t authM = __ballot(authU);  // DENSE: the neighbours that author a live message
   const uint64_t pushM = __ballot(pOff >= 0);  // senders whose copies were pushed
   GS_STAMP(0);
   const bool authV = d.nAuth[v] > 0;  // v authored a live message: author exclusion possible
@@ -1907,8 +1909,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
                      d.slotMid[slot], 2);
         if (pmRow != nullptr)  // DeliverMessage does not add the deliverer to drec.peers
           atomicAnd((unsigned long long*)&pmRow[slot], ~(1ull << ff));
-        if (DENSE && d.slotSrc[slot] != (sSnd[ff] & 0xFFFFFF))
-          atomicAdd((int*)sStart + ff, 1);  // v will not send it back to ff (fex below)
+        // v will not send it back to ff (fex below) unless ff authored it (the
+        // author check needs a load only for a neighbour that authors at all)
+        if (DENSE && (!((authM >> ff) & 1) || d.slotSrc[slot] != (sSnd[ff] & 0xFFFFFF)))
+          atomicAdd((int*)sStart + ff, 1);
         if (!noFwd) {
           if (rank < FC) Lv[rank] = (uint32_t)slot | ((uint32_t)ff << 16);
           else set_err(d, E_FCAP);

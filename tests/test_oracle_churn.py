@@ -6,7 +6,7 @@ the reference's own assertions restated on the simulator.
     later message reaches hosts 5-19, and the ones that left get nothing new.
   TestGossipsubGraft (gossipsub_test.go:584-627): hosts subscribe one by one on a
     sparse graph; every message reaches every host.
-  TestScoreRetention (score_test.go:859-902) at the simulator level: a dropped
+  TestScoreRetention (score_test.go:861-903) at the simulator level: a dropped
     connection's record stays (with its negative score) for RetainScore, then
     reads 0.
 The GPU engine is compared with the oracle on the same scenarios in

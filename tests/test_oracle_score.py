@@ -41,7 +41,7 @@ def test_score_time_in_mesh(olib):  # score_test.go:13-50
     olib.ops_free(ps)
 
 
-def test_score_time_in_mesh_cap(olib):  # score_test.go:52-82
+def test_score_time_in_mesh_cap(olib):  # score_test.go:52-84
     p = PeerScoreParams(AppSpecificScore=True)
     tp = TopicScoreParams(TopicWeight=0.5, TimeInMeshWeight=1, TimeInMeshQuantum=Millisecond, TimeInMeshCap=10)
     ps = mk(olib, p, {MYTOPIC: tp})
@@ -59,7 +59,7 @@ def _fmd_params(decay, cap):
                             FirstMessageDeliveriesCap=cap, TimeInMeshQuantum=Second)
 
 
-def test_score_first_message_deliveries(olib):  # score_test.go:84-119
+def test_score_first_message_deliveries(olib):  # score_test.go:86-124
     ps = mk(olib, PeerScoreParams(AppSpecificScore=True), {MYTOPIC: _fmd_params(1.0, 2000)})
     olib.ops_add_peer(ps, A)
     olib.ops_graft(ps, A, MYTOPIC, 0)
@@ -69,7 +69,7 @@ def test_score_first_message_deliveries(olib):  # score_test.go:84-119
     olib.ops_free(ps)
 
 
-def test_score_first_message_deliveries_cap(olib):  # score_test.go:121-156
+def test_score_first_message_deliveries_cap(olib):  # score_test.go:126-164
     ps = mk(olib, PeerScoreParams(AppSpecificScore=True), {MYTOPIC: _fmd_params(1.0, 50)})
     olib.ops_add_peer(ps, A)
     olib.ops_graft(ps, A, MYTOPIC, 0)
@@ -79,7 +79,7 @@ def test_score_first_message_deliveries_cap(olib):  # score_test.go:121-156
     olib.ops_free(ps)
 
 
-def test_score_first_message_deliveries_decay(olib):  # score_test.go:158-204
+def test_score_first_message_deliveries_decay(olib):  # score_test.go:166-215
     ps = mk(olib, PeerScoreParams(AppSpecificScore=True), {MYTOPIC: _fmd_params(0.9, 2000)})
     olib.ops_add_peer(ps, A)
     olib.ops_graft(ps, A, MYTOPIC, 0)
@@ -102,7 +102,7 @@ def _mmd_params(activation, decay, window=10 * Millisecond):
                             FirstMessageDeliveriesWeight=0, TimeInMeshQuantum=Second)
 
 
-def test_score_mesh_message_deliveries(olib):  # score_test.go:206-307
+def test_score_mesh_message_deliveries(olib):  # score_test.go:217-308
     tp = _mmd_params(Second, 1.0)
     ps = mk(olib, PeerScoreParams(AppSpecificScore=True), {MYTOPIC: tp})
     now = 0
@@ -129,7 +129,7 @@ def test_score_mesh_message_deliveries(olib):  # score_test.go:206-307
     olib.ops_free(ps)
 
 
-def test_score_mesh_message_deliveries_decay(olib):  # score_test.go:309-362
+def test_score_mesh_message_deliveries_decay(olib):  # score_test.go:310-369
     tp = _mmd_params(0, 0.9)
     ps = mk(olib, PeerScoreParams(AppSpecificScore=True), {MYTOPIC: tp})
     olib.ops_add_peer(ps, A)
@@ -148,7 +148,7 @@ def test_score_mesh_message_deliveries_decay(olib):  # score_test.go:309-362
     olib.ops_free(ps)
 
 
-def test_score_mesh_failure_penalty(olib):  # score_test.go:364-441
+def test_score_mesh_failure_penalty(olib):  # score_test.go:371-450
     tp = TopicScoreParams(TopicWeight=1, MeshFailurePenaltyWeight=-1, MeshFailurePenaltyDecay=1.0,
                           MeshMessageDeliveriesActivation=0, MeshMessageDeliveriesWindow=10 * Millisecond,
                           MeshMessageDeliveriesThreshold=20, MeshMessageDeliveriesCap=100,
@@ -180,7 +180,7 @@ REJECT = {n: i for i, n in enumerate([
     "validation failed", "validation ignored", "self originated message"])}
 
 
-def test_score_invalid_message_deliveries(olib):  # score_test.go:443-476
+def test_score_invalid_message_deliveries(olib):  # score_test.go:452-487
     ps = mk(olib, PeerScoreParams(AppSpecificScore=True), {MYTOPIC: _imd_params(1.0)})
     olib.ops_add_peer(ps, A)
     olib.ops_graft(ps, A, MYTOPIC, 0)
@@ -191,7 +191,7 @@ def test_score_invalid_message_deliveries(olib):  # score_test.go:443-476
     olib.ops_free(ps)
 
 
-def test_score_invalid_message_deliveries_decay(olib):  # score_test.go:478-520
+def test_score_invalid_message_deliveries_decay(olib):  # score_test.go:489-534
     ps = mk(olib, PeerScoreParams(AppSpecificScore=True), {MYTOPIC: _imd_params(0.9)})
     olib.ops_add_peer(ps, A)
     olib.ops_graft(ps, A, MYTOPIC, 0)
@@ -207,7 +207,7 @@ def test_score_invalid_message_deliveries_decay(olib):  # score_test.go:478-520
     olib.ops_free(ps)
 
 
-def test_score_reject_message_deliveries(olib):  # score_test.go:522-643
+def test_score_reject_message_deliveries(olib):  # score_test.go:536-666
     ps = mk(olib, PeerScoreParams(AppSpecificScore=True), {MYTOPIC: _imd_params(1.0)})
     olib.ops_add_peer(ps, A)
     olib.ops_add_peer(ps, B)
@@ -244,7 +244,7 @@ def test_score_reject_message_deliveries(olib):  # score_test.go:522-643
     olib.ops_free(ps)
 
 
-def test_score_application_score(olib):  # score_test.go:645-672
+def test_score_application_score(olib):  # score_test.go:668-694
     ps = mk(olib, PeerScoreParams(AppSpecificScore=True, AppSpecificWeight=0.5), {})
     olib.ops_add_peer(ps, A)
     olib.ops_graft(ps, A, MYTOPIC, 0)
@@ -265,7 +265,7 @@ def _set_ips(olib, ps, p, *ips):
     olib.ops_set_ips(ps, p, len(ips), arr)
 
 
-def test_score_ip_colocation(olib):  # score_test.go:674-720
+def test_score_ip_colocation(olib):  # score_test.go:696-744
     ps = mk(olib, PeerScoreParams(AppSpecificScore=True, IPColocationFactorThreshold=1,
                                   IPColocationFactorWeight=-1), {})
     for p in (A, B, Cp, D):
@@ -283,7 +283,7 @@ def test_score_ip_colocation(olib):  # score_test.go:674-720
     olib.ops_free(ps)
 
 
-def test_score_ip_colocation_whitelist(olib):  # score_test.go:722-778
+def test_score_ip_colocation_whitelist(olib):  # score_test.go:746-803
     ps = mk(olib, PeerScoreParams(AppSpecificScore=True, IPColocationFactorThreshold=1,
                                   IPColocationFactorWeight=-1), {})
     olib.ops_add_whitelist(ps, _ip("2.3.0.0"), 0xFFFF0000)
@@ -300,7 +300,7 @@ def test_score_ip_colocation_whitelist(olib):  # score_test.go:722-778
     olib.ops_free(ps)
 
 
-def test_score_behaviour_penalty(olib):  # score_test.go:780-833
+def test_score_behaviour_penalty(olib):  # score_test.go:805-859
     ps = mk(olib, PeerScoreParams(AppSpecificScore=True, BehaviourPenaltyWeight=-1,
                                   BehaviourPenaltyDecay=0.99), {})
     olib.ops_add_penalty(ps, A, 1)  # non-existent peer: no effect
@@ -316,7 +316,7 @@ def test_score_behaviour_penalty(olib):  # score_test.go:780-833
     olib.ops_free(ps)
 
 
-def test_score_retention(olib):  # score_test.go:835-877
+def test_score_retention(olib):  # score_test.go:861-903
     ps = mk(olib, PeerScoreParams(AppSpecificScore=True, AppSpecificWeight=1.0, RetainScore=Second), {})
     olib.ops_set_app_score(ps, A, -1000)
     olib.ops_add_peer(ps, A)
@@ -335,7 +335,7 @@ def test_score_retention(olib):  # score_test.go:835-877
     olib.ops_free(ps)
 
 
-def test_score_recap_topic_params(olib):  # score_test.go:879-968
+def test_score_recap_topic_params(olib):  # score_test.go:905-1000
     tp = TopicScoreParams(TopicWeight=1, MeshMessageDeliveriesWeight=-1,
                           MeshMessageDeliveriesActivation=Second, MeshMessageDeliveriesWindow=10 * Millisecond,
                           MeshMessageDeliveriesThreshold=20, MeshMessageDeliveriesCap=100,
@@ -364,7 +364,7 @@ def test_score_recap_topic_params(olib):  # score_test.go:879-968
     olib.ops_free(ps)
 
 
-def test_score_reset_topic_params(olib):  # score_test.go:970-1023
+def test_score_reset_topic_params(olib):  # score_test.go:1002-1062
     ps = mk(olib, PeerScoreParams(AppSpecificScore=True), {MYTOPIC: _imd_params(1.0)})
     olib.ops_add_peer(ps, A)
     for i in range(100):
