@@ -1545,6 +1545,24 @@ __device__ __forceinline__ void hb_pair(const Dev& d, int v, int64_t base, int d
   const bool noFwd = behaves(d, v, GS_BEHAVE_NO_FORWARD);
   const bool ihaveSpam = behaves(d, v, GS_BEHAVE_IHAVE_SPAM);
   const bool oppTick = ticks % d.OGT == 0;
+  // Steady topics: step 1 changes nothing for a topic
+  // whose mesh has no member scored below 0, is not above Dhi, and is below
+  // Dlo (or short of Dout outbound members) only where no candidate peer
+  // could be grafted (negative-score prune, Dlo / Dhi / Dout below;
+  // opportunistic ticks and GRAFT spammers are never steady).  Counted for
+  // every topic at once: lane t of a transposed edge mask holds topic t's
+  // edges (the lower half's edges are all of them).
+  const bool lo = lane < 32 && vm;
+  const uint64_t mL = lo ? meshl : 0ull;
+  // graft candidates of getPeers' filter in step 1: topic peers not in the
+  // mesh nor in backoff, not direct, score >= 0
+  const uint64_t cL = (lo && !dir && S >= 0) ? (subv & ~meshl & ~boM) : 0ull;
+  const int cntT = __popcll(wave_transpose64(mL)), outT = __popcll(wave_transpose64(ob ? mL : 0ull));
+  const bool negT = wave_transpose64(S < 0 ? mL : 0ull) != 0;
+  const bool candT = wave_transpose64(cL) != 0, obCandT = wave_transpose64(ob ? cL : 0ull) != 0;
+  const bool busyT = lane < d.T && ((joined >> lane) & 1) &&
+                     (negT || cntT > d.Dhi || (cntT < d.Dlo && candT) || (cntT >= d.Dlo && outT < d.Dout && obCandT));
+  const uint64_t busy = (oppTick || graftSpam) ? ~0ull : __ballot(busyT);
   uint64_t jm = joined;
   uint64_t myT = 0;  // the topics this half handled
   while (jm) {
@@ -1560,6 +1578,9 @@ __device__ __forceinline__ void hb_pair(const Dev& d, int v, int64_t base, int d
     const bool inTopic = vm && act && ((subv >> tt) & 1);
     bool m = vm && act && (meshl & bit);
     bool pr = false, gr = false;  // pruned / grafted at t in this pass
+    // both topics steady: step 1 changes nothing (wave-uniform)
+    const bool fast = !((busy >> ta) & 1) && (tb < 0 || !((busy >> tb) & 1));
+    if (!fast) {
     // ---- 1. decisions
     if (m && (S < 0 || (graftSpam && ticks == 1))) {
       pr = true;
@@ -1692,6 +1713,7 @@ __device__ __forceinline__ void hb_pair(const Dev& d, int v, int64_t base, int d
         if (be != 0 && be > now) spamGraft |= bit;
       }
     }
+    }  // (!fast)
     const unsigned long long c1 = GS_CLK();
     // ---- 2. stats writes and emitGossip's live scores, in topic order
     const int nmA = lane_get(nmT, ta), nmB = tb >= 0 ? lane_get(nmT, tb) : 0;
@@ -1699,6 +1721,12 @@ __device__ __forceinline__ void hb_pair(const Dev& d, int v, int64_t base, int d
     const bool emits = nm > 0 && !noFwd && !ihaveSpam;
     const bool baseE = emits && vm && inTopic && !m && !dir;
     bool cand = false;
+    // and no live score of this pair's candidates needs a refresh: step 2
+    // changes nothing either (the halves' live-score states are equal at a
+    // pair boundary and stay so)
+    if (fast && !__ballot(baseE && (dirty || (dirtyUp && !(Slive >= d.gossipThr)))))
+      cand = baseE && Slive >= d.gossipThr;
+    else
     for (int hh = 0; hh < 2; ++hh) {
       if (h == hh) {
         if (pr) {
