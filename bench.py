@@ -272,10 +272,29 @@ def cpu_baseline(wl, seconds=20.0):
     lib = os.path.join(REPO, "oracle", "_build", "libgossip_oracle.so")
     if not os.path.exists(lib):
         return None
-    threads = ctypes.CDLL(lib).gs_oracle_threads()  # OMP_NUM_THREADS: 16 on the GPU box (its CPU share)
+    olib = ctypes.CDLL(lib)
+    threads = olib.gs_oracle_threads()  # OMP_NUM_THREADS: 16 on the GPU box (its CPU share)
+    if hasattr(olib, "gs_oracle_set_threads"):
+        # one thread and all cores.  The one-thread leg first, on
+        # half the time budget; the headline value is the all-cores leg
+        olib.gs_oracle_set_threads(1)
+        one = cpu_baseline_at(wl, lib, 1, seconds / 2, scale=8)
+        olib.gs_oracle_set_threads(threads)
+        out = cpu_baseline_at(wl, lib, threads, seconds)
+        if one and out:
+            out["value_1thread"] = one["value"]
+            out["sample_1thread"] = one["sample"]
+            out["parallel_speedup"] = out["value"] / one["value"] if one["value"] else None
+        return out
+    return cpu_baseline_at(wl, lib, threads, seconds)
+
+
+def cpu_baseline_at(wl, lib, threads, seconds, scale=1):
+    """One leg of cpu_baseline: `scale` divides the sample's peer count (the
+    one-thread leg runs a smaller graph in a comparable time)."""
     if wl.get("router") in ("floodsub", "randomsub"):
-        return cpu_baseline_config2(wl, lib, threads, seconds)
-    n = 2000
+        return cpu_baseline_config2(wl, lib, threads, seconds, scale)
+    n = 2000 // scale
     swl = dict(wl, n=n)
     rounds = 8
     eng, _ = build_engine(swl, rounds + 2, 11, 0, lib=lib, n=n)
@@ -303,11 +322,11 @@ def cpu_baseline(wl, seconds=20.0):
                       f"after 1 warm-up round, {dt:.1f} s"}
 
 
-def cpu_baseline_config2(wl, lib, threads, seconds):
+def cpu_baseline_config2(wl, lib, threads, seconds, scale=1):
     """config2 on the oracle: the same router, degree and one-hop batches on a
-    20,000-peer graph, 200-message batches (each step fully propagated),
-    stepped until about `seconds` have passed."""
-    n, m = 20_000, 200
+    20,000-peer graph (divided by `scale`), 200-message batches (each step
+    fully propagated), stepped until about `seconds` have passed."""
+    n, m = 20_000 // scale, 200
     swl = dict(wl, n=n, msgs=m)
     hps = hops_per_step(wl)
     eng, _ = build_engine(swl, 50, 11, 0, lib=lib, n=n)

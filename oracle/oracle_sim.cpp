@@ -2280,6 +2280,10 @@ int gs_oracle_threads(void) {
   return n;
 }
 
+// Oracle-only: sets the OpenMP threads of the per-node phases (bench.py's
+// cpu_baseline times the sample at 1 thread and at the box's CPU share).
+void gs_oracle_set_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }
+
 int gs_read_exchange_stats(gs_engine*, double* host_ms, int64_t* bytes_in) {
   *host_ms = 0;
   *bytes_in = 0;
