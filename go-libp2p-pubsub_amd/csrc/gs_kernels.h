@@ -2323,6 +2323,8 @@ __global__ __launch_bounds__(64) void k_push(Dev d, int cur) {
   // the edges' sets
   const int Ln0 = d.fln[cur][u];
   const uint32_t ent0 = L[lane];
+  // the second 64 entries too (a list holds ~100 at config4), within the row
+  const uint32_t ent1 = L[64 + lane < d.FC ? 64 + lane : d.FC - 1];
   // every out-edge gets a record; one to a receiver on another rank travels
   // with the hop's exchange (gs_exchange.h k_xp_pack)
   const bool local = lane < deg;
@@ -2356,7 +2358,7 @@ __global__ __launch_bounds__(64) void k_push(Dev d, int cur) {
   const int nch = (Ln + 63) >> 6;
   int s0 = 0, s1 = 0;
   const uint64_t E0 = wave_transpose64(lane < Ln ? dest(ent0, s0) : 0ull);
-  const uint64_t E1 = nch > 1 ? wave_transpose64(64 + lane < Ln ? dest(L[64 + lane], s1) : 0ull) : 0ull;
+  const uint64_t E1 = nch > 1 ? wave_transpose64(64 + lane < Ln ? dest(ent1, s1) : 0ull) : 0ull;
   int cnt = __popcll(E0) + __popcll(E1);
   for (int c = 2; c < nch; ++c) {
     int slot;
