@@ -67,9 +67,12 @@
 // push arena: a region of this many 16-bit slots per owned sender
 #define GS_PUSHR 2048
 #define GS_PTX_BITS 10 // mcache.peertx hash slots per node: 2^10 (2^12 when IWANT spammers run)
-#define GS_CUTS 64     // IHAVE entries above MaxIHaveLength one node can cut per hop
-// phase B dynamic LDS: the MaxIHaveLength-cut tables (cut mode)
-#define GS_CUTLDS (256 * 4 + GS_CUTS * 4 + GS_CUTS * 16 + 64 * 16 + 128 * 4 + 16)
+#define GS_CUTS 64     // IHAVE items above MaxIHaveLength whose cut key one node keeps in LDS per hop
+                       // (more spill into the per-rank table Dev::cutSpK / cutSpM)
+#define GS_CUTSPILL (1 << 20)  // spilled cut keys per rank per hop
+// phase B dynamic LDS: the MaxIHaveLength-cut tables (cut mode): radix
+// histogram, per-word cut-bit prefix, item / sender cut keys, cut bits, count
+#define GS_CUTLDS (256 * 4 + 128 * 4 + GS_CUTS * 16 + 64 * 16 + 128 * 4 + 16)
 
 // device counter slots (same order as gs_counters)
 enum {
@@ -323,6 +326,11 @@ struct Dev {
   int64_t poolSubCap;
   int32_t poolSub;
   int32_t poolS0Mask;  // first sub-arena tried = block % poolSub & mask (0: sub-arena 0 first, tests)
+  // MaxIHaveLength item cuts past a node's GS_CUTS in LDS: (key, id) thresholds
+  // taken by bump (cutSpN, reset per hop) from GS_CUTSPILL entries per rank
+  unsigned long long* cutSpK;
+  int64_t* cutSpM;
+  unsigned long long* cutSpN;
   // message slots
   int32_t* slotSrc;
   int64_t* slotPubHop;

@@ -862,6 +862,9 @@ int gs_engine::start() {
   }
   for (int k = 0; k < 2; ++k) { x.pool[k] = dalloc<int32_t>((size_t)poolSeg * world); chk(x.pool[k]); }
   x.poolCnt = dalloc<unsigned long long>((size_t)2 * x.poolSub * 16); chk(x.poolCnt);
+  x.cutSpK = dalloc<unsigned long long>(GS_CUTSPILL); x.cutSpM = dalloc<int64_t>(GS_CUTSPILL);
+  x.cutSpN = dalloc<unsigned long long>(1);
+  chk(x.cutSpK); chk(x.cutSpM); chk(x.cutSpN);
   x.doPX = doPX ? 1 : 0;
   x.PrunePeers = gp.PrunePeers;
   x.acceptPX = thr.AcceptPXThreshold;
@@ -1565,6 +1568,7 @@ int gs_engine::stepOne() {
       }
     }
     const size_t ldsB = cutMode ? GS_CUTLDS : 0;
+    if (cutMode & 1) HIPCHECK(hipMemsetAsync(d.cutSpN, 0, 8, stream));
     if (nOwn) {
       const int rc = upload(dDev, &d, sizeof(Dev));
       if (rc) return rc;
@@ -1711,7 +1715,8 @@ int gs_engine::deviceErrorCode(int32_t err) {
       gs_set_error("a message was first delivered later than the message window allows; raise slots_per_topic");
       return GS_ECAPACITY;
     case E_TRUNCATE:
-      gs_set_error("more than 64 IHAVE entries above MaxIHaveLength reached one node in one hop");
+      gs_set_error("the MaxIHaveLength cut table overflowed (more than 64 over-length IHAVE items at a node "
+                   "spill into 2^20 entries per rank per hop), or a sender cut arose outside cut mode");
       return GS_ECAPACITY;
     case E_FCAP:
       gs_set_error("more first deliveries (plus own publishes) at one node in one hop than its "

@@ -808,22 +808,25 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
     // (GS_SITE_IWANT key, id) (handleIHave, :650-653).
     extern __shared__ __attribute__((aligned(16))) uint32_t smemB[];
     uint32_t* const cHist = smemB;                                  // [256] radix histogram
-    int* const cItem = (int*)(smemB + 256);                         // [GS_CUTS] cut items
-    unsigned long long* const cK = (unsigned long long*)(smemB + 256 + GS_CUTS);  // [GS_CUTS] threshold key
+    int* const cPre = (int*)(smemB + 256);                          // [128] cut bits below word j
+    unsigned long long* const cK = (unsigned long long*)(smemB + 256 + 128);  // [GS_CUTS] threshold key
     long long* const cM = (long long*)(cK + GS_CUTS);               // [GS_CUTS] threshold id
     unsigned long long* const iK = (unsigned long long*)(cM + GS_CUTS);  // [64] sender cut key
     long long* const iM = (long long*)(iK + 64);                   // [64] sender cut id
     uint32_t* const cBits = (uint32_t*)(iM + 64);                   // [128] item is cut
     int* const cN = (int*)(cBits + 128);
+    unsigned long long* const cSp = (unsigned long long*)(cN + 2);  // first spilled entry of this node
     // the item cuts' scratch lives in static LDS that is free until pass a:
     // select_kth_est's kept (key, id) pairs + counter in sH past sTm (sKey ..
-    // sCand are initialised after the cuts), the cut items' id counts in step
-    // 2's request offsets
+    // sCand are initialised after the cuts)
     unsigned long long* const cand = (unsigned long long*)(sH + 192);
     static_assert(192 * 4 + GS_SEL_CAP * 16 + 8 <= 768 * 4, "select_kth_est pairs must fit in sH past sTm");
-    int* const cNm = sReqOff;  // [GS_CUTS] ids of a cut item
-    static_assert(GS_CUTS <= 64, "cNm aliases sReqOff[64]");
+    // A cut item's index c is its rank among the cut bits (item order); c <
+    // GS_CUTS keeps its threshold in LDS, the rest in the rank's spill table
+    // from *cSp on (emitGossip truncates every over-length item,
+    // gossipsub.go:1700-1710, however many reach one node)
     int nCut = 0;
+    unsigned long long spill0 = 0;
     if (cutMode & 1) {
       for (int k = lane; k < 128; k += 64) cBits[k] = 0u;
       if (lane == 0) *cN = 0;
@@ -846,25 +849,42 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
           for (int w = t * Wt; w < (t + 1) * Wt; ++w) nm += __popcll(d.gw[(int64_t)uu * W + w]);
         }
         if (nm > d.MaxIHaveLength && (!waveSum || lane == 0)) {
-          const int pos = atomicAdd(cN, 1);
-          if (pos < GS_CUTS) {
-            cItem[pos] = tb;
-            cNm[pos] = nm;
-            atomicOr(&cBits[tb >> 5], 1u << (tb & 31));
-          } else {
-            set_err(d, E_TRUNCATE);
-          }
+          atomicAdd(cN, 1);
+          atomicOr(&cBits[tb >> 5], 1u << (tb & 31));
         }
       }
       __syncthreads();
-      nCut = min(*cN, GS_CUTS);
+      nCut = *cN;
+      {
+        int tot0, tot1;
+        const int p0 = lane_prefix(__popc(cBits[lane]), &tot0);
+        const int p1 = lane_prefix(__popc(cBits[lane + 64]), &tot1);
+        cPre[lane] = p0;
+        cPre[lane + 64] = tot0 + p1;
+      }
+      if (nCut > GS_CUTS) {
+        if (lane == 0) {
+          const unsigned long long b = atomicAdd(d.cutSpN, (unsigned long long)(nCut - GS_CUTS));
+          *cSp = b;
+          if (b + (unsigned long long)(nCut - GS_CUTS) > (unsigned long long)GS_CUTSPILL) set_err(d, E_TRUNCATE);
+        }
+      }
+      __syncthreads();
+      if (nCut > GS_CUTS) spill0 = *cSp;
+      int cw = 0;
+      uint32_t cb = cBits[0];
       for (int c = 0; c < nCut; ++c) {
-        const int tb = cItem[c];
+        while (cb == 0u) cb = cBits[++cw];  // the c-th cut item in item order
+        const int tb = cw * 32 + __ffs(cb) - 1;
+        cb &= cb - 1u;
         int k;
         const int i = item_sender(sIt, tb * nCh, k);
         const int t = kth_bit(sTm[i], k / nCh);
         const int uu = sNode[i];
         const uint64_t* const g = d.gw + (int64_t)uu * W + t * Wt;  // the sender's words of topic t
+        int nm = 0;  // its ids
+        for (int w = lane; w < Wt; w += 64) nm += __popcll(g[w]);
+        nm = wave_last(wave_incl_sum(nm));
         unsigned long long K;
         long long M;
         // every gossip id of the sender's topic t in word order, by units: a
@@ -963,14 +983,36 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
             }
           }
         };
-        select_kth_est(each, d.MaxIHaveLength, cNm[c], cHist, cand, K, M);
+        select_kth_est(each, d.MaxIHaveLength, nm, cHist, cand, K, M);
         if (lane == 0) {
-          cK[c] = K;
-          cM[c] = M;
+          if (c < GS_CUTS) {
+            cK[c] = K;
+            cM[c] = M;
+          } else if (spill0 + (unsigned long long)(c - GS_CUTS) < (unsigned long long)GS_CUTSPILL) {
+            d.cutSpK[spill0 + (c - GS_CUTS)] = K;
+            d.cutSpM[spill0 + (c - GS_CUTS)] = M;
+          }
         }
         __syncthreads();
       }
     }
+    // item tb's cut threshold (K, M); false: tb is not cut
+    auto cutOf = [&](int tb, unsigned long long& K, long long& M) {
+      if (!nCut) return false;
+      const uint32_t wb = cBits[tb >> 5];
+      if (!((wb >> (tb & 31)) & 1u)) return false;
+      const int c = cPre[tb >> 5] + __popc(wb & ((1u << (tb & 31)) - 1u));
+      if (c < GS_CUTS) {
+        K = cK[c];
+        M = cM[c];
+      } else {
+        const unsigned long long s = spill0 + (unsigned long long)(c - GS_CUTS);
+        const bool in = s < (unsigned long long)GS_CUTSPILL;  // (else E_TRUNCATE is set)
+        K = in ? d.cutSpK[s] : ~0ull;
+        M = in ? (long long)d.cutSpM[s] : INT64_MAX;
+      }
+      return true;
+    };
     // (sH past sTm was the cuts' scratch until here)
     sKey[lane] = ~0ull;
     sMid[lane] = INT64_MAX;
@@ -980,11 +1022,9 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
     // the advertised wants of item b (topic t, chunk ch): fn(w, want) per word
     // with a want
     auto wants = [&](int b, int uu, int t, int ch, auto&& fn) {
-      int ci = -1;
-      const int tb = b / nCh;  // the (sender, topic) item
-      if (nCut && ((cBits[tb >> 5] >> (tb & 31)) & 1))
-        for (int c = 0; c < nCut; ++c)
-          if (cItem[c] == tb) ci = c;
+      unsigned long long K = 0;
+      long long M = 0;
+      const bool cut = cutOf(b / nCh, K, M);  // the (sender, topic) item's cut
       const int wBeg = nCh > 1 ? t * Wt + 16 * ch : t * Wt;
       const int wEnd = nCh > 1 ? min(wBeg + 16, (t + 1) * Wt) : (t + 1) * Wt;
       for (int w0 = wBeg; w0 < wEnd; w0 += 4) {
@@ -994,10 +1034,8 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           uint64_t want = w0 + q < wEnd ? g[q] & ~sseen[w0 + q] : 0ull;
-          if (want && ci >= 0) {
+          if (want && cut) {
             // keep the ids of the sender's subset for v
-            const unsigned long long K = cK[ci];
-            const long long M = cM[ci];
             uint64_t y = want;
             while (y) {
               const int bb = __ffsll((long long)y) - 1;
@@ -1086,19 +1124,18 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
           for (int k = 0; k < nItems; ++k) {
             const int t = kth_bit(sTm[i], k);
             const int b = b0 + k;
-            int ci = -1;
-            if (nCut && ((cBits[b >> 5] >> (b & 31)) & 1))
-              for (int c = 0; c < nCut; ++c)
-                if (cItem[c] == b) ci = c;
+            unsigned long long cK0 = 0;
+            long long cM0 = 0;
+            const bool cut = cutOf(b, cK0, cM0);
             for (int w = t * Wt + lane; w < (t + 1) * Wt; w += 64) {
               uint64_t y = d.gw[(int64_t)uu * W + w] & ~sseen[w];
               while (y) {
                 const int bb = __ffsll((long long)y) - 1;
                 y &= y - 1;
                 const int64_t mid = d.slotMid[(int64_t)w * 64 + bb];
-                if (ci >= 0) {
+                if (cut) {
                   const unsigned long long ke = gs_key64_mid(d.seed, GS_SITE_EMIT_MIDS, uu, v, (uint32_t)mid, (uint32_t)(h - 1));
-                  if (ke > cK[ci] || (ke == cK[ci] && mid > cM[ci])) continue;
+                  if (ke > cK0 || (ke == cK0 && mid > cM0)) continue;
                 }
                 fn(gs_key64_mid(d.seed, GS_SITE_IWANT, v, uu, (uint32_t)mid, (uint32_t)h), mid);
               }

@@ -191,7 +191,21 @@ HEAVY = {
     # publish of a 150-message burst by node 0 to its 24 peers, T = 4
     "push_overflow": lambda lib, x=(): gossipsub_scored(lib, n=200, k=24, topics=4, flood=True, window=512,
                                                         msgs=400, hb=10, seed=27, burst=(0, 150, 40), extra=x),
+    # emitGossip's MaxIHaveLength truncation (gossipsub.go:1700-1710) on more
+    # (sender, topic) items per node and hop than phase B keeps in LDS (GS_CUTS
+    # = 64): 16 topics, MaxIHaveLength 3, gossip to every non-mesh peer, so a
+    # heartbeat's IHAVE hop brings ~250 over-length items to each node and the
+    # thresholds past the 64th spill into the rank's cut table
+    "cut_spill_16t": lambda lib, x=(): gossipsub_scored(lib, n=200, k=24, topics=16, window=128, msgs=600, hb=12,
+                                                        seed=29, params=_cut_spill_params(), extra=x),
 }
+
+
+def _cut_spill_params():
+    p = GossipSubParams()
+    p.MaxIHaveLength = 3
+    p.GossipFactor = 1.0
+    return p
 SCENARIOS.update(HEAVY)
 
 

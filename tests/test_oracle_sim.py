@@ -74,3 +74,22 @@ def test_cut_honest_4t_reaches_the_sender_cut_mode(oracle_path):
     e.step(hops)
     c = e.counters()
     assert c["ihave_sent"] > 0 and c["iwant_sent"] > 0 and c["deliveries"] == 9000 * 199
+
+
+def test_cut_spill_16t_cuts_more_items_than_lds_holds(oracle_path):
+    """cut_spill_16t must bring more over-length IHAVE items to one node in one
+    hop than phase B keeps in LDS (GS_CUTS = 64), so the GPU runs its cut-table
+    spill.  Traced IHAVE lists are cut to MaxIHaveLength (3) ids by the host
+    (include/gs_trace.h); the gossip windows of this schedule hold ~11 ids per
+    topic, so an item of 3 ids is a cut one."""
+    from test_trace_rpc import run as trace_run, blocks, RECV
+    from pubsub_amd import _abi
+    _, _, ev = trace_run(oracle_path, "cut_spill_16t", [0, 7])
+    per = {}
+    for head, items in blocks(ev):
+        if head["type"] != RECV:
+            continue
+        n = np.bincount(items["topic"][items["reason"] == _abi.GS_RPC_ITEM_IHAVE].astype(np.int64), minlength=16)
+        key = (int(head["node"]), int(head["hop"]))
+        per[key] = per.get(key, 0) + int((n >= 3).sum())
+    assert max(per.values()) > 2 * 64, max(per.values())

@@ -135,6 +135,8 @@ def run_partitioned(world, name, oracle):
     (2, "c4shape"),
     (3, "cut_honest_4t"),
     (2, "push_overflow"),
+    # MaxIHaveLength cuts past GS_CUTS per node: each rank's own cut table
+    (2, "cut_spill_16t"),
     # randomsub: a sender's per-message target masks (d.sel) travel with its
     # frontier list entries (gs_exchange.h k_x_sel); at T >= 4 k_push applies
     # them on the sender's rank
