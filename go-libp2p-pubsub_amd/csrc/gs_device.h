@@ -109,7 +109,7 @@ __device__ __forceinline__ int64_t quantum_div(int64_t mt, const TopicP& tp) {
 struct AcctT {
   int32_t msgF;       // RPC.publish entry of a message of the topic
   int32_t graftEnt;   // ControlMessage.graft entry
-  int32_t pruneEnt;   // ControlMessage.prune entry (makePrune: topic + backoff)
+  int32_t pruneBody;  // ControlPrune body (makePrune: topic + backoff; PX entries add acctPiF each)
   int32_t pruneEnt10; // the same to a gossipsub v1.0 peer (topic only, gossipsub.go:1804-1807)
   int32_t ihaveHead;  // ControlIHave topicID field (the ids add acctIdF each)
 };
@@ -141,6 +141,7 @@ struct Dev {
   unsigned long long* rpcN;    // [E] RPCs sent over edge e
   const AcctT* acc;            // [T]
   int32_t acctIdF;             // one message id inside an IHAVE / IWANT
+  int32_t acctPiF;             // one PX PeerInfo inside a ControlPrune
   // EventTracer of the hosts with traced[u] != 0 (gs_set_trace); nullptr = off
   const uint8_t* traced;
   gs_trace_event* trace;
@@ -365,7 +366,7 @@ __device__ __forceinline__ bool px_peer(const Dev& d, int64_t e) {
   return d.proto == nullptr || d.proto[e] == GS_PROTO_GOSSIPSUB_V11;
 }
 // makePrune's ControlPrune entry size for the peer of edge e (RPC accounting)
-__device__ __forceinline__ int64_t prune_entry(const Dev& d, int64_t e, int t);
+__device__ __forceinline__ int64_t prune_entry(const Dev& d, int64_t e, int t, int npx);
 __device__ __forceinline__ bool behaves(const Dev& d, int v, unsigned bit) {
   return d.behave != nullptr && (d.behave[v] & bit) != 0;
 }
@@ -406,8 +407,9 @@ __device__ __forceinline__ void acct_send(const Dev& d, int64_t e, int64_t bytes
   d.rpcN[e] += (unsigned long long)n;
 }
 __device__ __forceinline__ bool has_record(const Dev& d, int64_t e) { return d.rstate == nullptr || d.rstate[e] != 0; }
-__device__ __forceinline__ int64_t prune_entry(const Dev& d, int64_t e, int t) {
-  return px_peer(d, e) ? d.acc[t].pruneEnt : d.acc[t].pruneEnt10;
+// the ControlMessage.prune entry of topic t to e's peer carrying npx PX peers
+__device__ __forceinline__ int64_t prune_entry(const Dev& d, int64_t e, int t, int npx) {
+  return px_peer(d, e) ? gs_pb_field((int64_t)d.acc[t].pruneBody + (int64_t)npx * d.acctPiF) : d.acc[t].pruneEnt10;
 }
 __device__ __forceinline__ void set_err(const Dev& d, int code);
 // n ids of this hop's arena (cur) for one wave or lane; ~0 = full (E_POOL

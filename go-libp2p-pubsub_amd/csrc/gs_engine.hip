@@ -188,6 +188,7 @@ struct gs_engine {
   bool acctOn = false;
   std::vector<int32_t> acctMsg, acctTl;
   int32_t acctIdLen = 0;
+  int32_t acctPidLen = 38, acctRecLen = 0;  // PX PeerInfo (gs_set_rpc_px_sizes)
   std::vector<int64_t> acctPend;        // (edge, bytes) pairs sent by the host side this hop
   int64_t* dAcctPend = nullptr;
   int64_t acctPendCap = 0;
@@ -502,10 +503,6 @@ int gs_engine::start() {
   if (!routerH.empty()) {
     anyRandom = false;
     for (uint8_t r : routerH) anyRandom = anyRandom || r == GS_ROUTER_RANDOMSUB;
-  }
-  if (doPX && acctOn) {
-    gs_set_error("peer exchange is supported without RPC accounting (PX record sizes are not modelled)");
-    return GS_EUNSUPPORTED;
   }
   if (doPX && N >= (1 << 26)) {  // a PX arena entry is topic << 26 | peer (gs_kernels_ctl.h px_append)
     gs_set_error("peer exchange supports fewer than 2^26 peers in this build");
@@ -1062,11 +1059,12 @@ int gs_engine::start() {
     for (int t = 0; t < T; ++t) {
       ah[t].msgF = (int32_t)gs_pb_field(acctMsg[t]);
       ah[t].graftEnt = (int32_t)gs_pb_field(gs_pb_graft(acctTl[t]));
-      ah[t].pruneEnt = (int32_t)gs_pb_field(gs_pb_prune(acctTl[t], bo));
+      ah[t].pruneBody = (int32_t)gs_pb_prune(acctTl[t], bo);
       ah[t].pruneEnt10 = (int32_t)gs_pb_field(gs_pb_prune_v10(acctTl[t]));
       ah[t].ihaveHead = (int32_t)gs_pb_field(acctTl[t]);
     }
     x.acctIdF = (int32_t)gs_pb_field(acctIdLen);
+    x.acctPiF = (int32_t)gs_pb_field(gs_pb_peerinfo(acctPidLen, acctRecLen));
     // the hello packet of every connection present at the start (pubsub.go:495)
     std::vector<unsigned long long> hb((size_t)E), hn((size_t)E, 1ull);
     for (int u = 0; u < N; ++u)
@@ -2497,6 +2495,14 @@ int gs_set_rpc_accounting(gs_engine* g, const int32_t* msg_size, int32_t id_len,
   g->acctMsg.assign(msg_size, msg_size + g->T);
   g->acctTl.assign(topic_len, topic_len + g->T);
   g->acctIdLen = id_len;
+  return GS_OK;
+}
+
+int gs_set_rpc_px_sizes(gs_engine* g, int32_t peer_id_len, int32_t record_len) {
+  if (g->started) { gs_set_error("gs_set_rpc_px_sizes: before the first step"); return GS_ESTATE; }
+  if (peer_id_len < 0 || record_len < 0) { gs_set_error("gs_set_rpc_px_sizes: negative size"); return GS_EINVAL; }
+  g->acctPidLen = peer_id_len;
+  g->acctRecLen = record_len;
   return GS_OK;
 }
 

@@ -1299,12 +1299,19 @@ __device__ __forceinline__ void phase_b_node(const Dev& d, const int v, int64_t 
           // with an empty control message (2 bytes); IWANT + PRUNEs for the
           // heartbeat RPC
           int64_t b = 0;
-          for (uint64_t m = joinRej; m; m &= m - 1) b += gs_pb_field(prune_entry(d, e, __ffsll((long long)m) - 1));
+          const int64_t pxA = d.doPX ? d.cPx[cur][r] : -1;  // the PRUNEs' PX lists
+          for (uint64_t m = joinRej; m; m &= m - 1) {
+            const int t = __ffsll((long long)m) - 1;
+            b += gs_pb_field(prune_entry(d, e, t, px_count(d, cur, pxA, 1ull << t)));
+          }
           if (srvB) b += (int64_t)srvB + 2;
           if (srvBS) b += (int64_t)srvBS + 2;
           if (iwantAny || prunesHb) {
             int64_t body = iwantAny ? gs_pb_field((int64_t)(iwantRec & 0xFFFFFF) * d.acctIdF) : 0;
-            for (uint64_t m = hbPr; m; m &= m - 1) body += prune_entry(d, e, __ffsll((long long)m) - 1);
+            for (uint64_t m = hbPr; m; m &= m - 1) {
+              const int t = __ffsll((long long)m) - 1;
+              body += prune_entry(d, e, t, px_count(d, cur, pxA, 1ull << t));
+            }
             b += gs_pb_field(body);
           }
           acct_send(d, e, b, nReplies);
@@ -2174,7 +2181,11 @@ __global__ __launch_bounds__(64) GS_OCC_HB void k_heartbeat(Dev d, int64_t hop, 
         body += gs_pb_field(d.acc[t].ihaveHead + (int64_t)sterm[t] * d.acctIdF);
       }
       for (uint64_t m = tograft; m; m &= m - 1) body += d.acc[__ffsll((long long)m) - 1].graftEnt;
-      for (uint64_t m = toprune; m; m &= m - 1) body += prune_entry(d, e, __ffsll((long long)m) - 1);
+      const int64_t pxA = d.doPX ? d.cPx[cur][rxi(d, e, d.rev[e])] : -1;  // the PRUNEs' PX lists
+      for (uint64_t m = toprune; m; m &= m - 1) {
+        const int t = __ffsll((long long)m) - 1;
+        body += prune_entry(d, e, t, px_count(d, cur, pxA, 1ull << t));
+      }
       acct_send(d, e, gs_pb_field(body), 1);
     }
   }
@@ -2524,7 +2535,11 @@ __global__ __launch_bounds__(64) void k_leave(Dev d, const int32_t* __restrict__
       d.cPre[cur][re] = (uint8_t)(d.cPre[cur][re] + __popcll(pruned));  // one sendPrune RPC per topic
       if (d.rpcB != nullptr) {
         int64_t b = 0;
-        for (uint64_t m = pruned; m; m &= m - 1) b += gs_pb_field(prune_entry(d, e, __ffsll((long long)m) - 1));
+        const int64_t pxA = d.doPX ? d.cPx[cur][re] : -1;  // the PRUNEs' PX lists
+        for (uint64_t m = pruned; m; m &= m - 1) {
+          const int t = __ffsll((long long)m) - 1;
+          b += gs_pb_field(prune_entry(d, e, t, px_count(d, cur, pxA, 1ull << t)));
+        }
         acct_send(d, e, b, __popcll(pruned));
       }
       if (rpc_traced(d, v, d.col[e]))

@@ -192,6 +192,7 @@ ABI_FUNCTIONS = [
       C.POINTER(i64), C.POINTER(u8)]),
     ("gs_read_deliveries", C.c_int, [P, i64, C.POINTER(i32), C.POINTER(i32)]),
     ("gs_set_rpc_accounting", C.c_int, [P, C.POINTER(i32), i32, C.POINTER(i32)]),
+    ("gs_set_rpc_px_sizes", C.c_int, [P, i32, i32]),
     ("gs_read_rpc_bytes", C.c_int, [P, C.POINTER(i64), C.POINTER(i64)]),
     ("gs_set_trace", C.c_int, [P, C.POINTER(u8), i64]),
     ("gs_set_trace_rpc", C.c_int, [P, i32]),

@@ -100,14 +100,16 @@ def WithDevice(dev):
     return ("device", int(dev))
 
 
-def WithRPCAccounting(msg_size, id_len=40, topic_len=None):
+def WithRPCAccounting(msg_size, id_len=40, topic_len=None, peer_id_len=38, record_len=0):
     """Per-edge RPC byte accounting (gs_set_rpc_accounting, SURVEY.md §8(f)
     rank 3): every RPC a host sends is measured as RPC.Size() (gossipsub.go:
     1121-1137) with messages of topic t msg_size[t] bytes (a scalar: all
     topics), ids id_len bytes, topic names topic_len[t] bytes (default: the
-    decimal index's length, as the trace encoder names topics).  Read with
-    Engine.rpc_bytes()."""
-    return ("rpc_acct", (msg_size, int(id_len), topic_len))
+    decimal index's length, as the trace encoder names topics), PX entries of
+    a PRUNE PeerInfo{peer id of peer_id_len bytes, signed record of record_len
+    bytes or none} (makePrune, gossipsub.go:1811-1836; gs_set_rpc_px_sizes).
+    Read with Engine.rpc_bytes()."""
+    return ("rpc_acct", (msg_size, int(id_len), topic_len, int(peer_id_len), int(record_len)))
 
 
 def WithEventTracer(nodes, capacity=1 << 22, rpc=False):
@@ -264,11 +266,12 @@ class Engine:
             _check(self.lib, self.lib.gs_set_frontier_mode(h, opts["frontier_mode"]))
         acct = opts.get("rpc_acct")
         if acct is not None:
-            ms, idl, tl = acct
+            ms, idl, tl, pid, rec = acct
             ms = np.ascontiguousarray(np.broadcast_to(np.asarray(ms, dtype=np.int32), (num_topics,)))
             tl = (np.array([len(str(t)) for t in range(num_topics)], dtype=np.int32) if tl is None
                   else np.ascontiguousarray(np.broadcast_to(np.asarray(tl, dtype=np.int32), (num_topics,))))
             _check(self.lib, self.lib.gs_set_rpc_accounting(h, _ptr(ms, C.c_int32), idl, _ptr(tl, C.c_int32)))
+            _check(self.lib, self.lib.gs_set_rpc_px_sizes(h, pid, rec))
         self.rpc_acct = acct is not None
         self.router = router
         self.hop_ns = cfg.hop_ns

@@ -448,6 +448,12 @@ int gs_read_exchange_stats(gs_engine* eng, double* host_ms, int64_t* bytes_in);
  * the first step.  A partitioned rank counts the RPCs its own nodes send. */
 int gs_set_rpc_accounting(gs_engine* eng, const int32_t* msg_size /*[T]*/, int32_t id_len,
                           const int32_t* topic_len /*[T]*/);
+/* Peer exchange under accounting: a PRUNE's PX entries (makePrune,
+ * gossipsub.go:1811-1836) are PeerInfo{peerID, signedPeerRecord} of
+ * peer_id_len and record_len bytes (record_len 0: no certified address book,
+ * the record is nil and absent).  Defaults 38 (an Ed25519 peer id) and 0.
+ * Before the first step. */
+int gs_set_rpc_px_sizes(gs_engine* eng, int32_t peer_id_len, int32_t record_len);
 /* bytes[e], rpcs[e]: totals sent by node u to col[e] (rowptr[u] <= e <
  * rowptr[u+1]) since the start (either array may be NULL); a partitioned rank
  * fills its own edges and zeroes the others. */

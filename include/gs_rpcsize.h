@@ -12,7 +12,8 @@
  *   ControlIHave   topicID=1, messageIDs=2 (repeated string)
  *   ControlIWant   messageIDs=1
  *   ControlGraft   topicID=1
- *   ControlPrune   topicID=1, peers=2 (none: PX off), backoff=3 (uint64 varint)
+ *   ControlPrune   topicID=1, peers=2 (PeerInfo, PX on), backoff=3 (uint64 varint)
+ *   PeerInfo       peerID=1, signedPeerRecord=2 (nil without a certified address book: absent)
  * rpcWithControl (comm.go:179-195) always sets Control, so a reply that only
  * carries messages still has an empty ControlMessage (2 bytes); rpcWithMessages
  * and rpcWithSubs (comm.go:167-177) set none.
@@ -52,6 +53,16 @@ GS_PBFN int64_t gs_pb_graft(int64_t topic_len) { return gs_pb_field(topic_len); 
  * (gossipsub.go:1803-1839): topicID and backoff seconds */
 GS_PBFN int64_t gs_pb_prune(int64_t topic_len, uint64_t backoff_s) {
   return gs_pb_field(topic_len) + 1 + gs_pb_vlen(backoff_s);
+}
+
+/* PeerInfo body (makePrune's PX entry, gossipsub.go:1820-1833): the peer id
+ * and, when the peerstore holds a signed peer record for it, the record */
+GS_PBFN int64_t gs_pb_peerinfo(int64_t peer_id_len, int64_t record_len) {
+  return gs_pb_field(peer_id_len) + (record_len > 0 ? gs_pb_field(record_len) : 0);
+}
+/* ControlPrune body for a v1.1 peer with npx PeerInfo entries of body pi */
+GS_PBFN int64_t gs_pb_prune_px(int64_t topic_len, uint64_t backoff_s, int64_t npx, int64_t pi) {
+  return gs_pb_prune(topic_len, backoff_s) + npx * gs_pb_field(pi);
 }
 
 /* ControlPrune body for a gossipsub v1.0 peer: topicID only (makePrune

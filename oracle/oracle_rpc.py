@@ -91,10 +91,12 @@ class Prune:  # ControlPrune
     topic: Optional[str] = None
     peers: List[bytes] = field(default_factory=list)  # PeerInfo{peerID} each
     backoff: Optional[int] = None
+    records: Optional[List[bytes]] = None  # PeerInfo.signedPeerRecord per peer (None: nil)
 
     def marshal(self) -> bytes:
         out = _ld(1, self.topic.encode()) if self.topic is not None else b""
-        out += b"".join(_ld(2, _ld(1, p)) for p in self.peers)
+        recs = self.records or [b""] * len(self.peers)
+        out += b"".join(_ld(2, _ld(1, p) + (_ld(2, r) if r else b"")) for p, r in zip(self.peers, recs))
         if self.backoff is not None:
             out += _uvarint(3 << 3 | 0) + _uvarint(self.backoff)
         return out

@@ -205,6 +205,7 @@ struct Sim {
   bool acct = false;
   std::vector<int32_t> acctMsg, acctTl;
   int32_t acctId = 0;
+  int32_t acctPid = 38, acctRec = 0;  // PX PeerInfo: peer id and signed record lengths
   std::vector<int64_t> rpcBytes, rpcCount;
   void account(int u, int p, int64_t bytes) {
     if (!acct) return;
@@ -325,7 +326,9 @@ int64_t Sim::rpcSize(const RPC& r) const {
     if (!r.ctl.iwant.empty()) c += gs_pb_field(gs_pb_iwant((int64_t)r.ctl.iwant.size(), acctId));
     for (int t : r.ctl.graft) c += gs_pb_field(gs_pb_graft(acctTl[t]));
     for (const PruneEntry& pe : r.ctl.prune)
-      c += gs_pb_field(pe.hasBackoff ? gs_pb_prune(acctTl[pe.topic], pe.backoff) : gs_pb_prune_v10(acctTl[pe.topic]));
+      c += gs_pb_field(pe.hasBackoff ? gs_pb_prune_px(acctTl[pe.topic], pe.backoff, (int64_t)pe.px.size(),
+                                                      gs_pb_peerinfo(acctPid, acctRec))
+                                     : gs_pb_prune_v10(acctTl[pe.topic]));
     s += gs_pb_field(c);
   }
   return s;
@@ -2080,7 +2083,6 @@ int gs_set_dormant(gs_engine* g, int32_t n, const int32_t* a, const int32_t* b) 
 int gs_set_rpc_accounting(gs_engine* g, const int32_t* msg_size, int32_t id_len, const int32_t* topic_len) {
   Sim& sim = g->sim;
   if (sim.started) { set_error("gs_set_rpc_accounting: before the first step"); return GS_ESTATE; }
-  if (sim.doPX) { set_error("RPC byte accounting does not size peer-exchange records"); return GS_EUNSUPPORTED; }
   if (!msg_size || !topic_len || id_len < 0) { set_error("gs_set_rpc_accounting: bad arguments"); return GS_EINVAL; }
   for (int t = 0; t < sim.T; ++t)
     if (msg_size[t] < 0 || topic_len[t] < 0) { set_error("gs_set_rpc_accounting: negative size"); return GS_EINVAL; }
@@ -2088,6 +2090,17 @@ int gs_set_rpc_accounting(gs_engine* g, const int32_t* msg_size, int32_t id_len,
   sim.acctMsg.assign(msg_size, msg_size + sim.T);
   sim.acctTl.assign(topic_len, topic_len + sim.T);
   sim.acctId = id_len;
+  return GS_OK;
+}
+
+// makePrune's PX PeerInfo sizes (gossipsub.go:1820-1833): peer id bytes and
+// signed-peer-record bytes (0: the peerstore has no certified address book)
+int gs_set_rpc_px_sizes(gs_engine* g, int32_t peer_id_len, int32_t record_len) {
+  Sim& sim = g->sim;
+  if (sim.started) { set_error("gs_set_rpc_px_sizes: before the first step"); return GS_ESTATE; }
+  if (peer_id_len < 0 || record_len < 0) { set_error("gs_set_rpc_px_sizes: negative size"); return GS_EINVAL; }
+  sim.acctPid = peer_id_len;
+  sim.acctRec = record_len;
   return GS_OK;
 }
 

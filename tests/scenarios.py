@@ -768,6 +768,13 @@ PX = {
     # and the honest hosts' heartbeat prunes of negative-score peers, dials into
     # slots that start down, IWANT spam on the new connections
     "px_adversarial": lambda lib, x=(): adversarial_mix(lib, n=300, seed=67, hb=12, px=0.15, extra=x),
+    # PX under RPC byte accounting: every PRUNE carries its PeerInfo entries
+    # (makePrune, gossipsub.go:1811-1836; 38-byte peer ids, no signed records)
+    "acct_px_scored": lambda lib, x=(): px_scored(lib, extra=(_acct(1),) + tuple(x)),
+    "acct_px_adversarial": lambda lib, x=(): adversarial_mix(lib, n=300, seed=67, hb=12, px=0.15,
+                                                             extra=(_acct(1),) + tuple(x)),
+    "acct_px_star_records": lambda lib, x=(): px_star(lib, extra=(WithRPCAccounting(130, id_len=30, peer_id_len=39,
+                                                                                    record_len=200),) + tuple(x)),
 }
 SCENARIOS.update(PX)
 
@@ -864,6 +871,8 @@ MIXED = {
     "mixed_scored": lambda lib, x=(): mixed_scored(lib, extra=x),
     "mixed_randomsub": lambda lib, x=(): mixed_randomsub(lib, extra=x),
     "acct_mixed": lambda lib, x=(): mixed_scored(lib, px=False, seed=84, extra=(_acct(3),) + tuple(x)),
+    # with PX: v1.1 peers' PRUNEs carry PeerInfo entries, v1.0 peers' none
+    "acct_mixed_px": lambda lib, x=(): mixed_scored(lib, seed=86, extra=(_acct(3),) + tuple(x)),
     # T >= 4: k_push is on, so its randomsub filter (rs_host && sel) and the
     # floodsub-peer publish filter run in the pushed segments
     "mixed_scored_4t": lambda lib, x=(): mixed_scored(lib, topics=4, seed=85, msgs=400, extra=x),

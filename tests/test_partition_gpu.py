@@ -129,6 +129,8 @@ def run_partitioned(world, name, oracle):
     (3, "px_star"),
     (2, "direct_churn"),
     (2, "px_gater"),
+    # PX under RPC byte accounting: PRUNE sizes with their PeerInfo entries
+    (2, "acct_px_scored"),
     # T >= 4: k_push's segments of cross-rank edges travel in the exchange and
     # the receivers read them as local ones (gs_exchange.h k_xp_*); a sender
     # whose region overflows sends -1 records (its receivers walk its list)

@@ -149,12 +149,3 @@ def test_gpu_px_trace_equals_oracle(name, oracle_path):
     _, _, ew = _run(oracle_path, name, nodes)
     _, _, eg = _run(PRODUCT_LIB, name, nodes)
     assert len(eg) == len(ew) and np.array_equal(eg, ew)
-
-
-@pytest.mark.gpu
-def test_gpu_refuses_px_with_accounting():
-    from scenarios import _acct
-    with pytest.raises(GossipEngineError) as ei:
-        e, hops = scenarios.SCENARIOS["px_star"](PRODUCT_LIB, (_acct(1),))
-        e.step(1)
-    assert ei.value.code == _abi.GS_EUNSUPPORTED

@@ -53,6 +53,29 @@ def prune(tl, bo):
     return field(tl) + 1 + vlen(bo)
 
 
+def peerinfo(pid, rec):
+    return field(pid) + (field(rec) if rec else 0)
+
+
+def prune_px(tl, bo, npx, pi):
+    return prune(tl, bo) + npx * field(pi)
+
+
+def test_px_prune_size_matches_protobuf_encoder():
+    """makePrune with PX (gossipsub.go:1811-1836): PeerInfo{peerID,
+    signedPeerRecord} entries, the record absent when nil (gs_pb_peerinfo /
+    gs_pb_prune_px of include/gs_rpcsize.h)."""
+    rng = random.Random(11)
+    for _ in range(200):
+        tl = rng.choice([1, 5, 126, 200])
+        bo = rng.choice([0, 60, 128, 70000])
+        pid = rng.choice([34, 38, 39, 130])
+        rec = rng.choice([0, 0, 120, 300])
+        k = rng.choice([0, 1, 16, 40])
+        pr = pb.Prune("x" * tl, peers=[b"p" * pid] * k, backoff=bo, records=[b"r" * rec] * k if rec else None)
+        assert pb.size(pb.RPC(control=pb.Control(prune=[pr]))) == field(field(prune_px(tl, bo, k, peerinfo(pid, rec))))
+
+
 def _msg(ms, rng):
     """A pb.Message whose Size() is ms (from / seqno / topic set, data fills)."""
     base = pb.Message(from_=b"p" * 38, seqno=b"s" * 8, topic="t")
