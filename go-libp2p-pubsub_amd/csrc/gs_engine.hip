@@ -758,13 +758,17 @@ int gs_engine::start() {
   // promise lives until its message arrives or the first heartbeat after its
   // expiry (applyIwantPenalties), so a node holds at most
   // degree x (ceil(IWantFollowupTime / HeartbeatInterval) + 2) of them.  The
-  // table is sized to that bound (banks of 64, at most 8); beyond it E_PROMISES.
+  // table is sized to that bound in banks of 64 (E_PROMISES only guards it).
   {
     int64_t live = 1;
     if (cfg.router == GS_ROUTER_GOSSIPSUB && gp.HeartbeatInterval > 0)
       live = (gp.IWantFollowupTime + gp.HeartbeatInterval - 1) / gp.HeartbeatInterval + 2;
     const int64_t bound = std::max<int64_t>(1, (int64_t)maxdeg * live);
-    x.promCap = (int32_t)(64 * std::min<int64_t>(8, (bound + 63) / 64));
+    if (bound > (int64_t)1 << 24) {
+      gs_set_error("promise table bound too large (degree x (IWantFollowupTime / HeartbeatInterval + 2) > 2^24)");
+      return GS_EUNSUPPORTED;
+    }
+    x.promCap = (int32_t)(64 * ((bound + 63) / 64));
   }
   const size_t NQ = (size_t)nOwnN * x.promCap;
   x.promMid = dalloc<int64_t>(NQ); x.promExp = dalloc<int64_t>(NQ); x.promSlot = dalloc<int32_t>(NQ);
@@ -1702,8 +1706,8 @@ int gs_engine::deviceErrorCode(int32_t err) {
     case E_NONE: return GS_OK;
     case E_POOL: gs_set_error("IWANT payload arena overflow (max(2^24 / ranks, 4 x owned edges) ids per rank per hop)"); return GS_ECAPACITY;
     case E_PROMISES:
-      gs_set_error("per-node promise table overflow (degree x (IWantFollowupTime / HeartbeatInterval + 2) entries, "
-                   "at most 512)");
+      gs_set_error("per-node promise table overflow (sized degree x (IWantFollowupTime / HeartbeatInterval + 2) "
+                   "entries)");
       return GS_ECAPACITY;
     case E_PEERTX:
       gs_set_error("IWANT retransmission overflow table full (gs_set_peertx_capacity: 2^16 entries per rank "

@@ -463,14 +463,16 @@ def adversarial_mix(lib, n=400, k=16, seed=51, sybil_frac=0.2, queue=6, msgs=600
     return e, hb * 10 + 5
 
 
-def promise_flood(lib, leaves=60, seed=53, extra=()):
+def promise_flood(lib, leaves=60, seed=53, follow_s=None, beats=9, extra=()):
     """More live IWANT promises per node than one wave's 64-entry bank: host 0
     at the centre of a star of 60 IHAVE spammers, each advertising a phantom id
     every heartbeat (gossipsub_spam_test.go:135-270).  Host 0 asks each one,
     promises (gossip_tracer.go:48-77), and every promise breaks 3 s later; with
     no P7 weight the spammers stay above GossipThreshold, so about 4 x 60
     promises are alive at once (the table holds degree x (IWantFollowupTime /
-    HeartbeatInterval + 2) = 300 entries)."""
+    HeartbeatInterval + 2) = 300 entries).  follow_s: IWantFollowupTime in
+    seconds (with 12, about 13 x 60 promises live at once: the table's liveness
+    bound is 840 entries); beats: phantom rounds."""
     n = leaves + 1
     rowptr = np.concatenate([[0, leaves], leaves + np.arange(1, leaves + 1)]).astype(np.int64)
     col = np.concatenate([np.arange(1, n), np.zeros(leaves)]).astype(np.int32)
@@ -481,15 +483,19 @@ def promise_flood(lib, leaves=60, seed=53, extra=()):
     beh[1:] = GS_BEHAVE_IHAVE_SPAM
     e = NewGossipSub(n, 1, (rowptr, col, outbound), graphs.all_subscribed(n, 1), WithPeerScore(sp, eth2_thresholds()),
                      WithBehaviour(beh), WithRecordDeliveries(), WithSeed(seed), WithHop(HOP),
-                     WithMessageWindow(4096), *extra, lib=lib)
-    hops = np.repeat(np.arange(5, 95, 10), leaves).astype(np.int64)
-    src = np.tile(np.arange(1, n), 9).astype(np.int32)
+                     WithMessageWindow(4096),
+                     *(() if follow_s is None else (WithGossipSubParams(GossipSubParams(IWantFollowupTime=follow_s * Second)),)),
+                     *extra, lib=lib)
+    hops = np.repeat(np.arange(5, 10 * beats + 5, 10), leaves).astype(np.int64)
+    src = np.tile(np.arange(1, n), beats).astype(np.int32)
     e.publish(src, np.zeros(len(src), np.int32), hops, kind=np.full(len(src), GS_MSG_PHANTOM, np.uint8))
-    return e, 100
+    return e, 10 * beats + 10
 
 
 ADVERSARIAL = {
     "promise_flood": lambda lib, x=(): promise_flood(lib, extra=x),
+    # a promise table past 512 entries per node (its liveness bound, 840)
+    "promise_flood_long": lambda lib, x=(): promise_flood(lib, follow_s=12, beats=24, extra=x),
     "spam_iwant": lambda lib, x=(): spam_iwant(lib, extra=x),
     "spam_ihave": lambda lib, x=(): spam_ihave(lib, extra=x),
     "spam_ihave_2t": lambda lib, x=(): spam_ihave(lib, topics=2, per_topic=4000, extra=x),
