@@ -525,6 +525,35 @@ __device__ __forceinline__ void rs_select(const Dev& d, int u, int64_t base, int
   const unsigned long long m = __ballot(sel);
   if (lane == 0) d.sel[(int64_t)u * d.S + slot] = m;
 }
+// rs_select for two messages at once on a node of degree <= 32: half h =
+// lane >> 5 takes message (slotA, slotB)[h] over every edge (lane & 31), the
+// same candidates, keys and lowest-lane tie rule (select_k_half), so each
+// message's mask equals rs_select's.  p / subp hold lane el's values in lanes
+// 0..31 (mirrored here).
+__device__ __forceinline__ void rs_select2(const Dev& d, int u, int64_t base, int deg, int pIn, uint64_t subpIn,
+                                           int slotA, int ffA, int slotB, int ffB) {
+  const int lane = lane_id();
+  const int h = lane >> 5, el = lane & 31;
+  const int p = __shfl(pIn, el);
+  const uint64_t subp = shfl_u64(subpIn, el);
+  const int slot = h ? slotB : slotA;
+  const int ff = h ? ffB : ffA;
+  const int t = slot / d.St;
+  const int origin = d.slotSrc[slot];
+  const bool cand = el < deg && ((subp >> t) & 1) && el != ff && p != origin;
+  const bool fs = cand && d.proto != nullptr && d.proto[base + el] == GS_PROTO_FLOODSUB;
+  const bool rc = cand && !fs;
+  const int n = __popc((uint32_t)(__ballot(rc) >> (32 * h)));  // this half's candidates
+  bool sel = cand;
+  const int target = d.rsTarget < n ? d.rsTarget : n;
+  if (n > 6 && target < n) {  // (per half: select_k_half runs under divergence)
+    const uint64_t key = gs_key64(d.seed, GS_SITE_RANDOMSUB, u, (uint32_t)d.slotMid[slot], p, 0);
+    sel = fs || select_k_half(rc, key, target);
+  }
+  const unsigned long long m = __ballot(sel);
+  if (lane == 0) d.sel[(int64_t)u * d.S + slotA] = m & 0xFFFFFFFFull;
+  if (lane == 32) d.sel[(int64_t)u * d.S + slotB] = m >> 32;
+}
 
 // Word sets of the message window (W <= 256 words): bit w set = word w may
 // hold a message published within the delivery age bound.
@@ -1883,6 +1912,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
   uint8_t* const ffRow = record ? d.ffrom + (int64_t)v * d.S : nullptr;
   const int64_t* const pubHop = d.slotPubHop;
   uint64_t* const pmRow = prow >= 0 ? d.pmask + (int64_t)prow * d.S : nullptr;
+  // randomsub targets (rs_select): a node of degree <= 32 draws two messages'
+  // masks per wave step (rs_select2), the odd one last
+  const bool rsV = rs_host(d, v);
+  const bool pair2 = deg <= 32;
+  const int rsP = valid ? u : -1;
+  const uint64_t rsSub = (rsV && valid && edge_up(d, base + lane)) ? d.subA[u] : 0ull;
+  int pendSlot = -1, pendFf = 0;
 #pragma unroll
   for (int j = 0; j < WPL; ++j) {
     const int w = lane + 64 * j;
@@ -1945,7 +1981,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
         }
       }
     }
-    if (rs_host(d, v)) {  // randomsub: targets of every message first delivered here
+    if (rsV) {  // randomsub: targets of every message first delivered here
       unsigned long long lanesWith = __ballot(Ud != 0);
       while (lanesWith) {
         const int src = __ffsll((long long)lanesWith) - 1;
@@ -1956,12 +1992,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(pa_waves<NAR
         while (y) {
           const int b = __ffsll((long long)y) - 1;
           y &= y - 1;
-          rs_select(d, v, base, deg, valid ? u : -1, valid && edge_up(d, base + lane) ? d.subA[u] : 0, wsrc * 64 + b,
-                    sFirst[fidx(rks, b)]);
+          const int slot = wsrc * 64 + b, ff = sFirst[fidx(rks, b)];
+          if (!pair2) {
+            rs_select(d, v, base, deg, rsP, rsSub, slot, ff);
+          } else if (pendSlot < 0) {
+            pendSlot = slot;
+            pendFf = ff;
+          } else {
+            rs_select2(d, v, base, deg, rsP, rsSub, pendSlot, pendFf, slot, ff);
+            pendSlot = -1;
+          }
         }
       }
     }
   }
+  if (pendSlot >= 0) rs_select(d, v, base, deg, rsP, rsSub, pendSlot, pendFf);
   GS_STAMP(4);
   if (lane == 0) d.fln[cur][v] = behaves(d, v, GS_BEHAVE_NO_FORWARD) ? 0 : (running < FC ? running : FC);
   if constexpr (DENSE) {

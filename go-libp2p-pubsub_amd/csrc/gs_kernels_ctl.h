@@ -1517,47 +1517,6 @@ __device__ __forceinline__ uint64_t emit_gossip(const Dev& d, int v, int t, int6
   return sel ? (1ull << t) : 0;
 }
 
-// select_k per half-wave: each half (lanes 0..31, 32..63) selects its own k
-// (a lane-varying value, uniform within the half) of its own candidates; the
-// same radix selection and the same "lowest lanes first" tie rule as select_k.
-// Works under divergence: a half that is not executing contributes nothing.
-// (Keeping both halves' selection state in scalar registers, so that the
-// lanes only test their key bit per round, measured slower: the config4
-// heartbeat went 22.5 -> 28.3 ms per launch.)
-__device__ __forceinline__ bool select_k_half(bool cand, uint64_t key, int k) {
-  const int lane = lane_id();
-  const int sh = lane & 32, bl = lane & 31;
-  uint32_t act = (uint32_t)(__ballot(cand) >> sh);
-  int n = __popc(act);
-  if (k <= 0 || n <= k) return cand;
-  uint32_t sel = 0;
-  int need = k;
-  for (int b = 63; b >= 0; --b) {
-    const uint32_t z = (uint32_t)(__ballot(((act >> bl) & 1) && !((key >> b) & 1)) >> sh);
-    const int nz = __popc(z);
-    if (nz <= need) {
-      sel |= z;
-      need -= nz;
-      act &= ~z;
-      n -= nz;
-    } else {
-      act = z;
-      n = nz;
-    }
-    if (need == 0) break;
-    if (n == need) {
-      sel |= act;
-      need = 0;
-      break;
-    }
-  }
-  while (need > 0 && act) {
-    sel |= act & (~act + 1);
-    act &= act - 1;
-    need--;
-  }
-  return (sel >> bl) & 1;
-}
 // number of lanes of this lane's half with x set
 __device__ __forceinline__ int half_count(bool x) {
   const unsigned long long b = __ballot(x);
