@@ -131,6 +131,7 @@ def run_partitioned(world, name, oracle):
     (2, "px_gater"),
     # PX under RPC byte accounting: PRUNE sizes with their PeerInfo entries
     (2, "acct_px_scored"),
+    (3, "acct_px_adversarial"),
     # T >= 4: k_push's segments of cross-rank edges travel in the exchange and
     # the receivers read them as local ones (gs_exchange.h k_xp_*); a sender
     # whose region overflows sends -1 records (its receivers walk its list)
@@ -139,6 +140,8 @@ def run_partitioned(world, name, oracle):
     (2, "push_overflow"),
     # MaxIHaveLength cuts past GS_CUTS per node: each rank's own cut table
     (2, "cut_spill_16t"),
+    # the promise table past 512 entries on the rank owning the star's centre
+    (2, "promise_flood_long"),
     # randomsub: a sender's per-message target masks (d.sel) travel with its
     # frontier list entries (gs_exchange.h k_x_sel); at T >= 4 k_push applies
     # them on the sender's rank
